@@ -1,0 +1,235 @@
+#!/usr/bin/env python3
+"""Benchmark: frames/s and Mray/s at 1920x1080 on the dragon (stand-in),
+KD traversal, 1..N MI355X GPUs (BASELINE.json metric; configs C3/C4).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+
+A step is one frame: bg fill -> primary rays -> KD traversal -> Moller-
+Trumbore -> Phong into the u32 frame (one fused kernel), plus, for N > 1,
+the RCCL gather of every rank's screen bands to rank 0 and the unpack
+kernel there.  Frames are fixed-size (1920x1080), so N > 1 is strong
+scaling.  The scene is the seeded synthetic stand-in for
+dragon_vrip_mod.ply (missing from the reference; 871,414 triangles).
+Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "frames/sec + Mray/s at 1920×1080, Stanford dragon 800k tris, 1/2/4/8 GPU"
+W, H = 1920, 1080
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# bytes per interior visit, leaf visit, accepted hit, pixel
+B_INT, B_LEAF, B_HIT, B_PIX = 36, 40, 24, 4
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--scene", default="dragon", choices=["dragon", "happy"])
+    ap.add_argument("--width", type=int, default=W)
+    ap.add_argument("--height", type=int, default=H)
+    ap.add_argument("--mode", type=int, default=0, help="0 KD, 1 flat list")
+    ap.add_argument("--collective", default="gather", choices=["gather", "allgather"])
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def build_scene(name):
+    from cpp_cuda_raytracer_dev_amd import raytracer as R, scenes
+    v, f = scenes.standin(name)
+    pts, n, leafs = R.assemble_mesh(v, f)
+    nodes = R.kd_build(leafs)
+    return pts, leafs, nodes
+
+
+def cpu_baseline(pts, nodes, w, h, seconds, threads, mode):
+    """The oracle (C restatement, -O2, OpenMP over rows) on the same frame,
+    repeated for ~`seconds`.  Test infrastructure: the checker, timed beside
+    the GPU; never part of the product path."""
+    from oracle import _oracle as O
+    on = np.zeros(len(nodes), O.NODE_DTYPE)
+    for k in nodes.dtype.names:
+        on[k] = nodes[k]
+    s = O.Scene(pts, O.default_rad(len(pts)), on if mode == 0 else None, O.camera(w, h))
+    rows = (0, h)
+    if mode == 1:  # flat list is O(npix*ntri): sample a band of rows
+        rows = (h // 2 - 4, h // 2 + 4)
+    frames, t0 = 0, time.perf_counter()
+    while True:
+        s.render(mode, rows=rows, nthreads=threads, want_hit=False)
+        frames += 1
+        if time.perf_counter() - t0 >= seconds and frames >= 2:
+            break
+    dt = time.perf_counter() - t0
+    s.close()
+    frac = (rows[1] - rows[0]) / h
+    fps = frames * frac / dt
+    return {"value": round(fps, 3), "unit": "frames/s", "cores": threads, "kind": "port",
+            "mray_per_s": round(fps * w * h / 1e6, 3),
+            "sample": f"{frames} x rows {rows[0]}-{rows[1]} of the same {w}x{h} frame, oracle/oracle.c "
+                      f"(-O2 -ffp-contract=off, OpenMP {threads} threads), {dt:.1f} s"}
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+    from cpp_cuda_raytracer_dev_amd import raytracer as R
+    from cpp_cuda_raytracer_dev_amd.distributed import FrameGather
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            print(f"bench.py: --gpus {a.gpus} needs torch.distributed.run with {a.gpus} processes", file=sys.stderr)
+            return 2
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    w, h = a.width, a.height
+
+    pts, leafs, nodes = build_scene(a.scene)
+    trixel = R.Trixel(len(pts), pts, device=local)
+    trixel.set_kd_nodes(nodes)
+    cam = R.Camera.default(w, h, device=local)
+    obj = R.Object(trixel)
+    cam.add_object(obj)
+    xf = obj.quat.xform()
+    stream = torch.cuda.Stream(device=dev)
+    sptr = stream.cuda_stream
+    tile = (world, rank)
+
+    # Algorithmic counts of this rank's tiles (one untimed counting frame).
+    npk = R.packed_pixels(w, h, world) if world > 1 else w * h
+    scratch = torch.zeros(npk, dtype=torch.int32, device=dev)
+    cam.render_into(scratch, mode=a.mode, flags=R.RT_FLAG_COUNT, tile=tile if world > 1 else None, stream=sptr)
+    torch.cuda.synchronize(dev)
+    cnt = cam.counters(reset=True)
+    my_pix = int(np.count_nonzero(np.repeat(np.arange((h + 7) // 8) % world == rank, 8)[:h])) * w
+    bytes_per_launch = B_INT * int(cnt[0]) + B_LEAF * int(cnt[1]) + B_HIT * int(cnt[2]) + B_PIX * my_pix
+
+    if world > 1:
+        def unpack(g, f):
+            R.unpack_bands(local, w, h, world, g, f, stream=torch.cuda.current_stream(dev).cuda_stream)
+        fg = FrameGather(dist, w, h, dev, a.collective, unpack=unpack)
+        out = fg.local
+    else:
+        fg = None
+        out = torch.zeros(w * h, dtype=torch.int32, device=dev)
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+
+    def frame(i=None):
+        with torch.cuda.stream(stream):
+            if i is not None:
+                ev[i][0].record(stream)
+            cam.render_into(out, xform=xf, mode=a.mode, tile=tile if world > 1 else None, stream=sptr)
+            if i is not None:
+                ev[i][1].record(stream)
+            if fg is not None:
+                fg.gather()
+
+    for _ in range(a.warmup):
+        frame()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        frame(i)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms_max = float(t[0]), float(t[1])
+        tb = torch.tensor([bytes_per_launch], dtype=torch.float64, device=dev)
+        dist.all_reduce(tb, op=dist.ReduceOp.MAX)
+    else:
+        kern_ms_max = kern_ms
+
+    if rank == 0:
+        fps = a.steps / elapsed
+        achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+        traffic = None
+        if os.path.exists(a.traffic_json):
+            try:
+                tj = json.load(open(a.traffic_json))
+                key = f"{a.scene}_{w}x{h}_m{a.mode}_n{world}"
+                traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        res = {
+            "metric": METRIC,
+            "value": round(fps, 2),
+            "unit": "frames/s",
+            "mray_per_s": round(fps * w * h / 1e6, 2),
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1e3 * elapsed / a.steps, 5),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {
+                "workload": f"{a.scene} stand-in {w}x{h}, {'KD traversal' if a.mode == 0 else 'flat list'}, "
+                            "primary rays + Phong, u32 frame on GPU 0",
+                "scene": f"synthetic {a.scene} stand-in, {len(pts)} triangles (seed 20221015)",
+                "resolution": [w, h],
+                "parallelism": f"screen bands x{world}" + (f" + RCCL {a.collective} to rank 0" if world > 1 else ""),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "kernel": "k_trace_kd" if a.mode == 0 else "k_trace_flat",
+                "kernel_ms_avg": round(kern_ms, 5),
+                "kernel_ms_avg_max_rank": round(kern_ms_max, 5),
+                "algorithmic_bytes_per_launch": bytes_per_launch,
+                "counts_per_launch": {"interior": int(cnt[0]), "leaf": int(cnt[1]), "accept": int(cnt[2]),
+                                      "hit_pixels": int(cnt[3]), "pixels": my_pix},
+                "bytes_model": "36*V_int + 40*V_leaf + 24*H + 4*P (SURVEY.md 8d)",
+            },
+        }
+        if not a.no_cpu_baseline and world == 1:
+            res["cpu_baseline"] = cpu_baseline(pts, nodes, w, h, a.cpu_seconds, a.cpu_threads, a.mode)
+        else:
+            res["cpu_baseline"] = None
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,84 @@
+"""Build the in-tree HIP library (gfx950) and the headless driver.
+
+    python -m cpp_cuda_raytracer_dev_amd.build            # librt_mi355x.so
+    python -m cpp_cuda_raytracer_dev_amd.build --driver   # + tools/rt_headless
+
+Flags that are part of the parity contract:
+-ffp-contract=off (no FMA contraction), correctly rounded fp32 division,
+f32 denormals kept.  No fast-math.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import shutil
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB = os.path.join(PKG, "librt_mi355x.so")
+ARCH = os.environ.get("RT_OFFLOAD_ARCH", "gfx950")
+
+SOURCES = ["rt_kernels.hip", "rt_api.cpp", "scene_host.cpp"]
+HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt",
+             "-fno-gpu-flush-denormals-to-zero", "-Wall", f"--offload-arch={ARCH}"]
+
+
+def hipcc() -> str:
+    for c in (shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def _stale(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_lib(force: bool = False, verbose: bool = False) -> str:
+    deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(CSRC, "rt_internal.h"),
+                                                       os.path.join(ROOT, "include", "rt_mi355x.h")]
+    if not force and not _stale(LIB, deps):
+        return LIB
+    tmp = LIB + ".tmp"
+    cmd = [hipcc(), *HIP_FLAGS, "-shared", "-o", tmp, *[os.path.join(CSRC, s) for s in SOURCES], "-lpthread"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+def build_driver(verbose: bool = False) -> str:
+    src = os.path.join(ROOT, "tools", "rt_headless.cpp")
+    out = os.path.join(ROOT, "tools", "rt_headless")
+    if not os.path.exists(src):
+        return ""
+    if _stale(out, [src, LIB, os.path.join(ROOT, "include", "rt_facade.hpp")]):
+        cmd = ["g++", "-O2", "-std=c++17", "-I", os.path.join(ROOT, "include"), "-o", out, src, LIB,
+               f"-Wl,-rpath,{PKG}", "-lpthread"]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+    return out
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--driver", action="store_true")
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args(argv)
+    print(build_lib(a.force, a.verbose))
+    if a.driver:
+        print(build_driver(a.verbose))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

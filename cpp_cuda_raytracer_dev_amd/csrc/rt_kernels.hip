@@ -1,0 +1,493 @@
+// rt_kernels.hip -- gfx950 kernels of the per-pixel ray-cast hot path.
+//
+// One fused kernel per frame: primary ray -> object transform -> KD-tree DFS
+// (or the flat triangle list) -> Moller-Trumbore -> Phong -> u32 0x00RRGGBB.
+// One ray per lane; a block is a 32x8 pixel tile (four 8x8 wave64 tiles), so
+// a wave's rays are spatially coherent and walk the same upper tree.  The DFS
+// stack lives in LDS (per-lane columns of a [depth][256] array) with its top
+// entry in a register.  Blocks are remapped so each XCD's L2 serves a
+// contiguous band of screen tiles.
+//
+// Arithmetic follows the reference expression by expression (SURVEY.md §5
+// H1-H16): single precision with contraction off (-ffp-contract=off), the
+// reference's double-promoted epsilons evaluated in double, correctly
+// rounded float division (equal to the reference's (float)(1.0/f)), the
+// 21-step fast inverse square root, and the deterministic pow5 shared with the
+// oracle.  Every kernel cites the reference code it replaces.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rt_internal.h"
+
+namespace rt {
+namespace {
+
+constexpr double kEps = 1e-16;                  // TD/vector.cuh:10-11 (double literals)
+// Smallest float >= 1e-16: for a float x, (double)x < 1e-16 <=> x < kEpsF and
+// (double)x > -1e-16 <=> x > -kEpsF (1e-16 is not a float).  Checked in tests.
+constexpr float kEpsF = __builtin_bit_cast(float, 0x24e69595u);
+constexpr float kDrawDistance = 400.0f;         // TD/Trixel.cu:47
+constexpr uint32_t kBackground = 0x00F08200u;   // VEC4<T_uint>(240,130,0,0), TD/Camera.cpp:72
+constexpr uint32_t kMiss = 0xFFFFFFFFu;
+
+// device_inverse_sqrt, TD/vector.cuh:79-95 (seed from bits(s/2), 21 steps).
+__device__ __forceinline__ float rsqrt21(float x, float y, float z) {
+    float s = (x * x) + (y * y) + (z * z);
+    const float half = 0.5f * s;
+    uint32_t i = 0x5f375a86u - (__float_as_uint(half) >> 1);
+    float r = __uint_as_float(i);
+#pragma unroll
+    for (int k = 0; k < 21; k++) r = r * (1.5f - half * r * r);
+    return r;
+}
+
+// device_cross / device_dot, TD/vector.cuh:72-77,121-124
+__device__ __forceinline__ void cross3(float& cx, float& cy, float& cz, float ax, float ay,
+                                       float az, float bx, float by, float bz) {
+    cx = ay * bz - az * by;
+    cy = az * bx - ax * bz;
+    cz = ax * by - ay * bx;
+}
+__device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, float by, float bz) {
+    return (ax * bx) + (ay * by) + (az * bz);
+}
+
+// powf(|x|, 5) of TD/Camera.cu:45 as one deterministic rounding (H5).
+__device__ __forceinline__ float pow5(float x) {
+    double d = (double)x;
+    double d2 = d * d;
+    double d4 = d2 * d2;
+    return (float)(d4 * d);
+}
+
+// (u8)(float) with NaN -> 0 (H14).
+__device__ __forceinline__ uint32_t to_u8(float t) {
+    if (!(t >= 0.0f)) return 0u;
+    if (t >= 256.0f) return 255u;
+    return (uint32_t)(int)t;
+}
+
+// color_cam_cuda, TD/Camera.cu:27-60 (norm.x used twice in the dot, H1).
+__device__ uint32_t phong(const float pnt[3], const float nrm[3], const float rmd[3],
+                          const float rad[3]) {
+    float sdx = 2 - pnt[0], sdy = 2 - pnt[1], sdz = 2 - pnt[2];
+    const float r = rsqrt21(sdx, sdy, sdz);
+    sdx *= r; sdy *= r; sdz *= r;
+    const float dot_r_n = dot3(sdx, sdy, sdz, nrm[0], nrm[0], nrm[2]);
+    const float rx = (sdx - (2 * dot_r_n * nrm[0])) * rmd[0];
+    const float ry = (sdy - (2 * dot_r_n * nrm[1])) * rmd[1];
+    const float rz = (sdz - (2 * dot_r_n * nrm[2])) * rmd[2];
+    const float diff = (float)(.6 * (double)fabsf(dot_r_n));
+    const float spec = (float)((double)pow5(fabsf((rx + ry + rz))) * .3);
+    float pr = 0.0f, pg = 0.0f, pb = 0.0f;
+    pr += (rad[0] * diff) + (1 * spec);
+    pg += (rad[1] * diff) + (1 * spec);
+    pb += (rad[2] * diff) + (1 * spec);
+    const float mx = fmaxf(fmaxf(pr, pg), pb);
+    return (to_u8((pr / mx) * 255) << 16) | (to_u8((pg / mx) * 255) << 8) | to_u8((pb / mx) * 255);
+}
+
+// Block -> (tile_x, slot), XCD-aware: blocks b and b+8 share an XCD, so give
+// each XCD a contiguous run of tiles (bijective for any grid size).
+__device__ __forceinline__ void tile_of_block(int32_t tiles_x, int32_t nblocks, int32_t& tx,
+                                              int32_t& slot) {
+    const int32_t b = (int32_t)blockIdx.x;
+    const int32_t q = nblocks >> 3, rem = nblocks & 7;
+    const int32_t xcd = b & 7, k = b >> 3;
+    const int32_t t = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + k;
+    slot = t / tiles_x;
+    tx = t - slot * tiles_x;
+}
+
+struct Pixel {
+    int32_t x, y;      // frame coordinates (row 0 = bottom, TD/WinMain.cpp:32)
+    int64_t out;       // index into the (packed) output buffer
+};
+
+__device__ __forceinline__ bool pixel_of_thread(const TraceParams& P, Pixel& px) {
+    int32_t tx, slot;
+    tile_of_block(P.tiles_x, P.tiles_x * P.slots, tx, slot);
+    const int32_t lane = (int32_t)threadIdx.x & 63, wave = (int32_t)threadIdx.x >> 6;
+    const int32_t band = P.rank + slot * P.nranks;
+    const int32_t ly = lane >> 3;
+    px.x = tx * kTileW + wave * 8 + (lane & 7);
+    px.y = band * kTileH + ly;
+    px.out = (int64_t)(slot * kTileH + ly) * P.w + px.x;
+    return px.x < P.w && px.y < P.h;
+}
+
+// init_cam_mem_cuda, TD/Camera.cu:103-104: rmd = n + u*ix + v*iy, normalised.
+__device__ __forceinline__ void primary_ray(const TraceParams& P, int32_t ix, int32_t iy,
+                                            float rmd[3]) {
+    const float fx = (float)(uint64_t)ix, fy = (float)(uint64_t)iy;
+    float x = P.n_mod[0] + P.u_mod[0] * fx + P.v_mod[0] * fy;
+    float y = P.n_mod[1] + P.u_mod[1] * fx + P.v_mod[1] * fy;
+    float z = P.n_mod[2] + P.u_mod[2] * fx + P.v_mod[2] * fy;
+    const float r = rsqrt21(x, y, z);
+    rmd[0] = x * r; rmd[1] = y * r; rmd[2] = z * r;
+}
+
+__device__ __forceinline__ void wave_count_add(unsigned long long* dst, uint32_t v) {
+    // one atomic per wave: reduce with cross-lane shuffles first
+    unsigned long long s = v;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if (((int)threadIdx.x & 63) == 0 && s) atomicAdd(dst, s);
+}
+
+// ---------------------------------------------------------------- KD trace
+
+// intersect_voxel_cuda (TD/Trixel.cu:41-172) fused with set_cam_cuda +
+// color_cam_cuda (TD/Camera.cu:12-69).
+template <bool kTranslated, bool kWriteHit, bool kCount>
+__global__ __launch_bounds__(kBlock) void k_trace_kd(TraceParams P) {
+    __shared__ uint32_t stack[kMaxDepth * kBlock];
+    Pixel px;
+    const bool live = pixel_of_thread(P, px);
+    if (!live) return;  // no barriers in this kernel
+
+    float cam[3];
+    primary_ray(P, px.x, px.y, cam);
+    const float* X = P.xf;
+    // object transform of the ray, TD/Trixel.cu:60-66 (identity in every config)
+    const float odx = X[3], ody = X[7], odz = X[11];
+    const float rx = -1 * (X[0] * -cam[0] + X[1] * -cam[1] + X[2] * -cam[2]);
+    const float ry = -1 * (X[4] * -cam[0] + X[5] * -cam[1] + X[6] * -cam[2]);
+    const float rz = -1 * (X[8] * -cam[0] + X[9] * -cam[1] + X[10] * -cam[2]);
+    // per-ray invariants of the slab test (TD/Trixel.cu:76-95)
+    const float ix = 1 / rx, iy = 1 / ry, iz = 1 / rz;
+    const float ox = odx / rx, oy = ody / ry, oz = odz / rz;
+    const bool sx = rx > 0, sy = ry > 0, sz = rz > 0;
+    // dir and ds for each one-hot cut axis (TD/Trixel.cu:88-90)
+    const float dir_a[3] = {(rx * 1.0f) + (ry * 0.0f) + (rz * 0.0f),
+                            (rx * 0.0f) + (ry * 1.0f) + (rz * 0.0f),
+                            (rx * 0.0f) + (ry * 0.0f) + (rz * 1.0f)};
+    const float ds_a[3] = {(odx * 1.0f) + (ody * 0.0f) + (odz * 0.0f),
+                           (odx * 0.0f) + (ody * 1.0f) + (odz * 0.0f),
+                           (odx * 0.0f) + (ody * 0.0f) + (odz * 1.0f)};
+
+    float d = kDrawDistance;
+    uint32_t best = kMiss;
+    uint32_t n_int = 0, n_leaf = 0, n_acc = 0, n_desc = 0;
+    uint32_t* stk = stack + threadIdx.x;   // column of this lane: stk[k * kBlock]
+    int sp = 0;
+    uint32_t ref = P.root_ref;
+    for (;;) {
+        if (ref & kLeafBit) {
+            // Moller-Trumbore at a leaf, TD/Trixel.cu:98-145
+            const uint32_t t = ref & ~kLeafBit;
+            if (kCount) n_leaf++;
+            const float4 A = P.trec[4 * (size_t)t];
+            const float4 B = P.trec[4 * (size_t)t + 1];
+            const float4 Cq = P.trec[4 * (size_t)t + 2];
+            const float e1x = A.x, e1y = A.y, e1z = A.z;
+            const float e2x = A.w, e2y = B.x, e2z = B.y;
+            const float dtx = B.z, dty = B.w, dtz = Cq.x;
+            float qpx, qpy, qpz;
+            cross3(qpx, qpy, qpz, rx, ry, rz, e2x, e2y, e2z);
+            const float f = dot3(qpx, qpy, qpz, e1x, e1y, e1z);
+            if (!(f < kEpsF && f > -kEpsF)) {
+                const float pe1 = 1.0f / f;   // == (float)(1.0 / (double)f)
+                const float tx = dtx - odx, ty = dty - ody, tz = dtz - odz;
+                const float u = pe1 * dot3(qpx, qpy, qpz, tx, ty, tz);
+                float qx, qy, qz;
+                cross3(qx, qy, qz, tx, ty, tz, e1x, e1y, e1z);
+                const float v = pe1 * dot3(rx, ry, rz, qx, qy, qz);
+                const float w = pe1 * dot3(e2x, e2y, e2z, qx, qy, qz);
+                // (u+v) > 1 + 1e-16 is (u+v) > 1.0 in double
+                if ((w < d) && !((u < kEpsF) || (v < kEpsF) || ((u + v) > 1.0f) || (w < kEpsF))) {
+                    d = w;
+                    best = t;
+                    if (kCount) n_acc++;
+                }
+            }
+            if (sp == 0) break;
+            ref = stk[(--sp) * kBlock];
+            continue;
+        }
+        // interior node: slab test and split-plane child order, TD/Trixel.cu:76-95,146-168
+        if (kCount) n_int++;
+        const float4 a = P.inode[3 * (size_t)ref];
+        const float4 b = P.inode[3 * (size_t)ref + 1];
+        const uint4 c = reinterpret_cast<const uint4*>(P.inode)[3 * (size_t)ref + 2];
+        const float t0x = sx ? a.x * ix : a.y * ix;
+        const float t1x = sx ? a.y * ix : a.x * ix;
+        const float t0y = sy ? a.z * iy : a.w * iy;
+        const float t1y = sy ? a.w * iy : a.z * iy;
+        const float t0z = sz ? b.x * iz : b.y * iz;
+        const float t1z = sz ? b.y * iz : b.x * iz;
+        float maxt0 = fmaxf(t0z + oz, fmaxf(t0x + ox, t0y + oy));
+        float mint1 = fminf(t1z + oz, fminf(t1x + ox, t1y + oy));
+        if ((double)mint1 >= (double)maxt0 - kEps && (double)maxt0 > -kEps) {
+            if (kCount) n_desc++;
+            const uint32_t axis = c.z;
+            const float dir = axis == 0 ? dir_a[0] : axis == 1 ? dir_a[1] : dir_a[2];
+            maxt0 *= dir;
+            mint1 *= dir;
+            float s1, s2;
+            if (kTranslated) {
+                const float ds = axis == 0 ? ds_a[0] : axis == 1 ? ds_a[1] : ds_a[2];
+                s1 = (float)((double)b.z + kEps + (double)ds);
+                s2 = b.w + ds;
+            } else {
+                s1 = __uint_as_float(c.w);   // (float)((double)s1 + 1e-16), ds == 0
+                s2 = b.w;
+            }
+            const uint32_t L = c.x, R = c.y;
+            if ((double)maxt0 < (double)s2 + kEps) {
+                // pushes right (if) then left: left is popped first
+                if ((double)mint1 > (double)s2 - kEps) {
+                    if (sp >= P.max_depth) { atomicOr(P.err, 1); break; }
+                    stk[(sp++) * kBlock] = R;
+                }
+                ref = L;
+            } else {
+                // pushes left (if) then right: right is popped first
+                if (mint1 < s1 || maxt0 < s1) {
+                    if (sp >= P.max_depth) { atomicOr(P.err, 1); break; }
+                    stk[(sp++) * kBlock] = L;
+                }
+                ref = R;
+            }
+            continue;
+        }
+        if (sp == 0) break;
+        ref = stk[(--sp) * kBlock];
+    }
+
+    uint32_t argb = kBackground;
+    if (best != kMiss) {
+        // nearest-hit writes of TD/Trixel.cu:128-140, done once for the final hit
+        const float4 N = P.shade[2 * (size_t)best];
+        const float4 M = P.shade[2 * (size_t)best + 1];
+        const float pnt[3] = {d * rx + odx, d * ry + ody, d * rz + odz};
+        // norm.device_rotate(rot_m, i, -1), TD/vector.cuh:23-33
+        const float ax = -1 * N.x, ay = -1 * N.y, az = -1 * N.z;
+        const float nrm[3] = {(ax * X[0] + ay * X[1] + az * X[2]) * -1,
+                              (ax * X[4] + ay * X[5] + az * X[6]) * -1,
+                              (ax * X[8] + ay * X[9] + az * X[10]) * -1};
+        const float rad[3] = {M.x, M.y, M.z};
+        argb = phong(pnt, nrm, cam, rad);
+    }
+    P.argb[px.out] = argb;
+    if (kWriteHit) P.hit[px.out] = best == kMiss ? (int64_t)-1 : (int64_t)best;
+    if (kCount) {
+        wave_count_add(&P.counters[0], n_int);
+        wave_count_add(&P.counters[1], n_leaf);
+        wave_count_add(&P.counters[2], n_acc);
+        wave_count_add(&P.counters[3], best != kMiss ? 1u : 0u);
+        wave_count_add(&P.counters[4], n_desc);
+    }
+}
+
+// -------------------------------------------------------------- flat trace
+
+// intersect_trixel_cuda (TD/Trixel.cu:173-209) fused with the shading.  The
+// triangle loop index is wave-uniform, so its 64-B records arrive through the
+// scalar data cache into SGPRs; the exact sign tests below skip the division
+// for the (common) rays that cannot pass u >= eps, v >= eps or w >= eps.
+template <bool kWriteHit, bool kCount>
+__global__ __launch_bounds__(kBlock) void k_trace_flat(TraceParams P) {
+    Pixel px;
+    if (!pixel_of_thread(P, px)) return;
+    float rmd[3];
+    primary_ray(P, px.x, px.y, rmd);
+    const float rx = rmd[0], ry = rmd[1], rz = rmd[2];
+    float d = kDrawDistance;
+    uint32_t best = kMiss;
+    uint32_t n_acc = 0;
+    const float4* __restrict__ T = P.trec;
+    const uint32_t ntri = P.ntri;
+    for (uint32_t t = 0; t < ntri; t++) {
+        const float4 A = T[4 * (size_t)t];
+        const float4 B = T[4 * (size_t)t + 1];
+        const float4 Cq = T[4 * (size_t)t + 2];
+        const float4 D = T[4 * (size_t)t + 3];
+        float qpx, qpy, qpz;
+        cross3(qpx, qpy, qpz, rx, ry, rz, A.w, B.x, B.y);
+        const float f = dot3(qpx, qpy, qpz, A.x, A.y, A.z);
+        const float U = dot3(qpx, qpy, qpz, B.z, B.w, Cq.x);
+        const float V = dot3(rx, ry, rz, Cq.y, Cq.z, Cq.w);
+        const float W = D.x;
+        // u = pe1*U with sign(pe1) = sign(f): a zero or wrong-signed U makes
+        // u <= 0 < eps (NaN is never rejected here), likewise V and W.
+        const bool pos = f > 0;
+        const bool reject = (pos ? (U <= 0 || V <= 0 || W <= 0) : (U >= 0 || V >= 0 || W >= 0));
+        if (reject) continue;
+        if (!(f < kEpsF && f > -kEpsF)) {
+            const float pe1 = 1.0f / f;
+            const float u = pe1 * U;
+            const float v = pe1 * V;
+            const float w = pe1 * W;
+            if ((w < d) && !((u < kEpsF) || (v < kEpsF) || ((u + v) > 1.0f) || (w < kEpsF))) {
+                d = w;
+                best = t;
+                if (kCount) n_acc++;
+            }
+        }
+    }
+    uint32_t argb = kBackground;
+    if (best != kMiss) {
+        const float4 N = P.shade[2 * (size_t)best];
+        const float4 M = P.shade[2 * (size_t)best + 1];
+        const float pnt[3] = {d * rx, d * ry, d * rz};
+        const float nrm[3] = {N.x, N.y, N.z};
+        const float rad[3] = {M.x, M.y, M.z};
+        argb = phong(pnt, nrm, rmd, rad);
+    }
+    P.argb[px.out] = argb;
+    if (kWriteHit) P.hit[px.out] = best == kMiss ? (int64_t)-1 : (int64_t)best;
+    if (kCount) {
+        wave_count_add(&P.counters[1], ntri);
+        wave_count_add(&P.counters[2], n_acc);
+        wave_count_add(&P.counters[3], best != kMiss ? 1u : 0u);
+    }
+}
+
+// ------------------------------------------------------------------ prep
+
+// init_tri_mem_cuda, TD/Trixel.cu:11-27, plus the Color::rad copy.
+// tri_world = (p1.xyz, e1.x) (e1.yz, e2.xy) (e2.z, n.xyz); shade = (n, 0) (rad, 0)
+__global__ void k_tri_world(const float* __restrict__ pts, const float* __restrict__ rad,
+                            uint32_t ntri, float4* __restrict__ tw, float4* __restrict__ shade) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ntri) return;
+    const float* P = pts + 9 * (size_t)i;
+    const float e1x = P[3] - P[0], e1y = P[4] - P[1], e1z = P[5] - P[2];
+    const float e2x = P[6] - P[0], e2y = P[7] - P[1], e2z = P[8] - P[2];
+    float nx, ny, nz;
+    cross3(nx, ny, nz, e1x, e1y, e1z, e2x, e2y, e2z);
+    const float r = rsqrt21(nx, ny, nz);
+    nx *= r; ny *= r; nz *= r;
+    tw[3 * (size_t)i] = make_float4(P[0], P[1], P[2], e1x);
+    tw[3 * (size_t)i + 1] = make_float4(e1y, e1z, e2x, e2y);
+    tw[3 * (size_t)i + 2] = make_float4(e2z, nx, ny, nz);
+    shade[2 * (size_t)i] = make_float4(nx, ny, nz, 0.0f);
+    shade[2 * (size_t)i + 1] = make_float4(rad[3 * (size_t)i], rad[3 * (size_t)i + 1], rad[3 * (size_t)i + 2], 0.0f);
+}
+
+// init_cam_tri_mem_cuda, TD/Trixel.cu:29-36: d_t = cam - p1, d_q = d_t x e1, d_w = d_q . e2
+__global__ void k_cam_tri(const float4* __restrict__ tw, uint32_t ntri, float cx, float cy,
+                          float cz, float4* __restrict__ trec) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ntri) return;
+    const float4 A = tw[3 * (size_t)i], B = tw[3 * (size_t)i + 1], Cq = tw[3 * (size_t)i + 2];
+    const float e1x = A.w, e1y = B.x, e1z = B.y, e2x = B.z, e2y = B.w, e2z = Cq.x;
+    const float dtx = cx - A.x, dty = cy - A.y, dtz = cz - A.z;
+    float qx, qy, qz;
+    cross3(qx, qy, qz, dtx, dty, dtz, e1x, e1y, e1z);
+    const float dw = dot3(qx, qy, qz, e2x, e2y, e2z);
+    trec[4 * (size_t)i] = make_float4(e1x, e1y, e1z, e2x);
+    trec[4 * (size_t)i + 1] = make_float4(e2y, e2z, dtx, dty);
+    trec[4 * (size_t)i + 2] = make_float4(dtz, qx, qy, qz);
+    trec[4 * (size_t)i + 3] = make_float4(dw, 0.0f, 0.0f, 0.0f);
+}
+
+// init_cam_voxel_mem_cuda, TD/Camera.cu:137-162, into the dense interior
+// record layout (rt_internal.h).  obj_center is 0 (TD/Camera.cpp:167-170).
+__global__ void k_cam_nodes(const rt_kd_node* __restrict__ nodes, const int32_t* __restrict__ ids,
+                            const uint32_t* __restrict__ node_ref, int64_t ninterior, float cx,
+                            float cy, float cz, float4* __restrict__ out) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= ninterior) return;
+    const rt_kd_node nd = nodes[ids[k]];
+    const float ocx = 0.0f, ocy = 0.0f, ocz = 0.0f;
+    const float t0x = nd.x0 - cx + ocx, t1x = nd.x1 - cx + ocx;
+    const float t0y = nd.y0 - cy + ocy, t1y = nd.y1 - cy + ocy;
+    const float t0z = nd.z0 - cz + ocz, t1z = nd.z1 - cz + ocz;
+    const int cd = nd.cut_flag;
+    const float fx = (cd == 0 || cd == 3) ? 1.0f : 0.0f;
+    const float fy = (cd == 1 || cd == 4) ? 1.0f : 0.0f;
+    const float fz = (cd == 2 || cd == 5) ? 1.0f : 0.0f;
+    const float s1 = nd.s1 - (((cx + ocx) * fx) + ((cy + ocy) * fy) + ((cz + ocz) * fz));
+    const float s2 = nd.s2 - (((cx + ocx) * fx) + ((cy + ocy) * fy) + ((cz + ocx) * fz));
+    const float s1e = (float)((double)s1 + kEps);
+    const uint32_t axis = fx != 0.0f ? 0u : fy != 0.0f ? 1u : 2u;
+    out[3 * k] = make_float4(t0x, t1x, t0y, t1y);
+    out[3 * k + 1] = make_float4(t0z, t1z, s1, s2);
+    out[3 * k + 2] = make_float4(__uint_as_float(node_ref[nd.left]), __uint_as_float(node_ref[nd.right]),
+                                 __uint_as_float(axis), s1e);
+}
+
+// Rank 0's frame assembly after the gather: [rank][slot][8 rows][w] -> frame.
+__global__ void k_unpack(int32_t w, int32_t h, int32_t nranks, int32_t slots,
+                         const uint32_t* __restrict__ g, uint32_t* __restrict__ frame) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)w * h) return;
+    const int32_t y = (int32_t)(i / w), x = (int32_t)(i - (int64_t)y * w);
+    const int32_t band = y / kTileH, r = y - band * kTileH;
+    const int32_t rank = band % nranks, slot = band / nranks;
+    frame[i] = g[(((int64_t)rank * slots + slot) * kTileH + r) * w + x];
+}
+
+template <class K>
+int check_launch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(RT_ERR_HIP, "%s launch failed: %s", what, hipGetErrorString(e));
+    return RT_OK;
+}
+
+}  // namespace
+
+int launch_tri_world(const float* points9, const float* rad3, uint32_t ntri, float4* tri_world,
+                     float4* shade, void* stream) {
+    if (ntri == 0) return RT_OK;
+    k_tri_world<<<(ntri + 255) / 256, 256, 0, (hipStream_t)stream>>>(points9, rad3, ntri, tri_world, shade);
+    return check_launch<void>("k_tri_world");
+}
+
+int launch_cam_tri(const float4* tri_world, uint32_t ntri, const float pos[3], float4* trec,
+                   void* stream) {
+    if (ntri == 0) return RT_OK;
+    k_cam_tri<<<(ntri + 255) / 256, 256, 0, (hipStream_t)stream>>>(tri_world, ntri, pos[0], pos[1], pos[2], trec);
+    return check_launch<void>("k_cam_tri");
+}
+
+int launch_cam_nodes(const rt_kd_node* nodes, const int32_t* ids, const uint32_t* node_ref,
+                     int64_t ninterior, const float pos[3], float4* inode, void* stream) {
+    if (ninterior == 0) return RT_OK;
+    k_cam_nodes<<<(unsigned)((ninterior + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+        nodes, ids, node_ref, ninterior, pos[0], pos[1], pos[2], inode);
+    return check_launch<void>("k_cam_nodes");
+}
+
+int launch_trace(const TraceParams& p, uint32_t mode, uint32_t flags, void* stream) {
+    const unsigned grid = (unsigned)(p.tiles_x * p.slots);
+    if (grid == 0) return RT_OK;
+    hipStream_t s = (hipStream_t)stream;
+    const bool wh = (flags & RT_FLAG_WRITE_HIT) != 0, cnt = (flags & RT_FLAG_COUNT) != 0;
+    if (mode == RT_MODE_FLAT) {
+        if (wh && cnt) k_trace_flat<true, true><<<grid, kBlock, 0, s>>>(p);
+        else if (wh) k_trace_flat<true, false><<<grid, kBlock, 0, s>>>(p);
+        else if (cnt) k_trace_flat<false, true><<<grid, kBlock, 0, s>>>(p);
+        else k_trace_flat<false, false><<<grid, kBlock, 0, s>>>(p);
+        return check_launch<void>("k_trace_flat");
+    }
+    const bool tr = p.xf[3] != 0.0f || p.xf[7] != 0.0f || p.xf[11] != 0.0f;
+#define RT_KD(T, H, C) k_trace_kd<T, H, C><<<grid, kBlock, 0, s>>>(p)
+    if (tr) {
+        if (wh && cnt) RT_KD(true, true, true);
+        else if (wh) RT_KD(true, true, false);
+        else if (cnt) RT_KD(true, false, true);
+        else RT_KD(true, false, false);
+    } else {
+        if (wh && cnt) RT_KD(false, true, true);
+        else if (wh) RT_KD(false, true, false);
+        else if (cnt) RT_KD(false, false, true);
+        else RT_KD(false, false, false);
+    }
+#undef RT_KD
+    return check_launch<void>("k_trace_kd");
+}
+
+int launch_unpack(int32_t w, int32_t h, int32_t nranks, const uint32_t* gathered, uint32_t* frame,
+                  void* stream) {
+    const int32_t nbands = (h + kTileH - 1) / kTileH;
+    const int32_t slots = (nbands + nranks - 1) / nranks;
+    const int64_t n = (int64_t)w * h;
+    if (n == 0) return RT_OK;
+    k_unpack<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(w, h, nranks, slots, gathered, frame);
+    return check_launch<void>("k_unpack");
+}
+
+}  // namespace rt

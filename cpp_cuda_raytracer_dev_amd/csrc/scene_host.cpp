@@ -1,0 +1,468 @@
+// scene_host.cpp -- host-side scene construction behind the C ABI:
+// PLY input, the KD-tree builder and the camera basis.
+//
+// These are the producers of the hot path's inputs (SURVEY.md §8a rows a1,
+// a11).  They reproduce the reference's results exactly (tests compare them
+// with the oracle) but are organised for speed: the six merge sorts become
+// comparison sorts with the merge sort's tie order, and the per-level
+// partitions run in parallel because sibling ranges are disjoint.
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <numeric>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "rt_internal.h"
+
+namespace rt {
+
+static thread_local std::string g_last_error;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+namespace {
+
+// Runs body(i) for i in [0, n) on up to `threads` std::threads.
+template <class F>
+void parallel_for(int64_t n, int threads, F&& body) {
+    if (n <= 0) return;
+    if (threads <= 1 || n == 1) {
+        for (int64_t i = 0; i < n; i++) body(i);
+        return;
+    }
+    std::atomic<int64_t> next{0};
+    int t = (int)std::min<int64_t>(threads, n);
+    std::vector<std::thread> pool;
+    pool.reserve(t);
+    for (int k = 0; k < t; k++)
+        pool.emplace_back([&] {
+            for (int64_t i; (i = next.fetch_add(1)) < n;) body(i);
+        });
+    for (auto& th : pool) th.join();
+}
+
+int resolve_threads(int nthreads) {
+    if (nthreads > 0) return nthreads;
+    unsigned hc = std::thread::hardware_concurrency();
+    return hc ? (int)std::min(hc, 64u) : 4;
+}
+
+// ------------------------------------------------------------- PLY input
+
+// windows.h min/max as used by TD/read_ply.cpp:142-195 (order matters only
+// for the sign of zero, which is kept identical anyway).
+inline float wmin(float a, float b) { return (a < b) ? a : b; }
+inline float wmax(float a, float b) { return (a > b) ? a : b; }
+
+void aabb3(rt_leaf_aabb& lf, const float* a, const float* b, const float* c) {
+    lf.x0 = wmin(a[0], wmin(b[0], c[0])); lf.x1 = wmax(a[0], wmax(b[0], c[0]));
+    lf.y0 = wmin(a[1], wmin(b[1], c[1])); lf.y1 = wmax(a[1], wmax(b[1], c[1]));
+    lf.z0 = wmin(a[2], wmin(b[2], c[2])); lf.z1 = wmax(a[2], wmax(b[2], c[2]));
+}
+
+struct Cursor {
+    const char* p;
+    const char* end;
+    bool line(std::string& out) {
+        out.clear();
+        if (p >= end) return false;
+        while (p < end && *p != '\n') {
+            if (*p != '\r') out.push_back(*p);
+            p++;
+        }
+        if (p < end) p++;
+        return true;
+    }
+};
+
+bool is_count_line(const std::string& s) {
+    size_t i = 0;
+    while (i < s.size() && (s[i] == ' ' || s[i] == '\t')) i++;
+    size_t d = i;
+    while (i < s.size() && s[i] >= '0' && s[i] <= '9') i++;
+    if (i == d) return false;
+    while (i < s.size() && (s[i] == ' ' || s[i] == '\t')) i++;
+    return i == s.size();
+}
+
+}  // namespace
+}  // namespace rt
+
+using namespace rt;
+
+extern "C" void rt_host_free(void* p) { free(p); }
+
+extern "C" int rt_mesh_assemble(const float* verts, int64_t nvert, const int32_t* arity,
+                                const int32_t* idx, int64_t nface, float** points9,
+                                uint32_t* ntri_out, rt_leaf_aabb** leafs_out) {
+    if (!points9 || !ntri_out || !leafs_out || (nface > 0 && (!arity || !idx || !verts)))
+        return fail(RT_ERR_INVALID, "rt_mesh_assemble: null argument");
+    int64_t ntri = 0;
+    for (int64_t f = 0; f < nface; f++) {
+        if (arity[f] == 3) ntri += 1;
+        else if (arity[f] == 4) ntri += 2;
+        else return fail(RT_ERR_INVALID, "rt_mesh_assemble: face %lld has arity %d", (long long)f, arity[f]);
+    }
+    if (ntri >= (int64_t)kLeafBit) return fail(RT_ERR_INVALID, "rt_mesh_assemble: too many triangles");
+    float* pts = (float*)malloc(sizeof(float) * 9 * (size_t)std::max<int64_t>(ntri, 1));
+    rt_leaf_aabb* lf = (rt_leaf_aabb*)malloc(sizeof(rt_leaf_aabb) * (size_t)std::max<int64_t>(ntri, 1));
+    if (!pts || !lf) { free(pts); free(lf); return fail(RT_ERR_NOMEM, "rt_mesh_assemble: out of memory"); }
+    int64_t t = 0, k = 0;
+    auto put = [&](int64_t tri, int slot, const float* v) {
+        float* d = pts + 9 * tri + 3 * slot;
+        d[0] = v[0]; d[1] = v[1]; d[2] = v[2];
+    };
+    for (int64_t f = 0; f < nface; f++) {
+        const int a = arity[f];
+        for (int j = 0; j < a; j++)
+            if (idx[k + j] < 0 || idx[k + j] >= nvert) {
+                free(pts); free(lf);
+                return fail(RT_ERR_INVALID, "rt_mesh_assemble: face %lld index out of range", (long long)f);
+            }
+        if (a == 4) {  // TD/read_ply.cpp:130-185: ABCD -> (A,B,C), (A,C,D)
+            const float* A = verts + 3 * (int64_t)idx[k];
+            const float* B = verts + 3 * (int64_t)idx[k + 1];
+            const float* Cv = verts + 3 * (int64_t)idx[k + 2];
+            const float* D = verts + 3 * (int64_t)idx[k + 3];
+            aabb3(lf[t], A, B, Cv); lf[t].tri = t;
+            put(t, 0, A); put(t, 1, B); put(t, 2, Cv); t++;
+            aabb3(lf[t], A, D, Cv); lf[t].tri = t;
+            put(t, 0, A); put(t, 1, Cv); put(t, 2, D); t++;
+        } else {       // TD/read_ply.cpp:187-209: P1P2P3 stored as (P3,P1,P2)
+            const float* P1 = verts + 3 * (int64_t)idx[k];
+            const float* P2 = verts + 3 * (int64_t)idx[k + 1];
+            const float* P3 = verts + 3 * (int64_t)idx[k + 2];
+            aabb3(lf[t], P1, P2, P3); lf[t].tri = t;
+            put(t, 0, P3); put(t, 1, P1); put(t, 2, P2); t++;
+        }
+        k += a;
+    }
+    *points9 = pts;
+    *leafs_out = lf;
+    *ntri_out = (uint32_t)ntri;
+    return RT_OK;
+}
+
+extern "C" int rt_read_ply(const char* path, int mode, float** points9, uint32_t* ntri,
+                           rt_leaf_aabb** leafs) {
+    if (!path) return fail(RT_ERR_INVALID, "rt_read_ply: null path");
+    const int per_vertex = mode == 0 ? 3 : mode == 1 ? 5 : mode == 2 ? 6 : -1;
+    if (per_vertex < 0) return fail(RT_ERR_INVALID, "rt_read_ply: unsupported mode %d", mode);
+    FILE* fp = fopen(path, "rb");
+    if (!fp) return fail(RT_ERR_IO, "rt_read_ply: cannot open %s", path);
+    std::vector<char> buf;
+    fseek(fp, 0, SEEK_END);
+    long len = ftell(fp);
+    fseek(fp, 0, SEEK_SET);
+    buf.resize((size_t)len + 1);
+    size_t got = fread(buf.data(), 1, (size_t)len, fp);
+    fclose(fp);
+    buf[got] = 0;
+    Cursor cur{buf.data(), buf.data() + got};
+    std::string line;
+    long long nv = -1, nf = -1;
+    cur.line(line);
+    if (line == "ply") cur.line(line);
+    if (is_count_line(line)) {  // headerless prelude (H9 extension)
+        nv = atoll(line.c_str());
+        if (!cur.line(line) || !is_count_line(line)) return fail(RT_ERR_IO, "rt_read_ply: bad prelude in %s", path);
+        nf = atoll(line.c_str());
+    } else {                    // header loop, TD/read_ply.cpp:19-44
+        for (;;) {
+            char tag[64] = {0}, name[64] = {0};
+            long long val = -1;
+            if (sscanf(line.c_str(), "%63s %63s %lld", tag, name, &val) == 3 && !strcmp(tag, "element")) {
+                if (!strcmp(name, "vertex")) nv = val;
+                if (!strcmp(name, "face")) nf = val;
+            }
+            if (line == "end_header") break;
+            if (!cur.line(line)) return fail(RT_ERR_IO, "rt_read_ply: no end_header in %s", path);
+        }
+    }
+    if (nv < 0 || nf < 0) return fail(RT_ERR_IO, "rt_read_ply: missing vertex/face counts in %s", path);
+    std::vector<float> verts((size_t)nv * 3);
+    const char* p = cur.p;
+    for (long long i = 0; i < nv; i++)
+        for (int j = 0; j < per_vertex; j++) {
+            char* e;
+            float v = strtof(p, &e);
+            if (e == p) return fail(RT_ERR_IO, "rt_read_ply: bad vertex %lld in %s", i, path);
+            p = e;
+            if (j < 3) verts[(size_t)i * 3 + j] = v;
+        }
+    std::vector<int32_t> arity((size_t)nf), idx;
+    idx.reserve((size_t)nf * 3);
+    for (long long f = 0; f < nf; f++) {
+        char* e;
+        long c = strtol(p, &e, 10);
+        if (e == p || (c != 3 && c != 4)) return fail(RT_ERR_IO, "rt_read_ply: bad face %lld in %s", f, path);
+        p = e;
+        arity[(size_t)f] = (int32_t)c;
+        for (long j = 0; j < c; j++) {
+            long v = strtol(p, &e, 10);
+            if (e == p) return fail(RT_ERR_IO, "rt_read_ply: bad face %lld in %s", f, path);
+            p = e;
+            idx.push_back((int32_t)v);
+        }
+    }
+    return rt_mesh_assemble(verts.data(), nv, arity.data(), idx.data(), nf, points9, ntri, leafs);
+}
+
+// ---------------------------------------------------------------- KD build
+
+namespace {
+
+// Lists in cut-flag order (TD/Trixel.h:172-193): 0 x1, 1 y1, 2 z1, 3 x0, 4 y0, 5 z0.
+inline float list_key(const rt_leaf_aabb& a, int k) {
+    switch (k) {
+    case 0: return a.x1;
+    case 1: return a.y1;
+    case 2: return a.z1;
+    case 3: return a.x0;
+    case 4: return a.y0;
+    default: return a.z0;
+    }
+}
+
+struct Range { int64_t l, m, r; };
+
+}  // namespace
+
+extern "C" int rt_kd_build(const rt_leaf_aabb* leafs, uint32_t n, rt_kd_node* nodes, int nthreads) {
+    if (!leafs || !nodes || n == 0) return fail(RT_ERR_INVALID, "rt_kd_build: empty input");
+    if (n >= kLeafBit) return fail(RT_ERR_INVALID, "rt_kd_build: too many triangles");
+    const int T = resolve_threads(nthreads);
+    {   // tri_list_index must be a permutation (set_sorted_voxels indexes by it)
+        std::vector<uint8_t> seen(n, 0);
+        for (uint32_t i = 0; i < n; i++) {
+            int64_t t = leafs[i].tri;
+            if (t < 0 || t >= (int64_t)n || seen[(size_t)t]) return fail(RT_ERR_INVALID, "rt_kd_build: tri indices are not a permutation");
+            seen[(size_t)t] = 1;
+            for (int k = 0; k < 6; k++)
+                if (isnan(list_key(leafs[i], k))) return fail(RT_ERR_INVALID, "rt_kd_build: NaN bound at %u", i);
+        }
+    }
+    // Six sorted position lists.  merge_sort (TD/sort.h:25-60) takes the right
+    // run on ties, so equal keys end up in descending input position: sort by
+    // (key ascending, position descending).
+    std::vector<uint32_t> list[6];
+    parallel_for(6, T, [&](int64_t k) {
+        auto& L = list[k];
+        L.resize(n);
+        std::iota(L.begin(), L.end(), 0u);
+        std::sort(L.begin(), L.end(), [&](uint32_t a, uint32_t b) {
+            float ka = list_key(leafs[a], (int)k), kb = list_key(leafs[b], (int)k);
+            return ka < kb || (!(kb < ka) && a > b);
+        });
+    });
+    const int64_t nnode = 2 * (int64_t)n - 1;
+    std::vector<Range> rng((size_t)nnode);
+    std::vector<uint8_t> in_left(n, 0);
+    std::vector<uint32_t> scratch(n);
+    memset(nodes, 0, sizeof(rt_kd_node) * (size_t)nnode);
+
+    auto key_at = [&](int k, int64_t pos) { return list_key(leafs[list[k][(size_t)pos]], k); };
+
+    rt_kd_node& root = nodes[0];
+    root.parent = 0;
+    root.cut_flag = 5;
+    root.tri_index = -1;
+    root.z1 = key_at(2, n - 1); root.z0 = key_at(5, 0);
+    root.y1 = key_at(1, n - 1); root.y0 = key_at(4, 0);
+    root.x0 = key_at(3, 0);     root.x1 = key_at(0, n - 1);
+    rng[0] = {0, (int64_t)(n - 1) / 2, (int64_t)n - 1};
+
+    // BFS one level at a time: nodes [lv0, lv1) are siblings-at-depth with
+    // disjoint ranges, so their partitions are independent.
+    int64_t lv0 = 0, lv1 = 1, wr = 1;
+    std::vector<int64_t> child_base;
+    while (lv0 < lv1) {
+        const int64_t cnt = lv1 - lv0;
+        // child slots in BFS order (create_kd appends two per interior node)
+        child_base.assign((size_t)cnt, -1);
+        for (int64_t i = 0; i < cnt; i++) {
+            const Range& R = rng[(size_t)(lv0 + i)];
+            if (R.r != R.l) { child_base[(size_t)i] = wr; wr += 2; }
+        }
+        if (wr > nnode) return fail(RT_ERR_INVALID, "rt_kd_build: node overflow");
+        auto process = [&](int64_t i, int inner_threads) {
+            const int64_t id = lv0 + i;
+            rt_kd_node& nd = nodes[id];
+            const Range R = rng[(size_t)id];
+            // axis/key selection with strict `>` in the order x1,x0,y1,y0,z1,z0 (H11)
+            float best = key_at(0, R.r) - key_at(0, R.l);
+            int cut = 0;
+            static const int order[5] = {3, 1, 4, 2, 5};
+            for (int q = 0; q < 5; q++) {
+                const int k = order[q];
+                float span = key_at(k, R.r) - key_at(k, R.l);
+                if (span > best) { best = span; cut = k; }
+            }
+            if (R.r == R.l) {  // leaf: TD/Trixel.h:194-205
+                nd.cut_flag = nodes[nd.parent].cut_flag;
+                nd.is_leaf = 1;
+                nd.left = -1; nd.right = -1;
+                nd.tri_index = leafs[list[0][(size_t)R.l]].tri;
+                return;
+            }
+            nd.cut_flag = cut;
+            nd.is_leaf = 0;
+            nd.tri_index = -1;
+            const auto& C = list[cut];
+            for (int64_t p = R.l; p <= R.m; p++) in_left[C[(size_t)p]] = 1;
+            for (int64_t p = R.m + 1; p <= R.r; p++) in_left[C[(size_t)p]] = 0;
+            // stable partition of the other five lists (TD/Trixel.h:214-327)
+            int others[5], no = 0;
+            for (int k = 0; k < 6; k++) if (k != cut) others[no++] = k;
+            auto part = [&](int64_t j) {
+                auto& L = list[others[j]];
+                int64_t a = R.l, b = R.m + 1;
+                for (int64_t p = R.l; p <= R.r; p++) {
+                    uint32_t e = L[(size_t)p];
+                    scratch[(size_t)(in_left[e] ? a++ : b++)] = e;
+                }
+                // scratch is shared, but each list uses it in turn below
+                memcpy(&L[(size_t)R.l], &scratch[(size_t)R.l], sizeof(uint32_t) * (size_t)(R.r - R.l + 1));
+            };
+            if (inner_threads > 1) {
+                // big node: give every list its own scratch to partition concurrently
+                std::vector<uint32_t> own[5];
+                parallel_for(5, inner_threads, [&](int64_t j) {
+                    auto& L = list[others[j]];
+                    auto& S = own[j];
+                    S.resize((size_t)(R.r - R.l + 1));
+                    int64_t a = 0, b = R.m + 1 - R.l;
+                    for (int64_t p = R.l; p <= R.r; p++) {
+                        uint32_t e = L[(size_t)p];
+                        S[(size_t)(in_left[e] ? a++ : b++)] = e;
+                    }
+                    memcpy(&L[(size_t)R.l], S.data(), sizeof(uint32_t) * S.size());
+                });
+            } else {
+                for (int j = 0; j < 5; j++) part(j);
+            }
+            // children (TD/Trixel.h:329-352)
+            const int64_t cb = child_base[(size_t)i];
+            nd.left = cb; nd.right = cb + 1;
+            for (int br = 0; br < 2; br++) {
+                rt_kd_node& c = nodes[cb + br];
+                c.parent = id;
+                c.is_leaf = 0;
+                c.tri_index = -1;
+                int64_t nl = br == 0 ? R.l : R.m + 1, nr = br == 0 ? R.m : R.r;
+                rng[(size_t)(cb + br)] = {nl, ((nr - nl) / 2) + nl, nr};
+                c.x1 = key_at(0, nr); c.x0 = key_at(3, nl);
+                c.y1 = key_at(1, nr); c.y0 = key_at(4, nl);
+                c.z1 = key_at(2, nr); c.z0 = key_at(5, nl);
+            }
+            // s1 = left child's max, s2 = right child's min on the cut axis (:353-376)
+            const rt_kd_node& Lc = nodes[cb];
+            const rt_kd_node& Rc = nodes[cb + 1];
+            switch (cut) {
+            case 0: case 3: nd.s2 = Rc.x0; nd.s1 = Lc.x1; break;
+            case 1: case 4: nd.s2 = Rc.y0; nd.s1 = Lc.y1; break;
+            default:        nd.s2 = Rc.z0; nd.s1 = Lc.z1; break;
+            }
+        };
+        if (cnt < T) {
+            for (int64_t i = 0; i < cnt; i++) {
+                const Range& R = rng[(size_t)(lv0 + i)];
+                process(i, (R.r - R.l) > 65536 ? std::min(T, 5) : 1);
+            }
+        } else {
+            // scratch is indexed by position; sibling ranges are disjoint
+            parallel_for(cnt, T, [&](int64_t i) { process(i, 1); });
+        }
+        lv0 = lv1;
+        lv1 = wr;
+    }
+    if (wr != nnode) return fail(RT_ERR_INVALID, "rt_kd_build: built %lld of %lld nodes", (long long)wr, (long long)nnode);
+    return RT_OK;
+}
+
+// ------------------------------------------------------------------ camera
+
+namespace {
+
+// vector_norm, TD/vector.cpp:13-26 (8 Newton steps seeded from bits(s/2))
+float host_vector_norm(float s) {
+    const float half = 0.5f * s;
+    union { float f; uint32_t i; } u;
+    u.f = half;
+    u.i = 0x5f375a86u - (u.i >> 1);
+    for (int k = 0; k < 8; k++) u.f = u.f * (1.5f - half * u.f * u.f);
+    return u.f;
+}
+
+struct V4 {
+    float x, y, z, w;
+    void normalize() {  // normalize_Vector(VEC4*), TD/Vector.h:116-124
+        float s = x * x + y * y + z * z;
+        s = host_vector_norm(s);
+        x *= s; y *= s; z *= s;
+        w = 1 / s;
+    }
+    void cross(const V4& b) {  // VEC4::cross, TD/vector.cpp:31-36
+        float t0 = y * b.z - z * b.y;
+        float t1 = z * b.x - x * b.z;
+        float t2 = x * b.y - y * b.x;
+        x = t0; y = t1; z = t2;
+    }
+};
+
+}  // namespace
+
+extern "C" float rt_film_w(int32_t w, int32_t h) {
+    float ar = (float)w / (float)(uint32_t)h;  // TD/WinMain.cpp:29
+    return ar * 0.024f;                        // TD/WinMain.cpp:70
+}
+
+extern "C" int rt_camera_basis(int32_t w, int32_t h, float f_w, float f_h, float focal,
+                               const float pos[3], const float la[3], const float up[3],
+                               rt_camera_basis_t* out) {
+    if (!pos || !la || !up || !out || w <= 0 || h <= 0)
+        return fail(RT_ERR_INVALID, "rt_camera_basis: bad argument");
+    out->pix_w = f_w / (float)w;
+    out->pix_h = f_h / (float)h;
+    V4 n{la[0] - pos[0], la[1] - pos[1], la[2] - pos[2], 1.0f};
+    n.normalize();
+    out->n[0] = n.x; out->n[1] = n.y; out->n[2] = n.z;
+    V4 tu{up[0], up[1], up[2], 1.0f};
+    tu.normalize();
+    tu.cross(n);          // up x n
+    n.cross(tu);          // n x (up x n)
+    V4 v = n;
+    v.normalize();
+    out->v[0] = v.x; out->v[1] = v.y; out->v[2] = v.z;
+    for (int k = 0; k < 3; k++) out->v_mod[k] = out->v[k] * out->pix_h;
+    V4 nn{la[0] - pos[0], la[1] - pos[1], la[2] - pos[2], 1.0f};
+    nn.normalize();
+    v.cross(nn);          // u = v x n
+    out->u[0] = v.x; out->u[1] = v.y; out->u[2] = v.z;
+    for (int k = 0; k < 3; k++) out->u_mod[k] = out->u[k] * out->pix_w;
+    float adj_y = (float)((uint32_t)h >> 1);
+    float adj_x = (float)((uint32_t)w >> 1);
+    if (!((uint32_t)h & 1u)) adj_y = (float)((double)adj_y - .5);  // TD/Camera.cpp:62
+    if (!((uint32_t)w & 1u)) adj_x = (float)((double)adj_x - .5);  // TD/Camera.cpp:63
+    for (int k = 0; k < 3; k++)
+        out->n_mod[k] = (out->n[k] * focal) - (out->v_mod[k] * adj_y) - (out->u_mod[k] * adj_x);
+    return RT_OK;
+}
+
+extern "C" const char* rt_last_error_string(void) { return g_last_error.c_str(); }
+extern "C" int rt_abi_version(void) { return RT_ABI_VERSION; }

@@ -1,0 +1,88 @@
+"""Multi-GPU frame sharding: disjoint screen bands + a gather to rank 0.
+
+One process per GPU (torch.distributed; backend "nccl" is RCCL on ROCm,
+"gloo" for the CPU tests).  The scene is replicated on every GPU (built once
+per process from the same deterministic inputs).  Rows are cut into bands of
+8 and band b belongs to rank b % N, which interleaves the centrally placed
+object across ranks.  Each rank renders its bands into a packed buffer of
+equal size; rank 0 gathers the N buffers over xGMI and reassembles the frame
+with one kernel (rt_unpack_bands).  The reference is single-GPU
+(cudaSetDevice(0) everywhere, TD/Trixel.cu:213): this layer is new.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+BAND = 8  # rows per band; equals the kernels' tile height
+
+
+def nbands(h: int) -> int:
+    return (h + BAND - 1) // BAND
+
+
+def slots(h: int, nranks: int) -> int:
+    return (nbands(h) + nranks - 1) // nranks
+
+
+def packed_pixels(w: int, h: int, nranks: int) -> int:
+    return slots(h, nranks) * BAND * w
+
+
+def pack_bands_numpy(frame: np.ndarray, w: int, h: int, nranks: int, rank: int, fill=0) -> np.ndarray:
+    """The packed buffer rank `rank` renders: slot j holds band rank + j*nranks."""
+    out = np.full(packed_pixels(w, h, nranks), fill, dtype=frame.dtype)
+    f = frame.reshape(h, w)
+    for j in range(slots(h, nranks)):
+        b = rank + j * nranks
+        if b >= nbands(h):
+            break
+        y0, y1 = b * BAND, min(h, (b + 1) * BAND)
+        out[j * BAND * w:(j * BAND + (y1 - y0)) * w] = f[y0:y1].reshape(-1)
+    return out
+
+
+def unpack_bands_numpy(gathered: np.ndarray, w: int, h: int, nranks: int) -> np.ndarray:
+    """Inverse of the per-rank packing for the N buffers back to back."""
+    s = slots(h, nranks)
+    g = gathered.reshape(nranks, s, BAND, w)
+    y = np.arange(h)
+    band, r = y // BAND, y % BAND
+    return g[band % nranks, band // nranks, r].reshape(-1)
+
+
+class FrameGather:
+    """Rank-0 gather of the packed band buffers (torch tensors on each rank's device).
+
+    collective="gather": torch.distributed.gather (point-to-point sends to the
+    root, one xGMI link per peer); "allgather": all_gather_into_tensor.
+    """
+
+    def __init__(self, dist, w: int, h: int, device, collective: str = "gather", unpack=None):
+        import torch
+        self.dist = dist
+        self.w, self.h = w, h
+        self.rank = dist.get_rank()
+        self.world = dist.get_world_size()
+        self.npk = packed_pixels(w, h, self.world)
+        self.collective = collective
+        self.device = device
+        self.local = torch.zeros(self.npk, dtype=torch.int32, device=device)
+        self.gathered = torch.zeros(self.world * self.npk, dtype=torch.int32, device=device) \
+            if (self.rank == 0 or collective == "allgather") else None
+        self.frame = torch.zeros(w * h, dtype=torch.int32, device=device) if self.rank == 0 else None
+        self.unpack = unpack  # callable(gathered, frame) on rank 0; None -> numpy (CPU tests)
+
+    def gather(self) -> None:
+        d = self.dist
+        if self.collective == "allgather":
+            d.all_gather_into_tensor(self.gathered, self.local)
+        else:
+            parts = list(self.gathered.split(self.npk)) if self.rank == 0 else None
+            d.gather(self.local, gather_list=parts, dst=0)
+        if self.rank == 0:
+            if self.unpack is not None:
+                self.unpack(self.gathered, self.frame)
+            else:
+                import torch
+                g = self.gathered.cpu().numpy().view(np.uint32)
+                self.frame.copy_(torch.from_numpy(unpack_bands_numpy(g, self.w, self.h, self.world).view(np.int32)))

@@ -1,0 +1,276 @@
+"""Host-side mirror of the reference's construction API over the C ABI.
+
+Same names, argument meaning and error behaviour as the reference classes
+(TD/ = TEST_Dungeonrun/):
+
+* ``read_ply``           TD/read_ply.cpp:13        -> rt_read_ply
+* ``Trixel``             TD/Trixel.h:39-478        -> rt_scene_* / rt_kd_build
+* ``Camera``             TD/Camera.h:15-97         -> rt_camera_*
+* ``Object``             TD/Object.h:10-19         -> Trixel + Quaternion
+* ``Quaternion``         TD/Quaternion.h:5-24      (rot_m only; identity)
+
+The frame semantics are the steady state of the reference's loop
+(TD/WinMain.cpp:212-237): ``Object.render`` runs the fused bg-fill ->
+intersect -> Phong kernel, ``Camera.color_pixels`` copies the u32 frame to
+``Camera.h_color`` (the D2H of TD/Camera.cu:84).  Status codes follow the
+reference (0 = success); failures of the device path raise ``RtError``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import KD_NODE_DTYPE, LEAF_AABB_DTYPE, RT_FLAG_COUNT, RT_FLAG_WRITE_HIT, RT_MODE_FLAT, RT_MODE_KD
+
+SET_COLOR_TAG = 1      # TD/Camera.h:13
+PHONG_COLOR_TAG = 2    # TD/Camera.h:14
+TRIXEL_OBJECT_TAG = 0  # TD/Object.h:3
+BACKGROUND_ARGB = 0x00F08200  # TD/Camera.cpp:72
+
+#: Material of every triangle in the reference demo (TD/WinMain.cpp:117-121).
+DEFAULT_RAD = (np.float32(0.1), np.float32(0.55), np.float32(0.2))
+
+
+def read_ply(file_name: str, mode: int):
+    """read_ply(file_name, mode) -> (points [ntri, 9] f32, num_tri, kd_leafs).
+
+    mode: 0 "x y z", 1 "x y z confidence intensity", 2 "x y z nx ny nz"
+    (TD/WinMain.cpp:93-109).  Headerless "[ply] nv nf" files are accepted.
+    """
+    pts, leafs, n = C.c_void_p(), C.c_void_p(), C.c_uint32()
+    _lib.call("rt_read_ply", file_name.encode(), mode, C.byref(pts), C.byref(n), C.byref(leafs))
+    points = _lib.take_host(pts, 9 * n.value, np.float32).reshape(-1, 9)
+    return points, n.value, _lib.take_host(leafs, n.value, LEAF_AABB_DTYPE)
+
+
+def assemble_mesh(verts: np.ndarray, faces) -> tuple:
+    """read_ply's face assembly for an in-memory indexed mesh.
+
+    faces: an [nf, 3] or [nf, 4] int array, or a list of 3/4-element faces.
+    Returns (points [ntri, 9], num_tri, kd_leafs) like ``read_ply``.
+    """
+    verts = np.ascontiguousarray(verts, np.float32).reshape(-1, 3)
+    if isinstance(faces, np.ndarray) and faces.ndim == 2:
+        arity = np.full(len(faces), faces.shape[1], np.int32)
+        idx = np.ascontiguousarray(faces, np.int32).reshape(-1)
+    else:
+        arity = np.array([len(f) for f in faces], np.int32)
+        idx = np.array([i for f in faces for i in f], np.int32)
+    pts, leafs, n = C.c_void_p(), C.c_void_p(), C.c_uint32()
+    _lib.call("rt_mesh_assemble", _lib.ptr(verts), len(verts), _lib.ptr(arity), _lib.ptr(idx), len(arity),
+              C.byref(pts), C.byref(n), C.byref(leafs))
+    points = _lib.take_host(pts, 9 * n.value, np.float32).reshape(-1, 9)
+    return points, n.value, _lib.take_host(leafs, n.value, LEAF_AABB_DTYPE)
+
+
+def kd_build(kd_leafs: np.ndarray, nthreads: int = 0) -> np.ndarray:
+    """set_sorted_voxels + create_kd as one call: the BFS node array (KD_NODE_DTYPE)."""
+    leafs = np.ascontiguousarray(kd_leafs, LEAF_AABB_DTYPE)
+    nodes = np.zeros(max(2 * len(leafs) - 1, 1), KD_NODE_DTYPE)
+    _lib.call("rt_kd_build", _lib.ptr(leafs), len(leafs), _lib.ptr(nodes), nthreads)
+    return nodes
+
+
+def film_w(w: int, h: int) -> float:
+    """WinMain's film width ((float)w/h)*.024f (TD/WinMain.cpp:29,69-70)."""
+    return float(np.float32(_lib.lib().rt_film_w(w, h)))
+
+
+def camera_basis(w, h, f_w, f_h, focal, pos, look_at, up) -> dict:
+    b = _lib.RtCameraBasis()
+    f = lambda v: np.ascontiguousarray(v, np.float32)  # noqa: E731
+    p, la, u = f(pos), f(look_at), f(up)
+    _lib.call("rt_camera_basis", w, h, np.float32(f_w), np.float32(f_h), np.float32(focal),
+              _lib.ptr(p), _lib.ptr(la), _lib.ptr(u), C.byref(b))
+    return {k: np.array(getattr(b, k)[:], np.float32) for k in ("n", "u", "v", "n_mod", "u_mod", "v_mod")} | {
+        "pix_w": np.float32(b.pix_w), "pix_h": np.float32(b.pix_h)}
+
+
+class Quaternion:
+    """The object transform the hot kernel reads (d_rot_m, TD/Trixel.cu:60-66).
+
+    ``rot_m`` rows are (i, j, k, w) for x, y, z: a 3x3 rotation plus the
+    translation in column w.  Identity at construction (TD/Quaternion.cpp:16-23).
+    """
+
+    def __init__(self):
+        self.rot_m = np.array([[1, 0, 0, 0], [0, 1, 0, 0], [0, 0, 1, 0]], np.float32)
+
+    def xform(self) -> np.ndarray:
+        return np.ascontiguousarray(self.rot_m, np.float32).reshape(12)
+
+
+class Trixel:
+    """Triangles (+ KD tree) resident on one device (TD/Trixel.h:39-478)."""
+
+    def __init__(self, num_t: int, points_data: np.ndarray, color_data=None, device: int = 0):
+        points = np.ascontiguousarray(points_data, np.float32).reshape(-1, 9)[:num_t]
+        if len(points) != num_t:
+            raise ValueError("points_data holds fewer than num_t triangles")
+        if color_data is None:
+            rad = np.empty((num_t, 3), np.float32)
+            rad[:] = DEFAULT_RAD
+        else:
+            rad = np.ascontiguousarray(color_data, np.float32).reshape(-1, 3)[:num_t]
+        self.num_trixels = num_t
+        self.num_voxels = 2 * num_t - 1
+        self.device = device
+        self.h_points_init_data = points
+        self.rad = rad
+        self._leafs = None
+        self.h_nodes = None
+        h = C.c_void_p()
+        _lib.call("rt_scene_create", device, _lib.ptr(points), _lib.ptr(rad), num_t, C.byref(h))
+        self._h = h
+
+    def set_sorted_voxels(self, voxel_list: np.ndarray, num_leaf_voxels: int) -> int:
+        """TD/Trixel.h:386-473: keeps the leaf AABBs for create_kd."""
+        if num_leaf_voxels == 0:
+            return 0
+        self._leafs = np.ascontiguousarray(voxel_list, LEAF_AABB_DTYPE)[:num_leaf_voxels].copy()
+        return 0
+
+    def create_kd(self, nthreads: int = 0) -> int:
+        """TD/Trixel.h:135-385: -12 if set_sorted_voxels was not called."""
+        if self._leafs is None:
+            return -12
+        self.h_nodes = kd_build(self._leafs, nthreads)
+        _lib.call("rt_scene_set_kd", self._h, _lib.ptr(self.h_nodes), len(self.h_nodes))
+        self._leafs = None  # the reference frees the sorted lists (TD/Trixel.h:381-383)
+        return 0
+
+    def set_kd_nodes(self, nodes: np.ndarray) -> int:
+        """Upload an already built node array (e.g. cached on disk)."""
+        self.h_nodes = np.ascontiguousarray(nodes, KD_NODE_DTYPE)
+        _lib.call("rt_scene_set_kd", self._h, _lib.ptr(self.h_nodes), len(self.h_nodes))
+        return 0
+
+    def intersect_trixels(self, c: "Camera", q: Quaternion = None, m: int = RT_MODE_KD, flags: int = 0,
+                          stream=None) -> int:
+        """TD/Trixel.h:474-476.  Unlike the reference, ``m`` selects KD (0) or flat (1)."""
+        return c._render(self, q, m, flags, stream)
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            _lib.lib().rt_scene_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Object:
+    """A Trixel plus its own transform (TD/Object.h:10-19)."""
+
+    def __init__(self, x: Trixel, q: Quaternion = None):
+        self.object_tag = TRIXEL_OBJECT_TAG
+        self.trixel_list = x
+        self.quat = q if q is not None else Quaternion()
+
+    def getTag(self) -> int:  # noqa: N802 (reference name)
+        return self.object_tag
+
+    def render(self, c: "Camera", mode: int = RT_MODE_KD, flags: int = 0, stream=None) -> int:
+        """Object::render (TD/Object.cpp:10-12)."""
+        return self.trixel_list.intersect_trixels(c, self.quat, mode, flags, stream)
+
+
+class Camera:
+    """Camera (TD/Camera.h:15-97): rays, frame buffer, camera-relative scene data."""
+
+    def __init__(self, r_w, r_h, f_w, f_h, fclen, p_x, p_y, p_z, la_x, la_y, la_z, up_x, up_y, up_z,
+                 device: int = 0):
+        self.res = (int(r_w), int(r_h))
+        self.pos = np.array([p_x, p_y, p_z], np.float32)
+        self.la = np.array([la_x, la_y, la_z], np.float32)
+        self.up = np.array([up_x, up_y, up_z], np.float32)
+        self.device = device
+        self.o_prop = camera_basis(r_w, r_h, f_w, f_h, fclen, self.pos, self.la, self.up)
+        self.background_color = BACKGROUND_ARGB
+        self.object_list = []
+        h = C.c_void_p()
+        _lib.call("rt_camera_create", device, int(r_w), int(r_h), np.float32(f_w), np.float32(f_h),
+                  np.float32(fclen), _lib.ptr(self.pos), _lib.ptr(self.la), _lib.ptr(self.up), C.byref(h))
+        self._h = h
+        self.h_color = np.zeros(r_w * r_h, np.uint32)
+        self.h_rmi = np.full(r_w * r_h, -1, np.int64)
+
+    @classmethod
+    def default(cls, w: int, h: int, device: int = 0) -> "Camera":
+        """The WinMain camera (TD/WinMain.cpp:69-74) at w x h."""
+        return cls(w, h, film_w(w, h), np.float32(.024), np.float32(.055), 0.0, 0.10, -1.0, 0.0, 0.100, 0.0,
+                   0.0, 1.0, 0.0, device=device)
+
+    def add_object(self, new_object: Object) -> int:
+        """Camera::add_object (TD/Camera.cpp:118-142)."""
+        if new_object.getTag() != TRIXEL_OBJECT_TAG:
+            return 0
+        self.object_list.append(new_object)
+        _lib.call("rt_camera_add_object", self._h, new_object.trixel_list._h)
+        return 0
+
+    def _render(self, t: Trixel, q, mode, flags, stream) -> int:
+        xf = (q if q is not None else Quaternion()).xform()
+        s = C.c_void_p(stream) if isinstance(stream, int) else C.c_void_p(None)
+        _lib.call("rt_render", self._h, _lib.ptr(xf), mode, flags, None, s)
+        self._last_flags = flags
+        return 0
+
+    def render_into(self, argb, hit=None, xform=None, mode=RT_MODE_KD, flags=0, tile=None, stream=None) -> int:
+        """Render into caller-owned device buffers (torch tensors or raw pointers)."""
+        xf = np.ascontiguousarray(xform if xform is not None else Quaternion().xform(), np.float32)
+        t = None if tile is None else C.byref(_lib.RtTile(tile[0], tile[1]))
+        s = C.c_void_p(stream) if isinstance(stream, int) else C.c_void_p(None)
+        a = argb if isinstance(argb, C.c_void_p) else _lib.ptr(argb)
+        h = hit if isinstance(hit, C.c_void_p) else _lib.ptr(hit)
+        _lib.call("rt_render_into", self._h, _lib.ptr(xf), mode, flags, t, a, h, s)
+        return 0
+
+    def color_pixels(self, color_tag_select: int = PHONG_COLOR_TAG) -> int:
+        """Camera::color_pixels (TD/Camera.cpp:229): the frame D2H into h_color.
+
+        Shading is fused into ``Object.render``; both tags yield the steady
+        state frame (background where no hit, Phong where hit)."""
+        want_hit = bool(getattr(self, "_last_flags", 0) & RT_FLAG_WRITE_HIT)
+        _lib.call("rt_read_frame", self._h, _lib.ptr(self.h_color), _lib.ptr(self.h_rmi) if want_hit else None)
+        return 0
+
+    def counters(self, reset: bool = True) -> np.ndarray:
+        out = np.zeros(5, np.uint64)
+        _lib.call("rt_camera_counters", self._h, _lib.ptr(out), int(reset))
+        return out
+
+    def frame(self) -> np.ndarray:
+        """h_color as [h, w] u32, row 0 = bottom (the DIB is bottom-up)."""
+        w, h = self.res
+        return self.h_color.reshape(h, w)
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            _lib.lib().rt_camera_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def packed_pixels(w: int, h: int, nranks: int) -> int:
+    return int(_lib.lib().rt_tile_packed_pixels(w, h, nranks))
+
+
+def unpack_bands(device: int, w: int, h: int, nranks: int, gathered, frame, stream=None) -> None:
+    s = C.c_void_p(stream) if isinstance(stream, int) else C.c_void_p(None)
+    _lib.call("rt_unpack_bands", device, w, h, nranks, _lib.ptr(gathered), _lib.ptr(frame), s)
+
+
+__all__ = ["read_ply", "assemble_mesh", "kd_build", "film_w", "camera_basis", "Quaternion", "Trixel", "Object",
+           "Camera", "packed_pixels", "unpack_bands", "SET_COLOR_TAG", "PHONG_COLOR_TAG", "RT_MODE_KD",
+           "RT_MODE_FLAT", "RT_FLAG_WRITE_HIT", "RT_FLAG_COUNT", "BACKGROUND_ARGB", "DEFAULT_RAD"]

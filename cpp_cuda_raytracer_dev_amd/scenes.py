@@ -1,0 +1,100 @@
+"""Scene inputs for the benchmark configs (BASELINE.json).
+
+* ``fixture_mesh(name)``: the meshes that ship with the reference
+  (rabbit_70k.ply, tester.ply, dump.ply, dump_test.ply), stored under
+  tests/golden/meshes/ as raw vertex/face arrays (parsed with strtof, the
+  rounding of the PLY loader).
+* ``standin(name)``: seeded synthetic stand-ins for the two meshes missing
+  from the reference (.MISSING_LARGE_BLOBS: dragon_vrip_mod.ply,
+  happy_vrip_mod.ply).  Closed 2-manifold displaced blobs with exactly the
+  public Stanford triangle counts and approximately their bounding boxes
+  (SURVEY.md §8d).  Every report labels them "synthetic".
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+MESH_DIR = os.path.join(ROOT, "tests", "golden", "meshes")
+
+#: loader mode of each reference mesh (TD/WinMain.cpp:93-109)
+FIXTURE_MODES = {"rabbit_70k": 1, "tester": 2, "dump": 1, "dump_test": 0}
+
+STANDINS = {
+    # name: (triangles, bbox lo, bbox hi, (U, V) main blob, (U, V) small blob)
+    "dragon": (871_414, (-0.112, 0.052, -0.067), (0.093, 0.199, 0.054), (640, 681), (39, 14)),
+    "happy": (1_087_716, (-0.047, 0.055, -0.037), (0.044, 0.248, 0.047), (720, 756), (43, 7)),
+}
+STANDIN_SEED = 20221015
+
+
+def fixture_mesh(name: str):
+    """(verts [nv,3] f32, arity [nf] i32, idx [sum arity] i32) of a reference mesh."""
+    z = np.load(os.path.join(MESH_DIR, f"{name}.npz"), allow_pickle=False)
+    return z["verts"], z["arity"], z["idx"]
+
+
+def _uv_sphere(U: int, V: int):
+    """Unit-sphere vertices and triangle faces with 2*U*(V-1) triangles:
+    two poles, V-1 rings of U vertices."""
+    theta = np.pi * (np.arange(1, V, dtype=np.float64) / V)            # ring latitudes
+    phi = 2 * np.pi * (np.arange(U, dtype=np.float64) / U)
+    st, ct = np.sin(theta)[:, None], np.cos(theta)[:, None]
+    ring = np.stack([st * np.cos(phi)[None, :], ct * np.ones((1, U)), st * np.sin(phi)[None, :]], -1)
+    verts = np.concatenate([[[0.0, 1.0, 0.0]], ring.reshape(-1, 3), [[0.0, -1.0, 0.0]]])
+    south = 1 + (V - 1) * U
+    j = np.arange(U)
+    jn = (j + 1) % U
+    faces = [np.stack([np.zeros(U, np.int64), 1 + jn, 1 + j], -1)]
+    for r in range(V - 2):
+        a, b = 1 + r * U + j, 1 + r * U + jn
+        c, d = a + U, b + U
+        faces.append(np.stack([a, b, d], -1))
+        faces.append(np.stack([a, d, c], -1))
+    last = 1 + (V - 2) * U
+    faces.append(np.stack([last + j, last + jn, np.full(U, south)], -1))
+    return verts, np.concatenate(faces).astype(np.int32)
+
+
+def _displace(v: np.ndarray, rng: np.random.Generator, octaves: int, amp: float) -> np.ndarray:
+    r = np.ones(len(v))
+    for o in range(octaves):
+        k = 3.0 * (1.9 ** o)
+        for _ in range(4):
+            d = rng.normal(size=3)
+            d /= np.linalg.norm(d)
+            ph = rng.uniform(0, 2 * np.pi)
+            r += (amp / (1.7 ** o)) * np.sin(k * (v @ d) + ph)
+    return v * r[:, None]
+
+
+def standin(name: str):
+    """Synthetic stand-in mesh: (verts [nv,3] f32, faces [nf,3] i32)."""
+    ntri, lo, hi, (U, V), (u2, v2) = STANDINS[name]
+    rng = np.random.default_rng(STANDIN_SEED if name == "dragon" else STANDIN_SEED + 1)
+    lo, hi = np.asarray(lo), np.asarray(hi)
+    c, half = (lo + hi) / 2, (hi - lo) / 2
+    v, f = _uv_sphere(U, V)
+    v = _displace(v, rng, octaves=6, amp=0.06)
+    v = v / np.abs(v).max(axis=0)  # fill the box
+    body = c + half * v
+    # a small closed blob near the +x end (head/eye), fully inside the box
+    v2, f2 = _uv_sphere(u2, v2)
+    eye = c + half * np.array([0.78, 0.45, 0.30]) + 0.06 * half.min() * v2
+    verts = np.concatenate([body, eye]).astype(np.float32)
+    faces = np.concatenate([f, f2 + len(body)]).astype(np.int32)
+    assert len(faces) == ntri, (name, len(faces))
+    return verts, faces
+
+
+def write_ply(path: str, verts: np.ndarray, faces: np.ndarray) -> None:
+    """Mode-0 ASCII PLY (x y z per vertex); %.9g round-trips float32."""
+    with open(path, "w") as fp:
+        fp.write(f"ply\nformat ascii 1.0\nelement vertex {len(verts)}\nproperty float x\nproperty float y\n"
+                 f"property float z\nelement face {len(faces)}\nproperty list uchar int vertex_indices\n"
+                 "end_header\n")
+        np.savetxt(fp, verts.astype(np.float64), fmt="%.9g")
+        arity = np.full((len(faces), 1), faces.shape[1], np.int64)
+        np.savetxt(fp, np.concatenate([arity, faces.astype(np.int64)], 1), fmt="%d")

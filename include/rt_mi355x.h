@@ -1,0 +1,182 @@
+/*
+ * rt_mi355x.h -- C ABI of the MI355X-native ray-cast hot path.
+ *
+ * Drop-in boundary for ams3878/cpp_cuda_raytracer_dev (TD/ = TEST_Dungeonrun/).
+ * The reference's host objects (Camera, Trixel, Object, Quaternion) call the
+ * device through free functions that return cudaError_t; each rt_* entry
+ * point below names the reference function it replaces.  All functions
+ * return RT_OK (0) or a negative rt_status; rt_last_error_string() explains
+ * the last failure of the calling thread.  No torch types cross this ABI:
+ * plain pointers, sizes and an optional hipStream_t passed as void*.
+ *
+ * Threading: one host thread per handle; handles are not thread-safe.
+ * Rendering is stream-ordered; rt_read_frame synchronises.
+ */
+#ifndef RT_MI355X_H
+#define RT_MI355X_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+typedef enum rt_status {
+    RT_OK = 0,
+    RT_ERR_INVALID = -1,   /* bad argument / malformed input          */
+    RT_ERR_HIP = -2,       /* a HIP runtime call failed                */
+    RT_ERR_NOMEM = -3,     /* host or device allocation failed         */
+    RT_ERR_IO = -4,        /* file could not be read / parsed          */
+    RT_ERR_STATE = -5,     /* call out of order (e.g. render w/o tree) */
+    RT_ERR_OVERFLOW = -6   /* traversal stack overflow flagged by GPU  */
+} rt_status;
+
+/* Render modes: KD traversal (intersect_voxel_cuda, TD/Trixel.cu:41-172) or
+ * the flat triangle list (intersect_trixel_cuda, TD/Trixel.cu:173-209). */
+#define RT_MODE_KD 0u
+#define RT_MODE_FLAT 1u
+
+/* Render flags. */
+#define RT_FLAG_WRITE_HIT 1u   /* also write the per-pixel hit triangle (d_rmi.index) */
+#define RT_FLAG_COUNT 2u       /* accumulate traversal counters (rt_camera_counters)  */
+
+/* Per-triangle AABB = kd_leaf (TD/Trixel.h:31-37); `tri` = tri_list_index. */
+typedef struct rt_leaf_aabb {
+    float x0, x1, y0, y1, z0, z1;
+    int64_t tri;
+} rt_leaf_aabb;
+
+/* World-space tree node = Trixel::kd_tree::kd_tree_node (TD/Trixel.h:68-79),
+ * BFS order, right = left + 1, 2*ntri-1 nodes. */
+typedef struct rt_kd_node {
+    float x0, x1, y0, y1, z0, z1; /* h_bound                            */
+    float s1, s2;                 /* left child's max / right child's min on the cut axis */
+    int32_t cut_flag;             /* 0 x1, 1 y1, 2 z1, 3 x0, 4 y0, 5 z0 */
+    int32_t is_leaf;
+    int64_t tri_index;            /* leaf: triangle; interior: -1       */
+    int64_t left, right, parent;  /* leaf: -1, -1                       */
+} rt_kd_node; /* 72 bytes */
+
+/* Camera::o_prop basis (TD/Camera.h:32-42). */
+typedef struct rt_camera_basis_t {
+    float n[3], u[3], v[3];
+    float n_mod[3], u_mod[3], v_mod[3];
+    float pix_w, pix_h;
+} rt_camera_basis_t;
+
+/* Screen sharding: rows are cut into bands of 8; band b belongs to rank
+ * b % nranks.  A rank renders its bands into a packed buffer of
+ * rt_tile_packed_pixels() pixels (slot j = band rank + j*nranks). */
+typedef struct rt_tile {
+    int32_t nranks;
+    int32_t rank;
+} rt_tile;
+
+typedef struct rt_scene rt_scene;   /* Trixel: triangles + KD tree on one device */
+typedef struct rt_camera rt_camera; /* Camera: rays, frame, camera-relative object data */
+
+/* ------------------------------------------------ host-side construction */
+
+/* read_ply (TD/read_ply.cpp:13-152): mode 0 "x y z", 1 "x y z c i",
+ * 2 "x y z nx ny nz".  Accepts the "end_header" header and the headerless
+ * "[ply\n]nv\nnf\n" prelude (the reference hangs on those, H9).  Outputs are
+ * allocated by the library; release with rt_host_free. */
+int rt_read_ply(const char* path, int mode, float** points9, uint32_t* ntri,
+                rt_leaf_aabb** leafs);
+
+/* The face-assembly half of read_ply (TD/read_ply.cpp:128-210) on an indexed
+ * mesh: arity[f] in {3,4}, idx = concatenated face indices. */
+int rt_mesh_assemble(const float* verts, int64_t nvert, const int32_t* arity,
+                     const int32_t* idx, int64_t nface, float** points9,
+                     uint32_t* ntri, rt_leaf_aabb** leafs);
+
+void rt_host_free(void* p);
+
+/* Trixel::set_sorted_voxels + Trixel::create_kd (TD/Trixel.h:135-473,
+ * TD/sort.h:11-60): the identical node array, built in parallel.
+ * nodes must hold 2*ntri-1 entries.  nthreads <= 0: hardware concurrency. */
+int rt_kd_build(const rt_leaf_aabb* leafs, uint32_t ntri, rt_kd_node* nodes,
+                int nthreads);
+
+/* Camera::Camera basis (TD/Camera.cpp:5-67). */
+int rt_camera_basis(int32_t w, int32_t h, float f_w, float f_h, float focal,
+                    const float pos[3], const float look_at[3], const float up[3],
+                    rt_camera_basis_t* out);
+
+/* WinMain's film width ((float)w/h)*.024f (TD/WinMain.cpp:29,69-70). */
+float rt_film_w(int32_t w, int32_t h);
+
+/* ----------------------------------------------------------- device path */
+
+int rt_device_count(int* count);
+
+/* Trixel::Trixel + init_trixels_device_memory (TD/Trixel.h:87-133,
+ * TD/Trixel.cu:266-289 / init_tri_mem_cuda :11-27).  rad3 = Color::rad per
+ * triangle (r,g,b floats).  Copies its inputs. */
+int rt_scene_create(int device, const float* points9, const float* rad3,
+                    uint32_t ntri, rt_scene** out);
+
+/* The H2D copy at the end of Trixel::create_kd (TD/Trixel.h:380).  Validates
+ * the tree (BFS order, 2*ntri-1 nodes, leaves cover every triangle once). */
+int rt_scene_set_kd(rt_scene* s, const rt_kd_node* nodes, uint64_t nnode);
+
+/* Camera::Camera + init_camera_device_memory (TD/Camera.cpp:5-117,
+ * TD/Camera.cu:112-136). */
+int rt_camera_create(int device, int32_t w, int32_t h, float f_w, float f_h,
+                     float focal, const float pos[3], const float look_at[3],
+                     const float up[3], rt_camera** out);
+
+/* Camera::add_object -> init_camera_trixel_device_memory +
+ * init_camera_voxel_device_memory (TD/Camera.cpp:118-210,
+ * TD/Trixel.cu:244-264, TD/Camera.cu:137-187).  The reference keeps only the
+ * last object (object_list[0] colours, the second add overwrites the camera
+ * buffers); so does this. */
+int rt_camera_add_object(rt_camera* c, rt_scene* s);
+
+/* One frame: bg fill -> intersect -> Phong, i.e. the steady state of
+ * Object::render + Camera::color_pixels (TD/WinMain.cpp:212-237 ->
+ * intersect_trixels_device TD/Trixel.cu:210-242, color_camera_device
+ * TD/Camera.cu:70-87) without the D2H copy.  xform = the object's rot_m rows
+ * (x.i x.j x.k x.w, y.., z..) or NULL for identity.  tile NULL = full frame.
+ * stream = hipStream_t or NULL (default stream).  Writes the camera's own
+ * frame buffers. */
+int rt_render(rt_camera* c, const float* xform, uint32_t mode, uint32_t flags,
+              const rt_tile* tile, void* stream);
+
+/* As rt_render, into caller-owned device buffers (argb: packed pixels of the
+ * tile, hit: same count of int64 or NULL). */
+int rt_render_into(rt_camera* c, const float* xform, uint32_t mode, uint32_t flags,
+                   const rt_tile* tile, uint32_t* d_argb, int64_t* d_hit, void* stream);
+
+/* Pixels in one rank's packed buffer (uniform across ranks). */
+int64_t rt_tile_packed_pixels(int32_t w, int32_t h, int32_t nranks);
+
+/* Rank 0 side of the frame gather: d_gathered = nranks packed buffers back to
+ * back -> d_frame (w*h).  Runs on `stream`. */
+int rt_unpack_bands(int device, int32_t w, int32_t h, int32_t nranks,
+                    const uint32_t* d_gathered, uint32_t* d_frame, void* stream);
+
+/* The D2H copy of color_camera_device (TD/Camera.cu:84) and d_rmi.index.
+ * Synchronises the device.  argb: w*h u32 0x00RRGGBB; hit may be NULL. */
+int rt_read_frame(rt_camera* c, uint32_t* argb, int64_t* hit);
+
+/* Counters accumulated by RT_FLAG_COUNT renders: [0] interior visits,
+ * [1] leaf visits, [2] accepted hits, [3] hit pixels, [4] interior visits
+ * that descended.  reset != 0 zeroes them after reading.  Synchronises. */
+int rt_camera_counters(rt_camera* c, uint64_t out[5], int reset);
+
+/* Kernel launch geometry and the traversal stack depth in use. */
+int rt_camera_info(const rt_camera* c, int32_t* w, int32_t* h, int32_t* max_depth);
+
+void rt_scene_destroy(rt_scene* s);
+void rt_camera_destroy(rt_camera* c);
+
+const char* rt_last_error_string(void);
+int rt_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_MI355X_H */

@@ -1,0 +1,258 @@
+"""CPU tests: the C ABI library's host half, the oracle against its pins
+(golden fixtures from the independent numpy restatement, hand-derived
+known answers), and the sharding logic.  No GPU calls."""
+import hashlib
+import os
+import re
+
+import numpy as np
+import pytest
+
+from cpp_cuda_raytracer_dev_amd import _lib, raytracer as R, scenes
+from oracle import _oracle as O, np_oracle as N
+from tests import helpers as H
+
+REF = "/root/reference/TEST_Dungeonrun"
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "rt_mi355x.h")
+
+
+def test_library_exports_every_declared_symbol():
+    decl = set(re.findall(r"\b(rt_[a-z_0-9]+)\s*\(", open(HEADER).read()))
+    L = _lib.lib()
+    missing = [s for s in sorted(decl) if not hasattr(L, s)]
+    assert not missing, missing
+    assert decl == set(_lib.SIGNATURES), set(_lib.SIGNATURES) ^ decl
+    assert L.rt_abi_version() == 1
+
+
+def test_epsilon_threshold_is_exact():
+    c = np.array([0x24E69595], np.uint32).view(np.float32)[0]
+    assert np.float64(c) >= 1e-16
+    assert np.float64(np.nextafter(c, np.float32(0))) < 1e-16
+    assert np.float64(1) + 1e-16 == 1.0  # (u+v) > 1 + 1e-16  <=>  (u+v) > 1.0f
+
+
+@pytest.mark.parametrize("name", list(scenes.FIXTURE_MODES))
+def test_mesh_assembly_matches_oracle(name):
+    v, a, ix = scenes.fixture_mesh(name)
+    pts, n, leafs = R.assemble_mesh(v, H.faces_list(a, ix))
+    opts, oleafs = O.assemble(v, a, ix)
+    assert pts.tobytes() == opts.tobytes()
+    for f in ("x0", "x1", "y0", "y1", "z0", "z1"):
+        assert leafs[f].tobytes() == oleafs[f].tobytes()
+    assert (leafs["tri"] == np.arange(n)).all()
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference meshes only in the build container")
+@pytest.mark.parametrize("name,mode", list(scenes.FIXTURE_MODES.items()))
+def test_ply_loader_matches_oracle_and_fixture(name, mode):
+    path = os.path.join(REF, name + ".ply")
+    pts, n, leafs = R.read_ply(path, mode)
+    opts, oleafs = O.read_ply(path, mode)
+    v, a, ix = scenes.fixture_mesh(name)
+    fpts, _, _ = R.assemble_mesh(v, H.faces_list(a, ix))
+    assert pts.tobytes() == opts.tobytes() == fpts.tobytes()
+
+
+def test_ply_loader_errors(tmp_path):
+    p = tmp_path / "bad.ply"
+    p.write_text("ply\nformat ascii 1.0\nelement vertex 3\nelement face 1\nend_header\n0 0 0\n1 0 0\n0 1 0\n5 0 1 2 0 1\n")
+    with pytest.raises(_lib.RtError):
+        R.read_ply(str(p), 0)
+    with pytest.raises(_lib.RtError):
+        R.read_ply(str(tmp_path / "missing.ply"), 0)
+    q = tmp_path / "ok.ply"
+    scenes.write_ply(str(q), np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0], [1, 1, 0]], np.float32),
+                     np.array([[0, 1, 2], [1, 3, 2]], np.int32))
+    pts, n, _ = R.read_ply(str(q), 0)
+    assert n == 2 and pts[0, :3].tolist() == [0, 1, 0]  # 3-gon stored (P3, P1, P2)
+
+
+def _nodes_equal(a, b):
+    for f in ("cut_flag", "is_leaf", "tri_index", "left", "right", "parent"):
+        assert (a[f] == b[f]).all(), f
+    for f in ("x0", "x1", "y0", "y1", "z0", "z1"):
+        assert a[f].tobytes() == b[f].tobytes(), f
+    inner = a["is_leaf"] == 0
+    for f in ("s1", "s2"):
+        assert a[f][inner].tobytes() == b[f][inner].tobytes(), f
+
+
+@pytest.mark.parametrize("name", list(scenes.FIXTURE_MODES))
+def test_kd_build_matches_oracle(name):
+    pn, on = H.trees(name)
+    _nodes_equal(pn, on)
+
+
+def _random_leafs(n, seed, ties):
+    rng = np.random.default_rng(seed)
+    lo = rng.integers(0, 8, size=(n, 3)).astype(np.float32) if ties else rng.random((n, 3)).astype(np.float32)
+    hi = lo + (rng.integers(0, 3, size=(n, 3)).astype(np.float32) if ties else rng.random((n, 3)).astype(np.float32))
+    pl = np.zeros(n, _lib.LEAF_AABB_DTYPE)
+    ol = np.zeros(n, O.LEAF_DTYPE)
+    for i, f in enumerate(("x", "y", "z")):
+        for arr in (pl, ol):
+            arr[f + "0"] = lo[:, i]
+            arr[f + "1"] = hi[:, i]
+    pl["tri"] = np.arange(n)
+    ol["tri"] = np.arange(n)
+    return pl, ol
+
+
+@pytest.mark.parametrize("n,seed,ties", [(1, 0, False), (2, 1, False), (3, 2, True), (17, 3, True),
+                                         (1000, 4, True), (4097, 5, False), (30000, 6, True)])
+def test_kd_build_random_with_ties(n, seed, ties):
+    pl, ol = _random_leafs(n, seed, ties)
+    _nodes_equal(R.kd_build(pl, nthreads=4), O.build_kd(ol))
+
+
+def test_kd_invariants():
+    pts, leafs, _ = H.mesh("rabbit_70k")
+    nodes = H.trees("rabbit_70k")[0]
+    n = len(leafs)
+    assert len(nodes) == 2 * n - 1
+    leaf = nodes["is_leaf"] == 1
+    assert sorted(nodes["tri_index"][leaf]) == list(range(n))
+    inner = np.flatnonzero(~leaf)
+    assert (nodes["right"][inner] == nodes["left"][inner] + 1).all()
+    assert (nodes["left"][inner] > inner).all()
+    for side in ("left", "right"):
+        c = nodes[side][inner]
+        for f in ("x0", "y0", "z0"):
+            assert (nodes[f][c] >= nodes[f][inner]).all()
+        for f in ("x1", "y1", "z1"):
+            assert (nodes[f][c] <= nodes[f][inner]).all()
+    depth = np.zeros(len(nodes), int)
+    for i in inner:
+        depth[nodes["left"][i]] = depth[nodes["right"][i]] = depth[i] + 1
+    assert depth.max() + 1 <= int(np.ceil(np.log2(2 * n - 1)))  # the reference's stack size suffices
+
+
+@pytest.mark.parametrize("w,h", [(320, 180), (960, 540), (1920, 1080), (3840, 2160), (81, 45), (1, 1)])
+def test_camera_basis_matches_oracle(w, h):
+    c = O.camera(w, h)
+    b = R.camera_basis(w, h, R.film_w(w, h), np.float32(.024), np.float32(.055), (0, .1, -1), (0, .1, 0), (0, 1, 0))
+    for k in ("n", "u", "v", "n_mod", "u_mod", "v_mod"):
+        assert np.array(getattr(c, k)[:], np.float32).tobytes() == b[k].tobytes(), k
+    nb = N.camera(w, h)
+    for k in ("n_mod", "u_mod", "v_mod"):
+        assert np.array(nb[k], np.float32).tobytes() == b[k].tobytes(), k
+
+
+def test_fast_rsqrt_against_numpy_restatement():
+    rng = np.random.default_rng(0)
+    for s in rng.random(200).astype(np.float32) * 10:
+        a = np.float32(O.lib().orc_device_inverse_sqrt(s, 0.0, 0.0))
+        b = N.rsqrt(np.float32(s * s), 21)
+        assert a.tobytes() == b.tobytes()
+        c = np.float32(O.lib().orc_host_vector_norm(s))
+        assert c.tobytes() == N.rsqrt(s, 8).tobytes()
+
+
+# ---------------------------------------------------------------- oracle pins
+
+@pytest.mark.parametrize("name,w,h", [("dump_test", 64, 36), ("tester", 80, 45), ("dump", 48, 27)])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_oracle_matches_numpy_golden(name, w, h, mode):
+    g = H.golden()
+    argb, hit, _ = H.oracle_render(name, w, h, mode)
+    key = f"{name}_{w}x{h}_m{mode}"
+    assert (hit == g[key + "_hit"]).all()
+    assert (argb == g[key + "_argb"]).all()
+
+
+@pytest.mark.parametrize("key,name,w,h,mode", [("tester_320x180_m0", "tester", 320, 180, 0),
+                                               ("tester_320x180_m1", "tester", 320, 180, 1),
+                                               ("rabbit_70k_960x540_m0", "rabbit_70k", 960, 540, 0),
+                                               ("dump_320x180_m0", "dump", 320, 180, 0)])
+def test_oracle_matches_recorded_hashes(key, name, w, h, mode):
+    g = H.golden()
+    argb, hit, cnt = H.oracle_render(name, w, h, mode)
+    assert hashlib.sha256(argb.tobytes()).hexdigest() == str(g[key + "_argb_sha"])
+    assert hashlib.sha256(hit.tobytes()).hexdigest() == str(g[key + "_hit_sha"])
+    assert (cnt == g[key + "_counters"]).all()
+
+
+def test_numpy_crosscheck_with_transform():
+    """The two restatements agree on a non-identity object transform (rotated + translated)."""
+    v, a, ix = scenes.fixture_mesh("dump")
+    pts, boxes = N.assemble(v, a, ix)
+    nodes = N.build_kd(boxes)
+    ang = np.deg2rad(12.0)
+    c, s = np.float32(np.cos(ang)), np.float32(np.sin(ang))
+    X = np.array([c, 0, s, 0.004, 0, 1, 0, -0.002, -s, 0, c, 0.01], np.float32)
+    cam = N.camera(40, 24)
+    argb, hit = N.render(pts, nodes, cam, 0, xform=X)
+    oargb, ohit, _ = H.oracle_render("dump", 40, 24, 0, xform=X)
+    assert (hit >= 0).sum() > 5
+    assert (hit == ohit).all() and (argb == oargb).all()
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_known_answer_dump_test(mode):
+    """Hand-derived KAT on dump_test.ply: seven coplanar z=0 triangles, four of
+    them copies of {0,3,4} with permuted windings.  Every primary ray meets
+    the plane; a pixel must hit one of the triangles that contain its plane
+    point, and where exactly one triangle contains it (away from edges), that
+    triangle."""
+    w, h = 64, 36
+    argb, hit, _ = H.oracle_render("dump_test", w, h, mode)
+    v, a, ix = scenes.fixture_mesh("dump_test")
+    faces = np.asarray(ix).reshape(-1, 3)
+    assert (hit >= 0).all()
+    cam = O.camera(w, h)
+    P = v.astype(np.float64)
+
+    def side(u, v_, p):
+        return (v_[0] - u[0]) * (p[1] - u[1]) - (v_[1] - u[1]) * (p[0] - u[0])
+
+    def inside(p, tri, margin):
+        A, B, C = (P[i, :2] for i in tri)
+        d = np.array([side(A, B, p), side(B, C, p), side(C, A, p)])
+        return bool((d > margin).all() or (d < -margin).all())
+
+    unique = 0
+    for iy in range(h):
+        for ix_ in range(w):
+            r = np.zeros(3, np.float32)
+            O.lib().orc_primary_ray(cam, ix_, iy, r.ctypes.data)
+            t = 1.0 / r[2]
+            p = np.array([t * r[0], 0.1 + t * r[1]])
+            loose = [k for k, f in enumerate(faces) if inside(p, f, -1e-3)]
+            tight = [k for k, f in enumerate(faces) if inside(p, f, 1e-3)]
+            got = hit[iy * w + ix_]
+            assert got in loose, (ix_, iy, got, loose)
+            if len(loose) == 1 and len(tight) == 1:
+                assert got == tight[0]
+                unique += 1
+    assert unique > 500
+
+
+def test_single_triangle_analytic_distance():
+    """One triangle facing the camera: the hit distance is the analytic t."""
+    verts = np.array([[-4, -4, 0.5], [4, -4, 0.5], [0, 4, 0.5]], np.float32)
+    pts, n, leafs = R.assemble_mesh(verts, np.array([[0, 1, 2]], np.int32))
+    nodes = R.kd_build(leafs)
+    on = O.build_kd(O.assemble(verts, np.array([3], np.int32), np.array([0, 1, 2], np.int32))[1])
+    cam = O.camera(9, 5)
+    s = O.Scene(pts, O.default_rad(1), on, cam)
+    argb, hit, cnt = s.render(0)
+    assert (hit == 0).all() and len(nodes) == 1
+    assert (argb != R.BACKGROUND_ARGB).all()
+    # centre pixel: ray through (0, 0.1) direction ~ +z, distance ~ 1.5
+    r = np.zeros(3, np.float32)
+    O.lib().orc_primary_ray(cam, 4, 2, r.ctypes.data)
+    assert abs(1.5 / r[2] - 1.5) < 1e-3
+
+
+# ---------------------------------------------------------------- sharding
+
+def test_band_pack_unpack_roundtrip():
+    from cpp_cuda_raytracer_dev_amd import distributed as D
+    rng = np.random.default_rng(1)
+    for (w, h) in [(1920, 1080), (33, 17), (8, 8), (5, 3)]:
+        frame = rng.integers(0, 2**32, size=w * h, dtype=np.uint64).astype(np.uint32)
+        for n in (1, 2, 3, 8):
+            g = np.concatenate([D.pack_bands_numpy(frame, w, h, n, r) for r in range(n)])
+            assert D.packed_pixels(w, h, n) == R.packed_pixels(w, h, n)
+            assert (D.unpack_bands_numpy(g, w, h, n) == frame).all()
