@@ -44,6 +44,10 @@ def parse():
     ap.add_argument("--height", type=int, default=H)
     ap.add_argument("--mode", type=int, default=0, help="0 KD, 1 flat list")
     ap.add_argument("--collective", default="gather", choices=["gather", "allgather"])
+    ap.add_argument("--kernel", type=int, default=3,
+                    help="KD kernel: 1 per-lane DFS (own-box records), 2 per-lane DFS (child-box records), "
+                         "3 wave-cooperative item pool")
+    ap.add_argument("--tile-order", type=int, default=1, help="0 XCD-contiguous, 1 natural, 2 centre-out")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -111,6 +115,9 @@ def main():
     trixel = R.Trixel(len(pts), pts, device=local)
     trixel.set_kd_nodes(nodes)
     cam = R.Camera.default(w, h, device=local)
+    from cpp_cuda_raytracer_dev_amd import _lib
+    cam.set_option(_lib.RT_OPT_KERNEL, 2)  # the counting frame runs the reference's DFS order
+    cam.set_option(_lib.RT_OPT_TILE_ORDER, a.tile_order)
     obj = R.Object(trixel)
     cam.add_object(obj)
     xf = obj.quat.xform()
@@ -124,6 +131,9 @@ def main():
     cam.render_into(scratch, mode=a.mode, flags=R.RT_FLAG_COUNT, tile=tile if world > 1 else None, stream=sptr)
     torch.cuda.synchronize(dev)
     cnt = cam.counters(reset=True)
+    cam.set_option(_lib.RT_OPT_KERNEL, a.kernel)
+    cam.render_into(scratch, mode=a.mode, tile=tile if world > 1 else None, stream=sptr)  # re-prepares layout
+    torch.cuda.synchronize(dev)
     my_pix = int(np.count_nonzero(np.repeat(np.arange((h + 7) // 8) % world == rank, 8)[:h])) * w
     bytes_per_launch = B_INT * int(cnt[0]) + B_LEAF * int(cnt[1]) + B_HIT * int(cnt[2]) + B_PIX * my_pix
 
@@ -211,7 +221,9 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "k_trace_kd" if a.mode == 0 else "k_trace_flat",
+                "kernel": {1: "k_trace_kd", 2: "k_trace_kd2", 3: "k_trace_kd3"}[a.kernel] if a.mode == 0
+                          else "k_trace_flat",
+                "kernel_options": {"layout": a.kernel, "tile_order": a.tile_order},
                 "kernel_ms_avg": round(kern_ms, 5),
                 "kernel_ms_avg_max_rank": round(kern_ms_max, 5),
                 "algorithmic_bytes_per_launch": bytes_per_launch,

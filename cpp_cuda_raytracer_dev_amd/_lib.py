@@ -20,6 +20,10 @@ RT_MODE_KD = 0
 RT_MODE_FLAT = 1
 RT_FLAG_WRITE_HIT = 1
 RT_FLAG_COUNT = 2
+RT_OPT_KERNEL = 1
+RT_OPT_TILE_ORDER = 2
+RT_OPT_DEBUG = 100
+RT_OPT_POOL_CAP = 101
 
 LEAF_AABB_DTYPE = np.dtype([("x0", "<f4"), ("x1", "<f4"), ("y0", "<f4"), ("y1", "<f4"),
                             ("z0", "<f4"), ("z1", "<f4"), ("tri", "<i8")])
@@ -73,6 +77,8 @@ SIGNATURES = {
     "rt_read_frame": (C.c_int, [_P, _P, _P]),
     "rt_camera_counters": (C.c_int, [_P, _P, C.c_int]),
     "rt_camera_info": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "rt_camera_set_option": (C.c_int, [_P, C.c_int32, C.c_int32]),
+    "rt_camera_debug_read": (C.c_int64, [_P, _P, C.c_int64]),
     "rt_scene_destroy": (None, [_P]),
     "rt_camera_destroy": (None, [_P]),
     "rt_last_error_string": (C.c_char_p, []),

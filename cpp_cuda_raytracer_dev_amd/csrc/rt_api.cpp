@@ -27,6 +27,7 @@ struct rt_scene {
     uint32_t root_ref = 0;
     int32_t height = 0;
     uint64_t tree_version = 0;
+    rt_kd_node root{};               // host copy of node 0 (root box)
 };
 
 struct rt_camera {
@@ -43,7 +44,17 @@ struct rt_camera {
     float4* d_trec = nullptr;        // camera-relative triangle records
     float4* d_inode = nullptr;       // camera-relative interior nodes
     uint32_t trec_cap = 0;
-    int64_t inode_cap = 0;
+    int64_t inode_cap = 0;           // in float4
+    int prepared_layout = 0;         // interior record layout of d_inode (1 or 2)
+    int kernel_version = 3;          // kOptKernel (3 falls back to 2 on trees taller than 21)
+    int tile_order = 2;              // kOptTileOrder
+    int debug = 0;                   // kOptDebug (diagnostics)
+    int pool_cap = kPoolCapMax;      // kOptPoolCap
+    unsigned long long* d_dbg = nullptr;
+    int64_t dbg_cap = 0;             // in u64
+    int32_t* d_order = nullptr;      // centre-out tile permutation
+    int64_t order_cap = 0;
+    int64_t order_key[5] = {-1, -1, -1, -1, -1};
 };
 
 namespace {
@@ -78,10 +89,20 @@ void dev_free(T*& p) {
     p = nullptr;
 }
 
+// The KD kernel a render runs: the wave-cooperative kernel (3) encodes DFS
+// path codes in 21 bits, so taller trees use the per-lane DFS kernel (2).
+int effective_kernel(const rt_camera* c) {
+    if (c->kernel_version == 3 && c->obj && c->obj->height > 21) return 2;
+    return c->kernel_version;
+}
+
+int record_layout(int kernel) { return kernel == 1 ? 1 : 2; }
+
 int prepare_camera_object(rt_camera* c) {
     rt_scene* s = c->obj;
     if (!s) return fail(RT_ERR_STATE, "camera has no object (rt_camera_add_object)");
-    if (c->prepared_version == s->tree_version + 1) return RT_OK;
+    const int layout = record_layout(effective_kernel(c));
+    if (c->prepared_version == s->tree_version + 1 && c->prepared_layout == layout) return RT_OK;
     int rc;
     if (c->trec_cap < s->ntri) {
         dev_free(c->d_trec);
@@ -91,23 +112,54 @@ int prepare_camera_object(rt_camera* c) {
     // init_camera_trixel_device_memory (TD/Trixel.cu:244-264)
     if ((rc = launch_cam_tri(s->d_tri_world, s->ntri, c->pos, c->d_trec, nullptr))) return rc;
     if (s->d_nodes) {
-        if (c->inode_cap < s->ninterior) {
+        const int64_t need = std::max<int64_t>(s->ninterior, 1) * (layout == 1 ? 3 : 4);
+        if (c->inode_cap < need) {
             dev_free(c->d_inode);
-            if ((rc = dev_alloc(&c->d_inode, (size_t)std::max<int64_t>(s->ninterior, 1) * 3, "hipMalloc(inode)"))) return rc;
-            c->inode_cap = s->ninterior;
+            if ((rc = dev_alloc(&c->d_inode, (size_t)need, "hipMalloc(inode)"))) return rc;
+            c->inode_cap = need;
         }
         // init_camera_voxel_device_memory (TD/Camera.cu:163-187)
         if ((rc = launch_cam_nodes(s->d_nodes, s->d_interior_ids, s->d_node_ref, s->ninterior, c->pos,
-                                   c->d_inode, nullptr)))
+                                   c->d_inode, layout, nullptr)))
             return rc;
     }
     if ((rc = hip_check(hipDeviceSynchronize(), "camera object prep"))) return rc;
     c->prepared_version = s->tree_version + 1;
+    c->prepared_layout = layout;
     return RT_OK;
 }
 
-void fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t* argb, int64_t* hit,
-                 TraceParams& p) {
+// Centre-out permutation of the launch's tiles: blocks are dispatched in
+// index order, so the expensive tiles (the object sits mid-frame) start
+// first and the cheap background tiles fill in behind them.
+int ensure_order(rt_camera* c, int32_t tile_w, int32_t tiles_x, int32_t slots, int32_t nranks, int32_t rank) {
+    const int64_t key[5] = {tile_w, tiles_x, slots, nranks, rank};
+    if (std::equal(key, key + 5, c->order_key)) return RT_OK;
+    const int64_t n = (int64_t)tiles_x * slots;
+    std::vector<int32_t> order((size_t)n);
+    std::vector<double> dist2((size_t)n);
+    const double cx = 0.5 * c->w, cy = 0.5 * c->h;
+    for (int64_t t = 0; t < n; t++) {
+        const int64_t slot = t / tiles_x, tx = t % tiles_x;
+        const double x = (tx + 0.5) * tile_w, y = ((rank + slot * (int64_t)nranks) + 0.5) * kTileH;
+        dist2[(size_t)t] = (x - cx) * (x - cx) + (y - cy) * (y - cy);
+        order[(size_t)t] = (int32_t)t;
+    }
+    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return dist2[(size_t)a] < dist2[(size_t)b]; });
+    int rc;
+    if (c->order_cap < n) {
+        dev_free(c->d_order);
+        if ((rc = dev_alloc(&c->d_order, (size_t)n, "hipMalloc(order)"))) return rc;
+        c->order_cap = n;
+    }
+    if ((rc = hip_check(hipMemcpy(c->d_order, order.data(), sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice), "H2D order")))
+        return rc;
+    std::copy(key, key + 5, c->order_key);
+    return RT_OK;
+}
+
+int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t* argb, int64_t* hit,
+                uint32_t mode, TraceParams& p) {
     static const float ident[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
     const rt_scene* s = c->obj;
     p.inode = c->d_inode;
@@ -128,11 +180,36 @@ void fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t
     p.nranks = tile ? tile->nranks : 1;
     p.rank = tile ? tile->rank : 0;
     const int32_t nbands = (c->h + kTileH - 1) / kTileH;
-    p.tiles_x = (c->w + kTileW - 1) / kTileW;
+    p.tile_w = (mode == RT_MODE_KD && effective_kernel(c) != 1) ? kTileWKd : kTileWFlat;
+    p.tiles_x = (c->w + p.tile_w - 1) / p.tile_w;
     p.slots = (nbands + p.nranks - 1) / p.nranks;
     p.root_ref = s->root_ref;
     p.ntri = s->ntri;
     p.max_depth = kMaxDepth;
+    p.tile_order = c->tile_order;
+    p.order = nullptr;
+    p.debug = c->debug;
+    p.pool_cap = c->pool_cap;
+    p.dbg = nullptr;
+    if (c->debug & 2) {
+        const int64_t need = (int64_t)p.tiles_x * p.slots * (p.tile_w / 8) * 3;
+        if (c->dbg_cap < need) {
+            dev_free(c->d_dbg);
+            int rc = dev_alloc(&c->d_dbg, (size_t)need, "hipMalloc(dbg)");
+            if (rc) return rc;
+            c->dbg_cap = need;
+        }
+        p.dbg = c->d_dbg;
+        int rc = hip_check(hipMemset(c->d_dbg, 0, sizeof(uint64_t) * (size_t)need), "memset dbg");
+        if (rc) return rc;
+    }
+    camera_relative_box(s->root, c->pos, p.root_box);
+    if (c->tile_order == 2) {
+        int rc = ensure_order(c, p.tile_w, p.tiles_x, p.slots, p.nranks, p.rank);
+        if (rc) return rc;
+        p.order = c->d_order;
+    }
+    return RT_OK;
 }
 
 int check_tile(const rt_tile* tile) {
@@ -151,7 +228,7 @@ extern "C" int rt_device_count(int* count) {
 extern "C" int rt_scene_create(int device, const float* points9, const float* rad3, uint32_t ntri,
                                rt_scene** out) {
     if (!out || (ntri && (!points9 || !rad3))) return fail(RT_ERR_INVALID, "rt_scene_create: null argument");
-    if (ntri >= kLeafBit) return fail(RT_ERR_INVALID, "rt_scene_create: too many triangles");
+    if (ntri > kRefMask) return fail(RT_ERR_INVALID, "rt_scene_create: more than 2^29 triangles");
     *out = nullptr;
     DeviceGuard g(device);
     if (!g.ok) return fail(RT_ERR_HIP, "rt_scene_create: hipSetDevice(%d) failed", device);
@@ -230,6 +307,7 @@ extern "C" int rt_scene_set_kd(rt_scene* s, const rt_kd_node* nodes, uint64_t nn
         return rc;
     }
     s->nnode = n;
+    s->root = nodes[0];
     s->ninterior = ninterior;
     s->root_ref = ref[0];
     s->height = height;
@@ -294,8 +372,8 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
         return fail(RT_ERR_STATE, "rt_render: KD mode needs rt_scene_set_kd (Trixel::create_kd) first");
     if (c->obj->ntri == 0) return fail(RT_ERR_STATE, "rt_render: empty scene");
     TraceParams p;
-    fill_params(c, xform, tile, argb, hit, p);
-    return launch_trace(p, mode, flags, stream);
+    if ((rc = fill_params(c, xform, tile, argb, hit, mode, p))) return rc;
+    return launch_trace(p, mode, flags, effective_kernel(c), stream);
 }
 
 extern "C" int rt_render(rt_camera* c, const float* xform, uint32_t mode, uint32_t flags, const rt_tile* tile,
@@ -384,5 +462,53 @@ extern "C" void rt_camera_destroy(rt_camera* c) {
     dev_free(c->d_err);
     dev_free(c->d_trec);
     dev_free(c->d_inode);
+    dev_free(c->d_order);
+    dev_free(c->d_dbg);
     delete c;
+}
+
+extern "C" int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value) {
+    if (!c) return fail(RT_ERR_INVALID, "rt_camera_set_option: null camera");
+    switch (key) {
+    case kOptKernel:
+        if (value < 1 || value > 3) return fail(RT_ERR_INVALID, "kernel version %d", value);
+        c->kernel_version = value;
+        return RT_OK;
+    case kOptPoolCap:
+        // the 64 root items plus a DFS run of height <= 21 must fit
+        if (value < 64 + 22 || value > kPoolCapMax)
+            return fail(RT_ERR_INVALID, "pool cap %d (86..%d)", value, kPoolCapMax);
+        c->pool_cap = value;
+        return RT_OK;
+    case kOptDebug:
+        c->debug = value;
+        return RT_OK;
+    case kOptTileOrder:
+        if (value < 0 || value > 2) return fail(RT_ERR_INVALID, "tile order %d", value);
+        c->tile_order = value;
+        return RT_OK;
+    default:
+        return fail(RT_ERR_INVALID, "rt_camera_set_option: unknown key %d", key);
+    }
+}
+
+namespace rt {
+void camera_relative_box(const rt_kd_node& nd, const float pos[3], float b[6]) {
+    // init_cam_voxel_mem_cuda, TD/Camera.cu:142-147 (obj_center = 0); the
+    // same IEEE operations as the device-side rel_box
+    const float oc = 0.0f;
+    b[0] = nd.x0 - pos[0] + oc; b[1] = nd.x1 - pos[0] + oc;
+    b[2] = nd.y0 - pos[1] + oc; b[3] = nd.y1 - pos[1] + oc;
+    b[4] = nd.z0 - pos[2] + oc; b[5] = nd.z1 - pos[2] + oc;
+}
+}  // namespace rt
+
+extern "C" int64_t rt_camera_debug_read(rt_camera* c, uint64_t* out, int64_t n) {
+    if (!c || !out || !c->d_dbg) return fail(RT_ERR_STATE, "rt_camera_debug_read: no diagnostic buffer");
+    DeviceGuard g(c->device);
+    const int64_t m = std::min(n, c->dbg_cap);
+    if (hip_check(hipDeviceSynchronize(), "debug sync") ||
+        hip_check(hipMemcpy(out, c->d_dbg, sizeof(uint64_t) * (size_t)m, hipMemcpyDeviceToHost), "D2H dbg"))
+        return RT_ERR_HIP;
+    return m;
 }

@@ -22,11 +22,29 @@ constexpr uint32_t kLeafBit = 0x80000000u;
 // the maximum DFS occupancy of its balanced median tree; 24 covers 2^23 tris.
 constexpr int kMaxDepth = 24;
 
-// Threads per block for the per-pixel kernels: a 32x8 pixel tile, four
-// wave64s of 8x8 pixels each.
-constexpr int kTileW = 32;
+// Per-pixel kernels: a block is a tile_w x 8 pixel tile made of 8x8-pixel
+// wave64s (tile_w = 32 for the flat kernel, 16 for the KD kernel, whose LDS
+// stack is three words per entry).
 constexpr int kTileH = 8;
-constexpr int kBlock = kTileW * kTileH;
+constexpr int kTileWFlat = 32;
+constexpr int kTileWKd = 16;
+constexpr int kBlockMax = 256;
+
+// Interior record (64 B) of the v2 KD layout: the two children's
+// camera-relative boxes plus this node's split planes and child references.
+//   r0 = (L.t0x, L.t1x, L.t0y, L.t1y)   r1 = (L.t0z, L.t1z, R.t0x, R.t1x)
+//   r2 = (R.t0y, R.t1y, R.t0z, R.t1z)   r3 = (s1, s2, Lref | axis << 29, Rref)
+constexpr uint32_t kRefMask = 0x1FFFFFFFu;
+constexpr uint32_t kAxisShift = 29;
+
+// rt_camera_set_option keys.
+enum Option : int32_t {
+    kOptKernel = 1,     // KD kernel version: 1 (node-own box, 48 B) or 2 (child boxes, 64 B)
+    kOptTileOrder = 2,  // 0 XCD-contiguous, 1 natural, 2 centre-out
+    kOptDebug = 100,    // diagnostics: 1 = skip traversal, 2 = per-wave timestamps
+    kOptPoolCap = 101,  // tests: shrink kernel 3's item pool (66..kPoolCap) to force its fallback
+};
+constexpr int kPoolCapMax = 640;   // kernel 3 items per wave (peak measured <= 440, tools/pool_sim.c)
 
 // ---------------------------------------------------------------------------
 // Device layouts (all 16-byte aligned, read with dwordx4 loads).
@@ -60,6 +78,13 @@ struct TraceParams {
     int32_t w, h;
     int32_t nranks, rank;
     int32_t tiles_x, slots;        // grid = tiles_x * slots blocks
+    int32_t tile_w;                // pixels per block row (block = tile_w * 8 threads)
+    int32_t tile_order;            // Option kOptTileOrder
+    const int32_t* order;          // centre-out tile permutation (tile_order 2)
+    float root_box[6];             // camera-relative root AABB (t0x,t1x,t0y,t1y,t0z,t1z)
+    int32_t pool_cap;              // kernel 3 item-pool capacity in use (<= kPoolCap)
+    int32_t debug;                 // diagnostic builds only: 1 = skip traversal
+    unsigned long long* dbg;       // per-wave (t_start, t_end, visits) when non-null
     uint32_t root_ref;
     uint32_t ntri;
     int32_t max_depth;
@@ -75,8 +100,11 @@ int launch_cam_tri(const float4* tri_world, uint32_t ntri, const float pos[3],
                    float4* trec, void* stream);
 int launch_cam_nodes(const rt_kd_node* nodes, const int32_t* interior_ids,
                      const uint32_t* node_ref, int64_t ninterior, const float pos[3],
-                     float4* inode, void* stream);
-int launch_trace(const TraceParams& p, uint32_t mode, uint32_t flags, void* stream);
+                     float4* inode, int version, void* stream);
+int launch_trace(const TraceParams& p, uint32_t mode, uint32_t flags, int kernel_version,
+                 void* stream);
+// Camera-relative box of one world node, exactly as init_cam_voxel_mem_cuda.
+void camera_relative_box(const rt_kd_node& nd, const float pos[3], float out[6]);
 int launch_unpack(int32_t w, int32_t h, int32_t nranks, const uint32_t* gathered,
                   uint32_t* frame, void* stream);
 }  // namespace rt

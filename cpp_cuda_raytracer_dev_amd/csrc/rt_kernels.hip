@@ -87,16 +87,25 @@ __device__ uint32_t phong(const float pnt[3], const float nrm[3], const float rm
     return (to_u8((pr / mx) * 255) << 16) | (to_u8((pg / mx) * 255) << 8) | to_u8((pb / mx) * 255);
 }
 
-// Block -> (tile_x, slot), XCD-aware: blocks b and b+8 share an XCD, so give
-// each XCD a contiguous run of tiles (bijective for any grid size).
-__device__ __forceinline__ void tile_of_block(int32_t tiles_x, int32_t nblocks, int32_t& tx,
-                                              int32_t& slot) {
+// Block -> (tile_x, slot).  Order 0: blocks b and b+8 share an XCD, so give
+// each XCD a contiguous run of tiles (bijective for any grid size); order 1:
+// natural (neighbouring tiles on different XCDs); order 2: the host's
+// centre-out permutation, so the heavy centre tiles are dispatched first.
+__device__ __forceinline__ void tile_of_block(const TraceParams& P, int32_t& tx, int32_t& slot) {
     const int32_t b = (int32_t)blockIdx.x;
-    const int32_t q = nblocks >> 3, rem = nblocks & 7;
-    const int32_t xcd = b & 7, k = b >> 3;
-    const int32_t t = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + k;
-    slot = t / tiles_x;
-    tx = t - slot * tiles_x;
+    const int32_t nblocks = P.tiles_x * P.slots;
+    int32_t t;
+    if (P.tile_order == 0) {
+        const int32_t q = nblocks >> 3, rem = nblocks & 7;
+        const int32_t xcd = b & 7, k = b >> 3;
+        t = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + k;
+    } else if (P.tile_order == 2 && P.order) {
+        t = P.order[b];
+    } else {
+        t = b;
+    }
+    slot = t / P.tiles_x;
+    tx = t - slot * P.tiles_x;
 }
 
 struct Pixel {
@@ -106,11 +115,11 @@ struct Pixel {
 
 __device__ __forceinline__ bool pixel_of_thread(const TraceParams& P, Pixel& px) {
     int32_t tx, slot;
-    tile_of_block(P.tiles_x, P.tiles_x * P.slots, tx, slot);
+    tile_of_block(P, tx, slot);
     const int32_t lane = (int32_t)threadIdx.x & 63, wave = (int32_t)threadIdx.x >> 6;
     const int32_t band = P.rank + slot * P.nranks;
     const int32_t ly = lane >> 3;
-    px.x = tx * kTileW + wave * 8 + (lane & 7);
+    px.x = tx * P.tile_w + wave * 8 + (lane & 7);
     px.y = band * kTileH + ly;
     px.out = (int64_t)(slot * kTileH + ly) * P.w + px.x;
     return px.x < P.w && px.y < P.h;
@@ -128,11 +137,9 @@ __device__ __forceinline__ void primary_ray(const TraceParams& P, int32_t ix, in
 }
 
 __device__ __forceinline__ void wave_count_add(unsigned long long* dst, uint32_t v) {
-    // one atomic per wave: reduce with cross-lane shuffles first
-    unsigned long long s = v;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-    if (((int)threadIdx.x & 63) == 0 && s) atomicAdd(dst, s);
+    // counting builds only; the compiler's atomic optimizer folds the active
+    // lanes of a wave into one atomic (lanes of edge tiles may have exited)
+    if (v) atomicAdd(dst, (unsigned long long)v);
 }
 
 // ---------------------------------------------------------------- KD trace
@@ -140,7 +147,8 @@ __device__ __forceinline__ void wave_count_add(unsigned long long* dst, uint32_t
 // intersect_voxel_cuda (TD/Trixel.cu:41-172) fused with set_cam_cuda +
 // color_cam_cuda (TD/Camera.cu:12-69).
 template <bool kTranslated, bool kWriteHit, bool kCount>
-__global__ __launch_bounds__(kBlock) void k_trace_kd(TraceParams P) {
+__global__ __launch_bounds__(kTileWFlat * kTileH) void k_trace_kd(TraceParams P) {
+    constexpr int kBlock = kTileWFlat * kTileH;
     __shared__ uint32_t stack[kMaxDepth * kBlock];
     Pixel px;
     const bool live = pixel_of_thread(P, px);
@@ -280,6 +288,472 @@ __global__ __launch_bounds__(kBlock) void k_trace_kd(TraceParams P) {
     }
 }
 
+// ------------------------------------------------------------- KD trace v2
+
+// Issues the four dwordx4 loads of a 64-B record together and consumes them
+// before any branch, so a visit costs one memory round trip (left to itself
+// hipcc sinks the conditionally used loads into the branches: three
+// dependent round trips per visit).
+__device__ __forceinline__ void load_record(const float4* __restrict__ p, float4& r0, float4& r1,
+                                            float4& r2, float4& r3) {
+    r0 = p[0]; r1 = p[1]; r2 = p[2]; r3 = p[3];
+    asm volatile("" ::"v"(r0.x), "v"(r0.y), "v"(r0.z), "v"(r0.w), "v"(r1.x), "v"(r1.y), "v"(r1.z),
+                 "v"(r1.w), "v"(r2.x), "v"(r2.y), "v"(r2.z), "v"(r2.w), "v"(r3.x), "v"(r3.y), "v"(r3.z),
+                 "v"(r3.w));
+}
+
+struct Ray {
+    float rx, ry, rz;          // object-space direction, TD/Trixel.cu:64-66
+    float odx, ody, odz;       // object translation, TD/Trixel.cu:60-62
+    float ix, iy, iz;          // 1 / r
+    float ox, oy, oz;          // od / r
+    bool sx, sy, sz;           // r > 0
+};
+
+// Slab test of one node, TD/Trixel.cu:76-95,146: entry/exit parameters and
+// whether the reference descends into the node.
+__device__ __forceinline__ bool slab(const Ray& R, float lx, float hx, float ly, float hy, float lz,
+                                     float hz, float& maxt0, float& mint1) {
+    const float t0x = R.sx ? lx * R.ix : hx * R.ix;
+    const float t1x = R.sx ? hx * R.ix : lx * R.ix;
+    const float t0y = R.sy ? ly * R.iy : hy * R.iy;
+    const float t1y = R.sy ? hy * R.iy : ly * R.iy;
+    const float t0z = R.sz ? lz * R.iz : hz * R.iz;
+    const float t1z = R.sz ? hz * R.iz : lz * R.iz;
+    maxt0 = fmaxf(t0z + R.oz, fmaxf(t0x + R.ox, t0y + R.oy));
+    mint1 = fminf(t1z + R.oz, fminf(t1x + R.ox, t1y + R.oy));
+    return (double)mint1 >= (double)maxt0 - kEps && (double)maxt0 > -kEps;
+}
+
+// Moller-Trumbore at a leaf, TD/Trixel.cu:98-145; updates (d, best) on a
+// strictly nearer accepted hit.
+__device__ __forceinline__ bool leaf_test(const Ray& R, const float4* __restrict__ trec, uint32_t t,
+                                          float& d, uint32_t& best) {
+    const float4 A = trec[4 * (size_t)t];
+    const float4 B = trec[4 * (size_t)t + 1];
+    const float4 Cq = trec[4 * (size_t)t + 2];
+    const float e1x = A.x, e1y = A.y, e1z = A.z;
+    const float e2x = A.w, e2y = B.x, e2z = B.y;
+    const float dtx = B.z, dty = B.w, dtz = Cq.x;
+    float qpx, qpy, qpz;
+    cross3(qpx, qpy, qpz, R.rx, R.ry, R.rz, e2x, e2y, e2z);
+    const float f = dot3(qpx, qpy, qpz, e1x, e1y, e1z);
+    if (!(f < kEpsF && f > -kEpsF)) {
+        const float pe1 = 1.0f / f;   // == (float)(1.0 / (double)f)
+        const float tx = dtx - R.odx, ty = dty - R.ody, tz = dtz - R.odz;
+        const float u = pe1 * dot3(qpx, qpy, qpz, tx, ty, tz);
+        float qx, qy, qz;
+        cross3(qx, qy, qz, tx, ty, tz, e1x, e1y, e1z);
+        const float v = pe1 * dot3(R.rx, R.ry, R.rz, qx, qy, qz);
+        const float w = pe1 * dot3(e2x, e2y, e2z, qx, qy, qz);
+        // (u+v) > 1 + 1e-16 is (u+v) > 1.0 in double
+        if ((w < d) && !((u < kEpsF) || (v < kEpsF) || ((u + v) > 1.0f) || (w < kEpsF))) {
+            d = w;
+            best = t;
+            return true;
+        }
+    }
+    return false;
+}
+
+// intersect_voxel_cuda (TD/Trixel.cu:41-172) fused with set_cam_cuda +
+// color_cam_cuda (TD/Camera.cu:12-69), v2 layout.  A node's record carries its
+// children's boxes, so a child's slab test runs when the parent decides to
+// push it: children that the reference would pop and reject are never
+// fetched, the deferred sibling keeps its (maxt0, mint1) in LDS, and every
+// effectful visit happens in the reference's DFS order.
+template <bool kTranslated, bool kWriteHit, bool kCount>
+__global__ __launch_bounds__(kTileWKd * kTileH) void k_trace_kd2(TraceParams P) {
+    constexpr int kB = kTileWKd * kTileH;
+    __shared__ uint32_t s_ref[kMaxDepth * kB];
+    __shared__ float s_t0[kMaxDepth * kB];
+    __shared__ float s_t1[kMaxDepth * kB];
+    Pixel px;
+    if (!pixel_of_thread(P, px)) return;  // no barriers in this kernel
+    const unsigned long long t_start = P.dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
+
+    float cam[3];
+    primary_ray(P, px.x, px.y, cam);
+    const float* X = P.xf;
+    Ray R;
+    R.odx = X[3]; R.ody = X[7]; R.odz = X[11];
+    R.rx = -1 * (X[0] * -cam[0] + X[1] * -cam[1] + X[2] * -cam[2]);
+    R.ry = -1 * (X[4] * -cam[0] + X[5] * -cam[1] + X[6] * -cam[2]);
+    R.rz = -1 * (X[8] * -cam[0] + X[9] * -cam[1] + X[10] * -cam[2]);
+    R.ix = 1 / R.rx; R.iy = 1 / R.ry; R.iz = 1 / R.rz;
+    R.ox = R.odx / R.rx; R.oy = R.ody / R.ry; R.oz = R.odz / R.rz;
+    R.sx = R.rx > 0; R.sy = R.ry > 0; R.sz = R.rz > 0;
+    // dir and ds for each one-hot cut axis (TD/Trixel.cu:88-90)
+    const float dir_a[3] = {(R.rx * 1.0f) + (R.ry * 0.0f) + (R.rz * 0.0f),
+                            (R.rx * 0.0f) + (R.ry * 1.0f) + (R.rz * 0.0f),
+                            (R.rx * 0.0f) + (R.ry * 0.0f) + (R.rz * 1.0f)};
+    const float ds_a[3] = {(R.odx * 1.0f) + (R.ody * 0.0f) + (R.odz * 0.0f),
+                           (R.odx * 0.0f) + (R.ody * 1.0f) + (R.odz * 0.0f),
+                           (R.odx * 0.0f) + (R.ody * 0.0f) + (R.odz * 1.0f)};
+
+    float d = kDrawDistance;
+    uint32_t best = kMiss;
+    uint32_t n_int = 0, n_leaf = 0, n_acc = 0, n_desc = 0;
+    const int lane_col = (int)threadIdx.x;
+    int sp = 0;
+    uint32_t ref = P.root_ref;
+    float cmax = 0.0f, cmin = 0.0f;
+    bool have = true;
+    if (!(ref & kLeafBit)) {
+        if (kCount) n_int++;
+        have = slab(R, P.root_box[0], P.root_box[1], P.root_box[2], P.root_box[3], P.root_box[4],
+                    P.root_box[5], cmax, cmin);
+        if (kCount && have) n_desc++;
+    }
+    if (P.debug & 1) have = false;
+    uint32_t n_visit = 0;
+    while (have) {
+        if (P.dbg) n_visit++;
+        if (ref & kLeafBit) {
+            if (kCount) n_leaf++;
+            const bool acc = leaf_test(R, P.trec, ref & ~kLeafBit, d, best);
+            if (kCount && acc) n_acc++;
+        } else {
+            float4 r0, r1, r2, r3;
+            load_record(P.inode + 4 * (size_t)ref, r0, r1, r2, r3);
+            const uint32_t lw = __float_as_uint(r3.z);
+            const uint32_t axis = (lw >> kAxisShift) & 3u;
+            const uint32_t L = lw & ~(3u << kAxisShift), Rr = __float_as_uint(r3.w);
+            const float dir = axis == 0 ? dir_a[0] : axis == 1 ? dir_a[1] : dir_a[2];
+            const float mx = cmax * dir, mn = cmin * dir;
+            float s1, s2;
+            if (kTranslated) {
+                const float ds = axis == 0 ? ds_a[0] : axis == 1 ? ds_a[1] : ds_a[2];
+                s1 = (float)((double)r3.x + kEps + (double)ds);
+                s2 = r3.y + ds;
+            } else {  // ds == 0: the same values without the +0
+                s1 = (float)((double)r3.x + kEps);
+                s2 = r3.y;
+            }
+            // Push order of TD/Trixel.cu:155-168.  `first` is popped next,
+            // `second` (if pushed) after first's subtree.
+            bool left_first, push_second;
+            if ((double)mx < (double)s2 + kEps) {
+                left_first = true;
+                push_second = (double)mn > (double)s2 - kEps;
+            } else {
+                left_first = false;
+                push_second = (mn < s1 || mx < s1);
+            }
+            const uint32_t first = left_first ? L : Rr;
+            const uint32_t second = left_first ? Rr : L;
+            // slab tests of the children that would be popped (boxes in r0..r2)
+            float f0 = 0.0f, f1 = 0.0f, g0 = 0.0f, g1 = 0.0f;
+            bool keep_first = true, keep_second = push_second;
+            if (!(first & kLeafBit)) {
+                if (kCount) n_int++;
+                keep_first = left_first ? slab(R, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, f0, f1)
+                                        : slab(R, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w, f0, f1);
+                if (kCount && keep_first) n_desc++;
+            }
+            if (push_second && !(second & kLeafBit)) {
+                if (kCount) n_int++;
+                keep_second = left_first ? slab(R, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w, g0, g1)
+                                         : slab(R, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, g0, g1);
+                if (kCount && keep_second) n_desc++;
+            }
+            if (keep_first) {
+                if (keep_second) {
+                    if (sp >= P.max_depth) { atomicOr(P.err, 1); break; }
+                    const int k = sp * kB + lane_col;
+                    s_ref[k] = second; s_t0[k] = g0; s_t1[k] = g1;
+                    sp++;
+                }
+                ref = first; cmax = f0; cmin = f1;
+                continue;
+            }
+            if (keep_second) {
+                ref = second; cmax = g0; cmin = g1;
+                continue;
+            }
+        }
+        if (sp == 0) break;
+        sp--;
+        const int k = sp * kB + lane_col;
+        ref = s_ref[k]; cmax = s_t0[k]; cmin = s_t1[k];
+    }
+
+    uint32_t argb = kBackground;
+    if (best != kMiss) {
+        // nearest-hit writes of TD/Trixel.cu:128-140, done once for the final hit
+        const float4 N = P.shade[2 * (size_t)best];
+        const float4 M = P.shade[2 * (size_t)best + 1];
+        const float pnt[3] = {d * R.rx + R.odx, d * R.ry + R.ody, d * R.rz + R.odz};
+        // norm.device_rotate(rot_m, i, -1), TD/vector.cuh:23-33
+        const float ax = -1 * N.x, ay = -1 * N.y, az = -1 * N.z;
+        const float nrm[3] = {(ax * X[0] + ay * X[1] + az * X[2]) * -1,
+                              (ax * X[4] + ay * X[5] + az * X[6]) * -1,
+                              (ax * X[8] + ay * X[9] + az * X[10]) * -1};
+        const float rad[3] = {M.x, M.y, M.z};
+        argb = phong(pnt, nrm, cam, rad);
+    }
+    P.argb[px.out] = argb;
+    if (kWriteHit) P.hit[px.out] = best == kMiss ? (int64_t)-1 : (int64_t)best;
+    if (kCount) {
+        wave_count_add(&P.counters[0], n_int);
+        wave_count_add(&P.counters[1], n_leaf);
+        wave_count_add(&P.counters[2], n_acc);
+        wave_count_add(&P.counters[3], best != kMiss ? 1u : 0u);
+        wave_count_add(&P.counters[4], n_desc);
+    }
+    if (P.dbg) {  // diagnostic build: wave start/end clock and its max visits
+        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+        const size_t wv = (size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+        atomicMax(&P.dbg[3 * wv + 2], (unsigned long long)n_visit);
+        if (((int)threadIdx.x & 63) == __builtin_amdgcn_readfirstlane((int)threadIdx.x & 63)) {
+            P.dbg[3 * wv] = t_start;
+            P.dbg[3 * wv + 1] = t_end;
+        }
+    }
+}
+
+// ------------------------------------------------------------- KD trace v3
+
+// Wave-cooperative traversal.  With no early termination the SET of nodes a
+// ray visits does not depend on the order of the visits, and the reference's
+// result is the accepted candidate with the smallest w, ties going to the one
+// its DFS visits first (strict `w < d`, TD/Trixel.cu:127).  So a wave pools
+// the (ray, node) work items of its 64 rays in one LDS stack and every lane
+// takes an item per iteration, whatever ray it belongs to: the wave runs
+// ~sum(visits)/64 iterations instead of max(visits).  Each item carries its
+// DFS path code (bit = "second child popped" at each level, left aligned), so
+// the lexicographic minimum of (w, code) -- one 64-bit LDS atomic min per
+// candidate -- is exactly the reference's winner.
+constexpr int kPoolCap = kPoolCapMax;
+constexpr int kCodeBits = 21;         // path code bits: trees of height <= 21
+constexpr uint32_t kCodeMask = (1u << kCodeBits) - 1;
+
+struct Item {
+    uint32_t ref;      // node ref (kLeafBit | tri, or interior index)
+    float t0, t1;      // the node's (maxt0, mint1) for interior refs
+    uint32_t meta;     // ray << 26 | depth << 21 | code
+};
+
+template <bool kTranslated, bool kWriteHit, bool kCount>
+__global__ __launch_bounds__(kTileWKd * kTileH) void k_trace_kd3(TraceParams P) {
+    constexpr int kWaves = kTileWKd * kTileH / 64;
+    __shared__ uint4 s_items[kWaves][kPoolCap];
+    __shared__ float4 s_ray[kWaves][64][5];
+    __shared__ unsigned long long s_key[kWaves][64];
+    __shared__ uint32_t s_tri[kWaves][64];
+    const int wv = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
+    uint4* items = s_items[wv];
+    Pixel px;
+    const bool live = pixel_of_thread(P, px);  // every lane stays for the ballots
+    const unsigned long long t_start = P.dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    uint32_t iters = 0;
+
+    float cam[3] = {0.0f, 0.0f, 1.0f};
+    if (live) primary_ray(P, px.x, px.y, cam);
+    const float* X = P.xf;
+    Ray R;
+    R.odx = X[3]; R.ody = X[7]; R.odz = X[11];
+    R.rx = -1 * (X[0] * -cam[0] + X[1] * -cam[1] + X[2] * -cam[2]);
+    R.ry = -1 * (X[4] * -cam[0] + X[5] * -cam[1] + X[6] * -cam[2]);
+    R.rz = -1 * (X[8] * -cam[0] + X[9] * -cam[1] + X[10] * -cam[2]);
+    R.ix = 1 / R.rx; R.iy = 1 / R.ry; R.iz = 1 / R.rz;
+    R.ox = R.odx / R.rx; R.oy = R.ody / R.ry; R.oz = R.odz / R.rz;
+    R.sx = R.rx > 0; R.sy = R.ry > 0; R.sz = R.rz > 0;
+    {
+        // dir and ds for each one-hot cut axis (TD/Trixel.cu:88-90)
+        const float d0 = (R.rx * 1.0f) + (R.ry * 0.0f) + (R.rz * 0.0f);
+        const float d1 = (R.rx * 0.0f) + (R.ry * 1.0f) + (R.rz * 0.0f);
+        const float d2 = (R.rx * 0.0f) + (R.ry * 0.0f) + (R.rz * 1.0f);
+        const float e0 = (R.odx * 1.0f) + (R.ody * 0.0f) + (R.odz * 0.0f);
+        const float e1 = (R.odx * 0.0f) + (R.ody * 1.0f) + (R.odz * 0.0f);
+        const float e2 = (R.odx * 0.0f) + (R.ody * 0.0f) + (R.odz * 1.0f);
+        float4* rd = s_ray[wv][lane];
+        rd[0] = make_float4(R.rx, R.ry, R.rz, R.ix);
+        rd[1] = make_float4(R.iy, R.iz, R.ox, R.oy);
+        rd[2] = make_float4(R.oz, R.odx, R.ody, R.odz);
+        rd[3] = make_float4(d0, d1, d2, e0);
+        rd[4] = make_float4(e1, e2, 0.0f, 0.0f);
+    }
+    s_key[wv][lane] = ~0ull;
+    s_tri[wv][lane] = kMiss;
+
+    uint32_t n_int = 0, n_leaf = 0, n_acc = 0, n_desc = 0;
+    // the root item of every live ray whose root test passes (or a leaf root)
+    bool has = false;
+    float r0t0 = 0.0f, r0t1 = 0.0f;
+    if (live) {
+        if (P.root_ref & kLeafBit) {
+            has = true;
+        } else {
+            if (kCount) n_int++;
+            has = slab(R, P.root_box[0], P.root_box[1], P.root_box[2], P.root_box[3], P.root_box[4],
+                       P.root_box[5], r0t0, r0t1);
+            if (kCount && has) n_desc++;
+        }
+    }
+    if (P.debug & 1) has = false;
+    {
+        const unsigned long long b = __ballot(has);
+        const uint32_t off = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+        if (has) items[off] = make_uint4(P.root_ref, __float_as_uint(r0t0), __float_as_uint(r0t1), (uint32_t)lane << 26);
+    }
+    int n = __builtin_popcountll(__ballot(has));
+    const int cap = min(P.pool_cap, kPoolCap);
+    __builtin_amdgcn_wave_barrier();
+
+    while (n > 0) {
+        // Parallel pops while the pool has room for all their children plus
+        // the DFS slack below; single (DFS-like) pops otherwise.  A run of
+        // single pops starting at n0 never holds more than n0 + height items
+        // (height <= 21), and parallel pops leave n <= cap - 22, so the pool
+        // never overflows.
+        const int take = (n + 64 + kCodeBits + 1 <= cap) ? min(n, 64) : 1;
+        iters++;
+        const int base = n - take;
+        const bool act = lane < take;
+        uint4 it = make_uint4(0, 0, 0, 0);
+        if (act) it = items[base + lane];
+        __builtin_amdgcn_wave_barrier();
+        int nk = 0;
+        uint4 c0 = make_uint4(0, 0, 0, 0), c1 = make_uint4(0, 0, 0, 0);
+        bool cand = false;
+        unsigned long long key = 0;
+        uint32_t ray = 0, ctri = 0;
+        if (act) {
+            ray = it.w >> 26;
+            const uint32_t depth = (it.w >> kCodeBits) & 31u, code = it.w & kCodeMask;
+            const float4* rd = s_ray[wv][ray];
+            const float4 q0 = rd[0], q1 = rd[1], q2 = rd[2], q3 = rd[3], q4 = rd[4];
+            Ray Q;
+            Q.rx = q0.x; Q.ry = q0.y; Q.rz = q0.z; Q.ix = q0.w;
+            Q.iy = q1.x; Q.iz = q1.y; Q.ox = q1.z; Q.oy = q1.w;
+            Q.oz = q2.x; Q.odx = q2.y; Q.ody = q2.z; Q.odz = q2.w;
+            Q.sx = Q.rx > 0; Q.sy = Q.ry > 0; Q.sz = Q.rz > 0;
+            if (it.x & kLeafBit) {
+                if (kCount) n_leaf++;
+                float d = kDrawDistance;
+                uint32_t best = kMiss;
+                if (leaf_test(Q, P.trec, it.x & ~kLeafBit, d, best)) {
+                    cand = true;
+                    ctri = best;
+                    key = ((unsigned long long)__float_as_uint(d) << 32) | code;
+                    if (kCount) n_acc++;
+                }
+            } else {
+                float4 r0, r1, r2, r3;
+                load_record(P.inode + 4 * (size_t)it.x, r0, r1, r2, r3);
+                const uint32_t lw = __float_as_uint(r3.z);
+                const uint32_t axis = (lw >> kAxisShift) & 3u;
+                const uint32_t L = lw & ~(3u << kAxisShift), Rr = __float_as_uint(r3.w);
+                const float dir = axis == 0 ? q3.x : axis == 1 ? q3.y : q3.z;
+                const float mx = __uint_as_float(it.y) * dir, mn = __uint_as_float(it.z) * dir;
+                float s1, s2;
+                if (kTranslated) {
+                    const float ds = axis == 0 ? q3.w : axis == 1 ? q4.x : q4.y;
+                    s1 = (float)((double)r3.x + kEps + (double)ds);
+                    s2 = r3.y + ds;
+                } else {
+                    s1 = (float)((double)r3.x + kEps);
+                    s2 = r3.y;
+                }
+                bool left_first, push_second;
+                if ((double)mx < (double)s2 + kEps) {
+                    left_first = true;
+                    push_second = (double)mn > (double)s2 - kEps;
+                } else {
+                    left_first = false;
+                    push_second = (mn < s1 || mx < s1);
+                }
+                const uint32_t first = left_first ? L : Rr;
+                const uint32_t second = left_first ? Rr : L;
+                // children's slab tests from the boxes in this record
+                float lt0, lt1, rt0, rt1;
+                const bool lpass = slab(Q, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, lt0, lt1);
+                const bool rpass = slab(Q, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w, rt0, rt1);
+                const bool first_leaf = (first & kLeafBit) != 0, second_leaf = (second & kLeafBit) != 0;
+                const bool keep_first = first_leaf || (left_first ? lpass : rpass);
+                const bool keep_second = push_second && (second_leaf || (left_first ? rpass : lpass));
+                if (kCount) {
+                    n_int += (first_leaf ? 0u : 1u) + ((push_second && !second_leaf) ? 1u : 0u);
+                    n_desc += ((!first_leaf && keep_first) ? 1u : 0u) + ((push_second && !second_leaf && keep_second) ? 1u : 0u);
+                }
+                const uint32_t cd = depth + 1;
+                const uint32_t bit = 1u << (kCodeBits - cd);
+                const uint32_t meta_first = (ray << 26) | (cd << kCodeBits) | code;
+                const uint32_t meta_second = meta_first | bit;
+                const float f0 = left_first ? lt0 : rt0, f1 = left_first ? lt1 : rt1;
+                const float g0 = left_first ? rt0 : lt0, g1 = left_first ? rt1 : lt1;
+                const uint4 A = make_uint4(first, __float_as_uint(f0), __float_as_uint(f1), meta_first);
+                const uint4 B = make_uint4(second, __float_as_uint(g0), __float_as_uint(g1), meta_second);
+                if (keep_first) {
+                    c0 = A;
+                    nk = 1;
+                    if (keep_second) { c1 = B; nk = 2; }
+                } else if (keep_second) {
+                    c0 = B;
+                    nk = 1;
+                }
+            }
+        }
+        // nearest candidate per ray: 64-bit min of (w, path code), then the
+        // unique lane holding the minimum records its triangle
+        if (cand) atomicMin(&s_key[wv][ray], key);
+        __builtin_amdgcn_wave_barrier();
+        if (cand && s_key[wv][ray] == key) s_tri[wv][ray] = ctri;
+        // push the children: ballot compaction onto the pool
+        const unsigned long long b1 = __ballot(nk >= 1), b2 = __ballot(nk == 2);
+        const uint32_t off = __builtin_amdgcn_mbcnt_hi((uint32_t)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b1, 0u)) +
+                             __builtin_amdgcn_mbcnt_hi((uint32_t)(b2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b2, 0u));
+        const int total = __builtin_popcountll(b1) + __builtin_popcountll(b2);
+        if (base + total > cap) {  // unreachable by the pop rule above; guard anyway
+            if (lane == 0) atomicOr(P.err, 2);
+            break;
+        }
+        if (nk >= 1) items[base + off] = c0;
+        if (nk == 2) items[base + off + 1] = c1;
+        n = base + total;
+        __builtin_amdgcn_wave_barrier();
+    }
+
+    if (kCount) {
+        // every lane (also those past the frame edge) processed pool items;
+        // counter [2] counts valid candidates here (>= the DFS's accept events)
+        wave_count_add(&P.counters[0], n_int);
+        wave_count_add(&P.counters[1], n_leaf);
+        wave_count_add(&P.counters[2], n_acc);
+        wave_count_add(&P.counters[4], n_desc);
+    }
+    if (P.dbg) {  // diagnostic build: wave start/end clock and its pool iterations
+        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+        const size_t wvg = (size_t)blockIdx.x * (blockDim.x >> 6) + wv;
+        if (lane == 0) {
+            P.dbg[3 * wvg] = t_start;
+            P.dbg[3 * wvg + 1] = t_end;
+            P.dbg[3 * wvg + 2] = iters;
+        }
+    }
+    if (!live) return;
+    uint32_t argb = kBackground;
+    const unsigned long long kbest = s_key[wv][lane];
+    const uint32_t best = kbest == ~0ull ? kMiss : s_tri[wv][lane];
+    if (best != kMiss) {
+        const float d = __uint_as_float((uint32_t)(kbest >> 32));
+        const float4 N = P.shade[2 * (size_t)best];
+        const float4 M = P.shade[2 * (size_t)best + 1];
+        const float pnt[3] = {d * R.rx + R.odx, d * R.ry + R.ody, d * R.rz + R.odz};
+        // norm.device_rotate(rot_m, i, -1), TD/vector.cuh:23-33
+        const float ax = -1 * N.x, ay = -1 * N.y, az = -1 * N.z;
+        const float nrm[3] = {(ax * X[0] + ay * X[1] + az * X[2]) * -1,
+                              (ax * X[4] + ay * X[5] + az * X[6]) * -1,
+                              (ax * X[8] + ay * X[9] + az * X[10]) * -1};
+        const float rad[3] = {M.x, M.y, M.z};
+        argb = phong(pnt, nrm, cam, rad);
+    }
+    P.argb[px.out] = argb;
+    if (kWriteHit) P.hit[px.out] = best == kMiss ? (int64_t)-1 : (int64_t)best;
+    if (kCount) wave_count_add(&P.counters[3], best != kMiss ? 1u : 0u);
+}
+
 // -------------------------------------------------------------- flat trace
 
 // intersect_trixel_cuda (TD/Trixel.cu:173-209) fused with the shading.  The
@@ -287,7 +761,7 @@ __global__ __launch_bounds__(kBlock) void k_trace_kd(TraceParams P) {
 // scalar data cache into SGPRs; the exact sign tests below skip the division
 // for the (common) rays that cannot pass u >= eps, v >= eps or w >= eps.
 template <bool kWriteHit, bool kCount>
-__global__ __launch_bounds__(kBlock) void k_trace_flat(TraceParams P) {
+__global__ __launch_bounds__(kTileWFlat * kTileH) void k_trace_flat(TraceParams P) {
     Pixel px;
     if (!pixel_of_thread(P, px)) return;
     float rmd[3];
@@ -383,30 +857,58 @@ __global__ void k_cam_tri(const float4* __restrict__ tw, uint32_t ntri, float cx
     trec[4 * (size_t)i + 3] = make_float4(dw, 0.0f, 0.0f, 0.0f);
 }
 
-// init_cam_voxel_mem_cuda, TD/Camera.cu:137-162, into the dense interior
-// record layout (rt_internal.h).  obj_center is 0 (TD/Camera.cpp:167-170).
-__global__ void k_cam_nodes(const rt_kd_node* __restrict__ nodes, const int32_t* __restrict__ ids,
-                            const uint32_t* __restrict__ node_ref, int64_t ninterior, float cx,
-                            float cy, float cz, float4* __restrict__ out) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= ninterior) return;
-    const rt_kd_node nd = nodes[ids[k]];
+// Camera-relative box of a world node, init_cam_voxel_mem_cuda
+// (TD/Camera.cu:142-147); obj_center is 0 (TD/Camera.cpp:167-170).
+__device__ __forceinline__ void rel_box(const rt_kd_node& nd, float cx, float cy, float cz, float b[6]) {
+    const float oc = 0.0f;
+    b[0] = nd.x0 - cx + oc; b[1] = nd.x1 - cx + oc;
+    b[2] = nd.y0 - cy + oc; b[3] = nd.y1 - cy + oc;
+    b[4] = nd.z0 - cz + oc; b[5] = nd.z1 - cz + oc;
+}
+
+// Split planes minus the camera on the cut axis, TD/Camera.cu:155-160 (the
+// reference's obj_center.x typo on the z term of s2 is kept; it is 0).
+__device__ __forceinline__ void rel_split(const rt_kd_node& nd, float cx, float cy, float cz, float& s1,
+                                          float& s2, uint32_t& axis) {
     const float ocx = 0.0f, ocy = 0.0f, ocz = 0.0f;
-    const float t0x = nd.x0 - cx + ocx, t1x = nd.x1 - cx + ocx;
-    const float t0y = nd.y0 - cy + ocy, t1y = nd.y1 - cy + ocy;
-    const float t0z = nd.z0 - cz + ocz, t1z = nd.z1 - cz + ocz;
     const int cd = nd.cut_flag;
     const float fx = (cd == 0 || cd == 3) ? 1.0f : 0.0f;
     const float fy = (cd == 1 || cd == 4) ? 1.0f : 0.0f;
     const float fz = (cd == 2 || cd == 5) ? 1.0f : 0.0f;
-    const float s1 = nd.s1 - (((cx + ocx) * fx) + ((cy + ocy) * fy) + ((cz + ocz) * fz));
-    const float s2 = nd.s2 - (((cx + ocx) * fx) + ((cy + ocy) * fy) + ((cz + ocx) * fz));
-    const float s1e = (float)((double)s1 + kEps);
-    const uint32_t axis = fx != 0.0f ? 0u : fy != 0.0f ? 1u : 2u;
-    out[3 * k] = make_float4(t0x, t1x, t0y, t1y);
-    out[3 * k + 1] = make_float4(t0z, t1z, s1, s2);
-    out[3 * k + 2] = make_float4(__uint_as_float(node_ref[nd.left]), __uint_as_float(node_ref[nd.right]),
-                                 __uint_as_float(axis), s1e);
+    s1 = nd.s1 - (((cx + ocx) * fx) + ((cy + ocy) * fy) + ((cz + ocz) * fz));
+    s2 = nd.s2 - (((cx + ocx) * fx) + ((cy + ocy) * fy) + ((cz + ocx) * fz));
+    axis = fx != 0.0f ? 0u : fy != 0.0f ? 1u : 2u;
+}
+
+// init_cam_voxel_mem_cuda (TD/Camera.cu:137-162) into the dense interior
+// record layouts of rt_internal.h (v1: own box, 48 B; v2: children's boxes, 64 B).
+__global__ void k_cam_nodes(const rt_kd_node* __restrict__ nodes, const int32_t* __restrict__ ids,
+                            const uint32_t* __restrict__ node_ref, int64_t ninterior, float cx,
+                            float cy, float cz, float4* __restrict__ out, int version) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= ninterior) return;
+    const rt_kd_node nd = nodes[ids[k]];
+    float s1, s2;
+    uint32_t axis;
+    rel_split(nd, cx, cy, cz, s1, s2, axis);
+    if (version == 1) {
+        float b[6];
+        rel_box(nd, cx, cy, cz, b);
+        const float s1e = (float)((double)s1 + kEps);
+        out[3 * k] = make_float4(b[0], b[1], b[2], b[3]);
+        out[3 * k + 1] = make_float4(b[4], b[5], s1, s2);
+        out[3 * k + 2] = make_float4(__uint_as_float(node_ref[nd.left]), __uint_as_float(node_ref[nd.right]),
+                                     __uint_as_float(axis), s1e);
+        return;
+    }
+    float lb[6], rb[6];
+    rel_box(nodes[nd.left], cx, cy, cz, lb);
+    rel_box(nodes[nd.right], cx, cy, cz, rb);
+    out[4 * k] = make_float4(lb[0], lb[1], lb[2], lb[3]);
+    out[4 * k + 1] = make_float4(lb[4], lb[5], rb[0], rb[1]);
+    out[4 * k + 2] = make_float4(rb[2], rb[3], rb[4], rb[5]);
+    out[4 * k + 3] = make_float4(s1, s2, __uint_as_float(node_ref[nd.left] | (axis << kAxisShift)),
+                                 __uint_as_float(node_ref[nd.right]));
 }
 
 // Rank 0's frame assembly after the gather: [rank][slot][8 rows][w] -> frame.
@@ -444,38 +946,48 @@ int launch_cam_tri(const float4* tri_world, uint32_t ntri, const float pos[3], f
 }
 
 int launch_cam_nodes(const rt_kd_node* nodes, const int32_t* ids, const uint32_t* node_ref,
-                     int64_t ninterior, const float pos[3], float4* inode, void* stream) {
+                     int64_t ninterior, const float pos[3], float4* inode, int version, void* stream) {
     if (ninterior == 0) return RT_OK;
     k_cam_nodes<<<(unsigned)((ninterior + 255) / 256), 256, 0, (hipStream_t)stream>>>(
-        nodes, ids, node_ref, ninterior, pos[0], pos[1], pos[2], inode);
+        nodes, ids, node_ref, ninterior, pos[0], pos[1], pos[2], inode, version);
     return check_launch<void>("k_cam_nodes");
 }
 
-int launch_trace(const TraceParams& p, uint32_t mode, uint32_t flags, void* stream) {
+int launch_trace(const TraceParams& p, uint32_t mode, uint32_t flags, int kernel_version, void* stream) {
     const unsigned grid = (unsigned)(p.tiles_x * p.slots);
     if (grid == 0) return RT_OK;
     hipStream_t s = (hipStream_t)stream;
     const bool wh = (flags & RT_FLAG_WRITE_HIT) != 0, cnt = (flags & RT_FLAG_COUNT) != 0;
+    const unsigned threads = (unsigned)(p.tile_w * kTileH);
     if (mode == RT_MODE_FLAT) {
-        if (wh && cnt) k_trace_flat<true, true><<<grid, kBlock, 0, s>>>(p);
-        else if (wh) k_trace_flat<true, false><<<grid, kBlock, 0, s>>>(p);
-        else if (cnt) k_trace_flat<false, true><<<grid, kBlock, 0, s>>>(p);
-        else k_trace_flat<false, false><<<grid, kBlock, 0, s>>>(p);
+        if (wh && cnt) k_trace_flat<true, true><<<grid, threads, 0, s>>>(p);
+        else if (wh) k_trace_flat<true, false><<<grid, threads, 0, s>>>(p);
+        else if (cnt) k_trace_flat<false, true><<<grid, threads, 0, s>>>(p);
+        else k_trace_flat<false, false><<<grid, threads, 0, s>>>(p);
         return check_launch<void>("k_trace_flat");
     }
     const bool tr = p.xf[3] != 0.0f || p.xf[7] != 0.0f || p.xf[11] != 0.0f;
-#define RT_KD(T, H, C) k_trace_kd<T, H, C><<<grid, kBlock, 0, s>>>(p)
-    if (tr) {
-        if (wh && cnt) RT_KD(true, true, true);
-        else if (wh) RT_KD(true, true, false);
-        else if (cnt) RT_KD(true, false, true);
-        else RT_KD(true, false, false);
-    } else {
-        if (wh && cnt) RT_KD(false, true, true);
-        else if (wh) RT_KD(false, true, false);
-        else if (cnt) RT_KD(false, false, true);
-        else RT_KD(false, false, false);
+#define RT_KD(K, T, H, C) K<T, H, C><<<grid, threads, 0, s>>>(p)
+#define RT_KD_ALL(K)                                  \
+    if (tr) {                                         \
+        if (wh && cnt) RT_KD(K, true, true, true);    \
+        else if (wh) RT_KD(K, true, true, false);     \
+        else if (cnt) RT_KD(K, true, false, true);    \
+        else RT_KD(K, true, false, false);            \
+    } else {                                          \
+        if (wh && cnt) RT_KD(K, false, true, true);   \
+        else if (wh) RT_KD(K, false, true, false);    \
+        else if (cnt) RT_KD(K, false, false, true);   \
+        else RT_KD(K, false, false, false);           \
     }
+    if (kernel_version == 1) {
+        RT_KD_ALL(k_trace_kd)
+    } else if (kernel_version == 2) {
+        RT_KD_ALL(k_trace_kd2)
+    } else {
+        RT_KD_ALL(k_trace_kd3)
+    }
+#undef RT_KD_ALL
 #undef RT_KD
     return check_launch<void>("k_trace_kd");
 }

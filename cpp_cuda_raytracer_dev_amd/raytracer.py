@@ -240,6 +240,10 @@ class Camera:
         _lib.call("rt_read_frame", self._h, _lib.ptr(self.h_color), _lib.ptr(self.h_rmi) if want_hit else None)
         return 0
 
+    def set_option(self, key: int, value: int) -> None:
+        """Tuning knobs (_lib.RT_OPT_KERNEL, _lib.RT_OPT_TILE_ORDER); frames are identical."""
+        _lib.call("rt_camera_set_option", self._h, key, value)
+
     def counters(self, reset: bool = True) -> np.ndarray:
         out = np.zeros(5, np.uint64)
         _lib.call("rt_camera_counters", self._h, _lib.ptr(out), int(reset))

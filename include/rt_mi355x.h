@@ -170,6 +170,21 @@ int rt_camera_counters(rt_camera* c, uint64_t out[5], int reset);
 /* Kernel launch geometry and the traversal stack depth in use. */
 int rt_camera_info(const rt_camera* c, int32_t* w, int32_t* h, int32_t* max_depth);
 
+/* Tuning knobs (not in the reference): key 1 = KD kernel layout version
+ * (1: node-own box records, 2: child-box records, default), key 2 = tile
+ * dispatch order (0: XCD-contiguous, 1: natural, 2: centre-out, default).
+ * Every setting renders the identical frame. */
+#define RT_OPT_KERNEL 1
+#define RT_OPT_TILE_ORDER 2
+int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value);
+
+/* Diagnostics (key 100 of rt_camera_set_option: 1 = skip traversal,
+ * 2 = per-wave (start clock, end clock, max visits) records): copies up to
+ * n u64 of the record buffer; returns the count or a negative status. */
+#define RT_OPT_DEBUG 100
+#define RT_OPT_POOL_CAP 101 /* tests: shrink the wave-cooperative kernel's item pool (86..640) */
+int64_t rt_camera_debug_read(rt_camera* c, uint64_t* out, int64_t n);
+
 void rt_scene_destroy(rt_scene* s);
 void rt_camera_destroy(rt_camera* c);
 

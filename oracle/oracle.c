@@ -789,3 +789,27 @@ int orc_render(const orc_scene* s, const float xform[12], int mode, int32_t row0
     (void)nthreads;
     return status;
 }
+
+/* Per-pixel pop counts (interior + leaf) of the KD traversal: a workload
+ * profile for the kernels' load balance (not part of the reference). */
+int orc_pixel_visits(const orc_scene* s, const float xform[12], uint32_t* visits, int nthreads) {
+    static const float ident[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+    const float* X = xform ? xform : ident;
+    if (!s->bo) return -2;
+    const int32_t w = s->cam.w, h = s->cam.h;
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads)
+#endif
+    for (int32_t iy = 0; iy < h; iy++)
+        for (int32_t ix = 0; ix < w; ix++) {
+            uint64_t cnt[ORC_CNT_N] = {0};
+            float rmd[3];
+            orc_hit hh;
+            orc_primary_ray(&s->cam, ix, iy, rmd);
+            trace_kd(s, X, rmd, &hh, cnt);
+            visits[(int64_t)iy * w + ix] = (uint32_t)(cnt[ORC_CNT_INTERIOR] + cnt[ORC_CNT_LEAF]);
+        }
+    (void)nthreads;
+    return 0;
+}

@@ -119,6 +119,8 @@ int orc_render(const orc_scene* s, const float xform[12], int mode,
 void orc_primary_ray(const orc_camera* cam, int32_t ix, int32_t iy, float out[3]);
 
 /* Phong of one hit (color_cam_cuda, TD/Camera.cu:27-60). */
+int orc_pixel_visits(const orc_scene* s, const float xform[12], uint32_t* visits, int nthreads);
+
 uint32_t orc_phong(const float pnt[3], const float nrm[3], const float rmd[3],
                    const float rad[3]);
 

@@ -1,0 +1,72 @@
+"""Diagnostic: where does a KD frame spend its time?  (GPU; not a test.)
+
+Times the full kernel, the no-traversal variant (ray generation + root test
++ shading only) and records per-wave start/end clocks (s_memrealtime,
+100 MHz) with each wave's maximum visit count.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    from cpp_cuda_raytracer_dev_amd import _lib, raytracer as R
+    from tests import helpers as H
+    name = sys.argv[1] if len(sys.argv) > 1 else "dragon"
+    w, h = (int(sys.argv[2]), int(sys.argv[3])) if len(sys.argv) > 3 else (1920, 1080)
+    kernel = int(sys.argv[4]) if len(sys.argv) > 4 else 2
+    s = H.GpuScene(name, w, h, kernel=kernel, tile_order=1)
+    out = torch.zeros(w * h, dtype=torch.int32, device="cuda:0")
+    st = torch.cuda.Stream()
+
+    def timed(n=50):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for _ in range(5):
+            s.cam.render_into(out, stream=st.cuda_stream)
+        e0.record(st)
+        for _ in range(n):
+            s.cam.render_into(out, stream=st.cuda_stream)
+        e1.record(st)
+        st.synchronize()
+        return e0.elapsed_time(e1) / n
+
+    res = {"scene": name, "w": w, "h": h, "kernel": kernel, "full_ms": timed()}
+    s.cam.set_option(_lib.RT_OPT_DEBUG, 1)
+    res["no_traversal_ms"] = timed()
+    s.cam.set_option(_lib.RT_OPT_DEBUG, 2)
+    res["with_stamps_ms"] = timed(5)
+    nw = ((w + 15) // 16) * ((h + 7) // 8) * 2
+    buf = np.zeros(3 * nw, np.uint64)
+    got = _lib.lib().rt_camera_debug_read(s.cam._h, _lib.ptr(buf), len(buf))
+    rec = buf[:got].reshape(-1, 3).astype(np.int64)
+    rec = rec[rec[:, 1] > 0]
+    t0 = rec[:, 0].min()
+    start, end, vis = (rec[:, 0] - t0) * 10e-3, (rec[:, 1] - t0) * 10e-3, rec[:, 2]  # us
+    dur = end - start
+    res["span_us"] = float(end.max())
+    res["waves"] = int(len(rec))
+    heavy = vis > 1
+    res["heavy_waves"] = int(heavy.sum())
+    for tag, m in (("light", ~heavy), ("heavy", heavy)):
+        if m.any():
+            res[f"{tag}_dur_us_p50_p99_max"] = [float(np.percentile(dur[m], q)) for q in (50, 99, 100)]
+            res[f"{tag}_start_us_max"] = float(start[m].max())
+            res[f"{tag}_end_us_max"] = float(end[m].max())
+    if heavy.any():
+        k = np.argmax(dur)
+        res["longest_wave"] = {"dur_us": float(dur[k]), "visits": int(vis[k]), "start_us": float(start[k])}
+        res["us_per_visit_longest"] = float(dur[k] / max(vis[k], 1))
+        res["us_per_visit_median_heavy"] = float(np.median(dur[heavy] / np.maximum(vis[heavy], 1)))
+    # when do light waves finish vs heavy waves start
+    res["time_all_light_done_us"] = float(end[~heavy].max()) if (~heavy).any() else None
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
