@@ -47,7 +47,8 @@ def parse():
     ap.add_argument("--kernel", type=int, default=3,
                     help="KD kernel: 1 per-lane DFS (own-box records), 2 per-lane DFS (child-box records), "
                          "3 wave-cooperative item pool")
-    ap.add_argument("--tile-order", type=int, default=1, help="0 XCD-contiguous, 1 natural, 2 centre-out")
+    ap.add_argument("--tile-order", type=int, default=2, help="0 XCD-contiguous, 1 natural, 2 centre-out")
+    ap.add_argument("--rays", type=int, default=32, help="kernel 3: pixels per wave (64, 32, 16)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -132,6 +133,7 @@ def main():
     torch.cuda.synchronize(dev)
     cnt = cam.counters(reset=True)
     cam.set_option(_lib.RT_OPT_KERNEL, a.kernel)
+    cam.set_option(_lib.RT_OPT_RAYS, a.rays)
     cam.render_into(scratch, mode=a.mode, tile=tile if world > 1 else None, stream=sptr)  # re-prepares layout
     torch.cuda.synchronize(dev)
     my_pix = int(np.count_nonzero(np.repeat(np.arange((h + 7) // 8) % world == rank, 8)[:h])) * w
@@ -223,7 +225,7 @@ def main():
                 "traffic": traffic,
                 "kernel": {1: "k_trace_kd", 2: "k_trace_kd2", 3: "k_trace_kd3"}[a.kernel] if a.mode == 0
                           else "k_trace_flat",
-                "kernel_options": {"layout": a.kernel, "tile_order": a.tile_order},
+                "kernel_options": {"kernel": a.kernel, "tile_order": a.tile_order, "rays_per_wave": a.rays},
                 "kernel_ms_avg": round(kern_ms, 5),
                 "kernel_ms_avg_max_rank": round(kern_ms_max, 5),
                 "algorithmic_bytes_per_launch": bytes_per_launch,

@@ -22,6 +22,7 @@ RT_FLAG_WRITE_HIT = 1
 RT_FLAG_COUNT = 2
 RT_OPT_KERNEL = 1
 RT_OPT_TILE_ORDER = 2
+RT_OPT_RAYS = 3
 RT_OPT_DEBUG = 100
 RT_OPT_POOL_CAP = 101
 

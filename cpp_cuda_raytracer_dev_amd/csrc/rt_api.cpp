@@ -54,7 +54,8 @@ struct rt_camera {
     int64_t dbg_cap = 0;             // in u64
     int32_t* d_order = nullptr;      // centre-out tile permutation
     int64_t order_cap = 0;
-    int64_t order_key[5] = {-1, -1, -1, -1, -1};
+    int64_t order_key[6] = {-1, -1, -1, -1, -1, -1};
+    int rays = 32;                   // kOptRays: pixels per wave of kernel 3
 };
 
 namespace {
@@ -132,16 +133,19 @@ int prepare_camera_object(rt_camera* c) {
 // Centre-out permutation of the launch's tiles: blocks are dispatched in
 // index order, so the expensive tiles (the object sits mid-frame) start
 // first and the cheap background tiles fill in behind them.
-int ensure_order(rt_camera* c, int32_t tile_w, int32_t tiles_x, int32_t slots, int32_t nranks, int32_t rank) {
-    const int64_t key[5] = {tile_w, tiles_x, slots, nranks, rank};
-    if (std::equal(key, key + 5, c->order_key)) return RT_OK;
-    const int64_t n = (int64_t)tiles_x * slots;
+int ensure_order(rt_camera* c, const TraceParams& p) {
+    const int64_t key[6] = {p.tile_w, p.tile_h, p.tiles_x, p.block_rows, p.nranks, p.rank};
+    if (std::equal(key, key + 6, c->order_key)) return RT_OK;
+    const int64_t n = (int64_t)p.tiles_x * p.block_rows;
+    const int64_t per_band = kTileH / p.tile_h;
     std::vector<int32_t> order((size_t)n);
     std::vector<double> dist2((size_t)n);
     const double cx = 0.5 * c->w, cy = 0.5 * c->h;
     for (int64_t t = 0; t < n; t++) {
-        const int64_t slot = t / tiles_x, tx = t % tiles_x;
-        const double x = (tx + 0.5) * tile_w, y = ((rank + slot * (int64_t)nranks) + 0.5) * kTileH;
+        const int64_t row = t / p.tiles_x, tx = t % p.tiles_x;
+        const int64_t slot = row / per_band, yin = (row % per_band) * p.tile_h;
+        const double x = (tx + 0.5) * p.tile_w;
+        const double y = (double)((p.rank + slot * (int64_t)p.nranks) * kTileH + yin) + 0.5 * p.tile_h;
         dist2[(size_t)t] = (x - cx) * (x - cx) + (y - cy) * (y - cy);
         order[(size_t)t] = (int32_t)t;
     }
@@ -154,7 +158,7 @@ int ensure_order(rt_camera* c, int32_t tile_w, int32_t tiles_x, int32_t slots, i
     }
     if ((rc = hip_check(hipMemcpy(c->d_order, order.data(), sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice), "H2D order")))
         return rc;
-    std::copy(key, key + 5, c->order_key);
+    std::copy(key, key + 6, c->order_key);
     return RT_OK;
 }
 
@@ -180,9 +184,17 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
     p.nranks = tile ? tile->nranks : 1;
     p.rank = tile ? tile->rank : 0;
     const int32_t nbands = (c->h + kTileH - 1) / kTileH;
-    p.tile_w = (mode == RT_MODE_KD && effective_kernel(c) != 1) ? kTileWKd : kTileWFlat;
+    const int kernel = mode == RT_MODE_KD ? effective_kernel(c) : 0;
+    p.rays = kernel == 3 ? c->rays : 64;
+    if (kernel == 0 || kernel == 1) {        // flat / v1: 32x8 tiles, four 8x8 waves
+        p.tile_w = kTileWFlat; p.tile_h = kTileH;
+    } else if (p.rays == 64) {               // v2 / v3: 16x8 tiles, two 8x8 waves
+        p.tile_w = kTileWKd; p.tile_h = kTileH;
+    } else {                                 // v3, two stacked 8 x (rays/8) waves
+        p.tile_w = 8; p.tile_h = 2 * (p.rays / 8);
+    }
     p.tiles_x = (c->w + p.tile_w - 1) / p.tile_w;
-    p.slots = (nbands + p.nranks - 1) / p.nranks;
+    p.block_rows = ((nbands + p.nranks - 1) / p.nranks) * (kTileH / p.tile_h);
     p.root_ref = s->root_ref;
     p.ntri = s->ntri;
     p.max_depth = kMaxDepth;
@@ -192,7 +204,7 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
     p.pool_cap = c->pool_cap;
     p.dbg = nullptr;
     if (c->debug & 2) {
-        const int64_t need = (int64_t)p.tiles_x * p.slots * (p.tile_w / 8) * 3;
+        const int64_t need = (int64_t)p.tiles_x * p.block_rows * 4 * 3;  // <= 4 waves per block
         if (c->dbg_cap < need) {
             dev_free(c->d_dbg);
             int rc = dev_alloc(&c->d_dbg, (size_t)need, "hipMalloc(dbg)");
@@ -205,7 +217,7 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
     }
     camera_relative_box(s->root, c->pos, p.root_box);
     if (c->tile_order == 2) {
-        int rc = ensure_order(c, p.tile_w, p.tiles_x, p.slots, p.nranks, p.rank);
+        int rc = ensure_order(c, p);
         if (rc) return rc;
         p.order = c->d_order;
     }
@@ -473,6 +485,10 @@ extern "C" int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value) {
     case kOptKernel:
         if (value < 1 || value > 3) return fail(RT_ERR_INVALID, "kernel version %d", value);
         c->kernel_version = value;
+        return RT_OK;
+    case kOptRays:
+        if (value != 16 && value != 32 && value != 64) return fail(RT_ERR_INVALID, "rays per wave %d (16, 32, 64)", value);
+        c->rays = value;
         return RT_OK;
     case kOptPoolCap:
         // the 64 root items plus a DFS run of height <= 21 must fit

@@ -41,6 +41,7 @@ constexpr uint32_t kAxisShift = 29;
 enum Option : int32_t {
     kOptKernel = 1,     // KD kernel version: 1 (node-own box, 48 B) or 2 (child boxes, 64 B)
     kOptTileOrder = 2,  // 0 XCD-contiguous, 1 natural, 2 centre-out
+    kOptRays = 3,       // kernel 3 pixels per wave: 64, 32 or 16
     kOptDebug = 100,    // diagnostics: 1 = skip traversal, 2 = per-wave timestamps
     kOptPoolCap = 101,  // tests: shrink kernel 3's item pool (66..kPoolCap) to force its fallback
 };
@@ -77,8 +78,9 @@ struct TraceParams {
     float xf[12];
     int32_t w, h;
     int32_t nranks, rank;
-    int32_t tiles_x, slots;        // grid = tiles_x * slots blocks
-    int32_t tile_w;                // pixels per block row (block = tile_w * 8 threads)
+    int32_t tiles_x, block_rows;   // grid = tiles_x * block_rows blocks
+    int32_t tile_w, tile_h;        // pixels per block (tile_h divides the 8-row band)
+    int32_t rays;                  // pixels (rays) per wave: 64, 32 or 16
     int32_t tile_order;            // Option kOptTileOrder
     const int32_t* order;          // centre-out tile permutation (tile_order 2)
     float root_box[6];             // camera-relative root AABB (t0x,t1x,t0y,t1y,t0z,t1z)

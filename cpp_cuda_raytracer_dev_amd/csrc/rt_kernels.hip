@@ -93,7 +93,7 @@ __device__ uint32_t phong(const float pnt[3], const float nrm[3], const float rm
 // centre-out permutation, so the heavy centre tiles are dispatched first.
 __device__ __forceinline__ void tile_of_block(const TraceParams& P, int32_t& tx, int32_t& slot) {
     const int32_t b = (int32_t)blockIdx.x;
-    const int32_t nblocks = P.tiles_x * P.slots;
+    const int32_t nblocks = P.tiles_x * P.block_rows;
     int32_t t;
     if (P.tile_order == 0) {
         const int32_t q = nblocks >> 3, rem = nblocks & 7;
@@ -113,16 +113,23 @@ struct Pixel {
     int64_t out;       // index into the (packed) output buffer
 };
 
+// A block covers tile_w x tile_h pixels of one 8-row band; each wave owns an
+// 8 x (rays/8) sub-tile (side by side when tile_w > 8, stacked otherwise).
+// Lanes >= rays own no pixel (the wave-cooperative kernel's helper lanes).
 __device__ __forceinline__ bool pixel_of_thread(const TraceParams& P, Pixel& px) {
-    int32_t tx, slot;
-    tile_of_block(P, tx, slot);
+    int32_t tx, row;
+    tile_of_block(P, tx, row);
+    const int32_t per_band = kTileH / P.tile_h;
+    const int32_t slot = row / per_band, yin = (row - slot * per_band) * P.tile_h;
     const int32_t lane = (int32_t)threadIdx.x & 63, wave = (int32_t)threadIdx.x >> 6;
+    const int32_t wrows = P.rays >> 3;
+    const int32_t wx = P.tile_w > 8 ? wave * 8 : 0, wy = P.tile_w > 8 ? 0 : wave * wrows;
     const int32_t band = P.rank + slot * P.nranks;
-    const int32_t ly = lane >> 3;
-    px.x = tx * P.tile_w + wave * 8 + (lane & 7);
+    const int32_t ly = yin + wy + (lane >> 3);
+    px.x = tx * P.tile_w + wx + (lane & 7);
     px.y = band * kTileH + ly;
     px.out = (int64_t)(slot * kTileH + ly) * P.w + px.x;
-    return px.x < P.w && px.y < P.h;
+    return lane < P.rays && px.x < P.w && px.y < P.h;
 }
 
 // init_cam_mem_cuda, TD/Camera.cu:103-104: rmd = n + u*ix + v*iy, normalised.
@@ -534,13 +541,22 @@ struct Item {
     uint32_t meta;     // ray << 26 | depth << 21 | code
 };
 
-template <bool kTranslated, bool kWriteHit, bool kCount>
-__global__ __launch_bounds__(kTileWKd * kTileH) void k_trace_kd3(TraceParams P) {
-    constexpr int kWaves = kTileWKd * kTileH / 64;
-    __shared__ uint4 s_items[kWaves][kPoolCap];
-    __shared__ float4 s_ray[kWaves][64][5];
-    __shared__ unsigned long long s_key[kWaves][64];
-    __shared__ uint32_t s_tri[kWaves][64];
+// Pool capacity per wave for kRays rays (the DFS fallback keeps any
+// capacity >= 86 correct; these cover the measured peaks with margin).
+template <int kRays>
+constexpr int pool_cap_for() { return kRays == 64 ? kPoolCap : kRays == 32 ? 448 : 320; }
+
+// kRays pixels per wave (64: 8x8; 32: 8x4; 16: 8x2): fewer rays per wave
+// spread a heavy tile's items over more SIMDs, the other lanes only help.
+template <int kRays, bool kTranslated, bool kWriteHit, bool kCount>
+__global__ __launch_bounds__(128) void k_trace_kd3(TraceParams P) {
+    constexpr int kWaves = 2;
+    constexpr int kCap = pool_cap_for<kRays>();
+    constexpr int kRayVec = kTranslated ? 5 : 3;  // float4s of per-ray data in LDS
+    __shared__ uint4 s_items[kWaves][kCap];
+    __shared__ float4 s_ray[kWaves][kRays][kRayVec];
+    __shared__ unsigned long long s_key[kWaves][kRays];
+    __shared__ uint32_t s_tri[kWaves][kRays];
     const int wv = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
     uint4* items = s_items[wv];
     Pixel px;
@@ -567,15 +583,19 @@ __global__ __launch_bounds__(kTileWKd * kTileH) void k_trace_kd3(TraceParams P) 
         const float e0 = (R.odx * 1.0f) + (R.ody * 0.0f) + (R.odz * 0.0f);
         const float e1 = (R.odx * 0.0f) + (R.ody * 1.0f) + (R.odz * 0.0f);
         const float e2 = (R.odx * 0.0f) + (R.ody * 0.0f) + (R.odz * 1.0f);
-        float4* rd = s_ray[wv][lane];
-        rd[0] = make_float4(R.rx, R.ry, R.rz, R.ix);
-        rd[1] = make_float4(R.iy, R.iz, R.ox, R.oy);
-        rd[2] = make_float4(R.oz, R.odx, R.ody, R.odz);
-        rd[3] = make_float4(d0, d1, d2, e0);
-        rd[4] = make_float4(e1, e2, 0.0f, 0.0f);
+        if (lane < kRays) {
+            float4* rd = s_ray[wv][lane];
+            rd[0] = make_float4(R.rx, R.ry, R.rz, R.ix);
+            rd[1] = make_float4(R.iy, R.iz, R.ox, R.oy);
+            rd[2] = make_float4(R.oz, d0, d1, d2);
+            if (kTranslated) {
+                rd[kRayVec - 2] = make_float4(R.odx, R.ody, R.odz, e0);
+                rd[kRayVec - 1] = make_float4(e1, e2, 0.0f, 0.0f);
+            }
+            s_key[wv][lane] = ~0ull;
+            s_tri[wv][lane] = kMiss;
+        }
     }
-    s_key[wv][lane] = ~0ull;
-    s_tri[wv][lane] = kMiss;
 
     uint32_t n_int = 0, n_leaf = 0, n_acc = 0, n_desc = 0;
     // the root item of every live ray whose root test passes (or a leaf root)
@@ -598,7 +618,7 @@ __global__ __launch_bounds__(kTileWKd * kTileH) void k_trace_kd3(TraceParams P) 
         if (has) items[off] = make_uint4(P.root_ref, __float_as_uint(r0t0), __float_as_uint(r0t1), (uint32_t)lane << 26);
     }
     int n = __builtin_popcountll(__ballot(has));
-    const int cap = min(P.pool_cap, kPoolCap);
+    const int cap = min(P.pool_cap, kCap);
     __builtin_amdgcn_wave_barrier();
 
     while (n > 0) {
@@ -623,11 +643,15 @@ __global__ __launch_bounds__(kTileWKd * kTileH) void k_trace_kd3(TraceParams P) 
             ray = it.w >> 26;
             const uint32_t depth = (it.w >> kCodeBits) & 31u, code = it.w & kCodeMask;
             const float4* rd = s_ray[wv][ray];
-            const float4 q0 = rd[0], q1 = rd[1], q2 = rd[2], q3 = rd[3], q4 = rd[4];
+            const float4 q0 = rd[0], q1 = rd[1], q2 = rd[2];
+            const float4 q3 = kTranslated ? rd[kRayVec - 2] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            const float4 q4 = kTranslated ? rd[kRayVec - 1] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             Ray Q;
             Q.rx = q0.x; Q.ry = q0.y; Q.rz = q0.z; Q.ix = q0.w;
             Q.iy = q1.x; Q.iz = q1.y; Q.ox = q1.z; Q.oy = q1.w;
-            Q.oz = q2.x; Q.odx = q2.y; Q.ody = q2.z; Q.odz = q2.w;
+            Q.oz = q2.x;
+            // object translation (exact zeros when untranslated, as X[3], X[7], X[11] are)
+            Q.odx = kTranslated ? q3.x : 0.0f; Q.ody = kTranslated ? q3.y : 0.0f; Q.odz = kTranslated ? q3.z : 0.0f;
             Q.sx = Q.rx > 0; Q.sy = Q.ry > 0; Q.sz = Q.rz > 0;
             if (it.x & kLeafBit) {
                 if (kCount) n_leaf++;
@@ -645,7 +669,7 @@ __global__ __launch_bounds__(kTileWKd * kTileH) void k_trace_kd3(TraceParams P) 
                 const uint32_t lw = __float_as_uint(r3.z);
                 const uint32_t axis = (lw >> kAxisShift) & 3u;
                 const uint32_t L = lw & ~(3u << kAxisShift), Rr = __float_as_uint(r3.w);
-                const float dir = axis == 0 ? q3.x : axis == 1 ? q3.y : q3.z;
+                const float dir = axis == 0 ? q2.y : axis == 1 ? q2.z : q2.w;
                 const float mx = __uint_as_float(it.y) * dir, mn = __uint_as_float(it.z) * dir;
                 float s1, s2;
                 if (kTranslated) {
@@ -953,43 +977,38 @@ int launch_cam_nodes(const rt_kd_node* nodes, const int32_t* ids, const uint32_t
     return check_launch<void>("k_cam_nodes");
 }
 
+using TraceFn = void (*)(TraceParams);
+
+template <bool T, bool H, bool C>
+TraceFn kd_kernel(int version, int rays) {
+    if (version == 1) return k_trace_kd<T, H, C>;
+    if (version == 2) return k_trace_kd2<T, H, C>;
+    if (rays == 16) return k_trace_kd3<16, T, H, C>;
+    if (rays == 32) return k_trace_kd3<32, T, H, C>;
+    return k_trace_kd3<64, T, H, C>;
+}
+
 int launch_trace(const TraceParams& p, uint32_t mode, uint32_t flags, int kernel_version, void* stream) {
-    const unsigned grid = (unsigned)(p.tiles_x * p.slots);
+    const unsigned grid = (unsigned)(p.tiles_x * p.block_rows);
     if (grid == 0) return RT_OK;
     hipStream_t s = (hipStream_t)stream;
     const bool wh = (flags & RT_FLAG_WRITE_HIT) != 0, cnt = (flags & RT_FLAG_COUNT) != 0;
-    const unsigned threads = (unsigned)(p.tile_w * kTileH);
+    // waves per block = (tile_w / 8) * (tile_h / (rays / 8))
+    const unsigned threads = (unsigned)((p.tile_w / 8) * (p.tile_h / (p.rays / 8)) * 64);
+    TraceFn fn;
     if (mode == RT_MODE_FLAT) {
-        if (wh && cnt) k_trace_flat<true, true><<<grid, threads, 0, s>>>(p);
-        else if (wh) k_trace_flat<true, false><<<grid, threads, 0, s>>>(p);
-        else if (cnt) k_trace_flat<false, true><<<grid, threads, 0, s>>>(p);
-        else k_trace_flat<false, false><<<grid, threads, 0, s>>>(p);
-        return check_launch<void>("k_trace_flat");
-    }
-    const bool tr = p.xf[3] != 0.0f || p.xf[7] != 0.0f || p.xf[11] != 0.0f;
-#define RT_KD(K, T, H, C) K<T, H, C><<<grid, threads, 0, s>>>(p)
-#define RT_KD_ALL(K)                                  \
-    if (tr) {                                         \
-        if (wh && cnt) RT_KD(K, true, true, true);    \
-        else if (wh) RT_KD(K, true, true, false);     \
-        else if (cnt) RT_KD(K, true, false, true);    \
-        else RT_KD(K, true, false, false);            \
-    } else {                                          \
-        if (wh && cnt) RT_KD(K, false, true, true);   \
-        else if (wh) RT_KD(K, false, true, false);    \
-        else if (cnt) RT_KD(K, false, false, true);   \
-        else RT_KD(K, false, false, false);           \
-    }
-    if (kernel_version == 1) {
-        RT_KD_ALL(k_trace_kd)
-    } else if (kernel_version == 2) {
-        RT_KD_ALL(k_trace_kd2)
+        fn = wh ? (cnt ? k_trace_flat<true, true> : k_trace_flat<true, false>)
+                : (cnt ? k_trace_flat<false, true> : k_trace_flat<false, false>);
     } else {
-        RT_KD_ALL(k_trace_kd3)
+        const bool tr = p.xf[3] != 0.0f || p.xf[7] != 0.0f || p.xf[11] != 0.0f;
+        const int v = kernel_version, r = p.rays;
+        if (tr) fn = wh ? (cnt ? kd_kernel<true, true, true>(v, r) : kd_kernel<true, true, false>(v, r))
+                        : (cnt ? kd_kernel<true, false, true>(v, r) : kd_kernel<true, false, false>(v, r));
+        else fn = wh ? (cnt ? kd_kernel<false, true, true>(v, r) : kd_kernel<false, true, false>(v, r))
+                     : (cnt ? kd_kernel<false, false, true>(v, r) : kd_kernel<false, false, false>(v, r));
     }
-#undef RT_KD_ALL
-#undef RT_KD
-    return check_launch<void>("k_trace_kd");
+    fn<<<grid, threads, 0, s>>>(p);
+    return check_launch<void>(mode == RT_MODE_FLAT ? "k_trace_flat" : "k_trace_kd");
 }
 
 int launch_unpack(int32_t w, int32_t h, int32_t nranks, const uint32_t* gathered, uint32_t* frame,

@@ -44,7 +44,7 @@ def test_small_frames_vs_golden(name, w, h, mode):
     _assert_same((argb, hit), (oargb, ohit), key + " vs oracle")
 
 
-KERNELS = [(1, 0), (2, 2), (2, 1), (3, 1), (3, 2)]  # (KD kernel version, tile order)
+KERNELS = [(1, 0, 64), (2, 2, 64), (2, 1, 64), (3, 1, 64), (3, 2, 32), (3, 1, 32), (3, 2, 16)]  # (KD kernel, tile order, rays/wave)
 
 
 def _counters_match(cnt, ocnt, kernel):
@@ -60,9 +60,9 @@ def _counters_match(cnt, ocnt, kernel):
 
 
 @pytest.mark.parametrize("mode", [0, 1])
-@pytest.mark.parametrize("kernel,order", KERNELS)
-def test_tester_320x180(mode, kernel, order):
-    s = H.GpuScene("tester", 320, 180, kernel=kernel, tile_order=order)
+@pytest.mark.parametrize("kernel,order,rays", KERNELS)
+def test_tester_320x180(mode, kernel, order, rays):
+    s = H.GpuScene("tester", 320, 180, kernel=kernel, tile_order=order, rays=rays)
     argb, hit, cnt = s.render(mode, count=True)
     oargb, ohit, ocnt = H.oracle_render("tester", 320, 180, mode)
     _assert_same((argb, hit), (oargb, ohit), f"tester m{mode}")
@@ -70,9 +70,9 @@ def test_tester_320x180(mode, kernel, order):
         _counters_match(cnt, ocnt, kernel)
 
 
-@pytest.mark.parametrize("kernel,order", KERNELS)
-def test_rabbit_960x540_kd_and_counters(kernel, order):
-    s = H.GpuScene("rabbit_70k", 960, 540, kernel=kernel, tile_order=order)
+@pytest.mark.parametrize("kernel,order,rays", KERNELS)
+def test_rabbit_960x540_kd_and_counters(kernel, order, rays):
+    s = H.GpuScene("rabbit_70k", 960, 540, kernel=kernel, tile_order=order, rays=rays)
     argb, hit, cnt = s.render(0, count=True)
     oargb, ohit, ocnt = H.oracle_render("rabbit_70k", 960, 540, 0)
     _assert_same((argb, hit), (oargb, ohit), "rabbit kd")
@@ -97,9 +97,9 @@ def test_rabbit_960x540_flat_band():
 
 
 @pytest.mark.parametrize("w,h", [(960, 540), (1920, 1080)])
-@pytest.mark.parametrize("kernel,order", KERNELS)
-def test_dragon_standin_kd(w, h, kernel, order):
-    s = H.GpuScene("dragon", w, h, kernel=kernel, tile_order=order)
+@pytest.mark.parametrize("kernel,order,rays", KERNELS)
+def test_dragon_standin_kd(w, h, kernel, order, rays):
+    s = H.GpuScene("dragon", w, h, kernel=kernel, tile_order=order, rays=rays)
     argb, hit, cnt = s.render(0, count=True)
     oargb, ohit, ocnt = H.oracle_render("dragon", w, h, 0)
     _assert_same((argb, hit), (oargb, ohit), f"dragon {w}x{h}")
@@ -169,22 +169,22 @@ def test_pool_capacity_fallback(cap):
 
 
 @pytest.mark.parametrize("w,h", [(81, 45), (1, 1), (33, 9), (7, 130)])
-@pytest.mark.parametrize("kernel,order", KERNELS)
-def test_odd_resolutions(w, h, kernel, order):
+@pytest.mark.parametrize("kernel,order,rays", KERNELS)
+def test_odd_resolutions(w, h, kernel, order, rays):
     for mode in (0, 1):
-        s = H.GpuScene("tester", w, h, kernel=kernel, tile_order=order)
+        s = H.GpuScene("tester", w, h, kernel=kernel, tile_order=order, rays=rays)
         argb, hit, _ = s.render(mode)
         oargb, ohit, _ = H.oracle_render("tester", w, h, mode)
         _assert_same((argb, hit), (oargb, ohit), f"tester {w}x{h} m{mode}")
 
 
 @pytest.mark.parametrize("nranks", [2, 3, 8])
-@pytest.mark.parametrize("kernel,order", KERNELS)
-def test_band_tiles_unpack(nranks, kernel, order):
+@pytest.mark.parametrize("kernel,order,rays", KERNELS)
+def test_band_tiles_unpack(nranks, kernel, order, rays):
     import torch
     from cpp_cuda_raytracer_dev_amd import raytracer as R
     w, h = 1920, 1080
-    s = H.GpuScene("dragon", w, h, kernel=kernel, tile_order=order)
+    s = H.GpuScene("dragon", w, h, kernel=kernel, tile_order=order, rays=rays)
     full, fhit, _ = s.render(0)
     npk = R.packed_pixels(w, h, nranks)
     dev = torch.device("cuda:0")

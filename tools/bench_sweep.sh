@@ -1,6 +1,6 @@
 #!/bin/bash
-# Kernel-variant sweep on one GPU: bench.py under each (layout, tile order).
-# Usage: tools/bench_sweep.sh <tag> [extra bench args...]
+# Kernel-variant sweep on one GPU: bench.py under each (kernel, tile order,
+# rays per wave).  Usage: tools/bench_sweep.sh <tag> [extra bench args...]
 set -u
 TAG=${1:-sweep}
 shift || true
@@ -8,12 +8,13 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd "$ROOT"
-for v in "1 0" "2 1" "3 0" "3 1" "3 2"; do
-    set -- $v "$@"
-    k=$1; o=$2; shift 2
-    timeout -k 10 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --kernel "$k" --tile-order "$o" "$@" \
-        > "$OUT/bench_k${k}_o${o}.log" 2>&1
+VARIANTS=${VARIANTS:-"2,1,64 3,2,64 3,1,32 3,2,32 3,1,16 3,2,16"}
+for v in $VARIANTS; do
+    IFS=, read -r k o r <<< "$v"
+    log="$OUT/bench_k${k}_o${o}_r${r}.log"
+    timeout -k 10 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --kernel "$k" --tile-order "$o" \
+        --rays "$r" "$@" > "$log" 2>&1
     rc=$?
-    echo "kernel $k order $o exit $rc: $(grep -o '"value": [0-9.]*' "$OUT/bench_k${k}_o${o}.log") $(grep -o '"kernel_ms_avg": [0-9.]*' "$OUT/bench_k${k}_o${o}.log")"
-    if [ $rc -ne 0 ]; then tail -5 "$OUT/bench_k${k}_o${o}.log"; exit $rc; fi
+    echo "kernel $k order $o rays $r exit $rc: $(grep -o '"value": [0-9.]*' "$log") $(grep -o '"kernel_ms_avg": [0-9.]*' "$log")"
+    if [ $rc -ne 0 ]; then tail -5 "$log"; exit $rc; fi
 done
