@@ -25,6 +25,18 @@ def test_library_exports_every_declared_symbol():
     assert L.rt_abi_version() == 1
 
 
+def test_cpp_facade_and_headless_driver_compile(tmp_path):
+    """The reference-shaped C++ facade (include/rt_facade.hpp) and the
+    WinMain replacement build against the C ABI."""
+    import subprocess
+    root = os.path.dirname(HEADER)
+    src = os.path.join(os.path.dirname(root), "tools", "rt_headless.cpp")
+    out = tmp_path / "rt_headless"
+    subprocess.run(["g++", "-std=c++17", "-Wall", "-Werror", "-I", root, "-o", str(out), src, _lib.LIB_PATH],
+                   check=True)
+    assert out.exists()
+
+
 def test_epsilon_threshold_is_exact():
     c = np.array([0x24E69595], np.uint32).view(np.float32)[0]
     assert np.float64(c) >= 1e-16

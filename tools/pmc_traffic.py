@@ -1,0 +1,56 @@
+"""Summarise rocprofv3 --pmc passes of bench.py into profiles/pmc_traffic.json.
+
+    python tools/pmc_traffic.py <key> <kernel-substring> <pass_dir> [<pass_dir> ...]
+
+Each pass directory holds one rocprofv3 --pmc run (counters collected in
+separate passes: FETCH_SIZE and WRITE_SIZE do not fit one TCC pass).  Per
+dispatch of the matching kernel, counters are averaged.  HBM bytes per launch
+follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB, and on
+gfx950 FETCH_SIZE reports half the bytes of 16-B-per-lane reads, so the read
+side is doubled ("hbm_bytes_per_launch"); the raw sum is kept beside it.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def load(pass_dir, kernel_sub):
+    vals = defaultdict(list)
+    for path in glob.glob(os.path.join(pass_dir, "**", "*counter_collection.csv"), recursive=True):
+        with open(path) as fp:
+            for row in csv.DictReader(fp):
+                if kernel_sub not in row.get("Kernel_Name", ""):
+                    continue
+                vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in vals.items() if v}, {k: len(v) for k, v in vals.items()}
+
+
+def main():
+    key, kernel_sub, dirs = sys.argv[1], sys.argv[2], sys.argv[3:]
+    counters, n = {}, {}
+    for d in dirs:
+        c, m = load(d, kernel_sub)
+        counters.update(c)
+        n.update(m)
+    out_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    data = json.load(open(out_path)) if os.path.exists(out_path) else {}
+    entry = {"kernel": kernel_sub, "counters_per_dispatch": counters, "dispatches": n}
+    if "FETCH_SIZE" in counters and "WRITE_SIZE" in counters:
+        fetch, write = counters["FETCH_SIZE"] * 1024.0, counters["WRITE_SIZE"] * 1024.0
+        entry["hbm_bytes_per_launch_raw"] = fetch + write
+        entry["hbm_bytes_per_launch"] = 2.0 * fetch + write
+    if "TCC_HIT_sum" in counters and "TCC_MISS_sum" in counters:
+        h, m = counters["TCC_HIT_sum"], counters["TCC_MISS_sum"]
+        entry["l2_hit_rate"] = h / (h + m) if h + m else None
+    data[key] = entry
+    json.dump(data, open(out_path, "w"), indent=1, sort_keys=True)
+    print(json.dumps({key: entry}))
+
+
+if __name__ == "__main__":
+    main()
