@@ -125,7 +125,7 @@ public:
     Quaternion* quat = nullptr;
 
     explicit Object(Trixel* x) : trixel_list(x), quat(&own_) {}
-    Object(Trixel* x, Quaternion* q) : trixel_list(x), own_(*q), quat(&own_) {}
+    Object(Trixel* x, Quaternion* q) : trixel_list(x), quat(&own_), own_(*q) {}
     u8 getTag() const { return trixel_list->object_tag; }
     // Object::render (TD/Object.cpp:10-12)
     int render(Camera* c, u32 mode = RENDER_MODE_KD) { return trixel_list->intersect_trixels(c, quat, mode); }
