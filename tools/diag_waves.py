@@ -20,8 +20,10 @@ def main():
     from tests import helpers as H
     name = sys.argv[1] if len(sys.argv) > 1 else "dragon"
     w, h = (int(sys.argv[2]), int(sys.argv[3])) if len(sys.argv) > 3 else (1920, 1080)
-    kernel = int(sys.argv[4]) if len(sys.argv) > 4 else 2
-    s = H.GpuScene(name, w, h, kernel=kernel, tile_order=1)
+    kernel = int(sys.argv[4]) if len(sys.argv) > 4 else 3
+    rays = int(sys.argv[5]) if len(sys.argv) > 5 else 32
+    order = int(sys.argv[6]) if len(sys.argv) > 6 else 2
+    s = H.GpuScene(name, w, h, kernel=kernel, tile_order=order, rays=rays)
     out = torch.zeros(w * h, dtype=torch.int32, device="cuda:0")
     st = torch.cuda.Stream()
 
@@ -41,7 +43,7 @@ def main():
     res["no_traversal_ms"] = timed()
     s.cam.set_option(_lib.RT_OPT_DEBUG, 2)
     res["with_stamps_ms"] = timed(5)
-    nw = ((w + 15) // 16) * ((h + 7) // 8) * 2
+    nw = ((w + 7) // 8) * ((h + 7) // 8) * 8
     buf = np.zeros(3 * nw, np.uint64)
     got = _lib.lib().rt_camera_debug_read(s.cam._h, _lib.ptr(buf), len(buf))
     rec = buf[:got].reshape(-1, 3).astype(np.int64)
