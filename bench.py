@@ -49,6 +49,8 @@ def parse():
                          "3 wave-cooperative item pool")
     ap.add_argument("--tile-order", type=int, default=2, help="0 XCD-contiguous, 1 natural, 2 centre-out")
     ap.add_argument("--rays", type=int, default=32, help="kernel 3: pixels per wave (64, 32, 16)")
+    ap.add_argument("--shadow", action="store_true",
+                    help="one shadow ray per hit (config C5: --scene happy --width 3840 --height 2160 --shadow)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -64,7 +66,7 @@ def build_scene(name):
     return pts, leafs, nodes
 
 
-def cpu_baseline(pts, nodes, w, h, seconds, threads, mode):
+def cpu_baseline(pts, nodes, w, h, seconds, threads, mode, shadow=False, rays_per_frame=None):
     """The oracle (C restatement, -O2, OpenMP over rows) on the same frame,
     repeated for ~`seconds`.  Test infrastructure: the checker, timed beside
     the GPU; never part of the product path."""
@@ -78,7 +80,7 @@ def cpu_baseline(pts, nodes, w, h, seconds, threads, mode):
         rows = (h // 2 - 4, h // 2 + 4)
     frames, t0 = 0, time.perf_counter()
     while True:
-        s.render(mode, rows=rows, nthreads=threads, want_hit=False)
+        s.render(mode, rows=rows, nthreads=threads, want_hit=False, shadow=shadow)
         frames += 1
         if time.perf_counter() - t0 >= seconds and frames >= 2:
             break
@@ -87,7 +89,7 @@ def cpu_baseline(pts, nodes, w, h, seconds, threads, mode):
     frac = (rows[1] - rows[0]) / h
     fps = frames * frac / dt
     return {"value": round(fps, 3), "unit": "frames/s", "cores": threads, "kind": "port",
-            "mray_per_s": round(fps * w * h / 1e6, 3),
+            "mray_per_s": round(fps * (rays_per_frame or w * h) / 1e6, 3),
             "sample": f"{frames} x rows {rows[0]}-{rows[1]} of the same {w}x{h} frame, oracle/oracle.c "
                       f"(-O2 -ffp-contract=off, OpenMP {threads} threads), {dt:.1f} s"}
 
@@ -117,7 +119,9 @@ def main():
     trixel.set_kd_nodes(nodes)
     cam = R.Camera.default(w, h, device=local)
     from cpp_cuda_raytracer_dev_amd import _lib
-    cam.set_option(_lib.RT_OPT_KERNEL, 2)  # the counting frame runs the reference's DFS order
+    # the counting frame runs the reference's DFS order (kernel 2); shadow
+    # walks exist in kernel 3 only, whose accept count is the candidate count
+    cam.set_option(_lib.RT_OPT_KERNEL, 3 if a.shadow else 2)
     cam.set_option(_lib.RT_OPT_TILE_ORDER, a.tile_order)
     obj = R.Object(trixel)
     cam.add_object(obj)
@@ -129,12 +133,15 @@ def main():
     # Algorithmic counts of this rank's tiles (one untimed counting frame).
     npk = R.packed_pixels(w, h, world) if world > 1 else w * h
     scratch = torch.zeros(npk, dtype=torch.int32, device=dev)
-    cam.render_into(scratch, mode=a.mode, flags=R.RT_FLAG_COUNT, tile=tile if world > 1 else None, stream=sptr)
+    sflag = R.RT_FLAG_SHADOW if a.shadow else 0
+    cam.render_into(scratch, mode=a.mode, flags=R.RT_FLAG_COUNT | sflag, tile=tile if world > 1 else None,
+                    stream=sptr)
     torch.cuda.synchronize(dev)
     cnt = cam.counters(reset=True)
     cam.set_option(_lib.RT_OPT_KERNEL, a.kernel)
     cam.set_option(_lib.RT_OPT_RAYS, a.rays)
-    cam.render_into(scratch, mode=a.mode, tile=tile if world > 1 else None, stream=sptr)  # re-prepares layout
+    cam.render_into(scratch, mode=a.mode, flags=sflag, tile=tile if world > 1 else None,
+                    stream=sptr)  # re-prepares layout
     torch.cuda.synchronize(dev)
     my_pix = int(np.count_nonzero(np.repeat(np.arange((h + 7) // 8) % world == rank, 8)[:h])) * w
     bytes_per_launch = B_INT * int(cnt[0]) + B_LEAF * int(cnt[1]) + B_HIT * int(cnt[2]) + B_PIX * my_pix
@@ -154,7 +161,8 @@ def main():
         with torch.cuda.stream(stream):
             if i is not None:
                 ev[i][0].record(stream)
-            cam.render_into(out, xform=xf, mode=a.mode, tile=tile if world > 1 else None, stream=sptr)
+            cam.render_into(out, xform=xf, mode=a.mode, flags=sflag, tile=tile if world > 1 else None,
+                            stream=sptr)
             if i is not None:
                 ev[i][1].record(stream)
             if fg is not None:
@@ -181,8 +189,14 @@ def main():
         elapsed, kern_ms_max = float(t[0]), float(t[1])
         tb = torch.tensor([bytes_per_launch], dtype=torch.float64, device=dev)
         dist.all_reduce(tb, op=dist.ReduceOp.MAX)
+        th = torch.tensor([int(cnt[3])], dtype=torch.float64, device=dev)
+        dist.all_reduce(th, op=dist.ReduceOp.SUM)
+        hits_all = int(th[0])
     else:
         kern_ms_max = kern_ms
+        hits_all = int(cnt[3])
+    # rays per frame: every pixel's primary ray, plus a shadow ray per hit
+    rays_per_frame = w * h + (hits_all if a.shadow else 0)
 
     if rank == 0:
         fps = a.steps / elapsed
@@ -199,7 +213,7 @@ def main():
             "metric": METRIC,
             "value": round(fps, 2),
             "unit": "frames/s",
-            "mray_per_s": round(fps * w * h / 1e6, 2),
+            "mray_per_s": round(fps * rays_per_frame / 1e6, 2),
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
@@ -211,7 +225,9 @@ def main():
             "data": "synthetic",
             "config": {
                 "workload": f"{a.scene} stand-in {w}x{h}, {'KD traversal' if a.mode == 0 else 'flat list'}, "
-                            "primary rays + Phong, u32 frame on GPU 0",
+                            + ("primary + one shadow ray per hit" if a.shadow else "primary rays")
+                            + " + Phong, u32 frame on GPU 0",
+                "rays_per_frame": rays_per_frame,
                 "scene": f"synthetic {a.scene} stand-in, {len(pts)} triangles (seed 20221015)",
                 "resolution": [w, h],
                 "parallelism": f"screen bands x{world}" + (f" + RCCL {a.collective} to rank 0" if world > 1 else ""),
@@ -225,7 +241,8 @@ def main():
                 "traffic": traffic,
                 "kernel": {1: "k_trace_kd", 2: "k_trace_kd2", 3: "k_trace_kd3"}[a.kernel] if a.mode == 0
                           else "k_trace_flat",
-                "kernel_options": {"kernel": a.kernel, "tile_order": a.tile_order, "rays_per_wave": a.rays},
+                "kernel_options": {"kernel": a.kernel, "tile_order": a.tile_order, "rays_per_wave": a.rays,
+                                   "shadow": a.shadow},
                 "kernel_ms_avg": round(kern_ms, 5),
                 "kernel_ms_avg_max_rank": round(kern_ms_max, 5),
                 "algorithmic_bytes_per_launch": bytes_per_launch,
@@ -235,7 +252,8 @@ def main():
             },
         }
         if not a.no_cpu_baseline and world == 1:
-            res["cpu_baseline"] = cpu_baseline(pts, nodes, w, h, a.cpu_seconds, a.cpu_threads, a.mode)
+            res["cpu_baseline"] = cpu_baseline(pts, nodes, w, h, a.cpu_seconds, a.cpu_threads, a.mode, a.shadow,
+                                              rays_per_frame)
         else:
             res["cpu_baseline"] = None
         print(json.dumps(res), flush=True)

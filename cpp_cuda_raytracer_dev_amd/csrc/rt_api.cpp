@@ -383,6 +383,14 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
     if (mode == RT_MODE_KD && !c->obj->d_nodes)
         return fail(RT_ERR_STATE, "rt_render: KD mode needs rt_scene_set_kd (Trixel::create_kd) first");
     if (c->obj->ntri == 0) return fail(RT_ERR_STATE, "rt_render: empty scene");
+    if (flags & ~(RT_FLAG_WRITE_HIT | RT_FLAG_COUNT | RT_FLAG_SHADOW))
+        return fail(RT_ERR_INVALID, "rt_render: unknown flags 0x%x", flags);
+    if (flags & RT_FLAG_SHADOW) {
+        if (mode != RT_MODE_KD) return fail(RT_ERR_INVALID, "rt_render: RT_FLAG_SHADOW needs RT_MODE_KD");
+        if (effective_kernel(c) != 3)
+            return fail(RT_ERR_STATE, "rt_render: shadow rays run in the wave-cooperative kernel (3); kernel %d%s",
+                        effective_kernel(c), c->obj->height > 21 ? " (tree height > 21)" : "");
+    }
     TraceParams p;
     if ((rc = fill_params(c, xform, tile, argb, hit, mode, p))) return rc;
     return launch_trace(p, mode, flags, effective_kernel(c), stream);

@@ -546,59 +546,39 @@ struct Item {
 template <int kRays>
 constexpr int pool_cap_for() { return kRays == 64 ? kPoolCap : kRays == 32 ? 448 : 320; }
 
-// kRays pixels per wave (64: 8x8; 32: 8x4; 16: 8x2): fewer rays per wave
-// spread a heavy tile's items over more SIMDs, the other lanes only help.
-template <int kRays, bool kTranslated, bool kWriteHit, bool kCount>
-__global__ __launch_bounds__(128) void k_trace_kd3(TraceParams P) {
-    constexpr int kWaves = 2;
-    constexpr int kCap = pool_cap_for<kRays>();
-    constexpr int kRayVec = kTranslated ? 5 : 3;  // float4s of per-ray data in LDS
-    __shared__ uint4 s_items[kWaves][kCap];
-    __shared__ float4 s_ray[kWaves][kRays][kRayVec];
-    __shared__ unsigned long long s_key[kWaves][kRays];
-    __shared__ uint32_t s_tri[kWaves][kRays];
-    const int wv = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
-    uint4* items = s_items[wv];
-    Pixel px;
-    const bool live = pixel_of_thread(P, px);  // every lane stays for the ballots
-    const unsigned long long t_start = P.dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    uint32_t iters = 0;
-
-    float cam[3] = {0.0f, 0.0f, 1.0f};
-    if (live) primary_ray(P, px.x, px.y, cam);
-    const float* X = P.xf;
-    Ray R;
-    R.odx = X[3]; R.ody = X[7]; R.odz = X[11];
-    R.rx = -1 * (X[0] * -cam[0] + X[1] * -cam[1] + X[2] * -cam[2]);
-    R.ry = -1 * (X[4] * -cam[0] + X[5] * -cam[1] + X[6] * -cam[2]);
-    R.rz = -1 * (X[8] * -cam[0] + X[9] * -cam[1] + X[10] * -cam[2]);
-    R.ix = 1 / R.rx; R.iy = 1 / R.ry; R.iz = 1 / R.rz;
-    R.ox = R.odx / R.rx; R.oy = R.ody / R.ry; R.oz = R.odz / R.rz;
-    R.sx = R.rx > 0; R.sy = R.ry > 0; R.sz = R.rz > 0;
-    {
-        // dir and ds for each one-hot cut axis (TD/Trixel.cu:88-90)
-        const float d0 = (R.rx * 1.0f) + (R.ry * 0.0f) + (R.rz * 0.0f);
-        const float d1 = (R.rx * 0.0f) + (R.ry * 1.0f) + (R.rz * 0.0f);
-        const float d2 = (R.rx * 0.0f) + (R.ry * 0.0f) + (R.rz * 1.0f);
+// Per-ray data of the pool walk in LDS: rd[0] = (rx, ry, rz, 1/rx),
+// rd[1] = (1/ry, 1/rz, odx/rx, ody/ry), rd[2] = (odz/rz, dir per cut axis),
+// translated walks add rd[3] = (od, ds of axis 0), rd[4] = (ds of axes 1-2,
+// shadow walks: Lmax, hit triangle).
+__device__ __forceinline__ void store_ray(float4* rd, const Ray& R, bool translated, float lmax, uint32_t self) {
+    // dir and ds for each one-hot cut axis (TD/Trixel.cu:88-90)
+    const float d0 = (R.rx * 1.0f) + (R.ry * 0.0f) + (R.rz * 0.0f);
+    const float d1 = (R.rx * 0.0f) + (R.ry * 1.0f) + (R.rz * 0.0f);
+    const float d2 = (R.rx * 0.0f) + (R.ry * 0.0f) + (R.rz * 1.0f);
+    rd[0] = make_float4(R.rx, R.ry, R.rz, R.ix);
+    rd[1] = make_float4(R.iy, R.iz, R.ox, R.oy);
+    rd[2] = make_float4(R.oz, d0, d1, d2);
+    if (translated) {
         const float e0 = (R.odx * 1.0f) + (R.ody * 0.0f) + (R.odz * 0.0f);
         const float e1 = (R.odx * 0.0f) + (R.ody * 1.0f) + (R.odz * 0.0f);
         const float e2 = (R.odx * 0.0f) + (R.ody * 0.0f) + (R.odz * 1.0f);
-        if (lane < kRays) {
-            float4* rd = s_ray[wv][lane];
-            rd[0] = make_float4(R.rx, R.ry, R.rz, R.ix);
-            rd[1] = make_float4(R.iy, R.iz, R.ox, R.oy);
-            rd[2] = make_float4(R.oz, d0, d1, d2);
-            if (kTranslated) {
-                rd[kRayVec - 2] = make_float4(R.odx, R.ody, R.odz, e0);
-                rd[kRayVec - 1] = make_float4(e1, e2, 0.0f, 0.0f);
-            }
-            s_key[wv][lane] = ~0ull;
-            s_tri[wv][lane] = kMiss;
-        }
+        rd[3] = make_float4(R.odx, R.ody, R.odz, e0);
+        rd[4] = make_float4(e1, e2, lmax, __uint_as_float(self));
     }
+}
 
-    uint32_t n_int = 0, n_leaf = 0, n_acc = 0, n_desc = 0;
-    // the root item of every live ray whose root test passes (or a leaf root)
+// Derived fields of a ray whose direction and translation are set.
+__device__ __forceinline__ void finish_ray(Ray& R) {
+    R.ix = 1 / R.rx; R.iy = 1 / R.ry; R.iz = 1 / R.rz;
+    R.ox = R.odx / R.rx; R.oy = R.ody / R.ry; R.oz = R.odz / R.rz;
+    R.sx = R.rx > 0; R.sy = R.ry > 0; R.sz = R.rz > 0;
+}
+
+// Seeds the pool with the root item of every lane whose root test passes (or
+// a leaf root); returns the item count.
+template <bool kCount>
+__device__ __forceinline__ int seed_root(const TraceParams& P, uint4* items, const Ray& R, bool live, int lane,
+                                         uint32_t& n_int, uint32_t& n_desc) {
     bool has = false;
     float r0t0 = 0.0f, r0t1 = 0.0f;
     if (live) {
@@ -612,15 +592,23 @@ __global__ __launch_bounds__(128) void k_trace_kd3(TraceParams P) {
         }
     }
     if (P.debug & 1) has = false;
-    {
-        const unsigned long long b = __ballot(has);
-        const uint32_t off = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
-        if (has) items[off] = make_uint4(P.root_ref, __float_as_uint(r0t0), __float_as_uint(r0t1), (uint32_t)lane << 26);
-    }
-    int n = __builtin_popcountll(__ballot(has));
-    const int cap = min(P.pool_cap, kCap);
+    const unsigned long long b = __ballot(has);
+    const uint32_t off = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+    if (has) items[off] = make_uint4(P.root_ref, __float_as_uint(r0t0), __float_as_uint(r0t1), (uint32_t)lane << 26);
     __builtin_amdgcn_wave_barrier();
+    return __builtin_popcountll(b);
+}
 
+// The pool walk of one wave.  kAny = false: nearest hit per ray, key[ray] =
+// min (w, path code), tri[ray] = its triangle.  kAny = true (shadow rays): any
+// accepted leaf with w < Lmax other than the ray's own hit triangle sets
+// key[ray] = 0; without counters the items of such rays are dropped.
+template <int kCap, int kVec, bool kTranslated, bool kCount, bool kAny>
+__device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, const float4* s_ray,
+                                          unsigned long long* s_key, uint32_t* s_tri, int n, int lane,
+                                          uint32_t& iters, uint32_t& n_int, uint32_t& n_leaf, uint32_t& n_acc,
+                                          uint32_t& n_desc) {
+    const int cap = min(P.pool_cap, kCap);
     while (n > 0) {
         // Parallel pops while the pool has room for all their children plus
         // the DFS slack below; single (DFS-like) pops otherwise.  A run of
@@ -630,7 +618,7 @@ __global__ __launch_bounds__(128) void k_trace_kd3(TraceParams P) {
         const int take = (n + 64 + kCodeBits + 1 <= cap) ? min(n, 64) : 1;
         iters++;
         const int base = n - take;
-        const bool act = lane < take;
+        bool act = lane < take;
         uint4 it = make_uint4(0, 0, 0, 0);
         if (act) it = items[base + lane];
         __builtin_amdgcn_wave_barrier();
@@ -639,13 +627,16 @@ __global__ __launch_bounds__(128) void k_trace_kd3(TraceParams P) {
         bool cand = false;
         unsigned long long key = 0;
         uint32_t ray = 0, ctri = 0;
+        if (act) ray = it.w >> 26;
+        // any-hit: a ray already shadowed needs no more visits (kept when
+        // counting, so the counters match the oracle's full walk)
+        if (kAny && !kCount && act && s_key[ray] == 0ull) act = false;
         if (act) {
-            ray = it.w >> 26;
             const uint32_t depth = (it.w >> kCodeBits) & 31u, code = it.w & kCodeMask;
-            const float4* rd = s_ray[wv][ray];
+            const float4* rd = s_ray + (size_t)ray * kVec;
             const float4 q0 = rd[0], q1 = rd[1], q2 = rd[2];
-            const float4 q3 = kTranslated ? rd[kRayVec - 2] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            const float4 q4 = kTranslated ? rd[kRayVec - 1] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            const float4 q3 = kTranslated ? rd[3] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            const float4 q4 = kTranslated ? rd[4] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             Ray Q;
             Q.rx = q0.x; Q.ry = q0.y; Q.rz = q0.z; Q.ix = q0.w;
             Q.iy = q1.x; Q.iz = q1.y; Q.ox = q1.z; Q.oy = q1.w;
@@ -655,12 +646,13 @@ __global__ __launch_bounds__(128) void k_trace_kd3(TraceParams P) {
             Q.sx = Q.rx > 0; Q.sy = Q.ry > 0; Q.sz = Q.rz > 0;
             if (it.x & kLeafBit) {
                 if (kCount) n_leaf++;
-                float d = kDrawDistance;
+                float d = kAny ? q4.z : kDrawDistance;
                 uint32_t best = kMiss;
-                if (leaf_test(Q, P.trec, it.x & ~kLeafBit, d, best)) {
+                if (leaf_test(Q, P.trec, it.x & ~kLeafBit, d, best) &&
+                    (!kAny || best != __float_as_uint(q4.w))) {
                     cand = true;
                     ctri = best;
-                    key = ((unsigned long long)__float_as_uint(d) << 32) | code;
+                    key = kAny ? 0ull : ((unsigned long long)__float_as_uint(d) << 32) | code;
                     if (kCount) n_acc++;
                 }
             } else {
@@ -719,11 +711,15 @@ __global__ __launch_bounds__(128) void k_trace_kd3(TraceParams P) {
                 }
             }
         }
-        // nearest candidate per ray: 64-bit min of (w, path code), then the
-        // unique lane holding the minimum records its triangle
-        if (cand) atomicMin(&s_key[wv][ray], key);
-        __builtin_amdgcn_wave_barrier();
-        if (cand && s_key[wv][ray] == key) s_tri[wv][ray] = ctri;
+        if (kAny) {
+            if (cand) s_key[ray] = 0ull;
+        } else {
+            // nearest candidate per ray: 64-bit min of (w, path code), then the
+            // unique lane holding the minimum records its triangle
+            if (cand) atomicMin(&s_key[ray], key);
+            __builtin_amdgcn_wave_barrier();
+            if (cand && s_key[ray] == key) s_tri[ray] = ctri;
+        }
         // push the children: ballot compaction onto the pool
         const unsigned long long b1 = __ballot(nk >= 1), b2 = __ballot(nk == 2);
         const uint32_t off = __builtin_amdgcn_mbcnt_hi((uint32_t)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b1, 0u)) +
@@ -737,6 +733,82 @@ __global__ __launch_bounds__(128) void k_trace_kd3(TraceParams P) {
         if (nk == 2) items[base + off + 1] = c1;
         n = base + total;
         __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// kRays pixels per wave (64: 8x8; 32: 8x4; 16: 8x2): fewer rays per wave
+// spread a heavy tile's items over more SIMDs, the other lanes only help.
+// kShadow: a second pool walk traces one shadow ray per hit (SURVEY.md §8a
+// a12; definition in oracle/oracle.c trace_shadow): the segment from the light
+// (2,2,2) to the hit, walked from the light with the reference's rules.
+template <int kRays, bool kTranslated, bool kWriteHit, bool kCount, bool kShadow>
+__global__ __launch_bounds__(128) void k_trace_kd3(TraceParams P) {
+    constexpr int kWaves = 2;
+    constexpr int kCap = pool_cap_for<kRays>();
+    constexpr int kRayVec = (kTranslated || kShadow) ? 5 : 3;  // float4s of per-ray data in LDS
+    __shared__ uint4 s_items[kWaves][kCap];
+    __shared__ float4 s_ray[kWaves][kRays * kRayVec];
+    __shared__ unsigned long long s_key[kWaves][kRays];
+    __shared__ uint32_t s_tri[kWaves][kRays];
+    const int wv = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
+    uint4* items = s_items[wv];
+    Pixel px;
+    const bool live = pixel_of_thread(P, px);  // every lane stays for the ballots
+    const unsigned long long t_start = P.dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    uint32_t iters = 0;
+
+    float cam[3] = {0.0f, 0.0f, 1.0f};
+    if (live) primary_ray(P, px.x, px.y, cam);
+    const float* X = P.xf;
+    Ray R;
+    R.odx = X[3]; R.ody = X[7]; R.odz = X[11];
+    R.rx = -1 * (X[0] * -cam[0] + X[1] * -cam[1] + X[2] * -cam[2]);
+    R.ry = -1 * (X[4] * -cam[0] + X[5] * -cam[1] + X[6] * -cam[2]);
+    R.rz = -1 * (X[8] * -cam[0] + X[9] * -cam[1] + X[10] * -cam[2]);
+    finish_ray(R);
+    if (lane < kRays) {
+        store_ray(&s_ray[wv][lane * kRayVec], R, kTranslated, 0.0f, 0u);
+        s_key[wv][lane] = ~0ull;
+        s_tri[wv][lane] = kMiss;
+    }
+
+    uint32_t n_int = 0, n_leaf = 0, n_acc = 0, n_desc = 0;
+    int n = seed_root<kCount>(P, items, R, live, lane, n_int, n_desc);
+    pool_walk<kCap, kRayVec, kTranslated, kCount, false>(P, items, s_ray[wv], s_key[wv], s_tri[wv], n, lane, iters,
+                                                        n_int, n_leaf, n_acc, n_desc);
+    unsigned long long kbest = ~0ull;
+    uint32_t best = kMiss;
+    if (lane < kRays) {
+        kbest = s_key[wv][lane];
+        best = kbest == ~0ull ? kMiss : s_tri[wv][lane];
+    }
+    bool shadowed = false;
+    if (kShadow) {
+        // the shadow segment of each hit: from the light to H = d*r - od
+        const bool sh_live = live && best != kMiss;
+        Ray S;
+        S.odx = -2.0f; S.ody = -2.0f; S.odz = -2.0f;
+        S.rx = 1.0f; S.ry = 1.0f; S.rz = 1.0f;
+        float lmax = 0.0f;
+        if (sh_live) {
+            const float d = __uint_as_float((uint32_t)(kbest >> 32));
+            float sx = ((d * R.rx) - R.odx) - 2;
+            float sy = ((d * R.ry) - R.ody) - 2;
+            float sz = ((d * R.rz) - R.odz) - 2;
+            lmax = sqrtf((sx * sx) + (sy * sy) + (sz * sz)) * 0.9990234375f;  // correctly rounded sqrt
+            const float r = rsqrt21(sx, sy, sz);
+            S.rx = sx * r; S.ry = sy * r; S.rz = sz * r;
+        }
+        finish_ray(S);
+        if (lane < kRays) {
+            store_ray(&s_ray[wv][lane * kRayVec], S, true, lmax, best);
+            s_key[wv][lane] = ~0ull;
+        }
+        __builtin_amdgcn_wave_barrier();
+        n = seed_root<kCount>(P, items, S, sh_live, lane, n_int, n_desc);
+        pool_walk<kCap, kRayVec, true, kCount, true>(P, items, s_ray[wv], s_key[wv], s_tri[wv], n, lane, iters,
+                                                    n_int, n_leaf, n_acc, n_desc);
+        if (lane < kRays) shadowed = s_key[wv][lane] == 0ull;
     }
 
     if (kCount) {
@@ -758,9 +830,9 @@ __global__ __launch_bounds__(128) void k_trace_kd3(TraceParams P) {
     }
     if (!live) return;
     uint32_t argb = kBackground;
-    const unsigned long long kbest = s_key[wv][lane];
-    const uint32_t best = kbest == ~0ull ? kMiss : s_tri[wv][lane];
-    if (best != kMiss) {
+    if (shadowed) {
+        argb = 0x00000000u;  // point_rad stays 0: 0/0 -> (u8)NaN = 0 (H14)
+    } else if (best != kMiss) {
         const float d = __uint_as_float((uint32_t)(kbest >> 32));
         const float4 N = P.shade[2 * (size_t)best];
         const float4 M = P.shade[2 * (size_t)best + 1];
@@ -980,12 +1052,17 @@ int launch_cam_nodes(const rt_kd_node* nodes, const int32_t* ids, const uint32_t
 using TraceFn = void (*)(TraceParams);
 
 template <bool T, bool H, bool C>
-TraceFn kd_kernel(int version, int rays) {
+TraceFn kd_kernel(int version, int rays, bool shadow) {
     if (version == 1) return k_trace_kd<T, H, C>;
     if (version == 2) return k_trace_kd2<T, H, C>;
-    if (rays == 16) return k_trace_kd3<16, T, H, C>;
-    if (rays == 32) return k_trace_kd3<32, T, H, C>;
-    return k_trace_kd3<64, T, H, C>;
+    if (shadow) {
+        if (rays == 16) return k_trace_kd3<16, T, H, C, true>;
+        if (rays == 32) return k_trace_kd3<32, T, H, C, true>;
+        return k_trace_kd3<64, T, H, C, true>;
+    }
+    if (rays == 16) return k_trace_kd3<16, T, H, C, false>;
+    if (rays == 32) return k_trace_kd3<32, T, H, C, false>;
+    return k_trace_kd3<64, T, H, C, false>;
 }
 
 int launch_trace(const TraceParams& p, uint32_t mode, uint32_t flags, int kernel_version, void* stream) {
@@ -1002,10 +1079,11 @@ int launch_trace(const TraceParams& p, uint32_t mode, uint32_t flags, int kernel
     } else {
         const bool tr = p.xf[3] != 0.0f || p.xf[7] != 0.0f || p.xf[11] != 0.0f;
         const int v = kernel_version, r = p.rays;
-        if (tr) fn = wh ? (cnt ? kd_kernel<true, true, true>(v, r) : kd_kernel<true, true, false>(v, r))
-                        : (cnt ? kd_kernel<true, false, true>(v, r) : kd_kernel<true, false, false>(v, r));
-        else fn = wh ? (cnt ? kd_kernel<false, true, true>(v, r) : kd_kernel<false, true, false>(v, r))
-                     : (cnt ? kd_kernel<false, false, true>(v, r) : kd_kernel<false, false, false>(v, r));
+        const bool sh = (flags & RT_FLAG_SHADOW) != 0;  // kernel 3 only (checked by the caller)
+        if (tr) fn = wh ? (cnt ? kd_kernel<true, true, true>(v, r, sh) : kd_kernel<true, true, false>(v, r, sh))
+                        : (cnt ? kd_kernel<true, false, true>(v, r, sh) : kd_kernel<true, false, false>(v, r, sh));
+        else fn = wh ? (cnt ? kd_kernel<false, true, true>(v, r, sh) : kd_kernel<false, true, false>(v, r, sh))
+                     : (cnt ? kd_kernel<false, false, true>(v, r, sh) : kd_kernel<false, false, false>(v, r, sh));
     }
     fn<<<grid, threads, 0, s>>>(p);
     return check_launch<void>(mode == RT_MODE_FLAT ? "k_trace_flat" : "k_trace_kd");

@@ -41,6 +41,13 @@ typedef enum rt_status {
 /* Render flags. */
 #define RT_FLAG_WRITE_HIT 1u   /* also write the per-pixel hit triangle (d_rmi.index) */
 #define RT_FLAG_COUNT 2u       /* accumulate traversal counters (rt_camera_counters)  */
+/* One shadow ray per hit pixel (config C5; the reference's commented-out hook
+ * at TD/Camera.cu:28-34).  The segment from the light (2,2,2) to the hit is
+ * walked with the reference's traversal rules; a pixel with an occluder
+ * (any triangle but its own, w < 0.999*|segment|) is 0x00000000.  KD mode and
+ * the wave-cooperative kernel only (tree height <= 21); the shadow rays'
+ * visits are added to the same counters. */
+#define RT_FLAG_SHADOW 4u
 
 /* Per-triangle AABB = kd_leaf (TD/Trixel.h:31-37); `tri` = tri_list_index. */
 typedef struct rt_leaf_aabb {

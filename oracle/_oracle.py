@@ -13,6 +13,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+FLAG_SHADOW = 4  # ORC_FLAG_SHADOW
 
 LEAF_DTYPE = np.dtype([
     ("x0", "<f4"), ("x1", "<f4"), ("y0", "<f4"), ("y1", "<f4"), ("z0", "<f4"), ("z1", "<f4"),
@@ -70,6 +71,7 @@ def lib():
         L.orc_scene_create.restype = P
         L.orc_scene_destroy.argtypes = [P]
         L.orc_render.argtypes = [P, P, C.c_int, C.c_int32, C.c_int32, P, P, P, C.c_int]
+        L.orc_render_ex.argtypes = [P, P, C.c_int, C.c_int, C.c_int32, C.c_int32, P, P, P, C.c_int]
         L.orc_primary_ray.argtypes = [C.POINTER(OrcCamera), C.c_int32, C.c_int32, P]
         L.orc_phong.argtypes = [P, P, P, P]
         L.orc_phong.restype = C.c_uint32
@@ -151,15 +153,16 @@ class Scene:
                                          None if self.nodes is None else _ptr(self.nodes),
                                          C.byref(cam))
 
-    def render(self, mode=0, xform=None, rows=None, nthreads=0, want_hit=True):
+    def render(self, mode=0, xform=None, rows=None, nthreads=0, want_hit=True, shadow=False):
+        """shadow=True: one shadow ray per hit (ORC_FLAG_SHADOW, KD only)."""
         w, h = self.cam.w, self.cam.h
         argb = np.zeros(w * h, np.uint32)
         hit = np.full(w * h, -1, np.int64) if want_hit else None
         cnt = np.zeros(6, np.uint64)
         r0, r1 = (0, h) if rows is None else rows
         X = None if xform is None else np.ascontiguousarray(xform, np.float32)
-        rc = lib().orc_render(self._h, None if X is None else _ptr(X), mode, r0, r1, _ptr(argb),
-                              None if hit is None else _ptr(hit), _ptr(cnt), nthreads)
+        rc = lib().orc_render_ex(self._h, None if X is None else _ptr(X), mode, FLAG_SHADOW if shadow else 0,
+                                 r0, r1, _ptr(argb), None if hit is None else _ptr(hit), _ptr(cnt), nthreads)
         if rc != 0:
             raise RuntimeError(f"orc_render failed: {rc}")
         return argb, hit, cnt

@@ -193,13 +193,11 @@ def _mt_accept(u, v, w, d):
     return (w < d) and not ((D(u) < EPS) or (D(v) < EPS) or (D(F(u + v)) > D(1) + EPS) or (D(w) < EPS))
 
 
-def trace_kd(S, X, cam_rmd):
-    """intersect_voxel_cuda, TD/Trixel.cu:41-172."""
-    d, rmi, out = F(400.0), -1, None
-    X = [F(x) for x in X]
-    od = (X[3], X[7], X[11])
-    m = [F(-c) for c in cam_rmd]
-    r = [F(F(-1) * F(F(F(X[4 * k] * m[0]) + F(X[4 * k + 1] * m[1])) + F(X[4 * k + 2] * m[2]))) for k in range(3)]
+def _walk(S, r, od, on_leaf):
+    """The DFS of intersect_voxel_cuda (TD/Trixel.cu:70-170) for direction r and
+    translation od; on_leaf(t, u, v, w) sees every non-degenerate MT test."""
+    inv = [F(F(1) / r[k]) for k in range(3)]
+    o = [F(od[k] / r[k]) for k in range(3)]
     stack = [0]
     while stack:
         cni = stack.pop()
@@ -216,23 +214,14 @@ def trace_kd(S, X, cam_rmd):
                 q = cross(tt, e1)
                 v = F(pe1 * dot(r, q))
                 w = F(pe1 * dot(e2, q))
-                if _mt_accept(u, v, w, d):
-                    d, rmi = w, t
-                    pnt = [F(F(d * r[k]) + od[k]) for k in range(3)]
-                    n = S["nrm"][t]
-                    a = [F(F(-1) * n[k]) for k in range(3)]
-                    nr = [F(F(F(F(F(a[0] * X[4 * k]) + F(a[1] * X[4 * k + 1])) + F(a[2] * X[4 * k + 2]))) * F(-1))
-                          for k in range(3)]
-                    out = (pnt, nr)
+                on_leaf(t, u, v, w)
             continue
         bo = vx["bo"]
-        inv = [F(F(1) / r[k]) for k in range(3)]
         t0 = [F(bo[k] * inv[k]) if r[k] > 0 else F(bo[k + 3] * inv[k]) for k in range(3)]
         t1 = [F(bo[k + 3] * inv[k]) if r[k] > 0 else F(bo[k] * inv[k]) for k in range(3)]
         cf = vx["cf"]
         dr = F(F(F(r[0] * cf[0]) + F(r[1] * cf[1])) + F(r[2] * cf[2]))
         ds = F(F(F(od[0] * cf[0]) + F(od[1] * cf[1])) + F(od[2] * cf[2]))
-        o = [F(od[k] / r[k]) for k in range(3)]
         maxt0 = np.fmax(F(t0[2] + o[2]), np.fmax(F(t0[0] + o[0]), F(t0[1] + o[1])))
         mint1 = np.fmin(F(t1[2] + o[2]), np.fmin(F(t1[0] + o[0]), F(t1[1] + o[1])))
         if D(mint1) >= D(maxt0) - EPS and D(maxt0) > -EPS:
@@ -247,7 +236,50 @@ def trace_kd(S, X, cam_rmd):
                 if mint1 < s1 or maxt0 < s1:
                     stack.append(vx["left"])
                 stack.append(vx["right"])
-    return rmi, d, out
+
+
+def trace_kd(S, X, cam_rmd):
+    """intersect_voxel_cuda, TD/Trixel.cu:41-172.  Returns (rmi, d, (pnt, nrm),
+    (r, od)) -- the last pair is the object-space ray, for the shadow ray."""
+    X = [F(x) for x in X]
+    od = (X[3], X[7], X[11])
+    m = [F(-c) for c in cam_rmd]
+    r = [F(F(-1) * F(F(F(X[4 * k] * m[0]) + F(X[4 * k + 1] * m[1])) + F(X[4 * k + 2] * m[2]))) for k in range(3)]
+    st = dict(d=F(400.0), rmi=-1, out=None)
+
+    def leaf(t, u, v, w):
+        if _mt_accept(u, v, w, st["d"]):
+            st["d"], st["rmi"] = w, t
+            pnt = [F(F(w * r[k]) + od[k]) for k in range(3)]
+            n = S["nrm"][t]
+            a = [F(F(-1) * n[k]) for k in range(3)]
+            nr = [F(F(F(F(F(a[0] * X[4 * k]) + F(a[1] * X[4 * k + 1])) + F(a[2] * X[4 * k + 2]))) * F(-1))
+                  for k in range(3)]
+            st["out"] = (pnt, nr)
+
+    _walk(S, r, od, leaf)
+    return st["rmi"], st["d"], st["out"], (r, od)
+
+
+SHADOW_SCALE = F(0.9990234375)  # 1 - 2^-10
+
+
+def trace_shadow(S, rmi, d, ray):
+    """The shadow segment of a hit (oracle.c trace_shadow): from the light
+    (2,2,2) to H = d*r - od, walked from the light; True if occluded."""
+    r, od = ray
+    sv = [F(F(F(d * r[k]) - od[k]) - F(2)) for k in range(3)]
+    L2 = F(F(F(sv[0] * sv[0]) + F(sv[1] * sv[1])) + F(sv[2] * sv[2]))
+    lmax = F(F(np.sqrt(D(L2))) * SHADOW_SCALE)
+    s = dev_normalize(*sv)
+    hit = [False]
+
+    def leaf(t, u, v, w):
+        if t != rmi and _mt_accept(u, v, w, lmax):
+            hit[0] = True
+
+    _walk(S, list(s), (F(-2), F(-2), F(-2)), leaf)
+    return hit[0]
 
 
 def trace_flat(S, rmd):
@@ -296,7 +328,7 @@ def phong(pnt, nrm, rmd, rad):
 RAD = (F(0.1), F(0.55), F(0.2))
 
 
-def render(points9, nodes, cam, mode=0, xform=None):
+def render(points9, nodes, cam, mode=0, xform=None, shadow=False):
     S = prepare(points9, nodes if mode == 0 else None, cam)
     X = IDENT if xform is None else np.asarray(xform, F)
     w, h = cam["w"], cam["h"]
@@ -306,9 +338,14 @@ def render(points9, nodes, cam, mode=0, xform=None):
         for iy in range(h):
             for ix in range(w):
                 rmd = primary_ray(cam, ix, iy)
-                rmi, d, out = trace_kd(S, X, rmd) if mode == 0 else trace_flat(S, rmd)
+                if mode == 0:
+                    rmi, d, out, ray = trace_kd(S, X, rmd)
+                else:
+                    rmi, d, out = trace_flat(S, rmd)
                 i = iy * w + ix
                 hit[i] = rmi
                 if rmi >= 0:
                     argb[i] = phong(out[0], out[1], rmd, RAD)
+                    if shadow and trace_shadow(S, rmi, d, ray):
+                        argb[i] = 0
     return argb, hit

@@ -611,6 +611,7 @@ typedef struct {
     int64_t rmi;
     float d;
     float rad[3], pnt[3], nrm[3];
+    float r[3], od[3];   /* the object-space ray and translation used */
 } orc_hit;
 
 /* intersect_voxel_cuda, TD/Trixel.cu:41-172, one pixel. */
@@ -625,6 +626,8 @@ static int trace_kd(const orc_scene* s, const float* X, const float cam_rmd[3],
     float rx = -1 * (X[0] * -cam_rmd[0] + X[1] * -cam_rmd[1] + X[2] * -cam_rmd[2]);
     float ry = -1 * (X[4] * -cam_rmd[0] + X[5] * -cam_rmd[1] + X[6] * -cam_rmd[2]);
     float rz = -1 * (X[8] * -cam_rmd[0] + X[9] * -cam_rmd[1] + X[10] * -cam_rmd[2]);
+    out->r[0] = rx; out->r[1] = ry; out->r[2] = rz;
+    out->od[0] = odx; out->od[1] = ody; out->od[2] = odz;
     while (top >= 0) {
         int32_t cni = stack[top--];
         if (s->is_leaf[cni]) {
@@ -698,6 +701,107 @@ static int trace_kd(const orc_scene* s, const float* X, const float cam_rmd[3],
     return rc;
 }
 
+/* Shadow ray, one per hit.  Not in the
+ * reference: its hook is the commented-out test at TD/Camera.cu:28-34, so
+ * the definition is ours, shared bit for bit with the kernels:
+ *   - the occluder test is the segment between the light (2,2,2) of
+ *     TD/Camera.cu:32 and the primary hit H = d*r - od (the point the
+ *     traversal's own origin -od reaches, TD/Trixel.cu:90-109; H == pnt
+ *     for the identity transform);
+ *   - the segment is walked FROM THE LIGHT: the reference's box-entry rule
+ *     (maxt0 > -eps, TD/Trixel.cu:95) culls every box that contains the
+ *     origin, so a ray leaving the surface would cull the root.  From the
+ *     light (outside the model) the reference's rules apply unchanged:
+ *     origin via the translation od_L = -(2,2,2), direction
+ *     s = normalize(H - (2,2,2)) with the 21-step device rsqrt;
+ *   - it is shadowed iff some visited leaf other than the hit triangle passes
+ *     the MT tests (TD/Trixel.cu:104-120) with w < Lmax,
+ *     Lmax = |H - (2,2,2)| * (1 - 2^-10) (a relative bias, exact in f32);
+ *   - a shadowed pixel keeps point_rad = 0, so the reference's formula gives
+ *     0/0 -> (u8)NaN = 0 in every channel: 0x00000000 (H14).
+ * Any-hit is an OR over the visited leaves, so the result does not depend on
+ * the visiting order.  Every leaf is visited here (no early exit) so the visit
+ * counters are deterministic; the kernels stop early unless counting. */
+#define ORC_SHADOW_SCALE 0.9990234375f
+
+static int trace_shadow(const orc_scene* s, const float r[3], const float od[3], float L, int64_t self,
+                        uint64_t* cnt) {
+    int32_t stack[ORC_STACK_CAP];
+    int top = 0, shadowed = 0;
+    stack[0] = 0;
+    const float rx = r[0], ry = r[1], rz = r[2], odx = od[0], ody = od[1], odz = od[2];
+    while (top >= 0) {
+        int32_t cni = stack[top--];
+        if (s->is_leaf[cni]) {
+            cnt[ORC_CNT_LEAF]++;
+            int64_t t = s->tri[cni];
+            const float* e1 = s->e1 + 3 * t; const float* e2 = s->e2 + 3 * t;
+            const float* dt = s->dt + 3 * t;
+            float px, py, pz;
+            cross3(&px, &py, &pz, rx, ry, rz, e2[0], e2[1], e2[2]);
+            float f = dot3(px, py, pz, e1[0], e1[1], e1[2]);
+            if (!((double)f < ORC_EPS && (double)f > -ORC_EPS)) {
+                float pe1 = (float)(1.0 / (double)f);
+                float tx = dt[0] - odx, ty = dt[1] - ody, tz = dt[2] - odz;
+                float u = pe1 * dot3(px, py, pz, tx, ty, tz);
+                float qx, qy, qz;
+                cross3(&qx, &qy, &qz, tx, ty, tz, e1[0], e1[1], e1[2]);
+                float v = pe1 * dot3(rx, ry, rz, qx, qy, qz);
+                float w = pe1 * dot3(e2[0], e2[1], e2[2], qx, qy, qz);
+                if ((w < L) && !(((double)u < ORC_EPS) || ((double)v < ORC_EPS) ||
+                                 ((double)(u + v) > 1 + ORC_EPS) || ((double)w < ORC_EPS)) &&
+                    t != self) {
+                    cnt[ORC_CNT_ACCEPT]++;
+                    shadowed = 1;
+                }
+            }
+            continue;
+        }
+        cnt[ORC_CNT_INTERIOR]++;
+        const float* b = s->bo + 6 * (int64_t)cni;
+        float t0x = rx > 0 ? b[0] * (1 / rx) : b[3] * (1 / rx);
+        float t1x = rx > 0 ? b[3] * (1 / rx) : b[0] * (1 / rx);
+        float t0y = ry > 0 ? b[1] * (1 / ry) : b[4] * (1 / ry);
+        float t1y = ry > 0 ? b[4] * (1 / ry) : b[1] * (1 / ry);
+        float t0z = rz > 0 ? b[2] * (1 / rz) : b[5] * (1 / rz);
+        float t1z = rz > 0 ? b[5] * (1 / rz) : b[2] * (1 / rz);
+        const uint8_t* cf = s->cut + 3 * (int64_t)cni;
+        float dir = ((rx * cf[0]) + (ry * cf[1]) + (rz * cf[2]));
+        float ds = ((odx * cf[0]) + (ody * cf[1]) + (odz * cf[2]));
+        float maxt0 = fmaxf(t0z + odz / rz, fmaxf(t0x + odx / rx, t0y + ody / ry));
+        float mint1 = fminf(t1z + odz / rz, fminf(t1x + odx / rx, t1y + ody / ry));
+        if ((double)mint1 >= (double)maxt0 - ORC_EPS && (double)maxt0 > -ORC_EPS) {
+            cnt[ORC_CNT_DESCEND]++;
+            maxt0 *= dir; mint1 *= dir;
+            float s1 = (float)((double)s->s1[cni] + ORC_EPS + (double)ds);
+            float s2 = s->s2[cni] + ds;
+            int32_t Lc = (int32_t)s->left[cni], Rc = (int32_t)s->right[cni];
+            if ((double)maxt0 < (double)s2 + ORC_EPS) {
+                if ((double)mint1 > (double)s2 - ORC_EPS) stack[++top] = Rc;
+                stack[++top] = Lc;
+            } else {
+                if (mint1 < s1 || maxt0 < s1) stack[++top] = Lc;
+                stack[++top] = Rc;
+            }
+            if (top + 2 >= ORC_STACK_CAP) return -1;
+        }
+    }
+    return shadowed;
+}
+
+/* The shadow ray of a primary hit (see trace_shadow): direction, translated
+ * origin and segment length, exactly as the kernels compute them. */
+static void shadow_ray(const orc_hit* h, float sdir[3], float od_l[3], float* Lmax) {
+    float sx = ((h->d * h->r[0]) - h->od[0]) - 2;
+    float sy = ((h->d * h->r[1]) - h->od[1]) - 2;
+    float sz = ((h->d * h->r[2]) - h->od[2]) - 2;
+    float L = (float)sqrt((double)((sx * sx) + (sy * sy) + (sz * sz)));
+    *Lmax = L * ORC_SHADOW_SCALE;
+    dev_normalize(&sx, &sy, &sz);
+    sdir[0] = sx; sdir[1] = sy; sdir[2] = sz;
+    od_l[0] = -2; od_l[1] = -2; od_l[2] = -2;
+}
+
 /* intersect_trixel_cuda, TD/Trixel.cu:173-209, one pixel (never launched by
  * the reference; BASELINE config 2). */
 static void trace_flat(const orc_scene* s, const float rmd[3], orc_hit* out, uint64_t* cnt) {
@@ -734,12 +838,19 @@ static void trace_flat(const orc_scene* s, const float rmd[3], orc_hit* out, uin
 int orc_render(const orc_scene* s, const float xform[12], int mode, int32_t row0,
                int32_t row1, uint32_t* argb, int64_t* hit, uint64_t counters[ORC_CNT_N],
                int nthreads) {
+    return orc_render_ex(s, xform, mode, 0, row0, row1, argb, hit, counters, nthreads);
+}
+
+int orc_render_ex(const orc_scene* s, const float xform[12], int mode, int flags, int32_t row0,
+                  int32_t row1, uint32_t* argb, int64_t* hit, uint64_t counters[ORC_CNT_N],
+                  int nthreads) {
     static const float ident[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
     const float* X = xform ? xform : ident;
     const int32_t w = s->cam.w;
     if (row0 < 0) row0 = 0;
     if (row1 > s->cam.h) row1 = s->cam.h;
     if (mode == 0 && !s->bo) return -2;
+    if ((flags & ORC_FLAG_SHADOW) && mode != 0) return -3;
     int status = 0;
     uint64_t tot[ORC_CNT_N] = {0};
 #ifdef _OPENMP
@@ -768,6 +879,13 @@ int orc_render(const orc_scene* s, const float xform[12], int mode, int32_t row0
                 if (h.rmi >= 0) {
                     cnt[ORC_CNT_HITPIX]++;
                     c = orc_phong(h.pnt, h.nrm, rmd, h.rad);
+                    if (flags & ORC_FLAG_SHADOW) {
+                        float sd[3], odl[3], Lmax;
+                        shadow_ray(&h, sd, odl, &Lmax);
+                        int sh = trace_shadow(s, sd, odl, Lmax, h.rmi, cnt);
+                        if (sh < 0) st = -1;
+                        if (sh > 0) c = 0x00000000u;
+                    }
                 }
                 if (argb) argb[i] = c;
                 if (hit) hit[i] = h.rmi;

@@ -115,12 +115,22 @@ int orc_render(const orc_scene* s, const float xform[12], int mode,
                int32_t row0, int32_t row1, uint32_t* argb, int64_t* hit,
                uint64_t counters[ORC_CNT_N], int nthreads);
 
+/* orc_render with flags.  ORC_FLAG_SHADOW (KD mode only): one shadow ray
+ * per hit pixel (definition in oracle.c trace_shadow);
+ * shadowed pixels are 0x00000000 and the shadow rays' visits are added to
+ * the same counters.  Returns -3 for shadow with mode 1. */
+#define ORC_FLAG_SHADOW 4
+int orc_render_ex(const orc_scene* s, const float xform[12], int mode, int flags,
+                  int32_t row0, int32_t row1, uint32_t* argb, int64_t* hit,
+                  uint64_t counters[ORC_CNT_N], int nthreads);
+
 /* One primary ray (init_cam_mem_cuda, TD/Camera.cu:103-104). */
 void orc_primary_ray(const orc_camera* cam, int32_t ix, int32_t iy, float out[3]);
 
-/* Phong of one hit (color_cam_cuda, TD/Camera.cu:27-60). */
+/* Per-pixel visit counts (interior + leaf pops) of the KD traversal. */
 int orc_pixel_visits(const orc_scene* s, const float xform[12], uint32_t* visits, int nthreads);
 
+/* Phong of one hit (color_cam_cuda, TD/Camera.cu:27-60). */
 uint32_t orc_phong(const float pnt[3], const float nrm[3], const float rmd[3],
                    const float rad[3]);
 

@@ -46,13 +46,13 @@ def trees(name):
     return _tree_cache[name]
 
 
-def oracle_render(name, w, h, mode=0, xform=None, rows=None, cam_kw=None):
+def oracle_render(name, w, h, mode=0, xform=None, rows=None, cam_kw=None, shadow=False):
     pts, _, _ = mesh(name)
     onodes = trees(name)[1] if mode == 0 else None
     cam = O.camera(w, h, **(cam_kw or {}))
     s = O.Scene(pts, O.default_rad(len(pts)), onodes, cam)
     try:
-        return s.render(mode, xform=xform, rows=rows, nthreads=ORACLE_THREADS)
+        return s.render(mode, xform=xform, rows=rows, nthreads=ORACLE_THREADS, shadow=shadow)
     finally:
         s.close()
 
@@ -81,10 +81,10 @@ class GpuScene:
         self.obj = R.Object(self.trixel)
         self.cam.add_object(self.obj)
 
-    def render(self, mode=0, xform=None, count=False):
+    def render(self, mode=0, xform=None, count=False, shadow=False):
         if xform is not None:
             self.obj.quat.rot_m = np.asarray(xform, np.float32).reshape(3, 4)
-        flags = R.RT_FLAG_WRITE_HIT | (R.RT_FLAG_COUNT if count else 0)
+        flags = R.RT_FLAG_WRITE_HIT | (R.RT_FLAG_COUNT if count else 0) | (R.RT_FLAG_SHADOW if shadow else 0)
         self.obj.render(self.cam, mode=mode, flags=flags)
         self.cam.color_pixels(R.PHONG_COLOR_TAG)
         cnt = self.cam.counters() if count else None

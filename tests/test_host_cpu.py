@@ -257,6 +257,83 @@ def test_single_triangle_analytic_distance():
     assert abs(1.5 / r[2] - 1.5) < 1e-3
 
 
+# ---------------------------------------------------------------- shadow rays
+
+@pytest.mark.parametrize("name,w,h", [("dump", 40, 24), ("rabbit_70k", 64, 36)])
+def test_shadow_oracle_matches_numpy_golden(name, w, h):
+    """RT_FLAG_SHADOW: the C oracle against the numpy restatement's frames."""
+    g = H.golden()
+    argb, hit, _ = H.oracle_render(name, w, h, 0, shadow=True)
+    key = f"{name}_{w}x{h}_shadow"
+    assert (hit == g[key + "_hit"]).all()
+    assert (argb == g[key + "_argb"]).all()
+    assert ((argb == 0) & (hit >= 0)).sum() > 10
+
+
+@pytest.mark.parametrize("name,w,h", [("rabbit_70k", 960, 540), ("dump", 320, 180)])
+def test_shadow_oracle_matches_recorded_hashes(name, w, h):
+    g = H.golden()
+    argb, hit, cnt = H.oracle_render(name, w, h, 0, shadow=True)
+    key = f"{name}_{w}x{h}_shadow"
+    assert hashlib.sha256(argb.tobytes()).hexdigest() == str(g[key + "_argb_sha"])
+    assert (cnt == g[key + "_counters"]).all()
+
+
+def test_shadow_only_darkens_hit_pixels():
+    """Shadows change nothing but the colour of some hit pixels (to 0), and
+    add the shadow walks' visits to the counters."""
+    a0, h0, c0 = H.oracle_render("rabbit_70k", 320, 180, 0)
+    a1, h1, c1 = H.oracle_render("rabbit_70k", 320, 180, 0, shadow=True)
+    assert (h0 == h1).all()
+    changed = a0 != a1
+    assert (h0[changed] >= 0).all() and (a1[changed] == 0).all()
+    assert 0 < changed.sum() < (h0 >= 0).sum()
+    assert c1[3] == c0[3] and c1[0] > c0[0] and c1[1] > c0[1]
+
+
+def test_shadow_matches_bruteforce_segment_test():
+    """Geometric meaning of the shadow definition: the KD walk from the light
+    finds an occluder on the light->hit segment for (almost) exactly the
+    pixels a float64 brute-force test over every triangle does (the rest are
+    epsilon/boundary cases of the reference's traversal rules)."""
+    import ctypes as C
+    name, w, h = "rabbit_70k", 160, 90
+    pts, _, _ = H.mesh(name)
+    a0, hit, _ = H.oracle_render(name, w, h, 0)
+    a1, _, _ = H.oracle_render(name, w, h, 0, shadow=True)
+    cam = O.camera(w, h)
+    pos = np.array(cam.pos[:3], np.float64)
+    T = pts.reshape(-1, 3, 3).astype(np.float64) - pos
+    p0, e1, e2 = T[:, 0], T[:, 1] - T[:, 0], T[:, 2] - T[:, 0]
+
+    def mt(o, dv):
+        pv = np.cross(dv, e2)
+        det = (pv * e1).sum(1)
+        with np.errstate(all="ignore"):
+            inv = 1 / det
+            tv = o - p0
+            u = (tv * pv).sum(1) * inv
+            q = np.cross(tv, e1)
+            return u, (q * dv).sum(1) * inv, (q * e2).sum(1) * inv, np.abs(det) > 1e-20
+
+    idx = np.flatnonzero(hit >= 0)
+    out = (C.c_float * 3)()
+    agree = 0
+    for i in idx:
+        iy, ix = divmod(int(i), w)
+        O.lib().orc_primary_ray(C.byref(cam), ix, iy, out)
+        r = np.array(out[:], np.float64)
+        k = hit[i]
+        t_hit = mt(np.zeros(3), r)[2][k]
+        seg = t_hit * r - 2.0
+        L = np.linalg.norm(seg)
+        u, v, t, ok = mt(np.full(3, 2.0), seg / L)
+        occ = ok & (u >= 0) & (v >= 0) & (u + v <= 1) & (t > 1e-12) & (t < 0.999 * L)
+        occ[k] = False
+        agree += bool(occ.any()) == bool(a1[i] == 0)
+    assert len(idx) > 400 and agree >= 0.99 * len(idx)
+
+
 # ---------------------------------------------------------------- sharding
 
 def test_band_pack_unpack_roundtrip():
