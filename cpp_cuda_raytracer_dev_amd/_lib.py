@@ -24,6 +24,7 @@ RT_FLAG_SHADOW = 4
 RT_OPT_KERNEL = 1
 RT_OPT_TILE_ORDER = 2
 RT_OPT_RAYS = 3
+RT_OPT_ITEMS = 4
 RT_OPT_DEBUG = 100
 RT_OPT_POOL_CAP = 101
 

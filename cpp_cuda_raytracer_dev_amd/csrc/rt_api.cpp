@@ -55,7 +55,8 @@ struct rt_camera {
     int32_t* d_order = nullptr;      // centre-out tile permutation
     int64_t order_cap = 0;
     int64_t order_key[6] = {-1, -1, -1, -1, -1, -1};
-    int rays = 32;                   // kOptRays: pixels per wave of kernel 3
+    int rays = 16;                   // kOptRays: pixels per wave of kernel 3
+    int items = 2;                   // kOptItems: items per lane per pool iteration
 };
 
 namespace {
@@ -202,6 +203,7 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
     p.order = nullptr;
     p.debug = c->debug;
     p.pool_cap = c->pool_cap;
+    p.items = c->items;
     p.dbg = nullptr;
     if (c->debug & 2) {
         const int64_t need = (int64_t)p.tiles_x * p.block_rows * 4 * 3;  // <= 4 waves per block
@@ -497,6 +499,10 @@ extern "C" int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value) {
     case kOptRays:
         if (value != 16 && value != 32 && value != 64) return fail(RT_ERR_INVALID, "rays per wave %d (16, 32, 64)", value);
         c->rays = value;
+        return RT_OK;
+    case kOptItems:
+        if (value != 1 && value != 2) return fail(RT_ERR_INVALID, "items per lane %d (1, 2)", value);
+        c->items = value;
         return RT_OK;
     case kOptPoolCap:
         // the 64 root items plus a DFS run of height <= 21 must fit

@@ -42,6 +42,7 @@ enum Option : int32_t {
     kOptKernel = 1,     // KD kernel version: 1 (node-own box, 48 B) or 2 (child boxes, 64 B)
     kOptTileOrder = 2,  // 0 XCD-contiguous, 1 natural, 2 centre-out
     kOptRays = 3,       // kernel 3 pixels per wave: 64, 32 or 16
+    kOptItems = 4,      // kernel 3 items popped per lane per iteration: 1 or 2
     kOptDebug = 100,    // diagnostics: 1 = skip traversal, 2 = per-wave timestamps
     kOptPoolCap = 101,  // tests: shrink kernel 3's item pool (66..kPoolCap) to force its fallback
 };
@@ -85,6 +86,7 @@ struct TraceParams {
     const int32_t* order;          // centre-out tile permutation (tile_order 2)
     float root_box[6];             // camera-relative root AABB (t0x,t1x,t0y,t1y,t0z,t1z)
     int32_t pool_cap;              // kernel 3 item-pool capacity in use (<= kPoolCap)
+    int32_t items;                 // kernel 3 items per lane per iteration (1 or 2)
     int32_t debug;                 // diagnostic builds only: 1 = skip traversal
     unsigned long long* dbg;       // per-wave (t_start, t_end, visits) when non-null
     uint32_t root_ref;

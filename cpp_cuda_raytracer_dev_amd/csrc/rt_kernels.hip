@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+
 #include "rt_internal.h"
 
 namespace rt {
@@ -68,7 +69,7 @@ __device__ __forceinline__ uint32_t to_u8(float t) {
 }
 
 // color_cam_cuda, TD/Camera.cu:27-60 (norm.x used twice in the dot, H1).
-__device__ uint32_t phong(const float pnt[3], const float nrm[3], const float rmd[3],
+__device__ __forceinline__ uint32_t phong(const float pnt[3], const float nrm[3], const float rmd[3],
                           const float rad[3]) {
     float sdx = 2 - pnt[0], sdy = 2 - pnt[1], sdz = 2 - pnt[2];
     const float r = rsqrt21(sdx, sdy, sdz);
@@ -91,8 +92,7 @@ __device__ uint32_t phong(const float pnt[3], const float nrm[3], const float rm
 // each XCD a contiguous run of tiles (bijective for any grid size); order 1:
 // natural (neighbouring tiles on different XCDs); order 2: the host's
 // centre-out permutation, so the heavy centre tiles are dispatched first.
-__device__ __forceinline__ void tile_of_block(const TraceParams& P, int32_t& tx, int32_t& slot) {
-    const int32_t b = (int32_t)blockIdx.x;
+__device__ __forceinline__ void tile_of(const TraceParams& P, int32_t b, int32_t& tx, int32_t& slot) {
     const int32_t nblocks = P.tiles_x * P.block_rows;
     int32_t t;
     if (P.tile_order == 0) {
@@ -113,15 +113,16 @@ struct Pixel {
     int64_t out;       // index into the (packed) output buffer
 };
 
-// A block covers tile_w x tile_h pixels of one 8-row band; each wave owns an
-// 8 x (rays/8) sub-tile (side by side when tile_w > 8, stacked otherwise).
-// Lanes >= rays own no pixel (the wave-cooperative kernel's helper lanes).
-__device__ __forceinline__ bool pixel_of_thread(const TraceParams& P, Pixel& px) {
+// Tile b covers tile_w x tile_h pixels of one 8-row band; wave `wave` of it
+// owns an 8 x (rays/8) sub-tile (side by side when tile_w > 8, stacked
+// otherwise).  Lanes >= rays own no pixel (the wave-cooperative kernel's
+// helper lanes).
+__device__ __forceinline__ bool pixel_of(const TraceParams& P, int32_t b, int32_t wave, Pixel& px) {
     int32_t tx, row;
-    tile_of_block(P, tx, row);
+    tile_of(P, b, tx, row);
     const int32_t per_band = kTileH / P.tile_h;
     const int32_t slot = row / per_band, yin = (row - slot * per_band) * P.tile_h;
-    const int32_t lane = (int32_t)threadIdx.x & 63, wave = (int32_t)threadIdx.x >> 6;
+    const int32_t lane = (int32_t)threadIdx.x & 63;
     const int32_t wrows = P.rays >> 3;
     const int32_t wx = P.tile_w > 8 ? wave * 8 : 0, wy = P.tile_w > 8 ? 0 : wave * wrows;
     const int32_t band = P.rank + slot * P.nranks;
@@ -130,6 +131,11 @@ __device__ __forceinline__ bool pixel_of_thread(const TraceParams& P, Pixel& px)
     px.y = band * kTileH + ly;
     px.out = (int64_t)(slot * kTileH + ly) * P.w + px.x;
     return lane < P.rays && px.x < P.w && px.y < P.h;
+}
+
+// One tile per block (blockIdx), one sub-tile per wave.
+__device__ __forceinline__ bool pixel_of_thread(const TraceParams& P, Pixel& px) {
+    return pixel_of(P, (int32_t)blockIdx.x, (int32_t)threadIdx.x >> 6, px);
 }
 
 // init_cam_mem_cuda, TD/Camera.cu:103-104: rmd = n + u*ix + v*iy, normalised.
@@ -334,11 +340,8 @@ __device__ __forceinline__ bool slab(const Ray& R, float lx, float hx, float ly,
 
 // Moller-Trumbore at a leaf, TD/Trixel.cu:98-145; updates (d, best) on a
 // strictly nearer accepted hit.
-__device__ __forceinline__ bool leaf_test(const Ray& R, const float4* __restrict__ trec, uint32_t t,
-                                          float& d, uint32_t& best) {
-    const float4 A = trec[4 * (size_t)t];
-    const float4 B = trec[4 * (size_t)t + 1];
-    const float4 Cq = trec[4 * (size_t)t + 2];
+__device__ __forceinline__ bool leaf_test_rec(const Ray& R, const float4 A, const float4 B, const float4 Cq,
+                                              uint32_t t, float& d, uint32_t& best) {
     const float e1x = A.x, e1y = A.y, e1z = A.z;
     const float e2x = A.w, e2y = B.x, e2z = B.y;
     const float dtx = B.z, dty = B.w, dtz = Cq.x;
@@ -361,6 +364,11 @@ __device__ __forceinline__ bool leaf_test(const Ray& R, const float4* __restrict
         }
     }
     return false;
+}
+
+__device__ __forceinline__ bool leaf_test(const Ray& R, const float4* __restrict__ trec, uint32_t t,
+                                          float& d, uint32_t& best) {
+    return leaf_test_rec(R, trec[4 * (size_t)t], trec[4 * (size_t)t + 1], trec[4 * (size_t)t + 2], t, d, best);
 }
 
 // intersect_voxel_cuda (TD/Trixel.cu:41-172) fused with set_cam_cuda +
@@ -543,8 +551,14 @@ struct Item {
 
 // Pool capacity per wave for kRays rays (the DFS fallback keeps any
 // capacity >= 86 correct; these cover the measured peaks with margin).
+#ifndef RT_POOL_CAP_R32
+#define RT_POOL_CAP_R32 448
+#endif
+#ifndef RT_POOL_CAP_R16
+#define RT_POOL_CAP_R16 320
+#endif
 template <int kRays>
-constexpr int pool_cap_for() { return kRays == 64 ? kPoolCap : kRays == 32 ? 448 : 320; }
+constexpr int pool_cap_for() { return kRays == 64 ? kPoolCap : kRays == 32 ? RT_POOL_CAP_R32 : RT_POOL_CAP_R16; }
 
 // Per-ray data of the pool walk in LDS: rd[0] = (rx, ry, rz, 1/rx),
 // rd[1] = (1/ry, 1/rz, odx/rx, ody/ry), rd[2] = (odz/rz, dir per cut axis),
@@ -599,161 +613,220 @@ __device__ __forceinline__ int seed_root(const TraceParams& P, uint4* items, con
     return __builtin_popcountll(b);
 }
 
+// One popped item's outcome: up to two children and a candidate hit.
+struct Visit {
+    uint4 c0, c1;
+    int nk;
+    bool cand;
+    unsigned long long key;
+    uint32_t ctri;
+};
+
+// The 64-B record of an item: a node's child-box record, or a leaf's
+// triangle record (tri_world relative to the camera).
+__device__ __forceinline__ const float4* record_of(const TraceParams& P, uint32_t ref) {
+    return (ref & kLeafBit) ? P.trec + 4 * (size_t)(ref & ~kLeafBit) : P.inode + 4 * (size_t)ref;
+}
+
+// Visits one item whose record (r0..r3) has arrived: the leaf's MT test, or
+// the node's child ordering (TD/Trixel.cu:146-170) and the children's slab
+// tests.  kAny: shadow walk (Lmax and the hit triangle come from rd[4]).
+template <int kVec, bool kTranslated, bool kCount, bool kAny>
+__device__ __forceinline__ void visit_item(const float4* rd, uint4 it, float4 r0, float4 r1, float4 r2, float4 r3,
+                                           Visit& o, uint32_t& n_int, uint32_t& n_leaf, uint32_t& n_acc,
+                                           uint32_t& n_desc) {
+    const uint32_t ray = it.w >> 26;
+    const uint32_t depth = (it.w >> kCodeBits) & 31u, code = it.w & kCodeMask;
+    const float4 q0 = rd[0], q1 = rd[1], q2 = rd[2];
+    const float4 q3 = kTranslated ? rd[3] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const float4 q4 = kTranslated ? rd[4] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    Ray Q;
+    Q.rx = q0.x; Q.ry = q0.y; Q.rz = q0.z; Q.ix = q0.w;
+    Q.iy = q1.x; Q.iz = q1.y; Q.ox = q1.z; Q.oy = q1.w;
+    Q.oz = q2.x;
+    // object translation (exact zeros when untranslated, as X[3], X[7], X[11] are)
+    Q.odx = kTranslated ? q3.x : 0.0f; Q.ody = kTranslated ? q3.y : 0.0f; Q.odz = kTranslated ? q3.z : 0.0f;
+    Q.sx = Q.rx > 0; Q.sy = Q.ry > 0; Q.sz = Q.rz > 0;
+    if (it.x & kLeafBit) {
+        if (kCount) n_leaf++;
+        float d = kAny ? q4.z : kDrawDistance;
+        uint32_t best = kMiss;
+        if (leaf_test_rec(Q, r0, r1, r2, it.x & ~kLeafBit, d, best) && (!kAny || best != __float_as_uint(q4.w))) {
+            o.cand = true;
+            o.ctri = best;
+            o.key = kAny ? 0ull : ((unsigned long long)__float_as_uint(d) << 32) | code;
+            if (kCount) n_acc++;
+        }
+        return;
+    }
+    const uint32_t lw = __float_as_uint(r3.z);
+    const uint32_t axis = (lw >> kAxisShift) & 3u;
+    const uint32_t L = lw & ~(3u << kAxisShift), Rr = __float_as_uint(r3.w);
+    const float dir = axis == 0 ? q2.y : axis == 1 ? q2.z : q2.w;
+    const float mx = __uint_as_float(it.y) * dir, mn = __uint_as_float(it.z) * dir;
+    float s1, s2;
+    if (kTranslated) {
+        const float ds = axis == 0 ? q3.w : axis == 1 ? q4.x : q4.y;
+        s1 = (float)((double)r3.x + kEps + (double)ds);
+        s2 = r3.y + ds;
+    } else {
+        s1 = (float)((double)r3.x + kEps);
+        s2 = r3.y;
+    }
+    bool left_first, push_second;
+    if ((double)mx < (double)s2 + kEps) {
+        left_first = true;
+        push_second = (double)mn > (double)s2 - kEps;
+    } else {
+        left_first = false;
+        push_second = (mn < s1 || mx < s1);
+    }
+    const uint32_t first = left_first ? L : Rr;
+    const uint32_t second = left_first ? Rr : L;
+    // children's slab tests from the boxes in this record
+    float lt0, lt1, rt0, rt1;
+    const bool lpass = slab(Q, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, lt0, lt1);
+    const bool rpass = slab(Q, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w, rt0, rt1);
+    const bool first_leaf = (first & kLeafBit) != 0, second_leaf = (second & kLeafBit) != 0;
+    const bool keep_first = first_leaf || (left_first ? lpass : rpass);
+    const bool keep_second = push_second && (second_leaf || (left_first ? rpass : lpass));
+    if (kCount) {
+        n_int += (first_leaf ? 0u : 1u) + ((push_second && !second_leaf) ? 1u : 0u);
+        n_desc += ((!first_leaf && keep_first) ? 1u : 0u) + ((push_second && !second_leaf && keep_second) ? 1u : 0u);
+    }
+    const uint32_t cd = depth + 1;
+    const uint32_t bit = 1u << (kCodeBits - cd);
+    const uint32_t meta_first = (ray << 26) | (cd << kCodeBits) | code;
+    const uint32_t meta_second = meta_first | bit;
+    const float f0 = left_first ? lt0 : rt0, f1 = left_first ? lt1 : rt1;
+    const float g0 = left_first ? rt0 : lt0, g1 = left_first ? rt1 : lt1;
+    const uint4 A = make_uint4(first, __float_as_uint(f0), __float_as_uint(f1), meta_first);
+    const uint4 B = make_uint4(second, __float_as_uint(g0), __float_as_uint(g1), meta_second);
+    o.c0 = keep_first ? A : B;
+    o.c1 = B;
+    o.nk = (keep_first ? 1 : 0) + (keep_second ? 1 : 0);
+}
+
+__device__ __forceinline__ uint32_t lanes_below(unsigned long long b) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+}
+
 // The pool walk of one wave.  kAny = false: nearest hit per ray, key[ray] =
 // min (w, path code), tri[ray] = its triangle.  kAny = true (shadow rays): any
 // accepted leaf with w < Lmax other than the ray's own hit triangle sets
 // key[ray] = 0; without counters the items of such rays are dropped.
+// Each lane pops up to P.items (1 or 2) items per iteration and fetches their
+// records together, so a lane keeps two memory round trips in flight.
 template <int kCap, int kVec, bool kTranslated, bool kCount, bool kAny>
 __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, const float4* s_ray,
                                           unsigned long long* s_key, uint32_t* s_tri, int n, int lane,
                                           uint32_t& iters, uint32_t& n_int, uint32_t& n_leaf, uint32_t& n_acc,
                                           uint32_t& n_desc) {
     const int cap = min(P.pool_cap, kCap);
+    const int per = P.items > 1 ? 128 : 64;
     while (n > 0) {
-        // Parallel pops while the pool has room for all their children plus
-        // the DFS slack below; single (DFS-like) pops otherwise.  A run of
-        // single pops starting at n0 never holds more than n0 + height items
-        // (height <= 21), and parallel pops leave n <= cap - 22, so the pool
-        // never overflows.
-        const int take = (n + 64 + kCodeBits + 1 <= cap) ? min(n, 64) : 1;
+        // Pop as many items as the pool has room for the children of plus
+        // the DFS slack below; a single (DFS-like) pop when there is none.
+        // Popping k items pushes at most 2k, so a parallel pop leaves
+        // n <= cap - 22; a run of single pops starting at n0 never holds
+        // more than n0 + height items (height <= 21), so the pool never
+        // overflows.
+        int take = min(min(n, per), cap - kCodeBits - 1 - n);
+        if (take < 1) take = 1;
         iters++;
         const int base = n - take;
-        bool act = lane < take;
-        uint4 it = make_uint4(0, 0, 0, 0);
-        if (act) it = items[base + lane];
+        bool act0 = lane < take, act1 = lane + 64 < take;
+        uint4 it0 = make_uint4(0, 0, 0, 0), it1 = make_uint4(0, 0, 0, 0);
+        if (act0) it0 = items[base + lane];
+        if (act1) it1 = items[base + 64 + lane];
         __builtin_amdgcn_wave_barrier();
-        int nk = 0;
-        uint4 c0 = make_uint4(0, 0, 0, 0), c1 = make_uint4(0, 0, 0, 0);
-        bool cand = false;
-        unsigned long long key = 0;
-        uint32_t ray = 0, ctri = 0;
-        if (act) ray = it.w >> 26;
         // any-hit: a ray already shadowed needs no more visits (kept when
         // counting, so the counters match the oracle's full walk)
-        if (kAny && !kCount && act && s_key[ray] == 0ull) act = false;
-        if (act) {
-            const uint32_t depth = (it.w >> kCodeBits) & 31u, code = it.w & kCodeMask;
-            const float4* rd = s_ray + (size_t)ray * kVec;
-            const float4 q0 = rd[0], q1 = rd[1], q2 = rd[2];
-            const float4 q3 = kTranslated ? rd[3] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            const float4 q4 = kTranslated ? rd[4] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            Ray Q;
-            Q.rx = q0.x; Q.ry = q0.y; Q.rz = q0.z; Q.ix = q0.w;
-            Q.iy = q1.x; Q.iz = q1.y; Q.ox = q1.z; Q.oy = q1.w;
-            Q.oz = q2.x;
-            // object translation (exact zeros when untranslated, as X[3], X[7], X[11] are)
-            Q.odx = kTranslated ? q3.x : 0.0f; Q.ody = kTranslated ? q3.y : 0.0f; Q.odz = kTranslated ? q3.z : 0.0f;
-            Q.sx = Q.rx > 0; Q.sy = Q.ry > 0; Q.sz = Q.rz > 0;
-            if (it.x & kLeafBit) {
-                if (kCount) n_leaf++;
-                float d = kAny ? q4.z : kDrawDistance;
-                uint32_t best = kMiss;
-                if (leaf_test(Q, P.trec, it.x & ~kLeafBit, d, best) &&
-                    (!kAny || best != __float_as_uint(q4.w))) {
-                    cand = true;
-                    ctri = best;
-                    key = kAny ? 0ull : ((unsigned long long)__float_as_uint(d) << 32) | code;
-                    if (kCount) n_acc++;
-                }
-            } else {
-                float4 r0, r1, r2, r3;
-                load_record(P.inode + 4 * (size_t)it.x, r0, r1, r2, r3);
-                const uint32_t lw = __float_as_uint(r3.z);
-                const uint32_t axis = (lw >> kAxisShift) & 3u;
-                const uint32_t L = lw & ~(3u << kAxisShift), Rr = __float_as_uint(r3.w);
-                const float dir = axis == 0 ? q2.y : axis == 1 ? q2.z : q2.w;
-                const float mx = __uint_as_float(it.y) * dir, mn = __uint_as_float(it.z) * dir;
-                float s1, s2;
-                if (kTranslated) {
-                    const float ds = axis == 0 ? q3.w : axis == 1 ? q4.x : q4.y;
-                    s1 = (float)((double)r3.x + kEps + (double)ds);
-                    s2 = r3.y + ds;
-                } else {
-                    s1 = (float)((double)r3.x + kEps);
-                    s2 = r3.y;
-                }
-                bool left_first, push_second;
-                if ((double)mx < (double)s2 + kEps) {
-                    left_first = true;
-                    push_second = (double)mn > (double)s2 - kEps;
-                } else {
-                    left_first = false;
-                    push_second = (mn < s1 || mx < s1);
-                }
-                const uint32_t first = left_first ? L : Rr;
-                const uint32_t second = left_first ? Rr : L;
-                // children's slab tests from the boxes in this record
-                float lt0, lt1, rt0, rt1;
-                const bool lpass = slab(Q, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, lt0, lt1);
-                const bool rpass = slab(Q, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w, rt0, rt1);
-                const bool first_leaf = (first & kLeafBit) != 0, second_leaf = (second & kLeafBit) != 0;
-                const bool keep_first = first_leaf || (left_first ? lpass : rpass);
-                const bool keep_second = push_second && (second_leaf || (left_first ? rpass : lpass));
-                if (kCount) {
-                    n_int += (first_leaf ? 0u : 1u) + ((push_second && !second_leaf) ? 1u : 0u);
-                    n_desc += ((!first_leaf && keep_first) ? 1u : 0u) + ((push_second && !second_leaf && keep_second) ? 1u : 0u);
-                }
-                const uint32_t cd = depth + 1;
-                const uint32_t bit = 1u << (kCodeBits - cd);
-                const uint32_t meta_first = (ray << 26) | (cd << kCodeBits) | code;
-                const uint32_t meta_second = meta_first | bit;
-                const float f0 = left_first ? lt0 : rt0, f1 = left_first ? lt1 : rt1;
-                const float g0 = left_first ? rt0 : lt0, g1 = left_first ? rt1 : lt1;
-                const uint4 A = make_uint4(first, __float_as_uint(f0), __float_as_uint(f1), meta_first);
-                const uint4 B = make_uint4(second, __float_as_uint(g0), __float_as_uint(g1), meta_second);
-                if (keep_first) {
-                    c0 = A;
-                    nk = 1;
-                    if (keep_second) { c1 = B; nk = 2; }
-                } else if (keep_second) {
-                    c0 = B;
-                    nk = 1;
-                }
-            }
+        if (kAny && !kCount) {
+            if (act0 && s_key[it0.w >> 26] == 0ull) act0 = false;
+            if (act1 && s_key[it1.w >> 26] == 0ull) act1 = false;
         }
+        // both records in flight before either is consumed
+        float4 a0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), a1 = a0, a2 = a0, a3 = a0;
+        float4 b0 = a0, b1 = a0, b2 = a0, b3 = a0;
+        if (act0) {
+            const float4* p = record_of(P, it0.x);
+            a0 = p[0]; a1 = p[1]; a2 = p[2]; a3 = p[3];
+        }
+        if (act1) {
+            const float4* p = record_of(P, it1.x);
+            b0 = p[0]; b1 = p[1]; b2 = p[2]; b3 = p[3];
+        }
+        asm volatile("" ::"v"(a0.x), "v"(a0.y), "v"(a0.z), "v"(a0.w), "v"(a1.x), "v"(a1.y), "v"(a1.z), "v"(a1.w),
+                     "v"(a2.x), "v"(a2.y), "v"(a2.z), "v"(a2.w), "v"(a3.x), "v"(a3.y), "v"(a3.z), "v"(a3.w));
+        asm volatile("" ::"v"(b0.x), "v"(b0.y), "v"(b0.z), "v"(b0.w), "v"(b1.x), "v"(b1.y), "v"(b1.z), "v"(b1.w),
+                     "v"(b2.x), "v"(b2.y), "v"(b2.z), "v"(b2.w), "v"(b3.x), "v"(b3.y), "v"(b3.z), "v"(b3.w));
+        Visit v0, v1;
+        v0.nk = 0; v0.cand = false; v0.key = 0; v0.ctri = 0;
+        v0.c0 = v0.c1 = make_uint4(0, 0, 0, 0);
+        v1 = v0;
+        if (act0)
+            visit_item<kVec, kTranslated, kCount, kAny>(s_ray + (size_t)(it0.w >> 26) * kVec, it0, a0, a1, a2, a3, v0,
+                                                        n_int, n_leaf, n_acc, n_desc);
+        if (act1)
+            visit_item<kVec, kTranslated, kCount, kAny>(s_ray + (size_t)(it1.w >> 26) * kVec, it1, b0, b1, b2, b3, v1,
+                                                        n_int, n_leaf, n_acc, n_desc);
+        const uint32_t ray0 = it0.w >> 26, ray1 = it1.w >> 26;
         if (kAny) {
-            if (cand) s_key[ray] = 0ull;
+            if (v0.cand) s_key[ray0] = 0ull;
+            if (v1.cand) s_key[ray1] = 0ull;
         } else {
             // nearest candidate per ray: 64-bit min of (w, path code), then the
-            // unique lane holding the minimum records its triangle
-            if (cand) atomicMin(&s_key[ray], key);
+            // unique item holding the minimum records its triangle
+            if (v0.cand) atomicMin(&s_key[ray0], v0.key);
+            if (v1.cand) atomicMin(&s_key[ray1], v1.key);
             __builtin_amdgcn_wave_barrier();
-            if (cand && s_key[ray] == key) s_tri[ray] = ctri;
+            if (v0.cand && s_key[ray0] == v0.key) s_tri[ray0] = v0.ctri;
+            if (v1.cand && s_key[ray1] == v1.key) s_tri[ray1] = v1.ctri;
         }
-        // push the children: ballot compaction onto the pool
-        const unsigned long long b1 = __ballot(nk >= 1), b2 = __ballot(nk == 2);
-        const uint32_t off = __builtin_amdgcn_mbcnt_hi((uint32_t)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b1, 0u)) +
-                             __builtin_amdgcn_mbcnt_hi((uint32_t)(b2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b2, 0u));
-        const int total = __builtin_popcountll(b1) + __builtin_popcountll(b2);
+        // push the children (item 0's, then item 1's): ballot compaction
+        const int cnt = v0.nk + v1.nk;
+        const unsigned long long m1 = __ballot(cnt >= 1), m2 = __ballot(cnt >= 2);
+        const unsigned long long m3 = __ballot(cnt >= 3), m4 = __ballot(cnt >= 4);
+        const uint32_t off = lanes_below(m1) + lanes_below(m2) + lanes_below(m3) + lanes_below(m4);
+        const int total = __builtin_popcountll(m1) + __builtin_popcountll(m2) + __builtin_popcountll(m3) +
+                          __builtin_popcountll(m4);
         if (base + total > cap) {  // unreachable by the pop rule above; guard anyway
             if (lane == 0) atomicOr(P.err, 2);
             break;
         }
-        if (nk >= 1) items[base + off] = c0;
-        if (nk == 2) items[base + off + 1] = c1;
+        const uint4 s0 = v0.nk >= 1 ? v0.c0 : v1.c0;
+        const uint4 s1 = v0.nk == 2 ? v0.c1 : (v0.nk == 1 ? v1.c0 : v1.c1);
+        const uint4 s2 = v0.nk == 2 ? v1.c0 : v1.c1;
+        if (cnt >= 1) items[base + off] = s0;
+        if (cnt >= 2) items[base + off + 1] = s1;
+        if (cnt >= 3) items[base + off + 2] = s2;
+        if (cnt >= 4) items[base + off + 3] = v1.c1;
         n = base + total;
         __builtin_amdgcn_wave_barrier();
     }
 }
 
-// kRays pixels per wave (64: 8x8; 32: 8x4; 16: 8x2): fewer rays per wave
-// spread a heavy tile's items over more SIMDs, the other lanes only help.
-// kShadow: a second pool walk traces one shadow ray per hit (SURVEY.md §8a
-// a12; definition in oracle/oracle.c trace_shadow): the segment from the light
-// (2,2,2) to the hit, walked from the light with the reference's rules.
-template <int kRays, bool kTranslated, bool kWriteHit, bool kCount, bool kShadow>
-__global__ __launch_bounds__(128) void k_trace_kd3(TraceParams P) {
-    constexpr int kWaves = 2;
-    constexpr int kCap = pool_cap_for<kRays>();
-    constexpr int kRayVec = (kTranslated || kShadow) ? 5 : 3;  // float4s of per-ray data in LDS
-    __shared__ uint4 s_items[kWaves][kCap];
-    __shared__ float4 s_ray[kWaves][kRays * kRayVec];
-    __shared__ unsigned long long s_key[kWaves][kRays];
-    __shared__ uint32_t s_tri[kWaves][kRays];
-    const int wv = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
-    uint4* items = s_items[wv];
+// Per-wave LDS of the wave-cooperative kernel.
+template <int kRays, int kCap, int kRayVec>
+struct WaveLds {
+    uint4 items[kCap];
+    float4 ray[kRays * kRayVec];
+    unsigned long long key[kRays];
+    uint32_t tri[kRays];
+};
+
+struct Counts {
+    uint32_t n_int = 0, n_leaf = 0, n_acc = 0, n_desc = 0, n_hit = 0;
+};
+
+// One wave's unit of work: the kRays pixels of sub-tile `wave` of tile b.
+template <int kRays, int kCap, int kRayVec, bool kTranslated, bool kWriteHit, bool kCount, bool kShadow>
+__device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, kCap, kRayVec>& S_, int32_t b,
+                                           int32_t wave, int lane, size_t dbg_slot, Counts& C) {
+    uint4* items = S_.items;
     Pixel px;
-    const bool live = pixel_of_thread(P, px);  // every lane stays for the ballots
+    const bool live = pixel_of(P, b, wave, px);  // every lane stays for the ballots
     const unsigned long long t_start = P.dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
     uint32_t iters = 0;
 
@@ -767,28 +840,27 @@ __global__ __launch_bounds__(128) void k_trace_kd3(TraceParams P) {
     R.rz = -1 * (X[8] * -cam[0] + X[9] * -cam[1] + X[10] * -cam[2]);
     finish_ray(R);
     if (lane < kRays) {
-        store_ray(&s_ray[wv][lane * kRayVec], R, kTranslated, 0.0f, 0u);
-        s_key[wv][lane] = ~0ull;
-        s_tri[wv][lane] = kMiss;
+        store_ray(&S_.ray[lane * kRayVec], R, kTranslated, 0.0f, 0u);
+        S_.key[lane] = ~0ull;
+        S_.tri[lane] = kMiss;
     }
 
-    uint32_t n_int = 0, n_leaf = 0, n_acc = 0, n_desc = 0;
-    int n = seed_root<kCount>(P, items, R, live, lane, n_int, n_desc);
-    pool_walk<kCap, kRayVec, kTranslated, kCount, false>(P, items, s_ray[wv], s_key[wv], s_tri[wv], n, lane, iters,
-                                                        n_int, n_leaf, n_acc, n_desc);
+    int n = seed_root<kCount>(P, items, R, live, lane, C.n_int, C.n_desc);
+    pool_walk<kCap, kRayVec, kTranslated, kCount, false>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters, C.n_int,
+                                                        C.n_leaf, C.n_acc, C.n_desc);
     unsigned long long kbest = ~0ull;
     uint32_t best = kMiss;
     if (lane < kRays) {
-        kbest = s_key[wv][lane];
-        best = kbest == ~0ull ? kMiss : s_tri[wv][lane];
+        kbest = S_.key[lane];
+        best = kbest == ~0ull ? kMiss : S_.tri[lane];
     }
     bool shadowed = false;
     if (kShadow) {
         // the shadow segment of each hit: from the light to H = d*r - od
         const bool sh_live = live && best != kMiss;
-        Ray S;
-        S.odx = -2.0f; S.ody = -2.0f; S.odz = -2.0f;
-        S.rx = 1.0f; S.ry = 1.0f; S.rz = 1.0f;
+        Ray Sh;
+        Sh.odx = -2.0f; Sh.ody = -2.0f; Sh.odz = -2.0f;
+        Sh.rx = 1.0f; Sh.ry = 1.0f; Sh.rz = 1.0f;
         float lmax = 0.0f;
         if (sh_live) {
             const float d = __uint_as_float((uint32_t)(kbest >> 32));
@@ -797,37 +869,25 @@ __global__ __launch_bounds__(128) void k_trace_kd3(TraceParams P) {
             float sz = ((d * R.rz) - R.odz) - 2;
             lmax = sqrtf((sx * sx) + (sy * sy) + (sz * sz)) * 0.9990234375f;  // correctly rounded sqrt
             const float r = rsqrt21(sx, sy, sz);
-            S.rx = sx * r; S.ry = sy * r; S.rz = sz * r;
+            Sh.rx = sx * r; Sh.ry = sy * r; Sh.rz = sz * r;
         }
-        finish_ray(S);
+        finish_ray(Sh);
         if (lane < kRays) {
-            store_ray(&s_ray[wv][lane * kRayVec], S, true, lmax, best);
-            s_key[wv][lane] = ~0ull;
+            store_ray(&S_.ray[lane * kRayVec], Sh, true, lmax, best);
+            S_.key[lane] = ~0ull;
         }
         __builtin_amdgcn_wave_barrier();
-        n = seed_root<kCount>(P, items, S, sh_live, lane, n_int, n_desc);
-        pool_walk<kCap, kRayVec, true, kCount, true>(P, items, s_ray[wv], s_key[wv], s_tri[wv], n, lane, iters,
-                                                    n_int, n_leaf, n_acc, n_desc);
-        if (lane < kRays) shadowed = s_key[wv][lane] == 0ull;
+        n = seed_root<kCount>(P, items, Sh, sh_live, lane, C.n_int, C.n_desc);
+        pool_walk<kCap, kRayVec, true, kCount, true>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters, C.n_int,
+                                                    C.n_leaf, C.n_acc, C.n_desc);
+        if (lane < kRays) shadowed = S_.key[lane] == 0ull;
     }
-
-    if (kCount) {
-        // every lane (also those past the frame edge) processed pool items;
-        // counter [2] counts valid candidates here (>= the DFS's accept events)
-        wave_count_add(&P.counters[0], n_int);
-        wave_count_add(&P.counters[1], n_leaf);
-        wave_count_add(&P.counters[2], n_acc);
-        wave_count_add(&P.counters[4], n_desc);
+    if (P.dbg && lane == 0) {  // diagnostics: the unit's start/end clock (100 MHz) and pool iterations
+        P.dbg[3 * dbg_slot] = t_start;
+        P.dbg[3 * dbg_slot + 1] = __builtin_amdgcn_s_memrealtime();
+        P.dbg[3 * dbg_slot + 2] = iters;
     }
-    if (P.dbg) {  // diagnostic build: wave start/end clock and its pool iterations
-        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();  // 100 MHz
-        const size_t wvg = (size_t)blockIdx.x * (blockDim.x >> 6) + wv;
-        if (lane == 0) {
-            P.dbg[3 * wvg] = t_start;
-            P.dbg[3 * wvg + 1] = t_end;
-            P.dbg[3 * wvg + 2] = iters;
-        }
-    }
+    __builtin_amdgcn_wave_barrier();  // LDS of this unit is read; the next unit may overwrite it
     if (!live) return;
     uint32_t argb = kBackground;
     if (shadowed) {
@@ -847,7 +907,33 @@ __global__ __launch_bounds__(128) void k_trace_kd3(TraceParams P) {
     }
     P.argb[px.out] = argb;
     if (kWriteHit) P.hit[px.out] = best == kMiss ? (int64_t)-1 : (int64_t)best;
-    if (kCount) wave_count_add(&P.counters[3], best != kMiss ? 1u : 0u);
+    if (kCount && best != kMiss) C.n_hit++;
+}
+
+// kRays pixels per wave (64: 8x8; 32: 8x4; 16: 8x2): fewer rays per wave
+// spread a heavy tile's items over more SIMDs, the other lanes only help.
+// kShadow: a second pool walk traces one shadow ray per hit (SURVEY.md §8a
+// a12; definition in oracle/oracle.c trace_shadow): the segment from the light
+// (2,2,2) to the hit, walked from the light with the reference's rules.
+template <int kRays, bool kTranslated, bool kWriteHit, bool kCount, bool kShadow>
+__global__ __launch_bounds__(128) void k_trace_kd3(TraceParams P) {
+    constexpr int kWaves = 2;
+    constexpr int kCap = pool_cap_for<kRays>();
+    constexpr int kRayVec = (kTranslated || kShadow) ? 5 : 3;  // float4s of per-ray data in LDS
+    __shared__ WaveLds<kRays, kCap, kRayVec> s_lds[kWaves];
+    const int wv = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
+    Counts C;
+    trace_unit<kRays, kCap, kRayVec, kTranslated, kWriteHit, kCount, kShadow>(
+        P, s_lds[wv], (int32_t)blockIdx.x, wv, lane, (size_t)blockIdx.x * kWaves + wv, C);
+    if (kCount) {
+        // every lane (also those past the frame edge) processed pool items;
+        // counter [2] counts valid candidates here (>= the DFS's accept events)
+        wave_count_add(&P.counters[0], C.n_int);
+        wave_count_add(&P.counters[1], C.n_leaf);
+        wave_count_add(&P.counters[2], C.n_acc);
+        wave_count_add(&P.counters[3], C.n_hit);
+        wave_count_add(&P.counters[4], C.n_desc);
+    }
 }
 
 // -------------------------------------------------------------- flat trace
@@ -1051,18 +1137,18 @@ int launch_cam_nodes(const rt_kd_node* nodes, const int32_t* ids, const uint32_t
 
 using TraceFn = void (*)(TraceParams);
 
+template <bool T, bool H, bool C, bool S>
+TraceFn kd3_kernel(int rays) {
+    if (rays == 16) return k_trace_kd3<16, T, H, C, S>;
+    if (rays == 32) return k_trace_kd3<32, T, H, C, S>;
+    return k_trace_kd3<64, T, H, C, S>;
+}
+
 template <bool T, bool H, bool C>
 TraceFn kd_kernel(int version, int rays, bool shadow) {
     if (version == 1) return k_trace_kd<T, H, C>;
     if (version == 2) return k_trace_kd2<T, H, C>;
-    if (shadow) {
-        if (rays == 16) return k_trace_kd3<16, T, H, C, true>;
-        if (rays == 32) return k_trace_kd3<32, T, H, C, true>;
-        return k_trace_kd3<64, T, H, C, true>;
-    }
-    if (rays == 16) return k_trace_kd3<16, T, H, C, false>;
-    if (rays == 32) return k_trace_kd3<32, T, H, C, false>;
-    return k_trace_kd3<64, T, H, C, false>;
+    return shadow ? kd3_kernel<T, H, C, true>(rays) : kd3_kernel<T, H, C, false>(rays);
 }
 
 int launch_trace(const TraceParams& p, uint32_t mode, uint32_t flags, int kernel_version, void* stream) {

@@ -183,7 +183,8 @@ int rt_camera_info(const rt_camera* c, int32_t* w, int32_t* h, int32_t* max_dept
  * Every setting renders the identical frame. */
 #define RT_OPT_KERNEL 1
 #define RT_OPT_TILE_ORDER 2
-#define RT_OPT_RAYS 3 /* kernel 3: pixels per wave (64, 32 default, 16); the rest of the lanes help */
+#define RT_OPT_RAYS 3 /* kernel 3: pixels per wave (64, 32, 16 default); the rest of the lanes help */
+#define RT_OPT_ITEMS 4 /* kernel 3: items each lane pops per iteration (1, 2 default) */
 int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value);
 
 /* Diagnostics (key 100 of rt_camera_set_option: 1 = skip traversal,

@@ -60,7 +60,7 @@ def oracle_render(name, w, h, mode=0, xform=None, rows=None, cam_kw=None, shadow
 class GpuScene:
     """Trixel + Camera + Object through the product API."""
 
-    def __init__(self, name, w, h, cam_kw=None, device=0, kernel=None, tile_order=None, rays=None):
+    def __init__(self, name, w, h, cam_kw=None, device=0, kernel=None, tile_order=None, rays=None, items=None):
         pts, leafs, _ = mesh(name)
         self.trixel = R.Trixel(len(pts), pts, device=device)
         self.trixel.set_kd_nodes(trees(name)[0])
@@ -78,6 +78,8 @@ class GpuScene:
             self.cam.set_option(_lib.RT_OPT_TILE_ORDER, tile_order)
         if rays is not None:
             self.cam.set_option(_lib.RT_OPT_RAYS, rays)
+        if items is not None:
+            self.cam.set_option(_lib.RT_OPT_ITEMS, items)
         self.obj = R.Object(self.trixel)
         self.cam.add_object(self.obj)
 

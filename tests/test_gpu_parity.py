@@ -155,6 +155,18 @@ def test_camera_poses_rabbit(pose):
     _assert_same((argb, hit), (oargb, ohit), f"pose {pose}")
 
 
+@pytest.mark.parametrize("items", [1, 2])
+@pytest.mark.parametrize("rays", [64, 32, 16])
+@pytest.mark.parametrize("shadow", [False, True])
+def test_items_per_lane(items, rays, shadow):
+    """Kernel 3 pops one or two items per lane per iteration; same frame and counters."""
+    s = H.GpuScene("dragon", 960, 540, kernel=3, rays=rays, items=items)
+    argb, hit, cnt = s.render(0, count=True, shadow=shadow)
+    oargb, ohit, ocnt = H.oracle_render("dragon", 960, 540, 0, shadow=shadow)
+    _assert_same((argb, hit), (oargb, ohit), f"items {items} rays {rays}")
+    _counters_match(cnt, ocnt, 3)
+
+
 @pytest.mark.parametrize("cap", [86, 96, 200])
 def test_pool_capacity_fallback(cap):
     """A small item pool forces the wave-cooperative kernel's single-item

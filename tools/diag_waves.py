@@ -23,7 +23,8 @@ def main():
     kernel = int(sys.argv[4]) if len(sys.argv) > 4 else 3
     rays = int(sys.argv[5]) if len(sys.argv) > 5 else 32
     order = int(sys.argv[6]) if len(sys.argv) > 6 else 2
-    s = H.GpuScene(name, w, h, kernel=kernel, tile_order=order, rays=rays)
+    items = int(sys.argv[7]) if len(sys.argv) > 7 else 2
+    s = H.GpuScene(name, w, h, kernel=kernel, tile_order=order, rays=rays, items=items)
     out = torch.zeros(w * h, dtype=torch.int32, device="cuda:0")
     st = torch.cuda.Stream()
 
@@ -38,12 +39,12 @@ def main():
         st.synchronize()
         return e0.elapsed_time(e1) / n
 
-    res = {"scene": name, "w": w, "h": h, "kernel": kernel, "full_ms": timed()}
+    res = {"scene": name, "w": w, "h": h, "kernel": kernel, "rays": rays, "items": items, "full_ms": timed()}
     s.cam.set_option(_lib.RT_OPT_DEBUG, 1)
     res["no_traversal_ms"] = timed()
     s.cam.set_option(_lib.RT_OPT_DEBUG, 2)
     res["with_stamps_ms"] = timed(5)
-    nw = ((w + 7) // 8) * ((h + 7) // 8) * 8
+    nw = ((w + 7) // 8) * ((h + 7) // 8) * (64 // rays) * 2
     buf = np.zeros(3 * nw, np.uint64)
     got = _lib.lib().rt_camera_debug_read(s.cam._h, _lib.ptr(buf), len(buf))
     rec = buf[:got].reshape(-1, 3).astype(np.int64)

@@ -21,4 +21,4 @@ for ctr in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
     if [ $rc -ne 0 ]; then tail -20 "$OUT/pass$i.log"; exit $rc; fi
 done
 grep -h '^{' "$OUT/pass1.log" | head -1 > "$OUT/bench_line.json"
-python3 tools/pmc_traffic.py "${PMC_KEY:-dragon_1920x1080_m0_n1}" "${PMC_KERNEL:-k_trace_kd3<32}" "$OUT"/pass*
+python3 tools/pmc_traffic.py "${PMC_KEY:-dragon_1920x1080_m0_n1}" "${PMC_KERNEL:-k_trace_kd3<16}" "$OUT"/pass*
