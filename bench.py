@@ -47,9 +47,12 @@ def parse():
     ap.add_argument("--kernel", type=int, default=3,
                     help="KD kernel: 1 per-lane DFS (own-box records), 2 per-lane DFS (child-box records), "
                          "3 wave-cooperative item pool")
-    ap.add_argument("--tile-order", type=int, default=2, help="0 XCD-contiguous, 1 natural, 2 centre-out")
-    ap.add_argument("--rays", type=int, default=16, help="kernel 3: pixels per wave (64, 32, 16)")
+    ap.add_argument("--tile-order", type=int, default=3,
+                    help="0 XCD-contiguous, 1 natural, 2 centre-out, 3 by the cost an earlier frame measured")
+    ap.add_argument("--rays", type=int, default=16, help="kernel 3: pixels per wave (64, 32, 16, 8)")
     ap.add_argument("--items", type=int, default=2, help="kernel 3: items each lane pops per iteration (1, 2)")
+    ap.add_argument("--coarse", type=int, default=8,
+                    help="kernel 3: 8x8 groups per wave outside the root box's screen rectangle (0 = off)")
     ap.add_argument("--shadow", action="store_true",
                     help="one shadow ray per hit (config C5: --scene happy --width 3840 --height 2160 --shadow)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
@@ -142,6 +145,7 @@ def main():
     cam.set_option(_lib.RT_OPT_KERNEL, a.kernel)
     cam.set_option(_lib.RT_OPT_RAYS, a.rays)
     cam.set_option(_lib.RT_OPT_ITEMS, a.items)
+    cam.set_option(_lib.RT_OPT_COARSE, a.coarse)
     cam.render_into(scratch, mode=a.mode, flags=sflag, tile=tile if world > 1 else None,
                     stream=sptr)  # re-prepares layout
     torch.cuda.synchronize(dev)
@@ -241,10 +245,11 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": {1: "k_trace_kd", 2: "k_trace_kd2", 3: "k_trace_kd3"}[a.kernel] if a.mode == 0
+                "kernel": {1: "k_trace_kd", 2: "k_trace_kd2",
+                           3: "k_trace_kd3" + (" + k_coarse_kd3" if a.coarse else "")}[a.kernel] if a.mode == 0
                           else "k_trace_flat",
                 "kernel_options": {"kernel": a.kernel, "tile_order": a.tile_order, "rays_per_wave": a.rays,
-                                   "items_per_lane": a.items,
+                                   "items_per_lane": a.items, "coarse_groups_per_wave": a.coarse,
                                    "shadow": a.shadow},
                 "kernel_ms_avg": round(kern_ms, 5),
                 "kernel_ms_avg_max_rank": round(kern_ms_max, 5),

@@ -25,6 +25,7 @@ RT_OPT_KERNEL = 1
 RT_OPT_TILE_ORDER = 2
 RT_OPT_RAYS = 3
 RT_OPT_ITEMS = 4
+RT_OPT_COARSE = 5
 RT_OPT_DEBUG = 100
 RT_OPT_POOL_CAP = 101
 
@@ -99,6 +100,14 @@ def lib() -> C.CDLL:
             raise ImportError(
                 f"{LIB_PATH} is missing: build the HIP extension with "
                 "`python -m cpp_cuda_raytracer_dev_amd.build` (there is no CPU fallback)")
+        # torch bundles its own libamdhip64.so.7 (same soname as /opt/rocm's).
+        # Whichever loads first serves the whole process, and torch cannot
+        # initialise its devices on the other one. So load torch's runtime
+        # first, and let this library bind to it.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)

@@ -47,14 +47,28 @@ struct rt_camera {
     int64_t inode_cap = 0;           // in float4
     int prepared_layout = 0;         // interior record layout of d_inode (1 or 2)
     int kernel_version = 3;          // kOptKernel (3 falls back to 2 on trees taller than 21)
-    int tile_order = 2;              // kOptTileOrder
+    int tile_order = 3;              // kOptTileOrder
     int debug = 0;                   // kOptDebug (diagnostics)
     int pool_cap = kPoolCapMax;      // kOptPoolCap
     unsigned long long* d_dbg = nullptr;
     int64_t dbg_cap = 0;             // in u64
     int32_t* d_order = nullptr;      // centre-out tile permutation
     int64_t order_cap = 0;
-    int64_t order_key[6] = {-1, -1, -1, -1, -1, -1};
+    int64_t order_key[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+    int coarse = 8;                  // kOptCoarse: coarse groups per wave (0 = off)
+    std::vector<int32_t> centre;     // centre-out permutation of the current fine grid (host copy)
+    // tile order 3: each frame's per-unit pool iterations feed the next
+    // frames' dispatch order, read back asynchronously (never a sync).
+    uint32_t* d_cost = nullptr;      // [tile][2] iterations, written by every frame
+    int64_t cost_cap = 0;            // in u32
+    uint32_t* h_cost = nullptr;      // pinned D2H target
+    int32_t* h_order = nullptr;      // pinned H2D source
+    int64_t host_cap = 0;            // tiles h_cost / h_order hold
+    hipEvent_t cost_ev = nullptr, order_ev = nullptr;
+    bool cost_pending = false, order_pending = false;
+    int frames_since = 0;
+    uint64_t layout_gen = 0, cost_gen = 0;   // fine-grid generation, and the one h_cost was read for
+    uint64_t order_gen = ~0ull;              // generation whose cost order d_order holds
     int rays = 16;                   // kOptRays: pixels per wave of kernel 3
     int items = 2;                   // kOptItems: items per lane per pool iteration
 };
@@ -135,16 +149,16 @@ int prepare_camera_object(rt_camera* c) {
 // index order, so the expensive tiles (the object sits mid-frame) start
 // first and the cheap background tiles fill in behind them.
 int ensure_order(rt_camera* c, const TraceParams& p) {
-    const int64_t key[6] = {p.tile_w, p.tile_h, p.tiles_x, p.block_rows, p.nranks, p.rank};
-    if (std::equal(key, key + 6, c->order_key)) return RT_OK;
+    const int64_t key[8] = {p.tile_w, p.tile_h, p.tiles_x, p.block_rows, p.nranks, p.rank, p.fine_tx0, p.fine_s0};
+    if (std::equal(key, key + 8, c->order_key)) return RT_OK;
     const int64_t n = (int64_t)p.tiles_x * p.block_rows;
     const int64_t per_band = kTileH / p.tile_h;
     std::vector<int32_t> order((size_t)n);
     std::vector<double> dist2((size_t)n);
     const double cx = 0.5 * c->w, cy = 0.5 * c->h;
     for (int64_t t = 0; t < n; t++) {
-        const int64_t row = t / p.tiles_x, tx = t % p.tiles_x;
-        const int64_t slot = row / per_band, yin = (row % per_band) * p.tile_h;
+        const int64_t row = t / p.tiles_x, tx = t % p.tiles_x + p.fine_tx0;
+        const int64_t slot = row / per_band + p.fine_s0, yin = (row % per_band) * p.tile_h;
         const double x = (tx + 0.5) * p.tile_w;
         const double y = (double)((p.rank + slot * (int64_t)p.nranks) * kTileH + yin) + 0.5 * p.tile_h;
         dist2[(size_t)t] = (x - cx) * (x - cx) + (y - cy) * (y - cy);
@@ -159,8 +173,198 @@ int ensure_order(rt_camera* c, const TraceParams& p) {
     }
     if ((rc = hip_check(hipMemcpy(c->d_order, order.data(), sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice), "H2D order")))
         return rc;
-    std::copy(key, key + 6, c->order_key);
+    std::copy(key, key + 8, c->order_key);
+    c->centre.swap(order);
+    c->layout_gen++;
+    c->frames_since = 1 << 20;  // tile order 3: sample the new grid's costs at once
     return RT_OK;
+}
+
+constexpr int kCostPeriod = 16;  // frames between cost samples (tile order 3)
+
+// Buffers of tile order 3 for n fine tiles (allocated when the grid grows).
+int ensure_cost(rt_camera* c, int64_t n) {
+    int rc;
+    if (c->cost_cap < 2 * n) {
+        dev_free(c->d_cost);
+        if ((rc = dev_alloc(&c->d_cost, (size_t)(2 * n), "hipMalloc(cost)"))) return rc;
+        c->cost_cap = 2 * n;
+    }
+    if (c->host_cap < n) {
+        // copies in flight may still use the pinned buffers
+        if (c->cost_pending) (void)hipEventSynchronize(c->cost_ev);
+        if (c->order_pending) (void)hipEventSynchronize(c->order_ev);
+        if (c->h_cost) (void)hipHostFree(c->h_cost);
+        if (c->h_order) (void)hipHostFree(c->h_order);
+        c->h_cost = nullptr;
+        c->h_order = nullptr;
+        c->host_cap = 0;
+        c->cost_pending = c->order_pending = false;
+        if ((rc = hip_check(hipHostMalloc((void**)&c->h_cost, sizeof(uint32_t) * 2 * (size_t)n, 0), "hipHostMalloc(cost)")) ||
+            (rc = hip_check(hipHostMalloc((void**)&c->h_order, sizeof(int32_t) * (size_t)n, 0), "hipHostMalloc(order)")))
+            return rc;
+        c->host_cap = n;
+    }
+    if (!c->cost_ev && (rc = hip_check(hipEventCreateWithFlags(&c->cost_ev, hipEventDisableTiming), "cost event")))
+        return rc;
+    if (!c->order_ev && (rc = hip_check(hipEventCreateWithFlags(&c->order_ev, hipEventDisableTiming), "order event")))
+        return rc;
+    return RT_OK;
+}
+
+// After a tile-order-3 frame: when an earlier cost sample has arrived, order
+// the tiles by it (heaviest unit first, centre-out among equals) and upload
+// the order behind this frame; otherwise, every kCostPeriod frames, queue a
+// sample of this frame's costs.  Stream-ordered and non-blocking (events are
+// only queried); skipped while the stream is being captured into a graph.
+int cost_feedback(rt_camera* c, const TraceParams& p, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return RT_OK;
+    const int64_t n = (int64_t)p.tiles_x * p.block_rows;
+    if (c->cost_pending) {
+        if (hipEventQuery(c->cost_ev) != hipSuccess) return RT_OK;
+        if (c->order_pending && hipEventQuery(c->order_ev) != hipSuccess) return RT_OK;
+        c->cost_pending = c->order_pending = false;
+        c->frames_since = 0;
+        if (c->cost_gen != c->layout_gen || (int64_t)c->centre.size() != n) return RT_OK;  // stale sample
+        // counting sort by cost, descending; stable over the centre-out order
+        uint32_t mx = 0;
+        for (int64_t t = 0; t < n; t++) mx = std::max(mx, std::max(c->h_cost[2 * t], c->h_cost[2 * t + 1]));
+        mx = std::min<uint32_t>(mx, 1u << 16);
+        std::vector<int64_t> start((size_t)mx + 2, 0);
+        auto cost_of = [&](int32_t t) {
+            return std::min<uint32_t>(std::max(c->h_cost[2 * (size_t)t], c->h_cost[2 * (size_t)t + 1]), mx);
+        };
+        for (int32_t t : c->centre) start[(size_t)(mx - cost_of(t)) + 1]++;
+        for (size_t k = 1; k < start.size(); k++) start[k] += start[k - 1];
+        bool same = true;
+        for (int32_t t : c->centre) {
+            const int64_t at = start[(size_t)(mx - cost_of(t))]++;
+            same = same && c->h_order[at] == t;
+            c->h_order[at] = t;
+        }
+        if (same && c->order_gen == c->layout_gen) return RT_OK;  // d_order already holds it
+        int rc;
+        if ((rc = hip_check(hipMemcpyAsync(c->d_order, c->h_order, sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice, st),
+                            "H2D cost order")) ||
+            (rc = hip_check(hipEventRecord(c->order_ev, st), "order event")))
+            return rc;
+        c->order_pending = true;
+        c->order_gen = c->layout_gen;
+        return RT_OK;
+    }
+    if (++c->frames_since < kCostPeriod) return RT_OK;
+    int rc;
+    if ((rc = hip_check(hipMemcpyAsync(c->h_cost, c->d_cost, sizeof(uint32_t) * 2 * (size_t)n, hipMemcpyDeviceToHost, st),
+                        "D2H cost")) ||
+        (rc = hip_check(hipEventRecord(c->cost_ev, st), "cost event")))
+        return rc;
+    c->cost_pending = true;
+    c->cost_gen = c->layout_gen;
+    return RT_OK;
+}
+
+// Screen rectangle (inclusive pixel bounds, row 0 = bottom) that the root
+// box projects to, widened by a pixel.  Ray (ix, iy) points along
+// X3 * (u_mod*ix + v_mod*iy + n_mod) and the slab test of TD/Trixel.cu:76-95
+// sees the box shifted by the object translation od, so each corner c solves
+// A (a, b, s) = c with A = X3 [u v n]; pixel = (a/s, b/s).  Returns false when
+// the projection is not a bounded rectangle in front of the camera (a corner
+// at or behind the eye plane, a singular A): the whole frame is then fine.
+// The rectangle is a work-packing hint only -- pixels outside it still run the
+// exact root test (coarse groups), so it need not be conservative.
+bool root_rect(const rt_camera* c, const TraceParams& p, double r[4]) {
+    const float* X = p.xf;
+    const float* cols[3] = {c->basis.u_mod, c->basis.v_mod, c->basis.n_mod};
+    double A[3][3];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++)
+            A[i][j] = (double)X[4 * i] * cols[j][0] + (double)X[4 * i + 1] * cols[j][1] + (double)X[4 * i + 2] * cols[j][2];
+    const double det = A[0][0] * (A[1][1] * A[2][2] - A[1][2] * A[2][1]) - A[0][1] * (A[1][0] * A[2][2] - A[1][2] * A[2][0]) +
+                       A[0][2] * (A[1][0] * A[2][1] - A[1][1] * A[2][0]);
+    double scale = 0.0;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) scale = std::max(scale, fabs(A[i][j]));
+    if (!(fabs(det) > 1e-12 * scale * scale * scale)) return false;
+    double inv[3][3];
+    inv[0][0] = (A[1][1] * A[2][2] - A[1][2] * A[2][1]) / det;
+    inv[0][1] = (A[0][2] * A[2][1] - A[0][1] * A[2][2]) / det;
+    inv[0][2] = (A[0][1] * A[1][2] - A[0][2] * A[1][1]) / det;
+    inv[1][0] = (A[1][2] * A[2][0] - A[1][0] * A[2][2]) / det;
+    inv[1][1] = (A[0][0] * A[2][2] - A[0][2] * A[2][0]) / det;
+    inv[1][2] = (A[0][2] * A[1][0] - A[0][0] * A[1][2]) / det;
+    inv[2][0] = (A[1][0] * A[2][1] - A[1][1] * A[2][0]) / det;
+    inv[2][1] = (A[0][1] * A[2][0] - A[0][0] * A[2][1]) / det;
+    inv[2][2] = (A[0][0] * A[1][1] - A[0][1] * A[1][0]) / det;
+    const double od[3] = {X[3], X[7], X[11]};
+    r[0] = r[2] = INFINITY;
+    r[1] = r[3] = -INFINITY;
+    for (int k = 0; k < 8; k++) {
+        const double cc[3] = {p.root_box[(k & 1) ? 1 : 0] + od[0], p.root_box[(k & 2) ? 3 : 2] + od[1],
+                              p.root_box[(k & 4) ? 5 : 4] + od[2]};
+        double q[3];
+        for (int i = 0; i < 3; i++) q[i] = inv[i][0] * cc[0] + inv[i][1] * cc[1] + inv[i][2] * cc[2];
+        if (!(q[2] > 1e-9 * (fabs(q[0]) + fabs(q[1]) + fabs(q[2])))) return false;
+        const double x = q[0] / q[2], y = q[1] / q[2];
+        if (!std::isfinite(x) || !std::isfinite(y)) return false;
+        r[0] = std::min(r[0], x); r[1] = std::max(r[1], x);
+        r[2] = std::min(r[2], y); r[3] = std::max(r[3], y);
+    }
+    r[0] = floor(r[0]) - 1; r[1] = ceil(r[1]) + 1;
+    r[2] = floor(r[2]) - 1; r[3] = ceil(r[3]) + 1;
+    return true;
+}
+
+// Splits this rank's tiles into the fine region (one kRays unit per wave)
+// around the root box's screen rectangle and coarse 8x8 groups elsewhere
+// (`per_wave` to a wave; 0 = everything fine).
+void set_fine_region(const rt_camera* c, TraceParams& p, int per_wave) {
+    const int32_t nbands = (c->h + kTileH - 1) / kTileH;
+    const int32_t per_band = kTileH / p.tile_h;
+    p.groups_x = (c->w + 7) / 8;
+    p.nslots = (nbands + p.nranks - 1) / p.nranks;
+    p.fine_tx0 = p.fine_s0 = 0;
+    p.cg_x0 = 0; p.cg_x1 = p.groups_x;
+    p.cs0 = 0; p.cs1 = p.nslots;
+    p.coarse_per_wave = 1;
+    p.coarse_groups = 0;
+    p.coarse_blocks = 0;
+    double r[4];
+    if (per_wave <= 0 || !root_rect(c, p, r)) return;
+    if (c->debug & 4) r[0] = r[1] = r[2] = r[3] = -8.0;  // tests: every group coarse
+    const double x0 = std::max(r[0], 0.0), x1 = std::min(r[1], (double)c->w - 1);
+    const double y0 = std::max(r[2], 0.0), y1 = std::min(r[3], (double)c->h - 1);
+    int32_t tx0 = 0, tx1 = -1, s0 = 0, s1 = -1;
+    if (x0 <= x1 && y0 <= y1) {
+        tx0 = (int32_t)x0 / p.tile_w;
+        tx1 = (int32_t)x1 / p.tile_w;
+        const int32_t b0 = (int32_t)y0 / kTileH, b1 = (int32_t)y1 / kTileH;
+        // slots s of this rank with b0 <= rank + s*N <= b1
+        s0 = b0 <= p.rank ? 0 : (b0 - p.rank + p.nranks - 1) / p.nranks;
+        s1 = b1 < p.rank ? -1 : (b1 - p.rank) / p.nranks;
+        s1 = std::min(s1, p.nslots - 1);
+    }
+    if (tx1 < tx0 || s1 < s0) {  // nothing of the box on this rank: all coarse
+        tx0 = 0; tx1 = -1; s0 = 0; s1 = -1;
+    }
+    p.fine_tx0 = tx0;
+    p.fine_s0 = s0;
+    p.tiles_x = tx1 - tx0 + 1;
+    p.block_rows = (s1 - s0 + 1) * per_band;
+    p.cg_x0 = std::min(tx0 * p.tile_w / 8, p.groups_x);
+    p.cg_x1 = std::min((tx1 + 1) * p.tile_w / 8, p.groups_x);
+    p.cs0 = s0;
+    p.cs1 = s1 + 1;
+    if (p.tiles_x <= 0 || p.block_rows <= 0) {
+        p.tiles_x = p.block_rows = 0;
+        p.cg_x0 = p.cg_x1 = 0;
+        p.cs0 = p.cs1 = 0;
+    }
+    p.coarse_per_wave = per_wave;
+    p.coarse_groups = (int64_t)p.nslots * p.groups_x - (int64_t)(p.cs1 - p.cs0) * (p.cg_x1 - p.cg_x0);
+    const int64_t waves = (p.coarse_groups + per_wave - 1) / per_wave;
+    p.coarse_blocks = (int32_t)((waves + 1) / 2);  // kernel 3 runs two waves per block
 }
 
 int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t* argb, int64_t* hit,
@@ -196,6 +400,8 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
     }
     p.tiles_x = (c->w + p.tile_w - 1) / p.tile_w;
     p.block_rows = ((nbands + p.nranks - 1) / p.nranks) * (kTileH / p.tile_h);
+    camera_relative_box(s->root, c->pos, p.root_box);
+    set_fine_region(c, p, kernel == 3 ? c->coarse : 0);
     p.root_ref = s->root_ref;
     p.ntri = s->ntri;
     p.max_depth = kMaxDepth;
@@ -206,7 +412,7 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
     p.items = c->items;
     p.dbg = nullptr;
     if (c->debug & 2) {
-        const int64_t need = (int64_t)p.tiles_x * p.block_rows * 4 * 3;  // <= 4 waves per block
+        const int64_t need = ((int64_t)p.tiles_x * p.block_rows + p.coarse_blocks) * 4 * 3;  // <= 4 waves per block
         if (c->dbg_cap < need) {
             dev_free(c->d_dbg);
             int rc = dev_alloc(&c->d_dbg, (size_t)need, "hipMalloc(dbg)");
@@ -217,11 +423,15 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
         int rc = hip_check(hipMemset(c->d_dbg, 0, sizeof(uint64_t) * (size_t)need), "memset dbg");
         if (rc) return rc;
     }
-    camera_relative_box(s->root, c->pos, p.root_box);
-    if (c->tile_order == 2) {
+    p.cost = nullptr;
+    if (c->tile_order >= 2 && p.tiles_x * p.block_rows > 0) {
         int rc = ensure_order(c, p);
         if (rc) return rc;
         p.order = c->d_order;
+        if (c->tile_order == 3 && kernel == 3) {
+            if ((rc = ensure_cost(c, (int64_t)p.tiles_x * p.block_rows))) return rc;
+            p.cost = c->d_cost;
+        }
     }
     return RT_OK;
 }
@@ -395,7 +605,8 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
     }
     TraceParams p;
     if ((rc = fill_params(c, xform, tile, argb, hit, mode, p))) return rc;
-    return launch_trace(p, mode, flags, effective_kernel(c), stream);
+    if ((rc = launch_trace(p, mode, flags, effective_kernel(c), stream))) return rc;
+    return p.cost ? cost_feedback(c, p, stream) : RT_OK;
 }
 
 extern "C" int rt_render(rt_camera* c, const float* xform, uint32_t mode, uint32_t flags, const rt_tile* tile,
@@ -486,6 +697,11 @@ extern "C" void rt_camera_destroy(rt_camera* c) {
     dev_free(c->d_inode);
     dev_free(c->d_order);
     dev_free(c->d_dbg);
+    dev_free(c->d_cost);
+    if (c->h_cost) (void)hipHostFree(c->h_cost);
+    if (c->h_order) (void)hipHostFree(c->h_order);
+    if (c->cost_ev) (void)hipEventDestroy(c->cost_ev);
+    if (c->order_ev) (void)hipEventDestroy(c->order_ev);
     delete c;
 }
 
@@ -497,12 +713,17 @@ extern "C" int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value) {
         c->kernel_version = value;
         return RT_OK;
     case kOptRays:
-        if (value != 16 && value != 32 && value != 64) return fail(RT_ERR_INVALID, "rays per wave %d (16, 32, 64)", value);
+        if (value != 8 && value != 16 && value != 32 && value != 64)
+            return fail(RT_ERR_INVALID, "rays per wave %d (8, 16, 32, 64)", value);
         c->rays = value;
         return RT_OK;
     case kOptItems:
         if (value != 1 && value != 2) return fail(RT_ERR_INVALID, "items per lane %d (1, 2)", value);
         c->items = value;
+        return RT_OK;
+    case kOptCoarse:
+        if (value < 0 || value > 4096) return fail(RT_ERR_INVALID, "coarse groups per wave %d (0..4096)", value);
+        c->coarse = value;
         return RT_OK;
     case kOptPoolCap:
         // the 64 root items plus a DFS run of height <= 21 must fit
@@ -514,7 +735,7 @@ extern "C" int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value) {
         c->debug = value;
         return RT_OK;
     case kOptTileOrder:
-        if (value < 0 || value > 2) return fail(RT_ERR_INVALID, "tile order %d", value);
+        if (value < 0 || value > 3) return fail(RT_ERR_INVALID, "tile order %d (0..3)", value);
         c->tile_order = value;
         return RT_OK;
     default:

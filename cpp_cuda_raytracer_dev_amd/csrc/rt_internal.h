@@ -40,9 +40,10 @@ constexpr uint32_t kAxisShift = 29;
 // rt_camera_set_option keys.
 enum Option : int32_t {
     kOptKernel = 1,     // KD kernel version: 1 (node-own box, 48 B) or 2 (child boxes, 64 B)
-    kOptTileOrder = 2,  // 0 XCD-contiguous, 1 natural, 2 centre-out
+    kOptTileOrder = 2,  // 0 XCD-contiguous, 1 natural, 2 centre-out, 3 by measured cost (kernel 3)
     kOptRays = 3,       // kernel 3 pixels per wave: 64, 32 or 16
     kOptItems = 4,      // kernel 3 items popped per lane per iteration: 1 or 2
+    kOptCoarse = 5,     // kernel 3 coarse groups per wave outside the root box's rectangle (0 = off)
     kOptDebug = 100,    // diagnostics: 1 = skip traversal, 2 = per-wave timestamps
     kOptPoolCap = 101,  // tests: shrink kernel 3's item pool (66..kPoolCap) to force its fallback
 };
@@ -79,11 +80,24 @@ struct TraceParams {
     float xf[12];
     int32_t w, h;
     int32_t nranks, rank;
-    int32_t tiles_x, block_rows;   // grid = tiles_x * block_rows blocks
+    int32_t tiles_x, block_rows;   // fine grid = tiles_x * block_rows blocks
+    // Fine region (kernel 3): the tiles covering the root box's screen
+    // rectangle start at tile column fine_tx0 and band slot fine_s0; every
+    // other 8x8 group of this rank's bands is a coarse group, handled
+    // `coarse_per_wave` to a wave after the fine blocks (exact either way:
+    // a coarse group runs the same root test and traces what passes).
+    int32_t fine_tx0, fine_s0;
+    int32_t groups_x, nslots;      // 8-px groups per row, band slots of this rank
+    int32_t cg_x0, cg_x1;          // fine region in 8-px groups [x0, x1)
+    int32_t cs0, cs1;              // fine region in slots [s0, s1)
+    int32_t coarse_per_wave;       // coarse groups per wave
+    int32_t coarse_blocks;         // blocks after the fine grid
+    int64_t coarse_groups;         // total coarse groups
     int32_t tile_w, tile_h;        // pixels per block (tile_h divides the 8-row band)
     int32_t rays;                  // pixels (rays) per wave: 64, 32 or 16
     int32_t tile_order;            // Option kOptTileOrder
-    const int32_t* order;          // centre-out tile permutation (tile_order 2)
+    const int32_t* order;          // tile permutation (tile_order 2: centre-out, 3: by cost)
+    uint32_t* cost;                // tile_order 3: pool iterations per fine unit [tile][2], or null
     float root_box[6];             // camera-relative root AABB (t0x,t1x,t0y,t1y,t0z,t1z)
     int32_t pool_cap;              // kernel 3 item-pool capacity in use (<= kPoolCap)
     int32_t items;                 // kernel 3 items per lane per iteration (1 or 2)

@@ -91,21 +91,26 @@ __device__ __forceinline__ uint32_t phong(const float pnt[3], const float nrm[3]
 // Block -> (tile_x, slot).  Order 0: blocks b and b+8 share an XCD, so give
 // each XCD a contiguous run of tiles (bijective for any grid size); order 1:
 // natural (neighbouring tiles on different XCDs); order 2: the host's
-// centre-out permutation, so the heavy centre tiles are dispatched first.
-__device__ __forceinline__ void tile_of(const TraceParams& P, int32_t b, int32_t& tx, int32_t& slot) {
+// centre-out permutation, so the heavy centre tiles are dispatched first;
+// order 3: the host's permutation by the tiles' measured cost in an earlier
+// frame, heaviest first (centre-out until costs arrive).
+__device__ __forceinline__ int32_t tile_index(const TraceParams& P, int32_t b) {
     const int32_t nblocks = P.tiles_x * P.block_rows;
-    int32_t t;
     if (P.tile_order == 0) {
         const int32_t q = nblocks >> 3, rem = nblocks & 7;
         const int32_t xcd = b & 7, k = b >> 3;
-        t = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + k;
-    } else if (P.tile_order == 2 && P.order) {
-        t = P.order[b];
-    } else {
-        t = b;
+        return (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + k;
     }
+    if (P.tile_order >= 2 && P.order) return P.order[b];
+    return b;
+}
+
+__device__ __forceinline__ void tile_of(const TraceParams& P, int32_t b, int32_t& tx, int32_t& slot) {
+    const int32_t t = tile_index(P, b);
     slot = t / P.tiles_x;
     tx = t - slot * P.tiles_x;
+    tx += P.fine_tx0;
+    slot += P.fine_s0 * (kTileH / P.tile_h);
 }
 
 struct Pixel {
@@ -117,20 +122,64 @@ struct Pixel {
 // owns an 8 x (rays/8) sub-tile (side by side when tile_w > 8, stacked
 // otherwise).  Lanes >= rays own no pixel (the wave-cooperative kernel's
 // helper lanes).
-__device__ __forceinline__ bool pixel_of(const TraceParams& P, int32_t b, int32_t wave, Pixel& px) {
+// A wave's unit of pixels: 8 columns from x0, rows yin.. of band slot `slot`.
+struct Unit {
+    int32_t x0, slot, yin;
+};
+
+// Lane `lane`'s pixel of a unit (8 pixels per row, row-major); lanes >= rows*8
+// own no pixel.
+__device__ __forceinline__ bool unit_pixel(const TraceParams& P, const Unit& u, int32_t rows, int32_t lane,
+                                           Pixel& px) {
+    const int32_t band = P.rank + u.slot * P.nranks;
+    const int32_t ly = u.yin + (lane >> 3);
+    px.x = u.x0 + (lane & 7);
+    px.y = band * kTileH + ly;
+    px.out = (int64_t)(u.slot * kTileH + ly) * P.w + px.x;
+    return lane < rows * 8 && px.x < P.w && px.y < P.h;
+}
+
+// Sub-tile `wave` of fine tile b.
+__device__ __forceinline__ Unit unit_of(const TraceParams& P, int32_t b, int32_t wave) {
     int32_t tx, row;
     tile_of(P, b, tx, row);
     const int32_t per_band = kTileH / P.tile_h;
     const int32_t slot = row / per_band, yin = (row - slot * per_band) * P.tile_h;
-    const int32_t lane = (int32_t)threadIdx.x & 63;
     const int32_t wrows = P.rays >> 3;
     const int32_t wx = P.tile_w > 8 ? wave * 8 : 0, wy = P.tile_w > 8 ? 0 : wave * wrows;
-    const int32_t band = P.rank + slot * P.nranks;
-    const int32_t ly = yin + wy + (lane >> 3);
-    px.x = tx * P.tile_w + wx + (lane & 7);
-    px.y = band * kTileH + ly;
-    px.out = (int64_t)(slot * kTileH + ly) * P.w + px.x;
-    return lane < P.rays && px.x < P.w && px.y < P.h;
+    return Unit{tx * P.tile_w + wx, slot, yin + wy};
+}
+
+__device__ __forceinline__ bool pixel_of(const TraceParams& P, int32_t b, int32_t wave, Pixel& px) {
+    return unit_pixel(P, unit_of(P, b, wave), P.rays >> 3, (int32_t)threadIdx.x & 63, px);
+}
+
+// Coarse group j (row-major over this rank's slots and 8-px columns, skipping
+// the fine region) -> its 8x8 unit.
+__device__ __forceinline__ Unit coarse_unit(const TraceParams& P, int64_t j) {
+    const int64_t gx = P.groups_x;
+    const int64_t before = (int64_t)P.cs0 * gx;
+    int64_t slot, col;
+    if (j < before) {
+        slot = j / gx;
+        col = j - slot * gx;
+    } else {
+        j -= before;
+        const int64_t m = gx - (P.cg_x1 - P.cg_x0);
+        const int64_t mid = (int64_t)(P.cs1 - P.cs0) * m;
+        if (j < mid) {
+            const int64_t r = j / m;
+            slot = P.cs0 + r;
+            col = j - r * m;
+            if (col >= P.cg_x0) col += P.cg_x1 - P.cg_x0;
+        } else {
+            j -= mid;
+            const int64_t r = j / gx;
+            slot = P.cs1 + r;
+            col = j - r * gx;
+        }
+    }
+    return Unit{(int32_t)(col * 8), (int32_t)slot, 0};
 }
 
 // One tile per block (blockIdx), one sub-tile per wave.
@@ -557,8 +606,13 @@ struct Item {
 #ifndef RT_POOL_CAP_R16
 #define RT_POOL_CAP_R16 320
 #endif
+#ifndef RT_POOL_CAP_R8
+#define RT_POOL_CAP_R8 256
+#endif
 template <int kRays>
-constexpr int pool_cap_for() { return kRays == 64 ? kPoolCap : kRays == 32 ? RT_POOL_CAP_R32 : RT_POOL_CAP_R16; }
+constexpr int pool_cap_for() {
+    return kRays == 64 ? kPoolCap : kRays == 32 ? RT_POOL_CAP_R32 : kRays == 16 ? RT_POOL_CAP_R16 : RT_POOL_CAP_R8;
+}
 
 // Per-ray data of the pool walk in LDS: rd[0] = (rx, ry, rz, 1/rx),
 // rd[1] = (1/ry, 1/rz, odx/rx, ody/ry), rd[2] = (odz/rz, dir per cut axis),
@@ -588,24 +642,47 @@ __device__ __forceinline__ void finish_ray(Ray& R) {
     R.sx = R.rx > 0; R.sy = R.ry > 0; R.sz = R.rz > 0;
 }
 
-// Seeds the pool with the root item of every lane whose root test passes (or
-// a leaf root); returns the item count.
+// The primary ray of a pixel (TD/Camera.cu:103-104) and its object-space form
+// (TD/Trixel.cu:60-66); dead lanes get a harmless +z ray.
+__device__ __forceinline__ void camera_ray(const TraceParams& P, const Pixel& px, bool live, float cam[3], Ray& R) {
+    cam[0] = 0.0f; cam[1] = 0.0f; cam[2] = 1.0f;
+    if (live) primary_ray(P, px.x, px.y, cam);
+    const float* X = P.xf;
+    R.odx = X[3]; R.ody = X[7]; R.odz = X[11];
+    R.rx = -1 * (X[0] * -cam[0] + X[1] * -cam[1] + X[2] * -cam[2]);
+    R.ry = -1 * (X[4] * -cam[0] + X[5] * -cam[1] + X[6] * -cam[2]);
+    R.rz = -1 * (X[8] * -cam[0] + X[9] * -cam[1] + X[10] * -cam[2]);
+    finish_ray(R);
+}
+
+// The reference's root visit (TD/Trixel.cu:53,71-95): a leaf root is always
+// visited, an interior root when its slab test passes.
 template <bool kCount>
-__device__ __forceinline__ int seed_root(const TraceParams& P, uint4* items, const Ray& R, bool live, int lane,
-                                         uint32_t& n_int, uint32_t& n_desc) {
+__device__ __forceinline__ bool root_pass(const TraceParams& P, const Ray& R, bool live, float& t0, float& t1,
+                                          uint32_t& n_int, uint32_t& n_desc) {
     bool has = false;
-    float r0t0 = 0.0f, r0t1 = 0.0f;
+    t0 = 0.0f; t1 = 0.0f;
     if (live) {
         if (P.root_ref & kLeafBit) {
             has = true;
         } else {
             if (kCount) n_int++;
             has = slab(R, P.root_box[0], P.root_box[1], P.root_box[2], P.root_box[3], P.root_box[4],
-                       P.root_box[5], r0t0, r0t1);
+                       P.root_box[5], t0, t1);
             if (kCount && has) n_desc++;
         }
     }
     if (P.debug & 1) has = false;
+    return has;
+}
+
+// Seeds the pool with the root item of every lane whose root test passes (or
+// a leaf root); returns the item count.
+template <bool kCount>
+__device__ __forceinline__ int seed_root(const TraceParams& P, uint4* items, const Ray& R, bool live, int lane,
+                                         uint32_t& n_int, uint32_t& n_desc) {
+    float r0t0, r0t1;
+    const bool has = root_pass<kCount>(P, R, live, r0t0, r0t1, n_int, n_desc);
     const unsigned long long b = __ballot(has);
     const uint32_t off = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
     if (has) items[off] = make_uint4(P.root_ref, __float_as_uint(r0t0), __float_as_uint(r0t1), (uint32_t)lane << 26);
@@ -820,25 +897,21 @@ struct Counts {
     uint32_t n_int = 0, n_leaf = 0, n_acc = 0, n_desc = 0, n_hit = 0;
 };
 
-// One wave's unit of work: the kRays pixels of sub-tile `wave` of tile b.
+// One wave's unit of work: the kRays pixels (8 x kRays/8) of unit U.
+constexpr size_t kNoDbg = ~(size_t)0;
 template <int kRays, int kCap, int kRayVec, bool kTranslated, bool kWriteHit, bool kCount, bool kShadow>
-__device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, kCap, kRayVec>& S_, int32_t b,
-                                           int32_t wave, int lane, size_t dbg_slot, Counts& C) {
+__device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, kCap, kRayVec>& S_, const Unit& U,
+                                           int lane, size_t dbg_slot, uint32_t* cost, Counts& C) {
     uint4* items = S_.items;
     Pixel px;
-    const bool live = pixel_of(P, b, wave, px);  // every lane stays for the ballots
+    const bool live = unit_pixel(P, U, kRays / 8, lane, px);  // every lane stays for the ballots
     const unsigned long long t_start = P.dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
     uint32_t iters = 0;
 
-    float cam[3] = {0.0f, 0.0f, 1.0f};
-    if (live) primary_ray(P, px.x, px.y, cam);
-    const float* X = P.xf;
+    float cam[3];
     Ray R;
-    R.odx = X[3]; R.ody = X[7]; R.odz = X[11];
-    R.rx = -1 * (X[0] * -cam[0] + X[1] * -cam[1] + X[2] * -cam[2]);
-    R.ry = -1 * (X[4] * -cam[0] + X[5] * -cam[1] + X[6] * -cam[2]);
-    R.rz = -1 * (X[8] * -cam[0] + X[9] * -cam[1] + X[10] * -cam[2]);
-    finish_ray(R);
+    camera_ray(P, px, live, cam, R);
+    const float* X = P.xf;
     if (lane < kRays) {
         store_ray(&S_.ray[lane * kRayVec], R, kTranslated, 0.0f, 0u);
         S_.key[lane] = ~0ull;
@@ -882,11 +955,12 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
                                                     C.n_leaf, C.n_acc, C.n_desc);
         if (lane < kRays) shadowed = S_.key[lane] == 0ull;
     }
-    if (P.dbg && lane == 0) {  // diagnostics: the unit's start/end clock (100 MHz) and pool iterations
+    if (P.dbg && lane == 0 && dbg_slot != kNoDbg) {  // diagnostics: the unit's start/end clock (100 MHz) and pool iterations
         P.dbg[3 * dbg_slot] = t_start;
         P.dbg[3 * dbg_slot + 1] = __builtin_amdgcn_s_memrealtime();
         P.dbg[3 * dbg_slot + 2] = iters;
     }
+    if (cost && lane == 0) *cost = iters;  // tile order 3: this unit's pool iterations
     __builtin_amdgcn_wave_barrier();  // LDS of this unit is read; the next unit may overwrite it
     if (!live) return;
     uint32_t argb = kBackground;
@@ -910,11 +984,49 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
     if (kCount && best != kMiss) C.n_hit++;
 }
 
-// kRays pixels per wave (64: 8x8; 32: 8x4; 16: 8x2): fewer rays per wave
+__device__ __forceinline__ void count_flush(const TraceParams& P, const Counts& C) {
+    // every lane (also those past the frame edge) processed pool items;
+    // counter [2] counts valid candidates here (>= the DFS's accept events)
+    wave_count_add(&P.counters[0], C.n_int);
+    wave_count_add(&P.counters[1], C.n_leaf);
+    wave_count_add(&P.counters[2], C.n_acc);
+    wave_count_add(&P.counters[3], C.n_hit);
+    wave_count_add(&P.counters[4], C.n_desc);
+}
+
+// Root test of one coarse 8x8 group (all 64 lanes): returns the ballot of
+// lanes whose root test passes; lanes whose kRays-pixel sub-tile has no
+// passing ray write the background now.  The sub-tiles with a passing ray are
+// traced by trace_unit, which repeats the same root test, so a coarse group's
+// pixels are exactly what fine units would produce; only the packing of work
+// into waves differs.
+template <int kRays, bool kWriteHit, bool kCount>
+__device__ __forceinline__ unsigned long long coarse_root(const TraceParams& P, const Unit& G, int lane, Counts& C) {
+    Pixel px;
+    const bool live = unit_pixel(P, G, 8, lane, px);
+    float cam[3], t0, t1;
+    Ray R;
+    camera_ray(P, px, live, cam, R);
+    uint32_t ni = 0, nd = 0;
+    const bool has = root_pass<kCount>(P, R, live, t0, t1, ni, nd);
+    const unsigned long long b = __ballot(has);
+    constexpr unsigned long long kSub = kRays == 64 ? ~0ull : ((1ull << (kRays & 63)) - 1);
+    const bool traced = ((b >> ((lane / kRays) * kRays)) & kSub) != 0;
+    if (live && !traced) {
+        P.argb[px.out] = kBackground;
+        if (kWriteHit) P.hit[px.out] = (int64_t)-1;
+        if (kCount) C.n_int += ni;  // the root visit; no root test passed in this sub-tile
+    }
+    return b;
+}
+
+// kRays pixels per wave (64: 8x8; 32: 8x4; 16: 8x2; 8: 8x1): fewer rays per wave
 // spread a heavy tile's items over more SIMDs, the other lanes only help.
 // kShadow: a second pool walk traces one shadow ray per hit (SURVEY.md §8a
 // a12; definition in oracle/oracle.c trace_shadow): the segment from the light
 // (2,2,2) to the hit, walked from the light with the reference's rules.
+// One fine tile per block (the tiles covering the root box's screen
+// rectangle, or the whole frame), one unit per wave.
 template <int kRays, bool kTranslated, bool kWriteHit, bool kCount, bool kShadow>
 __global__ __launch_bounds__(128) void k_trace_kd3(TraceParams P) {
     constexpr int kWaves = 2;
@@ -923,17 +1035,44 @@ __global__ __launch_bounds__(128) void k_trace_kd3(TraceParams P) {
     __shared__ WaveLds<kRays, kCap, kRayVec> s_lds[kWaves];
     const int wv = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
     Counts C;
-    trace_unit<kRays, kCap, kRayVec, kTranslated, kWriteHit, kCount, kShadow>(
-        P, s_lds[wv], (int32_t)blockIdx.x, wv, lane, (size_t)blockIdx.x * kWaves + wv, C);
-    if (kCount) {
-        // every lane (also those past the frame edge) processed pool items;
-        // counter [2] counts valid candidates here (>= the DFS's accept events)
-        wave_count_add(&P.counters[0], C.n_int);
-        wave_count_add(&P.counters[1], C.n_leaf);
-        wave_count_add(&P.counters[2], C.n_acc);
-        wave_count_add(&P.counters[3], C.n_hit);
-        wave_count_add(&P.counters[4], C.n_desc);
+    const int32_t b = (int32_t)blockIdx.x;
+    uint32_t* cost = P.cost ? P.cost + 2 * (size_t)tile_index(P, b) + wv : nullptr;
+    trace_unit<kRays, kCap, kRayVec, kTranslated, kWriteHit, kCount, kShadow>(P, s_lds[wv], unit_of(P, b, wv), lane,
+                                                                             (size_t)b * kWaves + wv, cost, C);
+    if (kCount) count_flush(P, C);
+}
+
+// The coarse groups (every 8x8 group of this rank outside the fine tiles),
+// P.coarse_per_wave per wave.  A separate kernel: looping trace_unit inside
+// the fine kernel costs it a third of its occupancy (80 -> 113 VGPRs).
+template <int kRays, bool kTranslated, bool kWriteHit, bool kCount, bool kShadow>
+__global__ __launch_bounds__(128) void k_coarse_kd3(TraceParams P) {
+    constexpr int kWaves = 2;
+    constexpr int kCap = pool_cap_for<kRays>();
+    constexpr int kRayVec = (kTranslated || kShadow) ? 5 : 3;
+    constexpr unsigned long long kSub = kRays == 64 ? ~0ull : ((1ull << (kRays & 63)) - 1);
+    __shared__ WaveLds<kRays, kCap, kRayVec> s_lds[kWaves];
+    const int wv = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
+    Counts C;
+    const unsigned long long t_start = P.dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    const int64_t cw = (int64_t)blockIdx.x * kWaves + wv;
+    const int64_t j0 = cw * P.coarse_per_wave;
+    const int64_t j1 = min(j0 + (int64_t)P.coarse_per_wave, P.coarse_groups);
+    for (int64_t j = j0; j < j1; j++) {
+        const Unit G = coarse_unit(P, j);
+        const unsigned long long gmask = coarse_root<kRays, kWriteHit, kCount>(P, G, lane, C);
+        for (int k = 0; k < 64 / kRays; k++)
+            if ((gmask >> (k * kRays)) & kSub)
+                trace_unit<kRays, kCap, kRayVec, kTranslated, kWriteHit, kCount, kShadow>(
+                    P, s_lds[wv], Unit{G.x0, G.slot, k * (kRays / 8)}, lane, kNoDbg, nullptr, C);
     }
+    if (P.dbg && lane == 0) {  // after the fine kernel's slots
+        const size_t slot = (size_t)(P.tiles_x * P.block_rows + blockIdx.x) * kWaves + wv;
+        P.dbg[3 * slot] = t_start;
+        P.dbg[3 * slot + 1] = __builtin_amdgcn_s_memrealtime();
+        P.dbg[3 * slot + 2] = 0;
+    }
+    if (kCount) count_flush(P, C);
 }
 
 // -------------------------------------------------------------- flat trace
@@ -1138,41 +1277,57 @@ int launch_cam_nodes(const rt_kd_node* nodes, const int32_t* ids, const uint32_t
 using TraceFn = void (*)(TraceParams);
 
 template <bool T, bool H, bool C, bool S>
-TraceFn kd3_kernel(int rays) {
+TraceFn kd3_kernel(int rays, bool coarse) {
+    if (coarse) {
+        if (rays == 8) return k_coarse_kd3<8, T, H, C, S>;
+        if (rays == 16) return k_coarse_kd3<16, T, H, C, S>;
+        if (rays == 32) return k_coarse_kd3<32, T, H, C, S>;
+        return k_coarse_kd3<64, T, H, C, S>;
+    }
+    if (rays == 8) return k_trace_kd3<8, T, H, C, S>;
     if (rays == 16) return k_trace_kd3<16, T, H, C, S>;
     if (rays == 32) return k_trace_kd3<32, T, H, C, S>;
     return k_trace_kd3<64, T, H, C, S>;
 }
 
 template <bool T, bool H, bool C>
-TraceFn kd_kernel(int version, int rays, bool shadow) {
+TraceFn kd_kernel(int version, int rays, bool shadow, bool coarse) {
     if (version == 1) return k_trace_kd<T, H, C>;
     if (version == 2) return k_trace_kd2<T, H, C>;
-    return shadow ? kd3_kernel<T, H, C, true>(rays) : kd3_kernel<T, H, C, false>(rays);
+    return shadow ? kd3_kernel<T, H, C, true>(rays, coarse) : kd3_kernel<T, H, C, false>(rays, coarse);
 }
 
 int launch_trace(const TraceParams& p, uint32_t mode, uint32_t flags, int kernel_version, void* stream) {
-    const unsigned grid = (unsigned)(p.tiles_x * p.block_rows);
-    if (grid == 0) return RT_OK;
     hipStream_t s = (hipStream_t)stream;
     const bool wh = (flags & RT_FLAG_WRITE_HIT) != 0, cnt = (flags & RT_FLAG_COUNT) != 0;
+    const unsigned fine = (unsigned)(p.tiles_x * p.block_rows);
     // waves per block = (tile_w / 8) * (tile_h / (rays / 8))
     const unsigned threads = (unsigned)((p.tile_w / 8) * (p.tile_h / (p.rays / 8)) * 64);
-    TraceFn fn;
     if (mode == RT_MODE_FLAT) {
-        fn = wh ? (cnt ? k_trace_flat<true, true> : k_trace_flat<true, false>)
-                : (cnt ? k_trace_flat<false, true> : k_trace_flat<false, false>);
-    } else {
-        const bool tr = p.xf[3] != 0.0f || p.xf[7] != 0.0f || p.xf[11] != 0.0f;
-        const int v = kernel_version, r = p.rays;
-        const bool sh = (flags & RT_FLAG_SHADOW) != 0;  // kernel 3 only (checked by the caller)
-        if (tr) fn = wh ? (cnt ? kd_kernel<true, true, true>(v, r, sh) : kd_kernel<true, true, false>(v, r, sh))
-                        : (cnt ? kd_kernel<true, false, true>(v, r, sh) : kd_kernel<true, false, false>(v, r, sh));
-        else fn = wh ? (cnt ? kd_kernel<false, true, true>(v, r, sh) : kd_kernel<false, true, false>(v, r, sh))
-                     : (cnt ? kd_kernel<false, false, true>(v, r, sh) : kd_kernel<false, false, false>(v, r, sh));
+        if (fine == 0) return RT_OK;
+        TraceFn fn = wh ? (cnt ? k_trace_flat<true, true> : k_trace_flat<true, false>)
+                        : (cnt ? k_trace_flat<false, true> : k_trace_flat<false, false>);
+        fn<<<fine, threads, 0, s>>>(p);
+        return check_launch<void>("k_trace_flat");
     }
-    fn<<<grid, threads, 0, s>>>(p);
-    return check_launch<void>(mode == RT_MODE_FLAT ? "k_trace_flat" : "k_trace_kd");
+    const bool tr = p.xf[3] != 0.0f || p.xf[7] != 0.0f || p.xf[11] != 0.0f;
+    const int v = kernel_version, r = p.rays;
+    const bool sh = (flags & RT_FLAG_SHADOW) != 0;  // kernel 3 only (checked by the caller)
+    for (int pass = 0; pass < 2; pass++) {
+        // the coarse groups first (short), then the fine tiles
+        const bool coarse = pass == 0;
+        const unsigned grid = coarse ? (unsigned)p.coarse_blocks : fine;
+        if (grid == 0) continue;
+        TraceFn fn;
+        if (tr) fn = wh ? (cnt ? kd_kernel<true, true, true>(v, r, sh, coarse) : kd_kernel<true, true, false>(v, r, sh, coarse))
+                        : (cnt ? kd_kernel<true, false, true>(v, r, sh, coarse) : kd_kernel<true, false, false>(v, r, sh, coarse));
+        else fn = wh ? (cnt ? kd_kernel<false, true, true>(v, r, sh, coarse) : kd_kernel<false, true, false>(v, r, sh, coarse))
+                     : (cnt ? kd_kernel<false, false, true>(v, r, sh, coarse) : kd_kernel<false, false, false>(v, r, sh, coarse));
+        fn<<<grid, coarse ? 128u : threads, 0, s>>>(p);
+        int rc = check_launch<void>(coarse ? "k_coarse_kd3" : "k_trace_kd");
+        if (rc) return rc;
+    }
+    return RT_OK;
 }
 
 int launch_unpack(int32_t w, int32_t h, int32_t nranks, const uint32_t* gathered, uint32_t* frame,

@@ -177,14 +177,18 @@ int rt_camera_counters(rt_camera* c, uint64_t out[5], int reset);
 /* Kernel launch geometry and the traversal stack depth in use. */
 int rt_camera_info(const rt_camera* c, int32_t* w, int32_t* h, int32_t* max_depth);
 
-/* Tuning knobs (not in the reference): key 1 = KD kernel layout version
- * (1: node-own box records, 2: child-box records, default), key 2 = tile
- * dispatch order (0: XCD-contiguous, 1: natural, 2: centre-out, default).
+/* Tuning knobs (not in the reference): key 1 = KD kernel (1: per-lane DFS,
+ * node-own box records; 2: per-lane DFS, child-box records; 3: wave-
+ * cooperative item pool, default), key 2 = tile dispatch order (0: XCD-
+ * contiguous, 1: natural, 2: centre-out, 3: heaviest first by the cost an
+ * earlier frame measured, default; kernel 3 reads the costs back with
+ * stream-ordered async copies, skipped while the stream is captured).
  * Every setting renders the identical frame. */
 #define RT_OPT_KERNEL 1
 #define RT_OPT_TILE_ORDER 2
-#define RT_OPT_RAYS 3 /* kernel 3: pixels per wave (64, 32, 16 default); the rest of the lanes help */
+#define RT_OPT_RAYS 3 /* kernel 3: pixels per wave (64, 32, 16 default, 8); the rest of the lanes help */
 #define RT_OPT_ITEMS 4 /* kernel 3: items each lane pops per iteration (1, 2 default) */
+#define RT_OPT_COARSE 5 /* kernel 3: 8x8 groups per wave outside the root box's screen rectangle (8 default, 0 = off) */
 int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value);
 
 /* Diagnostics (key 100 of rt_camera_set_option: 1 = skip traversal,

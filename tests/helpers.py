@@ -60,7 +60,8 @@ def oracle_render(name, w, h, mode=0, xform=None, rows=None, cam_kw=None, shadow
 class GpuScene:
     """Trixel + Camera + Object through the product API."""
 
-    def __init__(self, name, w, h, cam_kw=None, device=0, kernel=None, tile_order=None, rays=None, items=None):
+    def __init__(self, name, w, h, cam_kw=None, device=0, kernel=None, tile_order=None, rays=None, items=None,
+                 coarse=None, debug=None):
         pts, leafs, _ = mesh(name)
         self.trixel = R.Trixel(len(pts), pts, device=device)
         self.trixel.set_kd_nodes(trees(name)[0])
@@ -80,6 +81,10 @@ class GpuScene:
             self.cam.set_option(_lib.RT_OPT_RAYS, rays)
         if items is not None:
             self.cam.set_option(_lib.RT_OPT_ITEMS, items)
+        if coarse is not None:
+            self.cam.set_option(_lib.RT_OPT_COARSE, coarse)
+        if debug is not None:
+            self.cam.set_option(_lib.RT_OPT_DEBUG, debug)
         self.obj = R.Object(self.trixel)
         self.cam.add_object(self.obj)
 

@@ -44,7 +44,8 @@ def test_small_frames_vs_golden(name, w, h, mode):
     _assert_same((argb, hit), (oargb, ohit), key + " vs oracle")
 
 
-KERNELS = [(1, 0, 64), (2, 2, 64), (2, 1, 64), (3, 1, 64), (3, 2, 32), (3, 1, 32), (3, 2, 16)]  # (KD kernel, tile order, rays/wave)
+KERNELS = [(1, 0, 64), (2, 2, 64), (2, 1, 64), (3, 1, 64), (3, 2, 32), (3, 1, 32), (3, 2, 16), (3, 2, 8), (3, 3, 16),
+           (3, 3, 8)]  # (KD kernel, tile order, rays/wave)
 
 
 def _counters_match(cnt, ocnt, kernel):
@@ -156,7 +157,7 @@ def test_camera_poses_rabbit(pose):
 
 
 @pytest.mark.parametrize("items", [1, 2])
-@pytest.mark.parametrize("rays", [64, 32, 16])
+@pytest.mark.parametrize("rays", [64, 32, 16, 8])
 @pytest.mark.parametrize("shadow", [False, True])
 def test_items_per_lane(items, rays, shadow):
     """Kernel 3 pops one or two items per lane per iteration; same frame and counters."""
@@ -232,7 +233,7 @@ def test_render_into_stream_and_repeat():
 # second pool walk against the oracle's trace_shadow.  The any-hit result does
 # not depend on visit order, so frames are bit-exact; with counters on, the
 # shadow walks visit every node the oracle visits (no early exit).
-SHADOW_KERNELS = [(3, 1, 64), (3, 2, 32), (3, 2, 16)]
+SHADOW_KERNELS = [(3, 1, 64), (3, 2, 32), (3, 2, 16), (3, 2, 8)]
 
 
 @pytest.mark.parametrize("name,w,h", [("rabbit_70k", 960, 540), ("dragon", 960, 540)])
@@ -319,3 +320,106 @@ def test_shadow_rejected_outside_kernel3_kd(kernel, mode):
     s = H.GpuScene("tester", 64, 36, kernel=kernel)
     with pytest.raises(_lib.RtError):
         s.render(mode, shadow=True)
+
+
+# ------------------------------------------------------- coarse background
+# Kernel 3 splits a frame into fine tiles (the root box's screen rectangle,
+# one unit per wave) and coarse 8x8 groups elsewhere (k_coarse_kd3, several
+# per wave), which run the same root test and trace any sub-tile where a ray
+# passes.  Frames and counters must not depend on the split: coarse off (0),
+# one or many groups per wave, and the diagnostic "every group coarse" (debug
+# bit 4), which sends the whole object through the coarse kernel's tracing.
+COARSE = [(0, None), (1, None), (8, None), (4096, None), (8, 4), (1, 4)]  # (groups per wave, debug)
+
+
+@pytest.mark.parametrize("coarse,debug", COARSE)
+@pytest.mark.parametrize("rays", [64, 32, 16, 8])
+@pytest.mark.parametrize("name,w,h", [("rabbit_70k", 320, 180), ("dragon", 960, 540), ("tester", 81, 45)])
+def test_coarse_split(name, w, h, rays, coarse, debug):
+    s = H.GpuScene(name, w, h, kernel=3, rays=rays, coarse=coarse, debug=debug)
+    argb, hit, cnt = s.render(0, count=True)
+    oargb, ohit, ocnt = H.oracle_render(name, w, h, 0)
+    _assert_same((argb, hit), (oargb, ohit), f"{name} coarse {coarse} debug {debug}")
+    _counters_match(cnt, ocnt, 3)
+    argb2, hit2, _ = s.render(0)
+    _assert_same((argb2, hit2), (oargb, ohit), f"{name} coarse {coarse} debug {debug} (no counters)")
+
+
+@pytest.mark.parametrize("debug", [None, 4])
+@pytest.mark.parametrize("pose", _poses(6, seed=11))
+def test_coarse_poses_and_transforms(pose, debug):
+    for xf in (None, _rot_y(23.0, (0.02, 0.0, -0.01))):
+        s = H.GpuScene("rabbit_70k", 200, 120, cam_kw=pose, kernel=3, debug=debug)
+        argb, hit, _ = s.render(0, xform=xf)
+        oargb, ohit, _ = H.oracle_render("rabbit_70k", 200, 120, 0, cam_kw=pose, xform=xf)
+        _assert_same((argb, hit), (oargb, ohit), f"pose {pose} xf {xf is not None} debug {debug}")
+
+
+@pytest.mark.parametrize("debug", [None, 4])
+def test_coarse_shadow(debug):
+    s = H.GpuScene("dragon", 960, 540, kernel=3, debug=debug)
+    argb, hit, cnt = s.render(0, count=True, shadow=True)
+    oargb, ohit, ocnt = H.oracle_render("dragon", 960, 540, 0, shadow=True)
+    _assert_same((argb, hit), (oargb, ohit), f"coarse shadow debug {debug}")
+    _counters_match(cnt, ocnt, 3)
+
+
+@pytest.mark.parametrize("debug", [None, 4])
+@pytest.mark.parametrize("nranks", [2, 3, 8])
+def test_coarse_band_tiles(nranks, debug):
+    import torch
+    from cpp_cuda_raytracer_dev_amd import raytracer as R
+    w, h = 960, 540
+    s = H.GpuScene("dragon", w, h, kernel=3, coarse=0)
+    full, _, _ = s.render(0)
+    t = H.GpuScene("dragon", w, h, kernel=3, debug=debug)
+    npk = R.packed_pixels(w, h, nranks)
+    gathered = torch.zeros(nranks * npk, dtype=torch.int32, device="cuda:0")
+    for r in range(nranks):
+        t.cam.render_into(gathered[r * npk:(r + 1) * npk], mode=0, tile=(nranks, r))
+    frame = torch.zeros(w * h, dtype=torch.int32, device="cuda:0")
+    R.unpack_bands(0, w, h, nranks, gathered, frame)
+    torch.cuda.synchronize()
+    assert (frame.cpu().numpy().view(np.uint32) == full).all()
+
+
+# ------------------------------------------------------ cost-ordered tiles
+# Tile order 3 dispatches fine tiles heaviest-first by the pool iterations an
+# earlier frame measured (read back asynchronously every few frames).  Any
+# permutation gives the same frame; these tests run enough frames for the
+# feedback to reorder the tiles, then compare with the oracle.
+@pytest.mark.parametrize("rays", [16, 8])
+@pytest.mark.parametrize("name,w,h", [("dragon", 960, 540), ("rabbit_70k", 320, 180)])
+def test_cost_order_feedback(name, w, h, rays):
+    import torch
+    s = H.GpuScene(name, w, h, kernel=3, tile_order=3, rays=rays)
+    oargb, ohit, ocnt = H.oracle_render(name, w, h, 0)
+    out = torch.zeros(w * h, dtype=torch.int32, device="cuda:0")
+    st = torch.cuda.Stream()
+    for _ in range(60):
+        s.cam.render_into(out, mode=0, stream=st.cuda_stream)
+        st.synchronize()  # lets the cost sample arrive between frames
+    assert (out.cpu().numpy().view(np.uint32) == oargb).all()
+    argb, hit, cnt = s.render(0, count=True)
+    _assert_same((argb, hit), (oargb, ohit), f"{name} cost order")
+    _counters_match(cnt, ocnt, 3)
+    # the order in use is a permutation of the fine tiles
+    for _ in range(3):
+        s.cam.render_into(out, mode=0, stream=st.cuda_stream)
+    st.synchronize()
+    assert (out.cpu().numpy().view(np.uint32) == oargb).all()
+
+
+def test_cost_order_pose_change():
+    """A new camera transform changes the fine grid; the stale cost sample is dropped."""
+    import torch
+    s = H.GpuScene("rabbit_70k", 320, 180, kernel=3, tile_order=3)
+    out = torch.zeros(320 * 180, dtype=torch.int32, device="cuda:0")
+    for i in range(40):
+        xf = _rot_y(float(i % 5) * 7.0, (0.01 * (i % 3), 0.0, 0.0))
+        s.obj.quat.rot_m = np.asarray(xf, np.float32).reshape(3, 4)
+        s.cam.render_into(out, xform=s.obj.quat.xform(), mode=0)
+    xf = _rot_y(14.0, (0.01, 0.0, 0.0))
+    argb, hit, _ = s.render(0, xform=xf)
+    oargb, ohit, _ = H.oracle_render("rabbit_70k", 320, 180, 0, xform=xf)
+    _assert_same((argb, hit), (oargb, ohit), "cost order after pose changes")
