@@ -212,6 +212,80 @@ int ensure_cost(rt_camera* c, int64_t n) {
     return RT_OK;
 }
 
+// Dispatch order from the sampled costs (pool iterations of each tile's
+// waves).  Order 3: heaviest tile first (counting sort, stable over the
+// centre-out order).  Order 4: the tiles in Morton order are cut into 8 runs
+// of equal total cost, one per XCD (blocks b and b + 8 share an XCD), each
+// run heaviest first, interleaved so block b takes the next tile of run b % 8:
+// the XCDs finish together and each L2 serves one screen region's subtrees.
+std::vector<int32_t> cost_order(const rt_camera* c, const TraceParams& p, bool xcd_split) {
+    const int64_t n = (int64_t)p.tiles_x * p.block_rows;
+    uint32_t mx = 0;
+    for (int64_t t = 0; t < n; t++) mx = std::max(mx, std::max(c->h_cost[2 * t], c->h_cost[2 * t + 1]));
+    mx = std::min<uint32_t>(mx, 1u << 16);
+    auto cost_of = [&](int32_t t) {
+        return std::min<uint32_t>(std::max(c->h_cost[2 * (size_t)t], c->h_cost[2 * (size_t)t + 1]), mx);
+    };
+    // stable counting sort of `in` by cost, descending, appended to `out`
+    std::vector<int64_t> start((size_t)mx + 2);
+    auto sort_desc = [&](const int32_t* in, int64_t m, int32_t* out) {
+        std::fill(start.begin(), start.end(), 0);
+        for (int64_t k = 0; k < m; k++) start[(size_t)(mx - cost_of(in[k])) + 1]++;
+        for (size_t k = 1; k < start.size(); k++) start[k] += start[k - 1];
+        for (int64_t k = 0; k < m; k++) out[start[(size_t)(mx - cost_of(in[k]))]++] = in[k];
+    };
+    std::vector<int32_t> ord((size_t)n);
+    if (!xcd_split) {
+        sort_desc(c->centre.data(), n, ord.data());
+        return ord;
+    }
+    // Morton order of the tiles (pixel-proportional coordinates)
+    std::vector<std::pair<uint64_t, int32_t>> mk((size_t)n);
+    auto spread = [](uint64_t v) {
+        v &= 0xFFFFFFFFull;
+        v = (v | (v << 16)) & 0x0000FFFF0000FFFFull;
+        v = (v | (v << 8)) & 0x00FF00FF00FF00FFull;
+        v = (v | (v << 4)) & 0x0F0F0F0F0F0F0F0Full;
+        v = (v | (v << 2)) & 0x3333333333333333ull;
+        v = (v | (v << 1)) & 0x5555555555555555ull;
+        return v;
+    };
+    for (int64_t t = 0; t < n; t++) {
+        const uint64_t x = (uint64_t)(t % p.tiles_x) * (uint64_t)p.tile_w, y = (uint64_t)(t / p.tiles_x) * (uint64_t)p.tile_h;
+        mk[(size_t)t] = {spread(x) | (spread(y) << 1), (int32_t)t};
+    }
+    std::sort(mk.begin(), mk.end());
+    double total = 0.0;
+    for (int64_t t = 0; t < n; t++) total += 1.0 + c->h_cost[2 * t] + c->h_cost[2 * t + 1];
+    constexpr int kXcd = 8;
+    std::vector<int32_t> runs((size_t)n);
+    int64_t cut[kXcd + 1] = {0};
+    double acc = 0.0;
+    int r = 1;
+    for (int64_t k = 0; k < n && r < kXcd; k++) {
+        const int32_t t = mk[(size_t)k].second;
+        acc += 1.0 + c->h_cost[2 * (size_t)t] + c->h_cost[2 * (size_t)t + 1];
+        while (r < kXcd && acc >= total * r / kXcd) cut[r++] = k + 1;
+    }
+    while (r <= kXcd) cut[r++] = n;
+    std::vector<int32_t> in((size_t)n);
+    for (int64_t k = 0; k < n; k++) in[(size_t)k] = mk[(size_t)k].second;
+    for (int x = 0; x < kXcd; x++) sort_desc(in.data() + cut[x], cut[x + 1] - cut[x], runs.data() + cut[x]);
+    int64_t pos[kXcd];
+    for (int x = 0; x < kXcd; x++) pos[x] = cut[x];
+    for (int64_t b = 0; b < n; b++) {
+        int x = (int)(b % kXcd);
+        if (pos[x] == cut[x + 1]) {  // run exhausted: the run with most tiles left
+            int best = -1;
+            for (int y = 0; y < kXcd; y++)
+                if (pos[y] < cut[y + 1] && (best < 0 || cut[y + 1] - pos[y] > cut[best + 1] - pos[best])) best = y;
+            x = best;
+        }
+        ord[(size_t)b] = runs[(size_t)pos[x]++];
+    }
+    return ord;
+}
+
 // After a tile-order-3 frame: when an earlier cost sample has arrived, order
 // the tiles by it (heaviest unit first, centre-out among equals) and upload
 // the order behind this frame; otherwise, every kCostPeriod frames, queue a
@@ -228,21 +302,11 @@ int cost_feedback(rt_camera* c, const TraceParams& p, void* stream) {
         c->cost_pending = c->order_pending = false;
         c->frames_since = 0;
         if (c->cost_gen != c->layout_gen || (int64_t)c->centre.size() != n) return RT_OK;  // stale sample
-        // counting sort by cost, descending; stable over the centre-out order
-        uint32_t mx = 0;
-        for (int64_t t = 0; t < n; t++) mx = std::max(mx, std::max(c->h_cost[2 * t], c->h_cost[2 * t + 1]));
-        mx = std::min<uint32_t>(mx, 1u << 16);
-        std::vector<int64_t> start((size_t)mx + 2, 0);
-        auto cost_of = [&](int32_t t) {
-            return std::min<uint32_t>(std::max(c->h_cost[2 * (size_t)t], c->h_cost[2 * (size_t)t + 1]), mx);
-        };
-        for (int32_t t : c->centre) start[(size_t)(mx - cost_of(t)) + 1]++;
-        for (size_t k = 1; k < start.size(); k++) start[k] += start[k - 1];
+        const std::vector<int32_t> ord = cost_order(c, p, c->tile_order == 4);
         bool same = true;
-        for (int32_t t : c->centre) {
-            const int64_t at = start[(size_t)(mx - cost_of(t))]++;
-            same = same && c->h_order[at] == t;
-            c->h_order[at] = t;
+        for (int64_t k = 0; k < n; k++) {
+            same = same && c->h_order[k] == ord[(size_t)k];
+            c->h_order[k] = ord[(size_t)k];
         }
         if (same && c->order_gen == c->layout_gen) return RT_OK;  // d_order already holds it
         int rc;
@@ -428,7 +492,7 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
         int rc = ensure_order(c, p);
         if (rc) return rc;
         p.order = c->d_order;
-        if (c->tile_order == 3 && kernel == 3) {
+        if (c->tile_order >= 3 && kernel == 3) {
             if ((rc = ensure_cost(c, (int64_t)p.tiles_x * p.block_rows))) return rc;
             p.cost = c->d_cost;
         }
@@ -735,7 +799,7 @@ extern "C" int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value) {
         c->debug = value;
         return RT_OK;
     case kOptTileOrder:
-        if (value < 0 || value > 3) return fail(RT_ERR_INVALID, "tile order %d (0..3)", value);
+        if (value < 0 || value > 4) return fail(RT_ERR_INVALID, "tile order %d (0..4)", value);
         c->tile_order = value;
         return RT_OK;
     default:

@@ -19,6 +19,7 @@
 
 
 #include "rt_internal.h"
+#include "rt_predicates.h"
 
 namespace rt {
 namespace {
@@ -93,7 +94,8 @@ __device__ __forceinline__ uint32_t phong(const float pnt[3], const float nrm[3]
 // natural (neighbouring tiles on different XCDs); order 2: the host's
 // centre-out permutation, so the heavy centre tiles are dispatched first;
 // order 3: the host's permutation by the tiles' measured cost in an earlier
-// frame, heaviest first (centre-out until costs arrive).
+// frame, heaviest first (centre-out until costs arrive); order 4: the same
+// per XCD over 8 screen regions of equal cost.
 __device__ __forceinline__ int32_t tile_index(const TraceParams& P, int32_t b) {
     const int32_t nblocks = P.tiles_x * P.block_rows;
     if (P.tile_order == 0) {
@@ -101,7 +103,7 @@ __device__ __forceinline__ int32_t tile_index(const TraceParams& P, int32_t b) {
         const int32_t xcd = b & 7, k = b >> 3;
         return (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + k;
     }
-    if (P.tile_order >= 2 && P.order) return P.order[b];
+    if (P.tile_order >= 2 && P.order) return P.order[b];  // orders 2-4: host permutation
     return b;
 }
 
@@ -288,7 +290,7 @@ __global__ __launch_bounds__(kTileWFlat * kTileH) void k_trace_kd(TraceParams P)
         const float t1z = sz ? b.y * iz : b.x * iz;
         float maxt0 = fmaxf(t0z + oz, fmaxf(t0x + ox, t0y + oy));
         float mint1 = fminf(t1z + oz, fminf(t1x + ox, t1y + oy));
-        if ((double)mint1 >= (double)maxt0 - kEps && (double)maxt0 > -kEps) {
+        if (pred::enter(maxt0, mint1)) {
             if (kCount) n_desc++;
             const uint32_t axis = c.z;
             const float dir = axis == 0 ? dir_a[0] : axis == 1 ? dir_a[1] : dir_a[2];
@@ -304,9 +306,9 @@ __global__ __launch_bounds__(kTileWFlat * kTileH) void k_trace_kd(TraceParams P)
                 s2 = b.w;
             }
             const uint32_t L = c.x, R = c.y;
-            if ((double)maxt0 < (double)s2 + kEps) {
+            if (pred::lt_eps(maxt0, s2)) {
                 // pushes right (if) then left: left is popped first
-                if ((double)mint1 > (double)s2 - kEps) {
+                if (pred::gt_eps(mint1, s2)) {
                     if (sp >= P.max_depth) { atomicOr(P.err, 1); break; }
                     stk[(sp++) * kBlock] = R;
                 }
@@ -384,7 +386,7 @@ __device__ __forceinline__ bool slab(const Ray& R, float lx, float hx, float ly,
     const float t1z = R.sz ? hz * R.iz : lz * R.iz;
     maxt0 = fmaxf(t0z + R.oz, fmaxf(t0x + R.ox, t0y + R.oy));
     mint1 = fminf(t1z + R.oz, fminf(t1x + R.ox, t1y + R.oy));
-    return (double)mint1 >= (double)maxt0 - kEps && (double)maxt0 > -kEps;
+    return pred::enter(maxt0, mint1);
 }
 
 // Moller-Trumbore at a leaf, TD/Trixel.cu:98-145; updates (d, best) on a
@@ -491,15 +493,15 @@ __global__ __launch_bounds__(kTileWKd * kTileH) void k_trace_kd2(TraceParams P) 
                 s1 = (float)((double)r3.x + kEps + (double)ds);
                 s2 = r3.y + ds;
             } else {  // ds == 0: the same values without the +0
-                s1 = (float)((double)r3.x + kEps);
+                s1 = pred::add_eps(r3.x);
                 s2 = r3.y;
             }
             // Push order of TD/Trixel.cu:155-168.  `first` is popped next,
             // `second` (if pushed) after first's subtree.
             bool left_first, push_second;
-            if ((double)mx < (double)s2 + kEps) {
+            if (pred::lt_eps(mx, s2)) {
                 left_first = true;
-                push_second = (double)mn > (double)s2 - kEps;
+                push_second = pred::gt_eps(mn, s2);
             } else {
                 left_first = false;
                 push_second = (mn < s1 || mx < s1);
@@ -604,7 +606,7 @@ struct Item {
 #define RT_POOL_CAP_R32 448
 #endif
 #ifndef RT_POOL_CAP_R16
-#define RT_POOL_CAP_R16 320
+#define RT_POOL_CAP_R16 384
 #endif
 #ifndef RT_POOL_CAP_R8
 #define RT_POOL_CAP_R8 256
@@ -747,13 +749,13 @@ __device__ __forceinline__ void visit_item(const float4* rd, uint4 it, float4 r0
         s1 = (float)((double)r3.x + kEps + (double)ds);
         s2 = r3.y + ds;
     } else {
-        s1 = (float)((double)r3.x + kEps);
+        s1 = pred::add_eps(r3.x);
         s2 = r3.y;
     }
     bool left_first, push_second;
-    if ((double)mx < (double)s2 + kEps) {
+    if (pred::lt_eps(mx, s2)) {
         left_first = true;
-        push_second = (double)mn > (double)s2 - kEps;
+        push_second = pred::gt_eps(mn, s2);
     } else {
         left_first = false;
         push_second = (mn < s1 || mx < s1);
@@ -797,7 +799,8 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long b) {
 template <int kCap, int kVec, bool kTranslated, bool kCount, bool kAny>
 __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, const float4* s_ray,
                                           unsigned long long* s_key, uint32_t* s_tri, int n, int lane,
-                                          uint32_t& iters, uint32_t& n_int, uint32_t& n_leaf, uint32_t& n_acc,
+                                          uint32_t& iters, uint32_t& popped, uint32_t& n_int, uint32_t& n_leaf,
+                                          uint32_t& n_acc,
                                           uint32_t& n_desc) {
     const int cap = min(P.pool_cap, kCap);
     const int per = P.items > 1 ? 128 : 64;
@@ -811,11 +814,15 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
         int take = min(min(n, per), cap - kCodeBits - 1 - n);
         if (take < 1) take = 1;
         iters++;
+        popped += (uint32_t)take;
         const int base = n - take;
+        // Both items and both records are read unconditionally (idle lanes
+        // re-read item `base`, a live item, whose record is a valid address):
+        // with guarded loads hipcc zero-fills the registers of the idle path
+        // and waits for the first record before issuing the second.
         bool act0 = lane < take, act1 = lane + 64 < take;
-        uint4 it0 = make_uint4(0, 0, 0, 0), it1 = make_uint4(0, 0, 0, 0);
-        if (act0) it0 = items[base + lane];
-        if (act1) it1 = items[base + 64 + lane];
+        const uint4 it0 = items[base + (act0 ? lane : 0)];
+        const uint4 it1 = items[base + (act1 ? lane + 64 : 0)];
         __builtin_amdgcn_wave_barrier();
         // any-hit: a ray already shadowed needs no more visits (kept when
         // counting, so the counters match the oracle's full walk)
@@ -824,24 +831,17 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
             if (act1 && s_key[it1.w >> 26] == 0ull) act1 = false;
         }
         // both records in flight before either is consumed
-        float4 a0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), a1 = a0, a2 = a0, a3 = a0;
-        float4 b0 = a0, b1 = a0, b2 = a0, b3 = a0;
-        if (act0) {
-            const float4* p = record_of(P, it0.x);
-            a0 = p[0]; a1 = p[1]; a2 = p[2]; a3 = p[3];
-        }
-        if (act1) {
-            const float4* p = record_of(P, it1.x);
-            b0 = p[0]; b1 = p[1]; b2 = p[2]; b3 = p[3];
-        }
+        const float4* p0 = record_of(P, it0.x);
+        const float4* p1 = record_of(P, it1.x);
+        const float4 a0 = p0[0], a1 = p0[1], a2 = p0[2], a3 = p0[3];
+        const float4 b0 = p1[0], b1 = p1[1], b2 = p1[2], b3 = p1[3];
         asm volatile("" ::"v"(a0.x), "v"(a0.y), "v"(a0.z), "v"(a0.w), "v"(a1.x), "v"(a1.y), "v"(a1.z), "v"(a1.w),
                      "v"(a2.x), "v"(a2.y), "v"(a2.z), "v"(a2.w), "v"(a3.x), "v"(a3.y), "v"(a3.z), "v"(a3.w));
         asm volatile("" ::"v"(b0.x), "v"(b0.y), "v"(b0.z), "v"(b0.w), "v"(b1.x), "v"(b1.y), "v"(b1.z), "v"(b1.w),
                      "v"(b2.x), "v"(b2.y), "v"(b2.z), "v"(b2.w), "v"(b3.x), "v"(b3.y), "v"(b3.z), "v"(b3.w));
-        Visit v0, v1;
-        v0.nk = 0; v0.cand = false; v0.key = 0; v0.ctri = 0;
-        v0.c0 = v0.c1 = make_uint4(0, 0, 0, 0);
-        v1 = v0;
+        Visit v0, v1;  // children / key fields are read only where nk / cand say so
+        v0.nk = 0; v0.cand = false;
+        v1.nk = 0; v1.cand = false;
         if (act0)
             visit_item<kVec, kTranslated, kCount, kAny>(s_ray + (size_t)(it0.w >> 26) * kVec, it0, a0, a1, a2, a3, v0,
                                                         n_int, n_leaf, n_acc, n_desc);
@@ -906,7 +906,7 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
     Pixel px;
     const bool live = unit_pixel(P, U, kRays / 8, lane, px);  // every lane stays for the ballots
     const unsigned long long t_start = P.dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    uint32_t iters = 0;
+    uint32_t iters = 0, popped = 0;
 
     float cam[3];
     Ray R;
@@ -919,7 +919,7 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
     }
 
     int n = seed_root<kCount>(P, items, R, live, lane, C.n_int, C.n_desc);
-    pool_walk<kCap, kRayVec, kTranslated, kCount, false>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters, C.n_int,
+    pool_walk<kCap, kRayVec, kTranslated, kCount, false>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters, popped, C.n_int,
                                                         C.n_leaf, C.n_acc, C.n_desc);
     unsigned long long kbest = ~0ull;
     uint32_t best = kMiss;
@@ -951,14 +951,14 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
         }
         __builtin_amdgcn_wave_barrier();
         n = seed_root<kCount>(P, items, Sh, sh_live, lane, C.n_int, C.n_desc);
-        pool_walk<kCap, kRayVec, true, kCount, true>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters, C.n_int,
+        pool_walk<kCap, kRayVec, true, kCount, true>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters, popped, C.n_int,
                                                     C.n_leaf, C.n_acc, C.n_desc);
         if (lane < kRays) shadowed = S_.key[lane] == 0ull;
     }
     if (P.dbg && lane == 0 && dbg_slot != kNoDbg) {  // diagnostics: the unit's start/end clock (100 MHz) and pool iterations
         P.dbg[3 * dbg_slot] = t_start;
         P.dbg[3 * dbg_slot + 1] = __builtin_amdgcn_s_memrealtime();
-        P.dbg[3 * dbg_slot + 2] = iters;
+        P.dbg[3 * dbg_slot + 2] = iters | ((unsigned long long)popped << 32);
     }
     if (cost && lane == 0) *cost = iters;  // tile order 3: this unit's pool iterations
     __builtin_amdgcn_wave_barrier();  // LDS of this unit is read; the next unit may overwrite it
@@ -1027,8 +1027,13 @@ __device__ __forceinline__ unsigned long long coarse_root(const TraceParams& P, 
 // (2,2,2) to the hit, walked from the light with the reference's rules.
 // One fine tile per block (the tiles covering the root box's screen
 // rectangle, or the whole frame), one unit per wave.
+#ifdef RT_KD3_WAVES_PER_SIMD
+#define RT_KD3_BOUNDS __launch_bounds__(128, RT_KD3_WAVES_PER_SIMD)
+#else
+#define RT_KD3_BOUNDS __launch_bounds__(128)
+#endif
 template <int kRays, bool kTranslated, bool kWriteHit, bool kCount, bool kShadow>
-__global__ __launch_bounds__(128) void k_trace_kd3(TraceParams P) {
+__global__ RT_KD3_BOUNDS void k_trace_kd3(TraceParams P) {
     constexpr int kWaves = 2;
     constexpr int kCap = pool_cap_for<kRays>();
     constexpr int kRayVec = (kTranslated || kShadow) ? 5 : 3;  // float4s of per-ray data in LDS

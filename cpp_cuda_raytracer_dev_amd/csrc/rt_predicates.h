@@ -1,0 +1,82 @@
+// rt_predicates.h -- the reference's double-promoted epsilon compares, and
+// exact single-precision forms of them for the traversal's hot loop.
+//
+// The reference evaluates its epsilon tests in double (the 1e-16 literals of
+// TD/vector.cuh:10-11 promote the float operands): the slab entry test
+// `mint1 >= maxt0 - 1e-16 && maxt0 > -1e-16` (TD/Trixel.cu:146) and the child
+// ordering `maxt0 < s2 + 1e-16`, `mint1 > s2 - 1e-16`, `s1 + 1e-16`
+// (TD/Trixel.cu:150-161).  For a float x with |x| >= 2^-20 the float spacing
+// around x (>= 2^-43) dwarfs 1e-16, so x -/+ 1e-16 rounded to double lies in
+// (pred(x), x] / [x, succ(x)) and each test reduces to a float compare with
+// one of its edge cases (equality) decided by the double form.  Tiny, NaN and
+// equal operands take the double form itself.  tests/test_predicates.py
+// checks every fast form against its double form on CPU (edge sets plus
+// random sweeps over all binades).  The kernels use the double forms unless
+// built with -DRT_FAST_PREDICATES: on gfx950 the branches of the fast forms
+// cost more than the double arithmetic they skip (0.126 vs 0.118 ms per
+// 1080p dragon frame, tools/ab_session.sh).
+#pragma once
+
+#include <math.h>
+#include <stdint.h>
+
+#ifdef __HIPCC__
+#define RT_HD __host__ __device__ __forceinline__
+#else
+#define RT_HD static inline
+#endif
+
+namespace rt {
+namespace pred {
+
+constexpr double kEps = 1e-16;
+constexpr float kSmall = 0x1p-20f;
+
+// Smallest float >= 1e-16 (1e-16 is not a float): (double)x > -1e-16 <=> x > -kEpsF.
+RT_HD float eps_f() {
+    union { uint32_t u; float f; } c = {0x24e69595u};
+    return c.f;
+}
+
+// TD/Trixel.cu:146: descend into a node whose box the ray enters.
+RT_HD bool enter_ref(float maxt0, float mint1) { return (double)mint1 >= (double)maxt0 - kEps && (double)maxt0 > -kEps; }
+RT_HD bool enter(float maxt0, float mint1) {
+#ifndef RT_FAST_PREDICATES
+    return enter_ref(maxt0, mint1);
+#endif
+    if (maxt0 >= kSmall) return mint1 >= maxt0;
+    if (maxt0 <= -kSmall) return false;
+    return enter_ref(maxt0, mint1);
+}
+
+// (double)a < (double)s + 1e-16 (TD/Trixel.cu:155).
+RT_HD bool lt_eps_ref(float a, float s) { return (double)a < (double)s + kEps; }
+RT_HD bool lt_eps(float a, float s) {
+#ifndef RT_FAST_PREDICATES
+    return lt_eps_ref(a, s);
+#endif
+    if (a != s && fabsf(s) >= kSmall) return a < s;
+    return lt_eps_ref(a, s);
+}
+
+// (double)a > (double)s - 1e-16 (TD/Trixel.cu:157).
+RT_HD bool gt_eps_ref(float a, float s) { return (double)a > (double)s - kEps; }
+RT_HD bool gt_eps(float a, float s) {
+#ifndef RT_FAST_PREDICATES
+    return gt_eps_ref(a, s);
+#endif
+    if (a != s && fabsf(s) >= kSmall) return a > s;
+    return gt_eps_ref(a, s);
+}
+
+// (float)((double)s + 1e-16) (TD/Trixel.cu:150 with a zero object offset).
+RT_HD float add_eps_ref(float s) { return (float)((double)s + kEps); }
+RT_HD float add_eps(float s) {
+#ifndef RT_FAST_PREDICATES
+    return add_eps_ref(s);
+#endif
+    return fabsf(s) >= kSmall ? s : add_eps_ref(s);
+}
+
+}  // namespace pred
+}  // namespace rt

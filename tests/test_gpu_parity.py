@@ -45,7 +45,7 @@ def test_small_frames_vs_golden(name, w, h, mode):
 
 
 KERNELS = [(1, 0, 64), (2, 2, 64), (2, 1, 64), (3, 1, 64), (3, 2, 32), (3, 1, 32), (3, 2, 16), (3, 2, 8), (3, 3, 16),
-           (3, 3, 8)]  # (KD kernel, tile order, rays/wave)
+           (3, 3, 8), (3, 4, 16)]  # (KD kernel, tile order, rays/wave)
 
 
 def _counters_match(cnt, ocnt, kernel):
@@ -388,11 +388,12 @@ def test_coarse_band_tiles(nranks, debug):
 # earlier frame measured (read back asynchronously every few frames).  Any
 # permutation gives the same frame; these tests run enough frames for the
 # feedback to reorder the tiles, then compare with the oracle.
+@pytest.mark.parametrize("order", [3, 4])
 @pytest.mark.parametrize("rays", [16, 8])
 @pytest.mark.parametrize("name,w,h", [("dragon", 960, 540), ("rabbit_70k", 320, 180)])
-def test_cost_order_feedback(name, w, h, rays):
+def test_cost_order_feedback(name, w, h, rays, order):
     import torch
-    s = H.GpuScene(name, w, h, kernel=3, tile_order=3, rays=rays)
+    s = H.GpuScene(name, w, h, kernel=3, tile_order=order, rays=rays)
     oargb, ohit, ocnt = H.oracle_render(name, w, h, 0)
     out = torch.zeros(w * h, dtype=torch.int32, device="cuda:0")
     st = torch.cuda.Stream()
@@ -410,10 +411,11 @@ def test_cost_order_feedback(name, w, h, rays):
     assert (out.cpu().numpy().view(np.uint32) == oargb).all()
 
 
-def test_cost_order_pose_change():
+@pytest.mark.parametrize("order", [3, 4])
+def test_cost_order_pose_change(order):
     """A new camera transform changes the fine grid; the stale cost sample is dropped."""
     import torch
-    s = H.GpuScene("rabbit_70k", 320, 180, kernel=3, tile_order=3)
+    s = H.GpuScene("rabbit_70k", 320, 180, kernel=3, tile_order=order)
     out = torch.zeros(320 * 180, dtype=torch.int32, device="cuda:0")
     for i in range(40):
         xf = _rot_y(float(i % 5) * 7.0, (0.01 * (i % 3), 0.0, 0.0))

@@ -50,7 +50,8 @@ def main():
     rec = buf[:got].reshape(-1, 3).astype(np.int64)
     rec = rec[rec[:, 1] > 0]
     t0 = rec[:, 0].min()
-    start, end, vis = (rec[:, 0] - t0) * 10e-3, (rec[:, 1] - t0) * 10e-3, rec[:, 2]  # us
+    start, end = (rec[:, 0] - t0) * 10e-3, (rec[:, 1] - t0) * 10e-3  # us
+    vis, popped = rec[:, 2] & 0xFFFFFFFF, rec[:, 2] >> 32  # pool iterations, items popped
     dur = end - start
     res["span_us"] = float(end.max())
     res["waves"] = int(len(rec))
@@ -66,6 +67,12 @@ def main():
         res["longest_wave"] = {"dur_us": float(dur[k]), "visits": int(vis[k]), "start_us": float(start[k])}
         res["us_per_visit_longest"] = float(dur[k] / max(vis[k], 1))
         res["us_per_visit_median_heavy"] = float(np.median(dur[heavy] / np.maximum(vis[heavy], 1)))
+        res["longest_wave"]["items"] = int(popped[k])
+        res["items_per_iter_heavy_p10_p50_p90"] = [float(np.percentile(popped[heavy] / np.maximum(vis[heavy], 1), q))
+                                                   for q in (10, 50, 90)]
+        top = np.argsort(-dur)[:200]
+        res["items_per_iter_200_longest"] = float(popped[top].sum() / max(vis[top].sum(), 1))
+        res["iters_200_longest_mean"] = float(vis[top].mean())
     # when do light waves finish vs heavy waves start
     res["time_all_light_done_us"] = float(end[~heavy].max()) if (~heavy).any() else None
     print(json.dumps(res))
