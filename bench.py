@@ -53,6 +53,13 @@ def parse():
     ap.add_argument("--items", type=int, default=2, help="kernel 3: items each lane pops per iteration (1, 2)")
     ap.add_argument("--coarse", type=int, default=8,
                     help="kernel 3: 8x8 groups per wave outside the root box's screen rectangle (0 = off)")
+    ap.add_argument("--prio", type=int, default=0,
+                    help="tile order 3/4: tiles costing >= this %% of the heaviest one run at raised priority")
+    ap.add_argument("--event-every", type=int, default=1,
+                    help="bracket every Nth timed frame with HIP events for the kernel time (each pair costs "
+                         "queue time, so N > 1 keeps the frame rate closer to the uninstrumented one)")
+    ap.add_argument("--side-coarse", action="store_true",
+                    help="kernel 3: run the coarse kernel beside the fine one on a side stream (default: before it)")
     ap.add_argument("--shadow", action="store_true",
                     help="one shadow ray per hit (config C5: --scene happy --width 3840 --height 2160 --shadow)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
@@ -146,6 +153,9 @@ def main():
     cam.set_option(_lib.RT_OPT_RAYS, a.rays)
     cam.set_option(_lib.RT_OPT_ITEMS, a.items)
     cam.set_option(_lib.RT_OPT_COARSE, a.coarse)
+    cam.set_option(_lib.RT_OPT_PRIO, a.prio)
+    if a.side_coarse:
+        cam.set_option(_lib.RT_OPT_DEBUG, 8)
     cam.render_into(scratch, mode=a.mode, flags=sflag, tile=tile if world > 1 else None,
                     stream=sptr)  # re-prepares layout
     torch.cuda.synchronize(dev)
@@ -161,15 +171,16 @@ def main():
         fg = None
         out = torch.zeros(w * h, dtype=torch.int32, device=dev)
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    timed_frames = list(range(0, a.steps, max(1, a.event_every)))
+    ev = {i: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for i in timed_frames}
 
     def frame(i=None):
         with torch.cuda.stream(stream):
-            if i is not None:
+            if i in ev:
                 ev[i][0].record(stream)
             cam.render_into(out, xform=xf, mode=a.mode, flags=sflag, tile=tile if world > 1 else None,
                             stream=sptr)
-            if i is not None:
+            if i in ev:
                 ev[i][1].record(stream)
             if fg is not None:
                 fg.gather()
@@ -188,7 +199,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev.values()]))
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -250,8 +261,10 @@ def main():
                           else "k_trace_flat",
                 "kernel_options": {"kernel": a.kernel, "tile_order": a.tile_order, "rays_per_wave": a.rays,
                                    "items_per_lane": a.items, "coarse_groups_per_wave": a.coarse,
+                                   "prio": a.prio,
                                    "shadow": a.shadow},
                 "kernel_ms_avg": round(kern_ms, 5),
+                "kernel_ms_frames": f"{len(ev)} of {a.steps} timed frames (every {max(1, a.event_every)})",
                 "kernel_ms_avg_max_rank": round(kern_ms_max, 5),
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "counts_per_launch": {"interior": int(cnt[0]), "leaf": int(cnt[1]), "accept": int(cnt[2]),

@@ -56,7 +56,17 @@ struct rt_camera {
     int64_t order_cap = 0;
     int64_t order_key[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
     int coarse = 8;                  // kOptCoarse: coarse groups per wave (0 = off)
+    int prio = 0;                    // kOptPrio: % of the heaviest tile's cost that earns raised priority
+    int32_t prio_blocks = 0;         // leading blocks of the current cost order at raised priority
     std::vector<int32_t> centre;     // centre-out permutation of the current fine grid (host copy)
+    // 8x8 groups (x / 8, y / 8) holding a pixel whose primary ray has a zero
+    // or tiny component (computed once, as the kernels compute the rays)
+    std::vector<std::pair<int32_t, int32_t>> tiny_groups;
+    bool tiny_done = false;
+    // kernel 3: the coarse groups run on a side stream beside the fine tiles
+    // (disjoint pixels), forked from and joined back into the caller's stream
+    hipStream_t side = nullptr;
+    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
     // tile order 3: each frame's per-unit pool iterations feed the next
     // frames' dispatch order, read back asynchronously (never a sync).
     uint32_t* d_cost = nullptr;      // [tile][2] iterations, written by every frame
@@ -303,6 +313,15 @@ int cost_feedback(rt_camera* c, const TraceParams& p, void* stream) {
         c->frames_since = 0;
         if (c->cost_gen != c->layout_gen || (int64_t)c->centre.size() != n) return RT_OK;  // stale sample
         const std::vector<int32_t> ord = cost_order(c, p, c->tile_order == 4);
+        c->prio_blocks = 0;
+        if (c->prio > 0) {  // tiles at >= prio % of the heaviest one's iterations
+            uint32_t mx = 0;
+            for (int64_t t = 0; t < n; t++) mx = std::max(mx, std::max(c->h_cost[2 * t], c->h_cost[2 * t + 1]));
+            const uint64_t bar = ((uint64_t)mx * (uint64_t)c->prio + 99) / 100;
+            int64_t heavy = 0;
+            for (int64_t t = 0; t < n; t++) heavy += std::max(c->h_cost[2 * t], c->h_cost[2 * t + 1]) >= bar ? 1 : 0;
+            c->prio_blocks = (int32_t)heavy;  // order 3 puts them first; order 4 roughly so
+        }
         bool same = true;
         for (int64_t k = 0; k < n; k++) {
             same = same && c->h_order[k] == ord[(size_t)k];
@@ -383,7 +402,37 @@ bool root_rect(const rt_camera* c, const TraceParams& p, double r[4]) {
 // Splits this rank's tiles into the fine region (one kRays unit per wave)
 // around the root box's screen rectangle and coarse 8x8 groups elsewhere
 // (`per_wave` to a wave; 0 = everything fine).
-void set_fine_region(const rt_camera* c, TraceParams& p, int per_wave) {
+// Groups with a pixel whose unnormalised primary ray q = n + u*x + v*y (the
+// kernels' float expression) has a component of magnitude <= 1e-30: their
+// slab tests may see 0/0 = NaN, so they never take the far-group shortcut.
+void find_tiny_groups(rt_camera* c) {
+    if (c->tiny_done) return;
+    const float* n = c->basis.n_mod;
+    const float* u = c->basis.u_mod;
+    const float* v = c->basis.v_mod;
+    for (int32_t y = 0; y < c->h; y++) {
+        const float fy = (float)(uint32_t)y;
+        for (int32_t x = 0; x < c->w; x++) {
+            const float fx = (float)(uint32_t)x;
+            const float qx = n[0] + u[0] * fx + v[0] * fy;
+            const float qy = n[1] + u[1] * fx + v[1] * fy;
+            const float qz = n[2] + u[2] * fx + v[2] * fy;
+            if (!(fabsf(qx) > 1e-30f && fabsf(qy) > 1e-30f && fabsf(qz) > 1e-30f)) {
+                const std::pair<int32_t, int32_t> g{x / 8, y / kTileH};
+                if (c->tiny_groups.empty() || c->tiny_groups.back() != g) c->tiny_groups.push_back(g);
+            }
+        }
+    }
+    std::sort(c->tiny_groups.begin(), c->tiny_groups.end());
+    c->tiny_groups.erase(std::unique(c->tiny_groups.begin(), c->tiny_groups.end()), c->tiny_groups.end());
+    c->tiny_done = true;
+}
+
+// fused: the caller wants the far groups filled by the fine kernel's extra
+// blocks; the fine region then covers every group that is not far, and
+// fusion is refused (returns false, region set as unfused) when a tiny-ray
+// group would fall outside it.
+bool set_fine_region(rt_camera* c, TraceParams& p, int per_wave, bool fused) {
     const int32_t nbands = (c->h + kTileH - 1) / kTileH;
     const int32_t per_band = kTileH / p.tile_h;
     p.groups_x = (c->w + 7) / 8;
@@ -394,8 +443,20 @@ void set_fine_region(const rt_camera* c, TraceParams& p, int per_wave) {
     p.coarse_per_wave = 1;
     p.coarse_groups = 0;
     p.coarse_blocks = 0;
+    // no group is "far" unless the projection below succeeds
+    p.far_rect[0] = p.far_rect[2] = INT32_MIN / 2;
+    p.far_rect[1] = p.far_rect[3] = INT32_MAX / 2;
+    p.fill_blocks = 0;
     double r[4];
-    if (per_wave <= 0 || !root_rect(c, p, r)) return;
+    // coarse groups are indexed in 32 bits (k_coarse_kd3)
+    if (per_wave <= 0 || (int64_t)p.nslots * p.groups_x >= ((int64_t)1 << 31) || !root_rect(c, p, r)) return false;
+    // r is the projection widened by a pixel; far groups lie 2 more outside
+    auto clampi = [](double v) { return (int32_t)std::max(-1e9, std::min(1e9, v)); };
+    p.far_rect[0] = clampi(r[0] - 2); p.far_rect[1] = clampi(r[1] + 2);
+    p.far_rect[2] = clampi(r[2] - 2); p.far_rect[3] = clampi(r[3] + 2);
+    if (fused) {  // fine tiles over everything within the far rectangle
+        r[0] -= 2; r[1] += 2; r[2] -= 2; r[3] += 2;
+    }
     if (c->debug & 4) r[0] = r[1] = r[2] = r[3] = -8.0;  // tests: every group coarse
     const double x0 = std::max(r[0], 0.0), x1 = std::min(r[1], (double)c->w - 1);
     const double y0 = std::max(r[2], 0.0), y1 = std::min(r[3], (double)c->h - 1);
@@ -429,6 +490,19 @@ void set_fine_region(const rt_camera* c, TraceParams& p, int per_wave) {
     p.coarse_groups = (int64_t)p.nslots * p.groups_x - (int64_t)(p.cs1 - p.cs0) * (p.cg_x1 - p.cg_x0);
     const int64_t waves = (p.coarse_groups + per_wave - 1) / per_wave;
     p.coarse_blocks = (int32_t)((waves + 1) / 2);  // kernel 3 runs two waves per block
+    if (fused) {
+        find_tiny_groups(c);
+        for (const auto& g : c->tiny_groups) {
+            const int32_t band = g.second;
+            if ((band - p.rank) % p.nranks != 0 || band < p.rank) continue;  // not this rank's band
+            const int32_t slot = (band - p.rank) / p.nranks;
+            if (g.first < p.cg_x0 || g.first >= p.cg_x1 || slot < p.cs0 || slot >= p.cs1)
+                return set_fine_region(c, p, per_wave, false);
+        }
+        p.fill_blocks = p.coarse_blocks;  // appended to the fine kernel's grid
+        p.coarse_blocks = 0;
+    }
+    return fused;
 }
 
 int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t* argb, int64_t* hit,
@@ -465,7 +539,16 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
     p.tiles_x = (c->w + p.tile_w - 1) / p.tile_w;
     p.block_rows = ((nbands + p.nranks - 1) / p.nranks) * (kTileH / p.tile_h);
     camera_relative_box(s->root, c->pos, p.root_box);
-    set_fine_region(c, p, kernel == 3 ? c->coarse : 0);
+    {
+        static const float eye[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+        p.plain_xf = 1;
+        for (int k = 0; k < 12; k++) p.plain_xf &= (p.xf[k] == eye[k]) ? 1 : 0;
+    }
+    // Far groups go to the fine kernel's extra blocks when every coarse group
+    // can be far (identity transform, interior root, no diagnostics);
+    // otherwise to k_coarse_kd3.
+    const bool fuse = kernel == 3 && p.plain_xf && !(s->root_ref & kLeafBit) && !(c->debug & (1 | 4 | 8));
+    set_fine_region(c, p, kernel == 3 ? c->coarse : 0, fuse);
     p.root_ref = s->root_ref;
     p.ntri = s->ntri;
     p.max_depth = kMaxDepth;
@@ -476,7 +559,7 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
     p.items = c->items;
     p.dbg = nullptr;
     if (c->debug & 2) {
-        const int64_t need = ((int64_t)p.tiles_x * p.block_rows + p.coarse_blocks) * 4 * 3;  // <= 4 waves per block
+        const int64_t need = ((int64_t)p.tiles_x * p.block_rows + p.coarse_blocks + p.fill_blocks) * 4 * 3;
         if (c->dbg_cap < need) {
             dev_free(c->d_dbg);
             int rc = dev_alloc(&c->d_dbg, (size_t)need, "hipMalloc(dbg)");
@@ -488,6 +571,7 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
         if (rc) return rc;
     }
     p.cost = nullptr;
+    p.prio_blocks = 0;
     if (c->tile_order >= 2 && p.tiles_x * p.block_rows > 0) {
         int rc = ensure_order(c, p);
         if (rc) return rc;
@@ -495,6 +579,7 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
         if (c->tile_order >= 3 && kernel == 3) {
             if ((rc = ensure_cost(c, (int64_t)p.tiles_x * p.block_rows))) return rc;
             p.cost = c->d_cost;
+            p.prio_blocks = c->order_gen == c->layout_gen ? c->prio_blocks : 0;
         }
     }
     return RT_OK;
@@ -504,6 +589,13 @@ int check_tile(const rt_tile* tile) {
     if (tile && (tile->nranks < 1 || tile->rank < 0 || tile->rank >= tile->nranks))
         return fail(RT_ERR_INVALID, "rt_tile: rank %d of %d", tile->rank, tile->nranks);
     return RT_OK;
+}
+
+// The device error word: 1 = DFS stack overflow (kernels 1-2), 2 = item pool
+// overflow (kernel 3), 4 = a fused far group that was not far (kernel 3).
+int device_error(int32_t err) {
+    return fail(RT_ERR_OVERFLOW, "device reported %s%s%s", (err & 1) ? "[traversal stack overflow]" : "",
+                (err & 2) ? "[item pool overflow]" : "", (err & 4) ? "[far-group check failed]" : "");
 }
 
 }  // namespace
@@ -647,6 +739,34 @@ extern "C" int rt_camera_add_object(rt_camera* c, rt_scene* s) {
     return prepare_camera_object(c);
 }
 
+// The trace launches of one frame: the coarse kernel, then the fine one, on
+// the caller's stream.  Debug bit 8 instead runs the coarse kernel on the
+// camera's side stream beside the fine one (forked after the caller's
+// earlier work, joined before its later work); measured slower, since its
+// waves take the slots the heaviest fine tiles need.
+static int launch_split(rt_camera* c, const TraceParams& p, uint32_t mode, uint32_t flags, void* stream) {
+    const int kernel = effective_kernel(c);
+    if (p.coarse_blocks == 0 || p.tiles_x * p.block_rows == 0 || !(c->debug & 8))
+        return launch_trace(p, mode, flags, kernel, stream, kPartAll);
+    int rc;
+    if (!c->side &&
+        (rc = hip_check(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking), "side stream")))
+        return rc;
+    if (!c->fork_ev && (rc = hip_check(hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming), "fork event")))
+        return rc;
+    if (!c->join_ev && (rc = hip_check(hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming), "join event")))
+        return rc;
+    hipStream_t st = (hipStream_t)stream;
+    if ((rc = hip_check(hipEventRecord(c->fork_ev, st), "fork record")) ||
+        (rc = launch_trace(p, mode, flags, kernel, stream, kPartFine)) ||
+        (rc = hip_check(hipStreamWaitEvent(c->side, c->fork_ev, 0), "fork wait")) ||
+        (rc = launch_trace(p, mode, flags, kernel, c->side, kPartCoarse)) ||
+        (rc = hip_check(hipEventRecord(c->join_ev, c->side), "join record")) ||
+        (rc = hip_check(hipStreamWaitEvent(st, c->join_ev, 0), "join wait")))
+        return rc;
+    return RT_OK;
+}
+
 static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32_t flags, const rt_tile* tile,
                          uint32_t* argb, int64_t* hit, void* stream) {
     if (!c) return fail(RT_ERR_INVALID, "rt_render: null camera");
@@ -669,7 +789,7 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
     }
     TraceParams p;
     if ((rc = fill_params(c, xform, tile, argb, hit, mode, p))) return rc;
-    if ((rc = launch_trace(p, mode, flags, effective_kernel(c), stream))) return rc;
+    if ((rc = launch_split(c, p, mode, flags, stream))) return rc;
     return p.cost ? cost_feedback(c, p, stream) : RT_OK;
 }
 
@@ -712,7 +832,7 @@ extern "C" int rt_read_frame(rt_camera* c, uint32_t* argb, int64_t* hit) {
         return rc;
     if (hit && (rc = hip_check(hipMemcpy(hit, c->d_hit, npix * sizeof(int64_t), hipMemcpyDeviceToHost), "D2H hit")))
         return rc;
-    if (err) return fail(RT_ERR_OVERFLOW, "traversal stack overflow reported by the device");
+    if (err) return device_error(err);
     return RT_OK;
 }
 
@@ -727,7 +847,7 @@ extern "C" int rt_camera_counters(rt_camera* c, uint64_t out[5], int reset) {
     if (reset && (rc = hip_check(hipMemset(c->d_counters, 0, sizeof tmp), "reset counters"))) return rc;
     int32_t err = 0;
     if ((rc = hip_check(hipMemcpy(&err, c->d_err, sizeof err, hipMemcpyDeviceToHost), "D2H err"))) return rc;
-    if (err) return fail(RT_ERR_OVERFLOW, "traversal stack overflow reported by the device");
+    if (err) return device_error(err);
     return RT_OK;
 }
 
@@ -766,6 +886,9 @@ extern "C" void rt_camera_destroy(rt_camera* c) {
     if (c->h_order) (void)hipHostFree(c->h_order);
     if (c->cost_ev) (void)hipEventDestroy(c->cost_ev);
     if (c->order_ev) (void)hipEventDestroy(c->order_ev);
+    if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
+    if (c->join_ev) (void)hipEventDestroy(c->join_ev);
+    if (c->side) (void)hipStreamDestroy(c->side);
     delete c;
 }
 
@@ -786,8 +909,12 @@ extern "C" int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value) {
         c->items = value;
         return RT_OK;
     case kOptCoarse:
-        if (value < 0 || value > 4096) return fail(RT_ERR_INVALID, "coarse groups per wave %d (0..4096)", value);
+        if (value < 0 || value > 32) return fail(RT_ERR_INVALID, "coarse groups per wave %d (0..32)", value);
         c->coarse = value;
+        return RT_OK;
+    case kOptPrio:
+        if (value < 0 || value > 100) return fail(RT_ERR_INVALID, "priority threshold %d (0..100 %%)", value);
+        c->prio = value;
         return RT_OK;
     case kOptPoolCap:
         // the 64 root items plus a DFS run of height <= 21 must fit

@@ -41,10 +41,12 @@ constexpr uint32_t kAxisShift = 29;
 enum Option : int32_t {
     kOptKernel = 1,     // KD kernel version: 1 (node-own box, 48 B) or 2 (child boxes, 64 B)
     kOptTileOrder = 2,  // 0 XCD-contiguous, 1 natural, 2 centre-out, 3 by measured cost (kernel 3)
-    kOptRays = 3,       // kernel 3 pixels per wave: 64, 32 or 16
+    kOptRays = 3,       // kernel 3 pixels per wave: 64, 32, 16 or 8
     kOptItems = 4,      // kernel 3 items popped per lane per iteration: 1 or 2
     kOptCoarse = 5,     // kernel 3 coarse groups per wave outside the root box's rectangle (0 = off)
-    kOptDebug = 100,    // diagnostics: 1 = skip traversal, 2 = per-wave timestamps
+    kOptPrio = 6,       // tile order 3/4: tiles costing >= this % of the heaviest run at raised priority (0 = off)
+    kOptDebug = 100,    // diagnostics: 1 = skip traversal, 2 = per-wave timestamps, 4 = every group
+                        // coarse, 8 = coarse kernel on a side stream beside the fine one
     kOptPoolCap = 101,  // tests: shrink kernel 3's item pool (66..kPoolCap) to force its fallback
 };
 constexpr int kPoolCapMax = 640;   // kernel 3 items per wave (peak measured <= 440, tools/pool_sim.c)
@@ -91,13 +93,17 @@ struct TraceParams {
     int32_t cg_x0, cg_x1;          // fine region in 8-px groups [x0, x1)
     int32_t cs0, cs1;              // fine region in slots [s0, s1)
     int32_t coarse_per_wave;       // coarse groups per wave
-    int32_t coarse_blocks;         // blocks after the fine grid
+    int32_t coarse_blocks;         // blocks of k_coarse_kd3
+    int32_t fill_blocks;           // blocks after the fine grid filling far groups (fused mode)
     int64_t coarse_groups;         // total coarse groups
+    int32_t plain_xf;              // object transform is the identity (rotation 1, offset 0)
+    int32_t far_rect[4];           // root box's screen rectangle + 2 px (x0, x1, y0, y1; frame pixels)
     int32_t tile_w, tile_h;        // pixels per block (tile_h divides the 8-row band)
     int32_t rays;                  // pixels (rays) per wave: 64, 32 or 16
     int32_t tile_order;            // Option kOptTileOrder
     const int32_t* order;          // tile permutation (tile_order 2: centre-out, 3: by cost)
     uint32_t* cost;                // tile_order 3: pool iterations per fine unit [tile][2], or null
+    int32_t prio_blocks;           // tile_order 3/4: leading blocks (the heaviest tiles) issue at high priority
     float root_box[6];             // camera-relative root AABB (t0x,t1x,t0y,t1y,t0z,t1z)
     int32_t pool_cap;              // kernel 3 item-pool capacity in use (<= kPoolCap)
     int32_t items;                 // kernel 3 items per lane per iteration (1 or 2)
@@ -119,8 +125,10 @@ int launch_cam_tri(const float4* tri_world, uint32_t ntri, const float pos[3],
 int launch_cam_nodes(const rt_kd_node* nodes, const int32_t* interior_ids,
                      const uint32_t* node_ref, int64_t ninterior, const float pos[3],
                      float4* inode, int version, void* stream);
+// part: the coarse groups then the fine tiles (kPartAll), or one of them.
+enum LaunchPart : int { kPartAll = 0, kPartFine = 1, kPartCoarse = 2 };
 int launch_trace(const TraceParams& p, uint32_t mode, uint32_t flags, int kernel_version,
-                 void* stream);
+                 void* stream, int part);
 // Camera-relative box of one world node, exactly as init_cam_voxel_mem_cuda.
 void camera_relative_box(const rt_kd_node& nd, const float pos[3], float out[6]);
 int launch_unpack(int32_t w, int32_t h, int32_t nranks, const uint32_t* gathered,

@@ -32,6 +32,11 @@ constexpr float kDrawDistance = 400.0f;         // TD/Trixel.cu:47
 constexpr uint32_t kBackground = 0x00F08200u;   // VEC4<T_uint>(240,130,0,0), TD/Camera.cpp:72
 constexpr uint32_t kMiss = 0xFFFFFFFFu;
 
+// The wave's index in its block, as a scalar (the compiler cannot see that
+// threadIdx.x >> 6 is wave-uniform and would keep it, and everything derived
+// from it, in vector registers).
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6); }
+
 // device_inverse_sqrt, TD/vector.cuh:79-95 (seed from bits(s/2), 21 steps).
 __device__ __forceinline__ float rsqrt21(float x, float y, float z) {
     float s = (x * x) + (y * y) + (z * z);
@@ -157,42 +162,44 @@ __device__ __forceinline__ bool pixel_of(const TraceParams& P, int32_t b, int32_
 }
 
 // Coarse group j (row-major over this rank's slots and 8-px columns, skipping
-// the fine region) -> its 8x8 unit.
-__device__ __forceinline__ Unit coarse_unit(const TraceParams& P, int64_t j) {
-    const int64_t gx = P.groups_x;
-    const int64_t before = (int64_t)P.cs0 * gx;
-    int64_t slot, col;
+// the fine region) -> its 8x8 unit.  32-bit arithmetic: the host keeps
+// coarse_groups below 2^31 (64-bit division is a long software sequence).
+__device__ __forceinline__ Unit coarse_unit(const TraceParams& P, int32_t j) {
+    const int32_t gx = P.groups_x;
+    const int32_t before = P.cs0 * gx;
+    int32_t slot, col;
     if (j < before) {
         slot = j / gx;
         col = j - slot * gx;
     } else {
         j -= before;
-        const int64_t m = gx - (P.cg_x1 - P.cg_x0);
-        const int64_t mid = (int64_t)(P.cs1 - P.cs0) * m;
+        const int32_t m = gx - (P.cg_x1 - P.cg_x0);
+        const int32_t mid = (P.cs1 - P.cs0) * m;
         if (j < mid) {
-            const int64_t r = j / m;
+            const int32_t r = j / m;
             slot = P.cs0 + r;
             col = j - r * m;
             if (col >= P.cg_x0) col += P.cg_x1 - P.cg_x0;
         } else {
             j -= mid;
-            const int64_t r = j / gx;
+            const int32_t r = j / gx;
             slot = P.cs1 + r;
             col = j - r * gx;
         }
     }
-    return Unit{(int32_t)(col * 8), (int32_t)slot, 0};
+    return Unit{col * 8, slot, 0};
 }
 
 // One tile per block (blockIdx), one sub-tile per wave.
 __device__ __forceinline__ bool pixel_of_thread(const TraceParams& P, Pixel& px) {
-    return pixel_of(P, (int32_t)blockIdx.x, (int32_t)threadIdx.x >> 6, px);
+    return pixel_of(P, (int32_t)blockIdx.x, wave_id(), px);
 }
 
 // init_cam_mem_cuda, TD/Camera.cu:103-104: rmd = n + u*ix + v*iy, normalised.
 __device__ __forceinline__ void primary_ray(const TraceParams& P, int32_t ix, int32_t iy,
                                             float rmd[3]) {
-    const float fx = (float)(uint64_t)ix, fy = (float)(uint64_t)iy;
+    // (float)ix of the reference's unsigned pixel index: exact and equal for any ix < 2^32
+    const float fx = (float)(uint32_t)ix, fy = (float)(uint32_t)iy;
     float x = P.n_mod[0] + P.u_mod[0] * fx + P.v_mod[0] * fy;
     float y = P.n_mod[1] + P.u_mod[1] * fx + P.v_mod[1] * fy;
     float z = P.n_mod[2] + P.u_mod[2] * fx + P.v_mod[2] * fy;
@@ -707,37 +714,52 @@ __device__ __forceinline__ const float4* record_of(const TraceParams& P, uint32_
     return (ref & kLeafBit) ? P.trec + 4 * (size_t)(ref & ~kLeafBit) : P.inode + 4 * (size_t)ref;
 }
 
-// Visits one item whose record (r0..r3) has arrived: the leaf's MT test, or
-// the node's child ordering (TD/Trixel.cu:146-170) and the children's slab
-// tests.  kAny: shadow walk (Lmax and the hit triangle come from rd[4]).
-template <int kVec, bool kTranslated, bool kCount, bool kAny>
-__device__ __forceinline__ void visit_item(const float4* rd, uint4 it, float4 r0, float4 r1, float4 r2, float4 r3,
-                                           Visit& o, uint32_t& n_int, uint32_t& n_leaf, uint32_t& n_acc,
-                                           uint32_t& n_desc) {
-    const uint32_t ray = it.w >> 26;
-    const uint32_t depth = (it.w >> kCodeBits) & 31u, code = it.w & kCodeMask;
-    const float4 q0 = rd[0], q1 = rd[1], q2 = rd[2];
-    const float4 q3 = kTranslated ? rd[3] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    const float4 q4 = kTranslated ? rd[4] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    Ray Q;
+// The per-ray data of an item's ray from LDS (see store_ray).
+template <bool kTranslated>
+__device__ __forceinline__ void ray_of(const float4* rd, Ray& Q, float4& q2, float4& q3, float4& q4) {
+    const float4 q0 = rd[0], q1 = rd[1];
+    q2 = rd[2];
+    q3 = kTranslated ? rd[3] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    q4 = kTranslated ? rd[4] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     Q.rx = q0.x; Q.ry = q0.y; Q.rz = q0.z; Q.ix = q0.w;
     Q.iy = q1.x; Q.iz = q1.y; Q.ox = q1.z; Q.oy = q1.w;
     Q.oz = q2.x;
     // object translation (exact zeros when untranslated, as X[3], X[7], X[11] are)
     Q.odx = kTranslated ? q3.x : 0.0f; Q.ody = kTranslated ? q3.y : 0.0f; Q.odz = kTranslated ? q3.z : 0.0f;
     Q.sx = Q.rx > 0; Q.sy = Q.ry > 0; Q.sz = Q.rz > 0;
-    if (it.x & kLeafBit) {
-        if (kCount) n_leaf++;
-        float d = kAny ? q4.z : kDrawDistance;
-        uint32_t best = kMiss;
-        if (leaf_test_rec(Q, r0, r1, r2, it.x & ~kLeafBit, d, best) && (!kAny || best != __float_as_uint(q4.w))) {
-            o.cand = true;
-            o.ctri = best;
-            o.key = kAny ? 0ull : ((unsigned long long)__float_as_uint(d) << 32) | code;
-            if (kCount) n_acc++;
-        }
-        return;
+}
+
+// A leaf item whose triangle record (r0..r2) has arrived: the MT test of
+// TD/Trixel.cu:98-145.  kAny: shadow walk (Lmax and the hit triangle come
+// from rd[4]).
+template <bool kTranslated, bool kCount, bool kAny>
+__device__ __forceinline__ void visit_leaf(const float4* rd, uint4 it, float4 r0, float4 r1, float4 r2, Visit& o,
+                                           uint32_t& n_leaf, uint32_t& n_acc) {
+    Ray Q;
+    float4 q2, q3, q4;
+    ray_of<kTranslated>(rd, Q, q2, q3, q4);
+    const uint32_t code = it.w & kCodeMask;
+    if (kCount) n_leaf++;
+    float d = kAny ? q4.z : kDrawDistance;
+    uint32_t best = kMiss;
+    if (leaf_test_rec(Q, r0, r1, r2, it.x & ~kLeafBit, d, best) && (!kAny || best != __float_as_uint(q4.w))) {
+        o.cand = true;
+        o.ctri = best;
+        o.key = kAny ? 0ull : ((unsigned long long)__float_as_uint(d) << 32) | code;
+        if (kCount) n_acc++;
     }
+}
+
+// An interior item whose child-box record (r0..r3) has arrived: the node's
+// child ordering (TD/Trixel.cu:146-170) and the children's slab tests.
+template <bool kTranslated, bool kCount>
+__device__ __forceinline__ void visit_interior(const float4* rd, uint4 it, float4 r0, float4 r1, float4 r2,
+                                               float4 r3, Visit& o, uint32_t& n_int, uint32_t& n_desc) {
+    Ray Q;
+    float4 q2, q3, q4;
+    ray_of<kTranslated>(rd, Q, q2, q3, q4);
+    const uint32_t ray = it.w >> 26;
+    const uint32_t depth = (it.w >> kCodeBits) & 31u, code = it.w & kCodeMask;
     const uint32_t lw = __float_as_uint(r3.z);
     const uint32_t axis = (lw >> kAxisShift) & 3u;
     const uint32_t L = lw & ~(3u << kAxisShift), Rr = __float_as_uint(r3.w);
@@ -786,8 +808,37 @@ __device__ __forceinline__ void visit_item(const float4* rd, uint4 it, float4 r0
     o.nk = (keep_first ? 1 : 0) + (keep_second ? 1 : 0);
 }
 
+// Visits one item whose record has arrived: a leaf's MT test or an interior
+// node's child ordering and slab tests.
+template <int kVec, bool kTranslated, bool kCount, bool kAny>
+__device__ __forceinline__ void visit_item(const float4* rd, uint4 it, float4 r0, float4 r1, float4 r2, float4 r3,
+                                           Visit& o, uint32_t& n_int, uint32_t& n_leaf, uint32_t& n_acc,
+                                           uint32_t& n_desc) {
+    if (it.x & kLeafBit) visit_leaf<kTranslated, kCount, kAny>(rd, it, r0, r1, r2, o, n_leaf, n_acc);
+    else visit_interior<kTranslated, kCount>(rd, it, r0, r1, r2, r3, o, n_int, n_desc);
+}
+
 __device__ __forceinline__ uint32_t lanes_below(unsigned long long b) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+}
+
+// Nearest-candidate / any-hit bookkeeping of two visited items.
+template <bool kAny>
+__device__ __forceinline__ void record_candidates(unsigned long long* s_key, uint32_t* s_tri, const uint4& it0,
+                                                  const uint4& it1, const Visit& v0, const Visit& v1) {
+    const uint32_t ray0 = it0.w >> 26, ray1 = it1.w >> 26;
+    if (kAny) {
+        if (v0.cand) s_key[ray0] = 0ull;
+        if (v1.cand) s_key[ray1] = 0ull;
+    } else {
+        // nearest candidate per ray: 64-bit min of (w, path code), then the
+        // unique item holding the minimum records its triangle
+        if (v0.cand) atomicMin(&s_key[ray0], v0.key);
+        if (v1.cand) atomicMin(&s_key[ray1], v1.key);
+        __builtin_amdgcn_wave_barrier();
+        if (v0.cand && s_key[ray0] == v0.key) s_tri[ray0] = v0.ctri;
+        if (v1.cand && s_key[ray1] == v1.key) s_tri[ray1] = v1.ctri;
+    }
 }
 
 // The pool walk of one wave.  kAny = false: nearest hit per ray, key[ray] =
@@ -848,19 +899,7 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
         if (act1)
             visit_item<kVec, kTranslated, kCount, kAny>(s_ray + (size_t)(it1.w >> 26) * kVec, it1, b0, b1, b2, b3, v1,
                                                         n_int, n_leaf, n_acc, n_desc);
-        const uint32_t ray0 = it0.w >> 26, ray1 = it1.w >> 26;
-        if (kAny) {
-            if (v0.cand) s_key[ray0] = 0ull;
-            if (v1.cand) s_key[ray1] = 0ull;
-        } else {
-            // nearest candidate per ray: 64-bit min of (w, path code), then the
-            // unique item holding the minimum records its triangle
-            if (v0.cand) atomicMin(&s_key[ray0], v0.key);
-            if (v1.cand) atomicMin(&s_key[ray1], v1.key);
-            __builtin_amdgcn_wave_barrier();
-            if (v0.cand && s_key[ray0] == v0.key) s_tri[ray0] = v0.ctri;
-            if (v1.cand && s_key[ray1] == v1.key) s_tri[ray1] = v1.ctri;
-        }
+        record_candidates<kAny>(s_key, s_tri, it0, it1, v0, v1);
         // push the children (item 0's, then item 1's): ballot compaction
         const int cnt = v0.nk + v1.nk;
         const unsigned long long m1 = __ballot(cnt >= 1), m2 = __ballot(cnt >= 2);
@@ -899,6 +938,7 @@ struct Counts {
 
 // One wave's unit of work: the kRays pixels (8 x kRays/8) of unit U.
 constexpr size_t kNoDbg = ~(size_t)0;
+constexpr int kCoarseMax = 32;  // coarse groups per wave (RT_OPT_COARSE <= 32)
 template <int kRays, int kCap, int kRayVec, bool kTranslated, bool kWriteHit, bool kCount, bool kShadow>
 __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, kCap, kRayVec>& S_, const Unit& U,
                                            int lane, size_t dbg_slot, uint32_t* cost, Counts& C) {
@@ -1000,10 +1040,88 @@ __device__ __forceinline__ void count_flush(const TraceParams& P, const Counts& 
 // traced by trace_unit, which repeats the same root test, so a coarse group's
 // pixels are exactly what fine units would produce; only the packing of work
 // into waves differs.
+//
+// With the identity object transform (P.plain_xf) a group first tries a
+// cheap test: the ray normalised by the hardware rsqrt / rcp instead of the
+// 21-step Newton loop and correctly rounded divisions.  Its slab parameters
+// are within ~1e-6 (relative) of the exact ones, so a pixel whose test fails
+// by a 1e-3 relative margin (or whose entry lies behind the eye by more than
+// 1e-12) fails the exact test too; rays with a zero or tiny component, a NaN,
+// or any doubt take the exact test.  When every pixel of the group is such a
+// certain miss the group is background without the exact rays.
+__device__ __forceinline__ bool root_certain_miss(const TraceParams& P, int32_t ix, int32_t iy) {
+    // (float)ix of the reference's unsigned pixel index: exact and equal for any ix < 2^32
+    const float fx = (float)(uint32_t)ix, fy = (float)(uint32_t)iy;
+    const float x = P.n_mod[0] + P.u_mod[0] * fx + P.v_mod[0] * fy;
+    const float y = P.n_mod[1] + P.u_mod[1] * fx + P.v_mod[1] * fy;
+    const float z = P.n_mod[2] + P.u_mod[2] * fx + P.v_mod[2] * fy;
+    const float r = __builtin_amdgcn_rsqf((x * x) + (y * y) + (z * z));
+    const float dx = x * r, dy = y * r, dz = z * r;
+    if (!(fabsf(dx) > 1e-6f && fabsf(dy) > 1e-6f && fabsf(dz) > 1e-6f)) return false;
+    const float ix_ = __builtin_amdgcn_rcpf(dx), iy_ = __builtin_amdgcn_rcpf(dy), iz_ = __builtin_amdgcn_rcpf(dz);
+    const float* b = P.root_box;
+    const float t0x = (dx > 0 ? b[0] : b[1]) * ix_, t1x = (dx > 0 ? b[1] : b[0]) * ix_;
+    const float t0y = (dy > 0 ? b[2] : b[3]) * iy_, t1y = (dy > 0 ? b[3] : b[2]) * iy_;
+    const float t0z = (dz > 0 ? b[4] : b[5]) * iz_, t1z = (dz > 0 ? b[5] : b[4]) * iz_;
+    const float maxt0 = fmaxf(t0z, fmaxf(t0x, t0y)), mint1 = fminf(t1z, fminf(t1x, t1y));
+    if (!(fabsf(maxt0) < 1e30f && fabsf(mint1) < 1e30f)) return false;  // NaN or huge: exact test
+    const float tol = 1e-3f * (fabsf(maxt0) + fabsf(mint1));
+    return mint1 < maxt0 - tol || (maxt0 < -tol && maxt0 < -1e-12f);
+}
+
+//
+// Groups at least 2 pixels outside the root box's screen rectangle
+// (P.far_rect, identity transform only) skip even that: the rectangle is the
+// box's exact projection (in double, from the same float basis), a pixel's
+// float ray deviates from its exact direction by ~1e-6 rad against the
+// ~1e-3 rad of two pixels, and with a zero object offset the slab parameters
+// are single roundings of bound / D, so the test fails -- unless a component
+// of the ray is zero (0/0 = NaN drops that axis from the test) or tiny,
+// which each pixel checks.
+__device__ __forceinline__ bool far_group(const TraceParams& P, const Unit& G) {
+    const int32_t y0 = (P.rank + G.slot * P.nranks) * kTileH;
+    return G.x0 + 7 < P.far_rect[0] || G.x0 > P.far_rect[1] || y0 + 7 < P.far_rect[2] || y0 > P.far_rect[3];
+}
+
+__device__ __forceinline__ bool ray_has_tiny_component(const TraceParams& P, int32_t ix, int32_t iy) {
+    const float fx = (float)(uint32_t)ix, fy = (float)(uint32_t)iy;
+    const float x = P.n_mod[0] + P.u_mod[0] * fx + P.v_mod[0] * fy;
+    const float y = P.n_mod[1] + P.u_mod[1] * fx + P.v_mod[1] * fy;
+    const float z = P.n_mod[2] + P.u_mod[2] * fx + P.v_mod[2] * fy;
+    return !(fabsf(x) > 1e-30f && fabsf(y) > 1e-30f && fabsf(z) > 1e-30f);
+}
+
+// A far group (see above) whose rays have no tiny component is background:
+// writes it and returns true; otherwise returns false and writes nothing.
+template <bool kWriteHit, bool kCount>
+__device__ __forceinline__ bool fill_far(const TraceParams& P, const Unit& G, int lane, Counts& C) {
+    if (!far_group(P, G)) return false;
+    Pixel px;
+    const bool live = unit_pixel(P, G, 8, lane, px);
+    if (__ballot(live && ray_has_tiny_component(P, px.x, px.y)) != 0ull) return false;
+    if (live) {
+        P.argb[px.out] = kBackground;
+        if (kWriteHit) P.hit[px.out] = (int64_t)-1;
+        if (kCount) C.n_int += 1u;  // the root visit, which fails
+    }
+    return true;
+}
+
 template <int kRays, bool kWriteHit, bool kCount>
 __device__ __forceinline__ unsigned long long coarse_root(const TraceParams& P, const Unit& G, int lane, Counts& C) {
     Pixel px;
     const bool live = unit_pixel(P, G, 8, lane, px);
+    if (P.plain_xf && !(P.root_ref & kLeafBit) && !(P.debug & 1)) {
+        const bool sure = !live || root_certain_miss(P, px.x, px.y);
+        if (__ballot(!sure) == 0ull) {
+            if (live) {
+                P.argb[px.out] = kBackground;
+                if (kWriteHit) P.hit[px.out] = (int64_t)-1;
+                if (kCount) C.n_int += 1u;  // the root visit, which fails
+            }
+            return 0ull;
+        }
+    }
     float cam[3], t0, t1;
     Ray R;
     camera_ray(P, px, live, cam, R);
@@ -1038,9 +1156,27 @@ __global__ RT_KD3_BOUNDS void k_trace_kd3(TraceParams P) {
     constexpr int kCap = pool_cap_for<kRays>();
     constexpr int kRayVec = (kTranslated || kShadow) ? 5 : 3;  // float4s of per-ray data in LDS
     __shared__ WaveLds<kRays, kCap, kRayVec> s_lds[kWaves];
-    const int wv = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
+    const int wv = wave_id(), lane = (int)threadIdx.x & 63;
     Counts C;
     const int32_t b = (int32_t)blockIdx.x;
+    if (b >= P.tiles_x * P.block_rows) {
+        // fused far fill: blocks after the fine tiles write the coarse groups,
+        // all far by construction (set_fine_region); unrolled as in k_coarse_kd3
+        const int32_t j0 = ((b - P.tiles_x * P.block_rows) * kWaves + wv) * P.coarse_per_wave;
+        const int32_t j1 = min(j0 + P.coarse_per_wave, (int32_t)P.coarse_groups);
+        bool ok = true;
+#pragma unroll 8
+        for (int g = 0; g < kCoarseMax; g++) {
+            const int32_t j = j0 + g;
+            if (j < j1) ok = fill_far<kWriteHit, kCount>(P, coarse_unit(P, j), lane, C) && ok;
+        }
+        if (!ok && lane == 0) atomicOr(P.err, 4);  // a group the host promised far was not
+        if (kCount) count_flush(P, C);
+        return;
+    }
+    // the heaviest tiles (dispatched first by the cost order) win instruction
+    // issue against the lighter waves sharing their SIMD
+    if (b < P.prio_blocks) __builtin_amdgcn_s_setprio(3);
     uint32_t* cost = P.cost ? P.cost + 2 * (size_t)tile_index(P, b) + wv : nullptr;
     trace_unit<kRays, kCap, kRayVec, kTranslated, kWriteHit, kCount, kShadow>(P, s_lds[wv], unit_of(P, b, wv), lane,
                                                                              (size_t)b * kWaves + wv, cost, C);
@@ -1048,7 +1184,7 @@ __global__ RT_KD3_BOUNDS void k_trace_kd3(TraceParams P) {
 }
 
 // The coarse groups (every 8x8 group of this rank outside the fine tiles),
-// P.coarse_per_wave per wave.  A separate kernel: looping trace_unit inside
+// P.coarse_per_wave (<= kCoarseMax) per wave.  A separate kernel: looping trace_unit inside
 // the fine kernel costs it a third of its occupancy (80 -> 113 VGPRs).
 template <int kRays, bool kTranslated, bool kWriteHit, bool kCount, bool kShadow>
 __global__ __launch_bounds__(128) void k_coarse_kd3(TraceParams P) {
@@ -1057,13 +1193,24 @@ __global__ __launch_bounds__(128) void k_coarse_kd3(TraceParams P) {
     constexpr int kRayVec = (kTranslated || kShadow) ? 5 : 3;
     constexpr unsigned long long kSub = kRays == 64 ? ~0ull : ((1ull << (kRays & 63)) - 1);
     __shared__ WaveLds<kRays, kCap, kRayVec> s_lds[kWaves];
-    const int wv = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
+    const int wv = wave_id(), lane = (int)threadIdx.x & 63;
     Counts C;
     const unsigned long long t_start = P.dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    const int64_t cw = (int64_t)blockIdx.x * kWaves + wv;
-    const int64_t j0 = cw * P.coarse_per_wave;
-    const int64_t j1 = min(j0 + (int64_t)P.coarse_per_wave, P.coarse_groups);
-    for (int64_t j = j0; j < j1; j++) {
+    const int32_t cw = (int32_t)blockIdx.x * kWaves + wv;
+    const int32_t j0 = cw * P.coarse_per_wave;
+    const int32_t j1 = min(j0 + P.coarse_per_wave, (int32_t)P.coarse_groups);
+    // Far groups first, unrolled so their short independent chains overlap
+    // (one after another they cost ~1 us each in latency); the rest after.
+    const bool far_ok = P.plain_xf && !(P.root_ref & kLeafBit) && !(P.debug & 1);
+    uint32_t pending = 0;
+#pragma unroll 8
+    for (int g = 0; g < kCoarseMax; g++) {
+        const int32_t j = j0 + g;
+        if (j < j1 && !(far_ok && fill_far<kWriteHit, kCount>(P, coarse_unit(P, j), lane, C))) pending |= 1u << g;
+    }
+    while (pending) {
+        const int32_t j = j0 + __builtin_ctz(pending);
+        pending &= pending - 1;
         const Unit G = coarse_unit(P, j);
         const unsigned long long gmask = coarse_root<kRays, kWriteHit, kCount>(P, G, lane, C);
         for (int k = 0; k < 64 / kRays; k++)
@@ -1075,7 +1222,7 @@ __global__ __launch_bounds__(128) void k_coarse_kd3(TraceParams P) {
         const size_t slot = (size_t)(P.tiles_x * P.block_rows + blockIdx.x) * kWaves + wv;
         P.dbg[3 * slot] = t_start;
         P.dbg[3 * slot + 1] = __builtin_amdgcn_s_memrealtime();
-        P.dbg[3 * slot + 2] = 0;
+        P.dbg[3 * slot + 2] = 0xFFFFFFFFull;  // marks a coarse wave
     }
     if (kCount) count_flush(P, C);
 }
@@ -1302,7 +1449,7 @@ TraceFn kd_kernel(int version, int rays, bool shadow, bool coarse) {
     return shadow ? kd3_kernel<T, H, C, true>(rays, coarse) : kd3_kernel<T, H, C, false>(rays, coarse);
 }
 
-int launch_trace(const TraceParams& p, uint32_t mode, uint32_t flags, int kernel_version, void* stream) {
+int launch_trace(const TraceParams& p, uint32_t mode, uint32_t flags, int kernel_version, void* stream, int part) {
     hipStream_t s = (hipStream_t)stream;
     const bool wh = (flags & RT_FLAG_WRITE_HIT) != 0, cnt = (flags & RT_FLAG_COUNT) != 0;
     const unsigned fine = (unsigned)(p.tiles_x * p.block_rows);
@@ -1319,9 +1466,10 @@ int launch_trace(const TraceParams& p, uint32_t mode, uint32_t flags, int kernel
     const int v = kernel_version, r = p.rays;
     const bool sh = (flags & RT_FLAG_SHADOW) != 0;  // kernel 3 only (checked by the caller)
     for (int pass = 0; pass < 2; pass++) {
-        // the coarse groups first (short), then the fine tiles
+        // the coarse groups first, then the fine tiles (or just one of them)
         const bool coarse = pass == 0;
-        const unsigned grid = coarse ? (unsigned)p.coarse_blocks : fine;
+        if ((coarse && part == kPartFine) || (!coarse && part == kPartCoarse)) continue;
+        const unsigned grid = coarse ? (unsigned)p.coarse_blocks : fine + (unsigned)p.fill_blocks;
         if (grid == 0) continue;
         TraceFn fn;
         if (tr) fn = wh ? (cnt ? kd_kernel<true, true, true>(v, r, sh, coarse) : kd_kernel<true, true, false>(v, r, sh, coarse))

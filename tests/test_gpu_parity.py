@@ -328,8 +328,12 @@ def test_shadow_rejected_outside_kernel3_kd(kernel, mode):
 # per wave), which run the same root test and trace any sub-tile where a ray
 # passes.  Frames and counters must not depend on the split: coarse off (0),
 # one or many groups per wave, and the diagnostic "every group coarse" (debug
-# bit 4), which sends the whole object through the coarse kernel's tracing.
-COARSE = [(0, None), (1, None), (8, None), (4096, None), (8, 4), (1, 4)]  # (groups per wave, debug)
+# bit 4), which sends the whole object through the coarse kernel's tracing;
+# debug bit 8 runs the coarse kernel on a side stream beside the fine one.
+# With the identity transform the coarse kernel first tries its certain-miss
+# test (hardware rsqrt/rcp with a 1e-3 margin); the transform cases take the
+# exact test only.
+COARSE = [(0, None), (1, None), (8, None), (32, None), (8, 4), (1, 4), (32, 4), (8, 8), (2, 12)]  # (groups per wave, debug)
 
 
 @pytest.mark.parametrize("coarse,debug", COARSE)

@@ -52,6 +52,15 @@ def main():
     t0 = rec[:, 0].min()
     start, end = (rec[:, 0] - t0) * 10e-3, (rec[:, 1] - t0) * 10e-3  # us
     vis, popped = rec[:, 2] & 0xFFFFFFFF, rec[:, 2] >> 32  # pool iterations, items popped
+    coarse = vis == 0xFFFFFFFF  # k_coarse_kd3 waves (whole wave: its groups)
+    if coarse.any():
+        cd = end[coarse] - start[coarse]
+        res["coarse_waves"] = int(coarse.sum())
+        res["coarse_dur_us_p50_p99_max"] = [float(np.percentile(cd, q)) for q in (50, 99, 100)]
+        res["coarse_start_us_min_max"] = [float(start[coarse].min()), float(start[coarse].max())]
+        res["coarse_end_us_max"] = float(end[coarse].max())
+        res["fine_start_us_min"] = float(start[~coarse].min())
+    start, end, vis, popped = start[~coarse], end[~coarse], vis[~coarse], popped[~coarse]
     dur = end - start
     res["span_us"] = float(end.max())
     res["waves"] = int(len(rec))
