@@ -613,7 +613,7 @@ struct Item {
 #define RT_POOL_CAP_R32 448
 #endif
 #ifndef RT_POOL_CAP_R16
-#define RT_POOL_CAP_R16 384
+#define RT_POOL_CAP_R16 352
 #endif
 #ifndef RT_POOL_CAP_R8
 #define RT_POOL_CAP_R8 256
