@@ -53,8 +53,6 @@ def parse():
     ap.add_argument("--items", type=int, default=2, help="kernel 3: items each lane pops per iteration (1, 2)")
     ap.add_argument("--coarse", type=int, default=8,
                     help="kernel 3: 8x8 groups per wave outside the root box's screen rectangle (0 = off)")
-    ap.add_argument("--prio", type=int, default=0,
-                    help="tile order 3/4: tiles costing >= this %% of the heaviest one run at raised priority")
     ap.add_argument("--event-every", type=int, default=1,
                     help="bracket every Nth timed frame with HIP events for the kernel time (each pair costs "
                          "queue time, so N > 1 keeps the frame rate closer to the uninstrumented one)")
@@ -153,7 +151,6 @@ def main():
     cam.set_option(_lib.RT_OPT_RAYS, a.rays)
     cam.set_option(_lib.RT_OPT_ITEMS, a.items)
     cam.set_option(_lib.RT_OPT_COARSE, a.coarse)
-    cam.set_option(_lib.RT_OPT_PRIO, a.prio)
     if a.side_coarse:
         cam.set_option(_lib.RT_OPT_DEBUG, 8)
     cam.render_into(scratch, mode=a.mode, flags=sflag, tile=tile if world > 1 else None,
@@ -256,12 +253,10 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": {1: "k_trace_kd", 2: "k_trace_kd2",
-                           3: "k_trace_kd3" + (" + k_coarse_kd3" if a.coarse else "")}[a.kernel] if a.mode == 0
+                "kernel": {1: "k_trace_kd", 2: "k_trace_kd2", 3: "k_trace_kd3"}[a.kernel] if a.mode == 0
                           else "k_trace_flat",
                 "kernel_options": {"kernel": a.kernel, "tile_order": a.tile_order, "rays_per_wave": a.rays,
                                    "items_per_lane": a.items, "coarse_groups_per_wave": a.coarse,
-                                   "prio": a.prio,
                                    "shadow": a.shadow},
                 "kernel_ms_avg": round(kern_ms, 5),
                 "kernel_ms_frames": f"{len(ev)} of {a.steps} timed frames (every {max(1, a.event_every)})",

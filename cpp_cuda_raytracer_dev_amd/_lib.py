@@ -26,7 +26,6 @@ RT_OPT_TILE_ORDER = 2
 RT_OPT_RAYS = 3
 RT_OPT_ITEMS = 4
 RT_OPT_COARSE = 5
-RT_OPT_PRIO = 6
 RT_OPT_DEBUG = 100
 RT_OPT_POOL_CAP = 101
 

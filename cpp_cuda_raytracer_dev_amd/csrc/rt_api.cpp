@@ -56,8 +56,6 @@ struct rt_camera {
     int64_t order_cap = 0;
     int64_t order_key[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
     int coarse = 8;                  // kOptCoarse: coarse groups per wave (0 = off)
-    int prio = 0;                    // kOptPrio: % of the heaviest tile's cost that earns raised priority
-    int32_t prio_blocks = 0;         // leading blocks of the current cost order at raised priority
     std::vector<int32_t> centre;     // centre-out permutation of the current fine grid (host copy)
     // 8x8 groups (x / 8, y / 8) holding a pixel whose primary ray has a zero
     // or tiny component (computed once, as the kernels compute the rays)
@@ -313,15 +311,6 @@ int cost_feedback(rt_camera* c, const TraceParams& p, void* stream) {
         c->frames_since = 0;
         if (c->cost_gen != c->layout_gen || (int64_t)c->centre.size() != n) return RT_OK;  // stale sample
         const std::vector<int32_t> ord = cost_order(c, p, c->tile_order == 4);
-        c->prio_blocks = 0;
-        if (c->prio > 0) {  // tiles at >= prio % of the heaviest one's iterations
-            uint32_t mx = 0;
-            for (int64_t t = 0; t < n; t++) mx = std::max(mx, std::max(c->h_cost[2 * t], c->h_cost[2 * t + 1]));
-            const uint64_t bar = ((uint64_t)mx * (uint64_t)c->prio + 99) / 100;
-            int64_t heavy = 0;
-            for (int64_t t = 0; t < n; t++) heavy += std::max(c->h_cost[2 * t], c->h_cost[2 * t + 1]) >= bar ? 1 : 0;
-            c->prio_blocks = (int32_t)heavy;  // order 3 puts them first; order 4 roughly so
-        }
         bool same = true;
         for (int64_t k = 0; k < n; k++) {
             same = same && c->h_order[k] == ord[(size_t)k];
@@ -571,7 +560,6 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
         if (rc) return rc;
     }
     p.cost = nullptr;
-    p.prio_blocks = 0;
     if (c->tile_order >= 2 && p.tiles_x * p.block_rows > 0) {
         int rc = ensure_order(c, p);
         if (rc) return rc;
@@ -579,7 +567,6 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
         if (c->tile_order >= 3 && kernel == 3) {
             if ((rc = ensure_cost(c, (int64_t)p.tiles_x * p.block_rows))) return rc;
             p.cost = c->d_cost;
-            p.prio_blocks = c->order_gen == c->layout_gen ? c->prio_blocks : 0;
         }
     }
     return RT_OK;
@@ -911,10 +898,6 @@ extern "C" int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value) {
     case kOptCoarse:
         if (value < 0 || value > 32) return fail(RT_ERR_INVALID, "coarse groups per wave %d (0..32)", value);
         c->coarse = value;
-        return RT_OK;
-    case kOptPrio:
-        if (value < 0 || value > 100) return fail(RT_ERR_INVALID, "priority threshold %d (0..100 %%)", value);
-        c->prio = value;
         return RT_OK;
     case kOptPoolCap:
         // the 64 root items plus a DFS run of height <= 21 must fit

@@ -44,7 +44,6 @@ enum Option : int32_t {
     kOptRays = 3,       // kernel 3 pixels per wave: 64, 32, 16 or 8
     kOptItems = 4,      // kernel 3 items popped per lane per iteration: 1 or 2
     kOptCoarse = 5,     // kernel 3 coarse groups per wave outside the root box's rectangle (0 = off)
-    kOptPrio = 6,       // tile order 3/4: tiles costing >= this % of the heaviest run at raised priority (0 = off)
     kOptDebug = 100,    // diagnostics: 1 = skip traversal, 2 = per-wave timestamps, 4 = every group
                         // coarse, 8 = coarse kernel on a side stream beside the fine one
     kOptPoolCap = 101,  // tests: shrink kernel 3's item pool (66..kPoolCap) to force its fallback
@@ -103,7 +102,6 @@ struct TraceParams {
     int32_t tile_order;            // Option kOptTileOrder
     const int32_t* order;          // tile permutation (tile_order 2: centre-out, 3: by cost)
     uint32_t* cost;                // tile_order 3: pool iterations per fine unit [tile][2], or null
-    int32_t prio_blocks;           // tile_order 3/4: leading blocks (the heaviest tiles) issue at high priority
     float root_box[6];             // camera-relative root AABB (t0x,t1x,t0y,t1y,t0z,t1z)
     int32_t pool_cap;              // kernel 3 item-pool capacity in use (<= kPoolCap)
     int32_t items;                 // kernel 3 items per lane per iteration (1 or 2)

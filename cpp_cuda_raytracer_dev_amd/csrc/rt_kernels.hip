@@ -1174,9 +1174,6 @@ __global__ RT_KD3_BOUNDS void k_trace_kd3(TraceParams P) {
         if (kCount) count_flush(P, C);
         return;
     }
-    // the heaviest tiles (dispatched first by the cost order) win instruction
-    // issue against the lighter waves sharing their SIMD
-    if (b < P.prio_blocks) __builtin_amdgcn_s_setprio(3);
     uint32_t* cost = P.cost ? P.cost + 2 * (size_t)tile_index(P, b) + wv : nullptr;
     trace_unit<kRays, kCap, kRayVec, kTranslated, kWriteHit, kCount, kShadow>(P, s_lds[wv], unit_of(P, b, wv), lane,
                                                                              (size_t)b * kWaves + wv, cost, C);

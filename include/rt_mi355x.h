@@ -188,7 +188,6 @@ int rt_camera_info(const rt_camera* c, int32_t* w, int32_t* h, int32_t* max_dept
 #define RT_OPT_TILE_ORDER 2
 #define RT_OPT_RAYS 3 /* kernel 3: pixels per wave (64, 32, 16 default, 8); the rest of the lanes help */
 #define RT_OPT_ITEMS 4 /* kernel 3: items each lane pops per iteration (1, 2 default) */
-#define RT_OPT_PRIO 6 /* tile order 3/4: tiles costing >= value % of the heaviest one run at raised issue priority (0 = off) */
 #define RT_OPT_COARSE 5 /* kernel 3: 8x8 groups per wave outside the root box's screen rectangle (0..32, 8 default, 0 = off) */
 int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value);
 
