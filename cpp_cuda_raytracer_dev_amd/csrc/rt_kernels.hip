@@ -701,8 +701,8 @@ __device__ __forceinline__ int seed_root(const TraceParams& P, uint4* items, con
 
 // One popped item's outcome: up to two children and a candidate hit.
 struct Visit {
-    uint4 c0, c1;
-    int nk;
+    uint4 ca, cb;      // the first and second child items (TD/Trixel.cu:155-168 order)
+    bool ka, kb;       // whether each is pushed
     bool cand;
     unsigned long long key;
     uint32_t ctri;
@@ -803,9 +803,10 @@ __device__ __forceinline__ void visit_interior(const float4* rd, uint4 it, float
     const float g0 = left_first ? rt0 : lt0, g1 = left_first ? rt1 : lt1;
     const uint4 A = make_uint4(first, __float_as_uint(f0), __float_as_uint(f1), meta_first);
     const uint4 B = make_uint4(second, __float_as_uint(g0), __float_as_uint(g1), meta_second);
-    o.c0 = keep_first ? A : B;
-    o.c1 = B;
-    o.nk = (keep_first ? 1 : 0) + (keep_second ? 1 : 0);
+    o.ca = A;
+    o.cb = B;
+    o.ka = keep_first;
+    o.kb = keep_second;
 }
 
 // Visits one item whose record has arrived: a leaf's MT test or an interior
@@ -841,6 +842,39 @@ __device__ __forceinline__ void record_candidates(unsigned long long* s_key, uin
     }
 }
 
+#ifndef RT_SEQ_PUSH
+#define RT_SEQ_PUSH 1
+#endif
+#ifndef RT_MAX_ITEMS
+#define RT_MAX_ITEMS 2
+#endif
+
+// One visited item's candidate: any-hit marks the ray; nearest-hit takes the
+// 64-bit min of (w, path code) and the unique holder of the minimum records
+// its triangle.
+template <bool kAny>
+__device__ __forceinline__ void record_candidate(unsigned long long* s_key, uint32_t* s_tri, const uint4& it,
+                                                 const Visit& v) {
+    const uint32_t ray = it.w >> 26;
+    if (kAny) {
+        if (v.cand) s_key[ray] = 0ull;
+    } else {
+        if (v.cand) atomicMin(&s_key[ray], v.key);
+        __builtin_amdgcn_wave_barrier();
+        if (v.cand && s_key[ray] == v.key) s_tri[ray] = v.ctri;
+    }
+}
+
+// Pushes one visited item's children (ballot compaction) at items[at...];
+// returns how many the wave pushed.
+__device__ __forceinline__ int push_children(uint4* items, int at, const Visit& v) {
+    const unsigned long long m1 = __ballot(v.ka), m2 = __ballot(v.kb);
+    const int n1 = __builtin_popcountll(m1);
+    if (v.ka) items[at + (int)lanes_below(m1)] = v.ca;
+    if (v.kb) items[at + n1 + (int)lanes_below(m2)] = v.cb;
+    return n1 + __builtin_popcountll(m2);
+}
+
 // The pool walk of one wave.  kAny = false: nearest hit per ray, key[ray] =
 // min (w, path code), tri[ray] = its triangle.  kAny = true (shadow rays): any
 // accepted leaf with w < Lmax other than the ray's own hit triangle sets
@@ -854,7 +888,8 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
                                           uint32_t& n_acc,
                                           uint32_t& n_desc) {
     const int cap = min(P.pool_cap, kCap);
-    const int per = P.items > 1 ? 128 : 64;
+    constexpr bool kTwo = RT_MAX_ITEMS > 1;  // compile-time: one-item builds drop item 1's registers
+    const int per = kTwo && P.items > 1 ? 128 : 64;
     while (n > 0) {
         // Pop as many items as the pool has room for the children of plus
         // the DFS slack below; a single (DFS-like) pop when there is none.
@@ -871,9 +906,9 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
         // re-read item `base`, a live item, whose record is a valid address):
         // with guarded loads hipcc zero-fills the registers of the idle path
         // and waits for the first record before issuing the second.
-        bool act0 = lane < take, act1 = lane + 64 < take;
+        bool act0 = lane < take, act1 = kTwo && lane + 64 < take;
         const uint4 it0 = items[base + (act0 ? lane : 0)];
-        const uint4 it1 = items[base + (act1 ? lane + 64 : 0)];
+        const uint4 it1 = kTwo ? items[base + (act1 ? lane + 64 : 0)] : it0;
         __builtin_amdgcn_wave_barrier();
         // any-hit: a ray already shadowed needs no more visits (kept when
         // counting, so the counters match the oracle's full walk)
@@ -885,14 +920,42 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
         const float4* p0 = record_of(P, it0.x);
         const float4* p1 = record_of(P, it1.x);
         const float4 a0 = p0[0], a1 = p0[1], a2 = p0[2], a3 = p0[3];
-        const float4 b0 = p1[0], b1 = p1[1], b2 = p1[2], b3 = p1[3];
+        const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        const float4 b0 = kTwo ? p1[0] : z, b1 = kTwo ? p1[1] : z, b2 = kTwo ? p1[2] : z, b3 = kTwo ? p1[3] : z;
         asm volatile("" ::"v"(a0.x), "v"(a0.y), "v"(a0.z), "v"(a0.w), "v"(a1.x), "v"(a1.y), "v"(a1.z), "v"(a1.w),
                      "v"(a2.x), "v"(a2.y), "v"(a2.z), "v"(a2.w), "v"(a3.x), "v"(a3.y), "v"(a3.z), "v"(a3.w));
         asm volatile("" ::"v"(b0.x), "v"(b0.y), "v"(b0.z), "v"(b0.w), "v"(b1.x), "v"(b1.y), "v"(b1.z), "v"(b1.w),
                      "v"(b2.x), "v"(b2.y), "v"(b2.z), "v"(b2.w), "v"(b3.x), "v"(b3.y), "v"(b3.z), "v"(b3.w));
+#if RT_SEQ_PUSH
+        // item 0 is visited, recorded and pushed before item 1 is visited, so
+        // its results die before item 1's are made (fewer live VGPRs)
+        int total = 0;
+        {
+            Visit v0;
+            v0.ka = v0.kb = false; v0.cand = false;
+            if (act0)
+                visit_item<kVec, kTranslated, kCount, kAny>(s_ray + (size_t)(it0.w >> 26) * kVec, it0, a0, a1, a2, a3,
+                                                            v0, n_int, n_leaf, n_acc, n_desc);
+            record_candidate<kAny>(s_key, s_tri, it0, v0);
+            total += push_children(items, base + total, v0);
+        }
+        {
+            Visit v1;
+            v1.ka = v1.kb = false; v1.cand = false;
+            if (act1)
+                visit_item<kVec, kTranslated, kCount, kAny>(s_ray + (size_t)(it1.w >> 26) * kVec, it1, b0, b1, b2, b3,
+                                                            v1, n_int, n_leaf, n_acc, n_desc);
+            record_candidate<kAny>(s_key, s_tri, it1, v1);
+            total += push_children(items, base + total, v1);
+        }
+        if (base + total > cap) {  // unreachable by the pop rule above; guard anyway
+            if (lane == 0) atomicOr(P.err, 2);
+            break;
+        }
+#else
         Visit v0, v1;  // children / key fields are read only where nk / cand say so
-        v0.nk = 0; v0.cand = false;
-        v1.nk = 0; v1.cand = false;
+        v0.ka = v0.kb = false; v0.cand = false;
+        v1.ka = v1.kb = false; v1.cand = false;
         if (act0)
             visit_item<kVec, kTranslated, kCount, kAny>(s_ray + (size_t)(it0.w >> 26) * kVec, it0, a0, a1, a2, a3, v0,
                                                         n_int, n_leaf, n_acc, n_desc);
@@ -900,24 +963,20 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
             visit_item<kVec, kTranslated, kCount, kAny>(s_ray + (size_t)(it1.w >> 26) * kVec, it1, b0, b1, b2, b3, v1,
                                                         n_int, n_leaf, n_acc, n_desc);
         record_candidates<kAny>(s_key, s_tri, it0, it1, v0, v1);
-        // push the children (item 0's, then item 1's): ballot compaction
-        const int cnt = v0.nk + v1.nk;
-        const unsigned long long m1 = __ballot(cnt >= 1), m2 = __ballot(cnt >= 2);
-        const unsigned long long m3 = __ballot(cnt >= 3), m4 = __ballot(cnt >= 4);
-        const uint32_t off = lanes_below(m1) + lanes_below(m2) + lanes_below(m3) + lanes_below(m4);
-        const int total = __builtin_popcountll(m1) + __builtin_popcountll(m2) + __builtin_popcountll(m3) +
-                          __builtin_popcountll(m4);
+        // push the children (all first children of item 0, all second ones, then item 1's): ballot compaction
+        const unsigned long long m1 = __ballot(v0.ka), m2 = __ballot(v0.kb);
+        const unsigned long long m3 = __ballot(v1.ka), m4 = __ballot(v1.kb);
+        const int n1 = __builtin_popcountll(m1), n2 = __builtin_popcountll(m2), n3 = __builtin_popcountll(m3);
+        const int total = n1 + n2 + n3 + __builtin_popcountll(m4);
         if (base + total > cap) {  // unreachable by the pop rule above; guard anyway
             if (lane == 0) atomicOr(P.err, 2);
             break;
         }
-        const uint4 s0 = v0.nk >= 1 ? v0.c0 : v1.c0;
-        const uint4 s1 = v0.nk == 2 ? v0.c1 : (v0.nk == 1 ? v1.c0 : v1.c1);
-        const uint4 s2 = v0.nk == 2 ? v1.c0 : v1.c1;
-        if (cnt >= 1) items[base + off] = s0;
-        if (cnt >= 2) items[base + off + 1] = s1;
-        if (cnt >= 3) items[base + off + 2] = s2;
-        if (cnt >= 4) items[base + off + 3] = v1.c1;
+        if (v0.ka) items[base + (int)lanes_below(m1)] = v0.ca;
+        if (v0.kb) items[base + n1 + (int)lanes_below(m2)] = v0.cb;
+        if (v1.ka) items[base + n1 + n2 + (int)lanes_below(m3)] = v1.ca;
+        if (v1.kb) items[base + n1 + n2 + n3 + (int)lanes_below(m4)] = v1.cb;
+#endif
         n = base + total;
         __builtin_amdgcn_wave_barrier();
     }
