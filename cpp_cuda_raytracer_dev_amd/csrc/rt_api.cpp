@@ -193,10 +193,12 @@ constexpr int kCostPeriod = 16;  // frames between cost samples (tile order 3)
 // Buffers of tile order 3 for n fine tiles (allocated when the grid grows).
 int ensure_cost(rt_camera* c, int64_t n) {
     int rc;
-    if (c->cost_cap < 2 * n) {
+    if (c->cost_cap < kCostSlots * n) {
         dev_free(c->d_cost);
-        if ((rc = dev_alloc(&c->d_cost, (size_t)(2 * n), "hipMalloc(cost)"))) return rc;
-        c->cost_cap = 2 * n;
+        if ((rc = dev_alloc(&c->d_cost, (size_t)(kCostSlots * n), "hipMalloc(cost)"))) return rc;
+        // slots of waves a tile does not have stay zero
+        if ((rc = hip_check(hipMemset(c->d_cost, 0, sizeof(uint32_t) * kCostSlots * (size_t)n), "memset cost"))) return rc;
+        c->cost_cap = kCostSlots * n;
     }
     if (c->host_cap < n) {
         // copies in flight may still use the pinned buffers
@@ -208,7 +210,7 @@ int ensure_cost(rt_camera* c, int64_t n) {
         c->h_order = nullptr;
         c->host_cap = 0;
         c->cost_pending = c->order_pending = false;
-        if ((rc = hip_check(hipHostMalloc((void**)&c->h_cost, sizeof(uint32_t) * 2 * (size_t)n, 0), "hipHostMalloc(cost)")) ||
+        if ((rc = hip_check(hipHostMalloc((void**)&c->h_cost, sizeof(uint32_t) * kCostSlots * (size_t)n, 0), "hipHostMalloc(cost)")) ||
             (rc = hip_check(hipHostMalloc((void**)&c->h_order, sizeof(int32_t) * (size_t)n, 0), "hipHostMalloc(order)")))
             return rc;
         c->host_cap = n;
@@ -229,11 +231,19 @@ int ensure_cost(rt_camera* c, int64_t n) {
 std::vector<int32_t> cost_order(const rt_camera* c, const TraceParams& p, bool xcd_split) {
     const int64_t n = (int64_t)p.tiles_x * p.block_rows;
     uint32_t mx = 0;
-    for (int64_t t = 0; t < n; t++) mx = std::max(mx, std::max(c->h_cost[2 * t], c->h_cost[2 * t + 1]));
-    mx = std::min<uint32_t>(mx, 1u << 16);
-    auto cost_of = [&](int32_t t) {
-        return std::min<uint32_t>(std::max(c->h_cost[2 * (size_t)t], c->h_cost[2 * (size_t)t + 1]), mx);
+    auto wave_max = [&](int64_t t) {
+        uint32_t m = 0;
+        for (int k = 0; k < kCostSlots; k++) m = std::max(m, c->h_cost[kCostSlots * (size_t)t + k]);
+        return m;
     };
+    auto wave_sum = [&](int64_t t) {
+        double m = 0;
+        for (int k = 0; k < kCostSlots; k++) m += c->h_cost[kCostSlots * (size_t)t + k];
+        return m;
+    };
+    for (int64_t t = 0; t < n; t++) mx = std::max(mx, wave_max(t));
+    mx = std::min<uint32_t>(mx, 1u << 16);
+    auto cost_of = [&](int32_t t) { return std::min<uint32_t>(wave_max(t), mx); };
     // stable counting sort of `in` by cost, descending, appended to `out`
     std::vector<int64_t> start((size_t)mx + 2);
     auto sort_desc = [&](const int32_t* in, int64_t m, int32_t* out) {
@@ -264,7 +274,7 @@ std::vector<int32_t> cost_order(const rt_camera* c, const TraceParams& p, bool x
     }
     std::sort(mk.begin(), mk.end());
     double total = 0.0;
-    for (int64_t t = 0; t < n; t++) total += 1.0 + c->h_cost[2 * t] + c->h_cost[2 * t + 1];
+    for (int64_t t = 0; t < n; t++) total += 1.0 + wave_sum(t);
     constexpr int kXcd = 8;
     std::vector<int32_t> runs((size_t)n);
     int64_t cut[kXcd + 1] = {0};
@@ -272,7 +282,7 @@ std::vector<int32_t> cost_order(const rt_camera* c, const TraceParams& p, bool x
     int r = 1;
     for (int64_t k = 0; k < n && r < kXcd; k++) {
         const int32_t t = mk[(size_t)k].second;
-        acc += 1.0 + c->h_cost[2 * (size_t)t] + c->h_cost[2 * (size_t)t + 1];
+        acc += 1.0 + wave_sum(t);
         while (r < kXcd && acc >= total * r / kXcd) cut[r++] = k + 1;
     }
     while (r <= kXcd) cut[r++] = n;
@@ -328,7 +338,7 @@ int cost_feedback(rt_camera* c, const TraceParams& p, void* stream) {
     }
     if (++c->frames_since < kCostPeriod) return RT_OK;
     int rc;
-    if ((rc = hip_check(hipMemcpyAsync(c->h_cost, c->d_cost, sizeof(uint32_t) * 2 * (size_t)n, hipMemcpyDeviceToHost, st),
+    if ((rc = hip_check(hipMemcpyAsync(c->h_cost, c->d_cost, sizeof(uint32_t) * kCostSlots * (size_t)n, hipMemcpyDeviceToHost, st),
                         "D2H cost")) ||
         (rc = hip_check(hipEventRecord(c->cost_ev, st), "cost event")))
         return rc;
@@ -488,7 +498,8 @@ bool set_fine_region(rt_camera* c, TraceParams& p, int per_wave, bool fused) {
             if (g.first < p.cg_x0 || g.first >= p.cg_x1 || slot < p.cs0 || slot >= p.cs1)
                 return set_fine_region(c, p, per_wave, false);
         }
-        p.fill_blocks = p.coarse_blocks;  // appended to the fine kernel's grid
+        // appended to the fine kernel's grid, kd3_waves(rays) waves per block
+        p.fill_blocks = (int32_t)((waves + kd3_waves(p.rays) - 1) / kd3_waves(p.rays));
         p.coarse_blocks = 0;
     }
     return fused;
@@ -523,7 +534,7 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
     } else if (p.rays == 64) {               // v2 / v3: 16x8 tiles, two 8x8 waves
         p.tile_w = kTileWKd; p.tile_h = kTileH;
     } else {                                 // v3, two stacked 8 x (rays/8) waves
-        p.tile_w = 8; p.tile_h = 2 * (p.rays / 8);
+        p.tile_w = 8; p.tile_h = kd3_waves(p.rays) * (p.rays / 8);
     }
     p.tiles_x = (c->w + p.tile_w - 1) / p.tile_w;
     p.block_rows = ((nbands + p.nranks - 1) / p.nranks) * (kTileH / p.tile_h);

@@ -48,7 +48,17 @@ enum Option : int32_t {
                         // coarse, 8 = coarse kernel on a side stream beside the fine one
     kOptPoolCap = 101,  // tests: shrink kernel 3's item pool (66..kPoolCap) to force its fallback
 };
-constexpr int kPoolCapMax = 640;   // kernel 3 items per wave (peak measured <= 440, tools/pool_sim.c)
+constexpr int kPoolCapMax = 640;
+
+// Waves per block of the wave-cooperative kernel: a block is one fine tile,
+// each wave one kRays-pixel unit of it.  16- and 8-ray units may run
+// RT_KD3_WAVES per block (2 or 4; the tile's waves share the CU's L1), 32-
+// and 64-ray units run 2.  The per-unit cost slots hold up to 4 waves.
+#ifndef RT_KD3_WAVES
+#define RT_KD3_WAVES 4
+#endif
+__host__ __device__ constexpr int kd3_waves(int rays) { return rays <= 16 ? RT_KD3_WAVES : 2; }
+constexpr int kCostSlots = 4;   // kernel 3 items per wave (peak measured <= 440, tools/pool_sim.c)
 
 // ---------------------------------------------------------------------------
 // Device layouts (all 16-byte aligned, read with dwordx4 loads).

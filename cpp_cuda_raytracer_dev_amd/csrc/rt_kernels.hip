@@ -1205,13 +1205,13 @@ __device__ __forceinline__ unsigned long long coarse_root(const TraceParams& P, 
 // One fine tile per block (the tiles covering the root box's screen
 // rectangle, or the whole frame), one unit per wave.
 #ifdef RT_KD3_WAVES_PER_SIMD
-#define RT_KD3_BOUNDS __launch_bounds__(128, RT_KD3_WAVES_PER_SIMD)
+#define RT_KD3_BOUNDS(threads) __launch_bounds__(threads, RT_KD3_WAVES_PER_SIMD)
 #else
-#define RT_KD3_BOUNDS __launch_bounds__(128)
+#define RT_KD3_BOUNDS(threads) __launch_bounds__(threads)
 #endif
 template <int kRays, bool kTranslated, bool kWriteHit, bool kCount, bool kShadow>
-__global__ RT_KD3_BOUNDS void k_trace_kd3(TraceParams P) {
-    constexpr int kWaves = 2;
+__global__ RT_KD3_BOUNDS(64 * kd3_waves(kRays)) void k_trace_kd3(TraceParams P) {
+    constexpr int kWaves = kd3_waves(kRays);
     constexpr int kCap = pool_cap_for<kRays>();
     constexpr int kRayVec = (kTranslated || kShadow) ? 5 : 3;  // float4s of per-ray data in LDS
     __shared__ WaveLds<kRays, kCap, kRayVec> s_lds[kWaves];
@@ -1233,7 +1233,7 @@ __global__ RT_KD3_BOUNDS void k_trace_kd3(TraceParams P) {
         if (kCount) count_flush(P, C);
         return;
     }
-    uint32_t* cost = P.cost ? P.cost + 2 * (size_t)tile_index(P, b) + wv : nullptr;
+    uint32_t* cost = P.cost ? P.cost + kCostSlots * (size_t)tile_index(P, b) + wv : nullptr;
     trace_unit<kRays, kCap, kRayVec, kTranslated, kWriteHit, kCount, kShadow>(P, s_lds[wv], unit_of(P, b, wv), lane,
                                                                              (size_t)b * kWaves + wv, cost, C);
     if (kCount) count_flush(P, C);
