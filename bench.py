@@ -58,6 +58,9 @@ def parse():
                          "queue time, so N > 1 keeps the frame rate closer to the uninstrumented one)")
     ap.add_argument("--side-coarse", action="store_true",
                     help="kernel 3: run the coarse kernel beside the fine one on a side stream (default: before it)")
+    ap.add_argument("--deliver", action="store_true",
+                    help="N=1: also time frames delivered to pinned host memory (render + async D2H, double "
+                         "buffered); reported in a 'delivery' object, never as value")
     ap.add_argument("--shadow", action="store_true",
                     help="one shadow ray per hit (config C5: --scene happy --width 3840 --height 2160 --shadow)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
@@ -101,6 +104,44 @@ def cpu_baseline(pts, nodes, w, h, seconds, threads, mode, shadow=False, rays_pe
             "mray_per_s": round(fps * (rays_per_frame or w * h) / 1e6, 3),
             "sample": f"{frames} x rows {rows[0]}-{rows[1]} of the same {w}x{h} frame, oracle/oracle.c "
                       f"(-O2 -ffp-contract=off, OpenMP {threads} threads), {dt:.1f} s"}
+
+
+def delivery(cam, R, torch, dev, w, h, xf, mode, sflag, steps, warmup):
+    """Frames delivered to the host: frame i renders
+    into device buffer i % 2 on the render stream while frame i - 1's D2H into
+    pinned host memory runs on a copy stream.  Returns frames/s and the D2H
+    rate; PCIe-inclusive, so reported beside `value`, never as it."""
+    npix = w * h
+    outs = [torch.zeros(npix, dtype=torch.int32, device=dev) for _ in range(2)]
+    pf = R.PinnedFrames(npix, 2)
+    rs, cs = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+    rendered = [torch.cuda.Event() for _ in range(2)]
+    copied = [torch.cuda.Event() for _ in range(2)]
+
+    def one(i):
+        k = i % 2
+        rs.wait_event(copied[k])  # the copy of frame i - 2 has left buffer k
+        cam.render_into(outs[k], xform=xf, mode=mode, flags=sflag, stream=rs.cuda_stream)
+        rendered[k].record(rs)
+        cs.wait_event(rendered[k])
+        pf.copy_async(k, dev.index, outs[k], stream=cs.cuda_stream)
+        copied[k].record(cs)
+
+    for k in range(2):
+        copied[k].record(cs)
+    for i in range(warmup):
+        one(i)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        one(i)
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    ok = bool((pf.frames[(steps - 1) % 2] == outs[(steps - 1) % 2].cpu().numpy().view(np.uint32)).all())
+    pf.close()
+    return {"frames_per_s": round(steps / dt, 2), "d2h_gb_per_s": round(steps * npix * 4 / dt / 1e9, 2),
+            "frame_bytes": npix * 4, "steps": steps, "host_frame_matches_device": ok,
+            "method": "render on one stream, D2H to pinned host memory on another, 2 buffers"}
 
 
 def main():
@@ -267,6 +308,8 @@ def main():
                 "bytes_model": "36*V_int + 40*V_leaf + 24*H + 4*P (SURVEY.md 8d)",
             },
         }
+        if a.deliver and world == 1:
+            res["delivery"] = delivery(cam, R, torch, dev, w, h, xf, a.mode, sflag, a.steps, a.warmup)
         if not a.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(pts, nodes, w, h, a.cpu_seconds, a.cpu_threads, a.mode, a.shadow,
                                               rays_per_frame)

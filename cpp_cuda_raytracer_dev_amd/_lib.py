@@ -80,6 +80,9 @@ SIGNATURES = {
     "rt_unpack_bands": (C.c_int, [C.c_int, C.c_int32, C.c_int32, C.c_int32, _P, _P, _P]),
     "rt_read_frame": (C.c_int, [_P, _P, _P]),
     "rt_camera_counters": (C.c_int, [_P, _P, C.c_int]),
+    "rt_pinned_alloc": (C.c_int, [C.c_size_t, C.POINTER(_P)]),
+    "rt_pinned_free": (None, [_P]),
+    "rt_frame_copy_async": (C.c_int, [C.c_int, _P, _P, C.c_int64, _P]),
     "rt_camera_info": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "rt_camera_set_option": (C.c_int, [_P, C.c_int32, C.c_int32]),
     "rt_camera_debug_read": (C.c_int64, [_P, _P, C.c_int64]),

@@ -834,6 +834,24 @@ extern "C" int rt_read_frame(rt_camera* c, uint32_t* argb, int64_t* hit) {
     return RT_OK;
 }
 
+extern "C" int rt_pinned_alloc(size_t bytes, void** out) {
+    if (!out) return fail(RT_ERR_INVALID, "rt_pinned_alloc: null out");
+    *out = nullptr;
+    return hip_check(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault), "hipHostMalloc");
+}
+
+extern "C" void rt_pinned_free(void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
+extern "C" int rt_frame_copy_async(int device, const uint32_t* d_argb, uint32_t* h_argb, int64_t npix, void* stream) {
+    if (!d_argb || !h_argb || npix < 0) return fail(RT_ERR_INVALID, "rt_frame_copy_async: bad argument");
+    if (npix == 0) return RT_OK;
+    DeviceGuard g(device);
+    return hip_check(hipMemcpyAsync(h_argb, d_argb, sizeof(uint32_t) * (size_t)npix, hipMemcpyDeviceToHost,
+                                    (hipStream_t)stream), "D2H frame");
+}
+
 extern "C" int rt_camera_counters(rt_camera* c, uint64_t out[5], int reset) {
     if (!c || !out) return fail(RT_ERR_INVALID, "rt_camera_counters: null argument");
     DeviceGuard g(c->device);

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <charconv>
 #include <numeric>
 #include <string>
 #include <thread>
@@ -158,6 +159,201 @@ extern "C" int rt_mesh_assemble(const float* verts, int64_t nvert, const int32_t
     return RT_OK;
 }
 
+namespace rt {
+namespace {
+
+// ---- PLY header (TD/read_ply.cpp:19-44, extended with property lists) ----
+
+enum PlyType { kNone = 0, kI8, kU8, kI16, kU16, kI32, kU32, kF32, kF64 };
+
+PlyType ply_type(const char* t) {
+    static const struct { const char* n; PlyType t; } names[] = {
+        {"char", kI8}, {"int8", kI8}, {"uchar", kU8}, {"uint8", kU8}, {"short", kI16}, {"int16", kI16},
+        {"ushort", kU16}, {"uint16", kU16}, {"int", kI32}, {"int32", kI32}, {"uint", kU32}, {"uint32", kU32},
+        {"float", kF32}, {"float32", kF32}, {"double", kF64}, {"float64", kF64}};
+    for (const auto& e : names)
+        if (!strcmp(t, e.n)) return e.t;
+    return kNone;
+}
+
+int ply_size(PlyType t) {
+    switch (t) {
+    case kI8: case kU8: return 1;
+    case kI16: case kU16: return 2;
+    case kI32: case kU32: case kF32: return 4;
+    case kF64: return 8;
+    default: return 0;
+    }
+}
+
+// Little-endian scalar of type t at p, as a double (exact for every type).
+double ply_get(const unsigned char* p, PlyType t) {
+    switch (t) {
+    case kI8: return (double)(int8_t)p[0];
+    case kU8: return (double)p[0];
+    case kI16: { int16_t v; memcpy(&v, p, 2); return v; }
+    case kU16: { uint16_t v; memcpy(&v, p, 2); return v; }
+    case kI32: { int32_t v; memcpy(&v, p, 4); return v; }
+    case kU32: { uint32_t v; memcpy(&v, p, 4); return v; }
+    case kF32: { float v; memcpy(&v, p, 4); return v; }
+    case kF64: { double v; memcpy(&v, p, 8); return v; }
+    default: return 0.0;
+    }
+}
+
+struct PlyProp {
+    std::string name;
+    PlyType type = kNone;        // scalar type, or the list's item type
+    PlyType count_type = kNone;  // list count type (kNone: scalar property)
+};
+
+struct PlyElem {
+    std::string name;
+    long long count = 0;
+    std::vector<PlyProp> props;
+};
+
+struct PlyHeader {
+    int format = 0;  // 0 ascii, 1 binary_little_endian, 2 binary_big_endian
+    std::vector<PlyElem> elems;
+    long long nv = -1, nf = -1;
+};
+
+bool is_space(char c) { return c == ' ' || c == '\t' || c == '\r' || c == '\n' || c == '\f' || c == '\v'; }
+
+// One line of ASCII body: up to `max` numbers parsed with std::from_chars (the
+// correctly rounded conversion strtof / strtol also perform).  Returns the
+// count, or -1 on a malformed token.
+template <class T>
+int parse_line(const char* p, const char* e, T* out, int max) {
+    int n = 0;
+    for (;;) {
+        while (p < e && is_space(*p)) p++;
+        if (p >= e) return n;
+        if (n == max) return max + 1;  // more tokens than the line may hold
+        if (*p == '+') p++;
+        const auto r = std::from_chars(p, e, out[n]);
+        if (r.ec != std::errc() || (r.ptr < e && !is_space(*r.ptr))) return -1;
+        p = r.ptr;
+        n++;
+    }
+}
+
+}  // namespace
+}  // namespace rt
+
+// Parallel ASCII body: one vertex (per_vertex numbers) and one face
+// ("n i0 .. i(n-1)", n = 3 or 4) per line, which is what every PLY writer
+// emits.  Files that do not keep to one record per line return false and take
+// the token-by-token reader below (the reference's `>>` semantics).
+static bool ply_ascii_lines(const char* p, const char* end, long long nv, long long nf, int per_vertex, int T,
+                            std::vector<float>& verts, std::vector<int32_t>& arity, std::vector<int32_t>& idx) {
+    std::vector<const char*> ls;  // starts of the first nv + nf non-blank lines
+    ls.reserve((size_t)(nv + nf + 1));
+    while (p < end && (long long)ls.size() < nv + nf) {
+        const char* q = (const char*)memchr(p, '\n', (size_t)(end - p));
+        const char* e = q ? q : end;
+        const char* t = p;
+        while (t < e && is_space(*t)) t++;
+        if (t < e) ls.push_back(p);
+        p = q ? q + 1 : end;
+    }
+    if ((long long)ls.size() < nv + nf) return false;
+    auto line_end = [&](const char* s) {
+        const char* q = (const char*)memchr(s, '\n', (size_t)(end - s));
+        return q ? q : end;
+    };
+    verts.assign((size_t)nv * 3, 0.0f);
+    arity.assign((size_t)nf, 0);
+    std::vector<int32_t> quad((size_t)nf * 4, 0);
+    std::atomic<bool> ok{true};
+    const int64_t chunk = 8192;
+    const int64_t nvc = (nv + chunk - 1) / chunk, nfc = (nf + chunk - 1) / chunk;
+    parallel_for(nvc + nfc, T, [&](int64_t c) {
+        if (c < nvc) {
+            for (int64_t i = c * chunk; i < std::min<int64_t>(nv, (c + 1) * chunk) && ok; i++) {
+                float v[8];
+                const char* s = ls[(size_t)i];
+                if (parse_line(s, line_end(s), v, per_vertex) != per_vertex) { ok = false; break; }
+                for (int j = 0; j < 3; j++) verts[(size_t)i * 3 + j] = v[j];
+            }
+        } else {
+            for (int64_t f = (c - nvc) * chunk; f < std::min<int64_t>(nf, (c - nvc + 1) * chunk) && ok; f++) {
+                long v[6];
+                const char* s = ls[(size_t)(nv + f)];
+                const int n = parse_line(s, line_end(s), v, 5);
+                if (n < 1 || (v[0] != 3 && v[0] != 4) || n != 1 + v[0]) { ok = false; break; }
+                arity[(size_t)f] = (int32_t)v[0];
+                for (int j = 0; j < v[0]; j++) quad[(size_t)f * 4 + j] = (int32_t)v[1 + j];
+            }
+        }
+    });
+    if (!ok) return false;
+    idx.clear();
+    idx.reserve((size_t)nf * 3);
+    for (int64_t f = 0; f < nf; f++)
+        for (int j = 0; j < arity[(size_t)f]; j++) idx.push_back(quad[(size_t)f * 4 + j]);
+    return true;
+}
+
+// binary_little_endian body (the reference recognises the format,
+// TD/read_ply.cpp:28, but reads no binary data): x, y, z of the vertex
+// element (any scalar type, converted to float) and the face element's
+// vertex-index list; other elements and properties are skipped by size.
+static int ply_binary(const char* path, const rt::PlyHeader& H, const unsigned char* p, const unsigned char* end,
+                      std::vector<float>& verts, std::vector<int32_t>& arity, std::vector<int32_t>& idx) {
+    using namespace rt;
+    for (const PlyElem& el : H.elems) {
+        const bool is_v = el.name == "vertex", is_f = el.name == "face";
+        int xyz[3] = {-1, -1, -1}, list = -1;
+        for (size_t k = 0; k < el.props.size(); k++) {
+            const PlyProp& pr = el.props[k];
+            if (is_v && pr.count_type == kNone) {
+                if (pr.name == "x") xyz[0] = (int)k;
+                if (pr.name == "y") xyz[1] = (int)k;
+                if (pr.name == "z") xyz[2] = (int)k;
+            }
+            if (is_f && pr.count_type != kNone && (list < 0 || pr.name == "vertex_indices" || pr.name == "vertex_index"))
+                list = (int)k;
+        }
+        if (is_v) {
+            if (xyz[0] < 0 || xyz[1] < 0 || xyz[2] < 0) return fail(RT_ERR_IO, "rt_read_ply: vertex x/y/z missing in %s", path);
+            verts.assign((size_t)el.count * 3, 0.0f);
+        }
+        if (is_f) {
+            if (list < 0) return fail(RT_ERR_IO, "rt_read_ply: face list missing in %s", path);
+            arity.assign((size_t)el.count, 0);
+            idx.reserve((size_t)el.count * 3);
+        }
+        for (long long i = 0; i < el.count; i++) {
+            for (size_t k = 0; k < el.props.size(); k++) {
+                const PlyProp& pr = el.props[k];
+                if (pr.count_type == kNone) {
+                    const int sz = ply_size(pr.type);
+                    if (p + sz > end) return fail(RT_ERR_IO, "rt_read_ply: truncated %s", path);
+                    if (is_v)
+                        for (int j = 0; j < 3; j++)
+                            if ((int)k == xyz[j]) verts[(size_t)i * 3 + j] = (float)ply_get(p, pr.type);
+                    p += sz;
+                } else {
+                    const int csz = ply_size(pr.count_type), isz = ply_size(pr.type);
+                    if (p + csz > end) return fail(RT_ERR_IO, "rt_read_ply: truncated %s", path);
+                    const double cnt = ply_get(p, pr.count_type);
+                    p += csz;
+                    if (!(cnt >= 0) || p + (size_t)cnt * isz > end) return fail(RT_ERR_IO, "rt_read_ply: truncated %s", path);
+                    if (is_f && (int)k == list) {
+                        if (cnt != 3 && cnt != 4) return fail(RT_ERR_IO, "rt_read_ply: face %lld has %g vertices in %s", i, cnt, path);
+                        arity[(size_t)i] = (int32_t)cnt;
+                        for (int j = 0; j < (int)cnt; j++) idx.push_back((int32_t)ply_get(p + (size_t)j * isz, pr.type));
+                    }
+                    p += (size_t)cnt * isz;
+                }
+            }
+        }
+    }
+    return RT_OK;
+}
+
 extern "C" int rt_read_ply(const char* path, int mode, float** points9, uint32_t* ntri,
                            rt_leaf_aabb** leafs) {
     if (!path) return fail(RT_ERR_INVALID, "rt_read_ply: null path");
@@ -175,49 +371,84 @@ extern "C" int rt_read_ply(const char* path, int mode, float** points9, uint32_t
     buf[got] = 0;
     Cursor cur{buf.data(), buf.data() + got};
     std::string line;
-    long long nv = -1, nf = -1;
+    PlyHeader H;
     cur.line(line);
     if (line == "ply") cur.line(line);
     if (is_count_line(line)) {  // headerless prelude (H9 extension)
-        nv = atoll(line.c_str());
+        H.nv = atoll(line.c_str());
         if (!cur.line(line) || !is_count_line(line)) return fail(RT_ERR_IO, "rt_read_ply: bad prelude in %s", path);
-        nf = atoll(line.c_str());
+        H.nf = atoll(line.c_str());
     } else {                    // header loop, TD/read_ply.cpp:19-44
         for (;;) {
-            char tag[64] = {0}, name[64] = {0};
-            long long val = -1;
-            if (sscanf(line.c_str(), "%63s %63s %lld", tag, name, &val) == 3 && !strcmp(tag, "element")) {
-                if (!strcmp(name, "vertex")) nv = val;
-                if (!strcmp(name, "face")) nf = val;
+            char tag[64] = {0}, a1[64] = {0}, a2[64] = {0}, a3[64] = {0}, a4[64] = {0};
+            const int nt = sscanf(line.c_str(), "%63s %63s %63s %63s %63s", tag, a1, a2, a3, a4);
+            if (nt >= 2 && !strcmp(tag, "format")) {
+                if (!strcmp(a1, "binary_little_endian")) H.format = 1;
+                else if (!strcmp(a1, "binary_big_endian")) H.format = 2;
+            } else if (nt >= 3 && !strcmp(tag, "element")) {
+                PlyElem el;
+                el.name = a1;
+                el.count = atoll(a2);
+                H.elems.push_back(el);
+                if (el.name == "vertex") H.nv = el.count;
+                if (el.name == "face") H.nf = el.count;
+            } else if (nt >= 3 && !strcmp(tag, "property") && !H.elems.empty()) {
+                PlyProp pr;
+                if (!strcmp(a1, "list") && nt >= 5) {
+                    pr.count_type = ply_type(a2);
+                    pr.type = pr.count_type == kNone ? kNone : ply_type(a3);  // unknown types fail binary files
+                    pr.name = a4;
+                } else {
+                    pr.type = ply_type(a1);
+                    pr.name = a2;
+                }
+                H.elems.back().props.push_back(pr);
             }
             if (line == "end_header") break;
             if (!cur.line(line)) return fail(RT_ERR_IO, "rt_read_ply: no end_header in %s", path);
         }
     }
-    if (nv < 0 || nf < 0) return fail(RT_ERR_IO, "rt_read_ply: missing vertex/face counts in %s", path);
-    std::vector<float> verts((size_t)nv * 3);
-    const char* p = cur.p;
-    for (long long i = 0; i < nv; i++)
-        for (int j = 0; j < per_vertex; j++) {
+    if (H.nv < 0 || H.nf < 0) return fail(RT_ERR_IO, "rt_read_ply: missing vertex/face counts in %s", path);
+    std::vector<float> verts;
+    std::vector<int32_t> arity, idx;
+    if (H.format == 2) return fail(RT_ERR_IO, "rt_read_ply: binary_big_endian is not supported (%s)", path);
+    if (H.format == 1) {
+        for (const PlyElem& el : H.elems)
+            for (const PlyProp& pr : el.props)
+                if (pr.type == kNone)
+                    return fail(RT_ERR_IO, "rt_read_ply: unknown property type in %s", path);
+        int rc = ply_binary(path, H, (const unsigned char*)cur.p, (const unsigned char*)cur.end, verts, arity, idx);
+        if (rc) return rc;
+        return rt_mesh_assemble(verts.data(), H.nv, arity.data(), idx.data(), H.nf, points9, ntri, leafs);
+    }
+    const long long nv = H.nv, nf = H.nf;
+    if (!ply_ascii_lines(cur.p, cur.end, nv, nf, per_vertex, resolve_threads(0), verts, arity, idx)) {
+        // token-by-token reader: the reference's sequential `>>` semantics
+        verts.assign((size_t)nv * 3, 0.0f);
+        const char* p = cur.p;
+        for (long long i = 0; i < nv; i++)
+            for (int j = 0; j < per_vertex; j++) {
+                char* e;
+                float v = strtof(p, &e);
+                if (e == p) return fail(RT_ERR_IO, "rt_read_ply: bad vertex %lld in %s", i, path);
+                p = e;
+                if (j < 3) verts[(size_t)i * 3 + j] = v;
+            }
+        arity.assign((size_t)nf, 0);
+        idx.clear();
+        idx.reserve((size_t)nf * 3);
+        for (long long f = 0; f < nf; f++) {
             char* e;
-            float v = strtof(p, &e);
-            if (e == p) return fail(RT_ERR_IO, "rt_read_ply: bad vertex %lld in %s", i, path);
+            long c = strtol(p, &e, 10);
+            if (e == p || (c != 3 && c != 4)) return fail(RT_ERR_IO, "rt_read_ply: bad face %lld in %s", f, path);
             p = e;
-            if (j < 3) verts[(size_t)i * 3 + j] = v;
-        }
-    std::vector<int32_t> arity((size_t)nf), idx;
-    idx.reserve((size_t)nf * 3);
-    for (long long f = 0; f < nf; f++) {
-        char* e;
-        long c = strtol(p, &e, 10);
-        if (e == p || (c != 3 && c != 4)) return fail(RT_ERR_IO, "rt_read_ply: bad face %lld in %s", f, path);
-        p = e;
-        arity[(size_t)f] = (int32_t)c;
-        for (long j = 0; j < c; j++) {
-            long v = strtol(p, &e, 10);
-            if (e == p) return fail(RT_ERR_IO, "rt_read_ply: bad face %lld in %s", f, path);
-            p = e;
-            idx.push_back((int32_t)v);
+            arity[(size_t)f] = (int32_t)c;
+            for (long j = 0; j < c; j++) {
+                long v = strtol(p, &e, 10);
+                if (e == p) return fail(RT_ERR_IO, "rt_read_ply: bad face %lld in %s", f, path);
+                p = e;
+                idx.push_back((int32_t)v);
+            }
         }
     }
     return rt_mesh_assemble(verts.data(), nv, arity.data(), idx.data(), nf, points9, ntri, leafs);

@@ -275,6 +275,41 @@ def unpack_bands(device: int, w: int, h: int, nranks: int, gathered, frame, stre
     _lib.call("rt_unpack_bands", device, w, h, nranks, _lib.ptr(gathered), _lib.ptr(frame), s)
 
 
+class PinnedFrames:
+    """Frame delivery: `count` page-locked host frames
+    of `npix` u32 each, filled by stream-ordered D2H copies so the copy of
+    frame k overlaps the render of frame k+1 (the reference copies
+    synchronously, TD/Camera.cu:84)."""
+
+    def __init__(self, npix: int, count: int = 2):
+        self.npix = int(npix)
+        self._ptrs = []
+        self.frames = []
+        for _ in range(count):
+            p = C.c_void_p()
+            _lib.call("rt_pinned_alloc", C.c_size_t(4 * max(self.npix, 1)), C.byref(p))
+            self._ptrs.append(p)
+            buf = (C.c_uint32 * max(self.npix, 1)).from_address(p.value)
+            self.frames.append(np.frombuffer(buf, dtype=np.uint32)[: self.npix])
+
+    def copy_async(self, k: int, device: int, d_argb, stream=None) -> None:
+        """Enqueue the D2H of device frame d_argb into host frame k on `stream`."""
+        s = C.c_void_p(stream) if isinstance(stream, int) else C.c_void_p(None)
+        _lib.call("rt_frame_copy_async", device, _lib.ptr(d_argb), self._ptrs[k], self.npix, s)
+
+    def close(self) -> None:
+        self.frames = []
+        for p in self._ptrs:
+            _lib.lib().rt_pinned_free(p)
+        self._ptrs = []
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 __all__ = ["read_ply", "assemble_mesh", "kd_build", "film_w", "camera_basis", "Quaternion", "Trixel", "Object",
-           "Camera", "packed_pixels", "unpack_bands", "SET_COLOR_TAG", "PHONG_COLOR_TAG", "RT_MODE_KD",
+           "Camera", "PinnedFrames", "packed_pixels", "unpack_bands", "SET_COLOR_TAG", "PHONG_COLOR_TAG", "RT_MODE_KD",
            "RT_MODE_FLAT", "RT_FLAG_WRITE_HIT", "RT_FLAG_COUNT", "RT_FLAG_SHADOW", "BACKGROUND_ARGB", "DEFAULT_RAD"]

@@ -169,6 +169,17 @@ int rt_unpack_bands(int device, int32_t w, int32_t h, int32_t nranks,
  * Synchronises the device.  argb: w*h u32 0x00RRGGBB; hit may be NULL. */
 int rt_read_frame(rt_camera* c, uint32_t* argb, int64_t* hit);
 
+/* Frame delivery: the reference copies every frame
+ * to the host synchronously (cudaMemcpy in color_camera_device,
+ * TD/Camera.cu:84; blit in TD/WinMain.cpp:217).  These let a frame loop copy
+ * frame k to pinned host memory on a copy stream while frame k+1 renders.
+ * rt_pinned_alloc / rt_pinned_free: page-locked host memory (hipHostMalloc).
+ * rt_frame_copy_async: npix u32 from device d_argb to host h_argb, ordered
+ * on `stream` (a hipStream_t or NULL); no synchronisation. */
+int rt_pinned_alloc(size_t bytes, void** out);
+void rt_pinned_free(void* p);
+int rt_frame_copy_async(int device, const uint32_t* d_argb, uint32_t* h_argb, int64_t npix, void* stream);
+
 /* Counters accumulated by RT_FLAG_COUNT renders: [0] interior visits,
  * [1] leaf visits, [2] accepted hits, [3] hit pixels, [4] interior visits
  * that descended.  reset != 0 zeroes them after reading.  Synchronises. */

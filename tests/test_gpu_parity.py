@@ -429,3 +429,58 @@ def test_cost_order_pose_change(order):
     argb, hit, _ = s.render(0, xform=xf)
     oargb, ohit, _ = H.oracle_render("rabbit_70k", 320, 180, 0, xform=xf)
     _assert_same((argb, hit), (oargb, ohit), "cost order after pose changes")
+
+
+# ------------------------------------------------------- frame delivery
+# frames copied to pinned host memory on a copy stream
+# while the next frame renders (rt_pinned_alloc / rt_frame_copy_async).
+def test_frame_delivery_pinned_double_buffered():
+    import torch
+    from cpp_cuda_raytracer_dev_amd import raytracer as R
+    w, h = 320, 180
+    s = H.GpuScene("rabbit_70k", w, h, kernel=3)
+    xfs = [_rot_y(float(a), (0.0, 0.0, 0.005 * k)) for k, a in enumerate((0, 7, 14, 21, 28))]
+    want = [H.oracle_render("rabbit_70k", w, h, 0, xform=xf)[0] for xf in xfs]
+    dev = torch.device("cuda:0")
+    outs = [torch.zeros(w * h, dtype=torch.int32, device=dev) for _ in range(2)]
+    pf = R.PinnedFrames(w * h, 2)
+    rs, cs = torch.cuda.Stream(), torch.cuda.Stream()
+    rendered = [torch.cuda.Event() for _ in range(2)]
+    copied = [torch.cuda.Event() for _ in range(2)]
+    for k in range(2):
+        copied[k].record(cs)
+    got = []
+    for i, xf in enumerate(xfs):
+        k = i % 2
+        if i >= 2:
+            copied[k].synchronize()
+            got.append(pf.frames[k].copy())  # frame i - 2, before its buffer is reused
+        rs.wait_event(copied[k])
+        s.cam.render_into(outs[k], xform=xf, mode=0, stream=rs.cuda_stream)
+        rendered[k].record(rs)
+        cs.wait_event(rendered[k])
+        pf.copy_async(k, 0, outs[k], stream=cs.cuda_stream)
+        copied[k].record(cs)
+    torch.cuda.synchronize()
+    for i in range(len(xfs) - 2, len(xfs)):
+        got.append(pf.frames[i % 2].copy())
+    pf.close()
+    assert len(got) == len(xfs)
+    for i, (g, wnt) in enumerate(zip(got, want)):
+        assert (g == wnt).all(), f"delivered frame {i} differs from the oracle"
+
+
+# ------------------------------------------------------- binary PLY mesh
+# 3_walls.ply (the reference's binary file, read by rt_read_ply's binary
+# path; fixture bytes in tests/golden/meshes/3_walls.npz) through the KD
+# kernels, two poses that see its walls.
+@pytest.mark.parametrize("kernel", [2, 3])
+@pytest.mark.parametrize("pose", [dict(pos=(-100.0, 20.0, -50.0), look_at=(-307.0, 0.0, 2.0)),
+                                  dict(pos=(-150.0, -60.0, 120.0), look_at=(-307.0, 10.0, 0.0))])
+def test_binary_mesh_3_walls(pose, kernel):
+    s = H.GpuScene("3_walls", 160, 90, cam_kw=pose, kernel=kernel)
+    argb, hit, cnt = s.render(0, count=True)
+    oargb, ohit, ocnt = H.oracle_render("3_walls", 160, 90, 0, cam_kw=pose)
+    assert (ohit >= 0).sum() > 1000
+    _assert_same((argb, hit), (oargb, ohit), "3_walls")
+    _counters_match(cnt, ocnt, kernel)
