@@ -61,6 +61,11 @@ def parse():
     ap.add_argument("--deliver", action="store_true",
                     help="N=1: also time frames delivered to pinned host memory (render + async D2H, double "
                          "buffered); reported in a 'delivery' object, never as value")
+    ap.add_argument("--shadow-order", type=int, default=-1,
+                    help="kernel 3 any-hit push order 0..3, -1 = timed choice (default)")
+    ap.add_argument("--animate", default="",
+                    help="held keys per frame, cycled: letters R W S Q E T, '+' joins keys held together, '.' is "
+                         "a tick with none; one input tick (TD/WinMain.cpp:186-209) before each frame, timed")
     ap.add_argument("--shadow", action="store_true",
                     help="one shadow ray per hit (config C5: --scene happy --width 3840 --height 2160 --shadow)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
@@ -144,6 +149,28 @@ def delivery(cam, R, torch, dev, w, h, xf, mode, sflag, steps, warmup):
             "method": "render on one stream, D2H to pinned host memory on another, 2 buffers"}
 
 
+def key_masks(spec: str) -> list:
+    """"R+W.Q" -> [R|W, 0, Q] (bits of raytracer.KEY_*), as tools/rt_headless reads it."""
+    from cpp_cuda_raytracer_dev_amd import raytracer as R
+    bits = {"R": R.KEY_R, "W": R.KEY_W, "S": R.KEY_S, "Q": R.KEY_Q, "E": R.KEY_E, "T": R.KEY_T, ".": 0}
+    out = []
+    k = 0
+    while k < len(spec):
+        m = 0
+        while True:
+            c = spec[k]
+            if c not in bits:
+                raise ValueError(f"--animate: unknown key {c!r}")
+            m |= bits[c]
+            k += 1
+            if k < len(spec) and spec[k] == "+":
+                k += 1
+                continue
+            break
+        out.append(m)
+    return out
+
+
 def main():
     a = parse()
     import torch
@@ -184,14 +211,31 @@ def main():
     npk = R.packed_pixels(w, h, world) if world > 1 else w * h
     scratch = torch.zeros(npk, dtype=torch.int32, device=dev)
     sflag = R.RT_FLAG_SHADOW if a.shadow else 0
-    cam.render_into(scratch, mode=a.mode, flags=R.RT_FLAG_COUNT | sflag, tile=tile if world > 1 else None,
-                    stream=sptr)
-    torch.cuda.synchronize(dev)
-    cnt = cam.counters(reset=True)
+    masks = key_masks(a.animate) if a.animate else []
+    if masks:
+        # every timed frame has its own pose: count each of them (untimed),
+        # replaying the same ticks on a separate motion state
+        mo = R.ObjectMotion(cam.pos, cam.o_prop["n"], cam.o_prop["u"], cam.cam_speed)
+        acc = np.zeros(5, np.float64)
+        for i in range(a.warmup + a.steps):
+            mo.tick(masks[i % len(masks)])
+            if i >= a.warmup:
+                cam.render_into(scratch, xform=mo.xform(), mode=a.mode, flags=R.RT_FLAG_COUNT | sflag,
+                                tile=tile if world > 1 else None, stream=sptr)
+                torch.cuda.synchronize(dev)
+                acc += cam.counters(reset=True)
+        mo.close()
+        cnt = acc / a.steps  # mean per frame
+    else:
+        cam.render_into(scratch, mode=a.mode, flags=R.RT_FLAG_COUNT | sflag, tile=tile if world > 1 else None,
+                        stream=sptr)
+        torch.cuda.synchronize(dev)
+        cnt = cam.counters(reset=True)
     cam.set_option(_lib.RT_OPT_KERNEL, a.kernel)
     cam.set_option(_lib.RT_OPT_RAYS, a.rays)
     cam.set_option(_lib.RT_OPT_ITEMS, a.items)
     cam.set_option(_lib.RT_OPT_COARSE, a.coarse)
+    cam.set_option(_lib.RT_OPT_SHADOW_ORDER, a.shadow_order)
     if a.side_coarse:
         cam.set_option(_lib.RT_OPT_DEBUG, 8)
     cam.render_into(scratch, mode=a.mode, flags=sflag, tile=tile if world > 1 else None,
@@ -212,7 +256,14 @@ def main():
     timed_frames = list(range(0, a.steps, max(1, a.event_every)))
     ev = {i: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for i in timed_frames}
 
+    tick = [0]
+
     def frame(i=None):
+        nonlocal xf
+        if masks:  # one input tick, then the frame at the new pose
+            obj.key_tick(masks[tick[0] % len(masks)])
+            tick[0] += 1
+            xf = obj.quat.xform()
         with torch.cuda.stream(stream):
             if i in ev:
                 ev[i][0].record(stream)
@@ -238,6 +289,18 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev.values()]))
+    full_walk = None
+    if a.shadow and not masks:
+        # shadow walks stop at their first occluder; the counting frame above
+        # walked them in full (the oracle's counters).  Count the timed walk
+        # (same push order) for the algorithmic bytes, untimed.
+        full_walk = cnt
+        cam.set_option(_lib.RT_OPT_DEBUG, 16 | (8 if a.side_coarse else 0))
+        cam.render_into(scratch, xform=xf, mode=a.mode, flags=R.RT_FLAG_COUNT | sflag,
+                        tile=tile if world > 1 else None, stream=sptr)
+        torch.cuda.synchronize(dev)
+        cnt = cam.counters(reset=True)
+        bytes_per_launch = B_INT * int(cnt[0]) + B_LEAF * int(cnt[1]) + B_HIT * int(cnt[2]) + B_PIX * my_pix
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -281,7 +344,8 @@ def main():
             "config": {
                 "workload": f"{a.scene} stand-in {w}x{h}, {'KD traversal' if a.mode == 0 else 'flat list'}, "
                             + ("primary + one shadow ray per hit" if a.shadow else "primary rays")
-                            + " + Phong, u32 frame on GPU 0",
+                            + " + Phong, u32 frame on GPU 0"
+                            + (f", object moved by keys {a.animate!r} (one tick per frame)" if masks else ""),
                 "rays_per_frame": rays_per_frame,
                 "scene": f"synthetic {a.scene} stand-in, {len(pts)} triangles (seed 20221015)",
                 "resolution": [w, h],
@@ -298,13 +362,18 @@ def main():
                           else "k_trace_flat",
                 "kernel_options": {"kernel": a.kernel, "tile_order": a.tile_order, "rays_per_wave": a.rays,
                                    "items_per_lane": a.items, "coarse_groups_per_wave": a.coarse,
-                                   "shadow": a.shadow},
+                                   "shadow": a.shadow,
+                                   **({"shadow_push_order": cam.get_option(_lib.RT_OPT_SHADOW_ORDER),
+                                       "shadow_push_order_mode": "timed" if a.shadow_order < 0 else "fixed"}
+                                      if a.shadow else {})},
                 "kernel_ms_avg": round(kern_ms, 5),
                 "kernel_ms_frames": f"{len(ev)} of {a.steps} timed frames (every {max(1, a.event_every)})",
                 "kernel_ms_avg_max_rank": round(kern_ms_max, 5),
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "counts_per_launch": {"interior": int(cnt[0]), "leaf": int(cnt[1]), "accept": int(cnt[2]),
                                       "hit_pixels": int(cnt[3]), "pixels": my_pix},
+                **({"counts_full_shadow_walk": {"interior": int(full_walk[0]), "leaf": int(full_walk[1]),
+                                                "accept": int(full_walk[2])}} if full_walk is not None else {}),
                 "bytes_model": "36*V_int + 40*V_leaf + 24*H + 4*P (SURVEY.md 8d)",
             },
         }

@@ -26,6 +26,7 @@ RT_OPT_TILE_ORDER = 2
 RT_OPT_RAYS = 3
 RT_OPT_ITEMS = 4
 RT_OPT_COARSE = 5
+RT_OPT_SHADOW_ORDER = 6
 RT_OPT_DEBUG = 100
 RT_OPT_POOL_CAP = 101
 
@@ -83,8 +84,15 @@ SIGNATURES = {
     "rt_pinned_alloc": (C.c_int, [C.c_size_t, C.POINTER(_P)]),
     "rt_pinned_free": (None, [_P]),
     "rt_frame_copy_async": (C.c_int, [C.c_int, _P, _P, C.c_int64, _P]),
+    "rt_object_create": (C.c_int, [_P, _P, _P, C.c_float, C.POINTER(_P)]),
+    "rt_object_transform": (C.c_int, [_P, _P, C.c_int32]),
+    "rt_object_tick": (C.c_int, [_P, C.c_uint32]),
+    "rt_object_xform": (C.c_int, [_P, _P]),
+    "rt_object_state": (C.c_int, [_P, _P, _P, _P, _P]),
+    "rt_object_destroy": (None, [_P]),
     "rt_camera_info": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "rt_camera_set_option": (C.c_int, [_P, C.c_int32, C.c_int32]),
+    "rt_camera_get_option": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_int32)]),
     "rt_camera_debug_read": (C.c_int64, [_P, _P, C.c_int64]),
     "rt_scene_destroy": (None, [_P]),
     "rt_camera_destroy": (None, [_P]),

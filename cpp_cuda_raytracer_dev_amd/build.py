@@ -21,7 +21,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "librt_mi355x.so")
 ARCH = os.environ.get("RT_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["rt_kernels.hip", "rt_api.cpp", "scene_host.cpp"]
+SOURCES = ["rt_kernels.hip", "rt_api.cpp", "scene_host.cpp", "motion.cpp"]
 # -fno-slp-vectorize: hipcc's packed-math (v_pk_*) SLP pairs cost more register
 # moves than they save in the traversal loop (0.0851 vs 0.0871 ms per 1080p
 # dragon frame); the arithmetic per lane is the same IEEE operations either way.
@@ -44,7 +44,7 @@ def _stale(target: str, deps) -> bool:
 
 
 def build_lib(force: bool = False, verbose: bool = False) -> str:
-    deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(CSRC, "rt_internal.h"),
+    deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(CSRC, "rt_internal.h"), os.path.join(CSRC, "rt_predicates.h"),
                                                        os.path.join(ROOT, "include", "rt_mi355x.h")]
     if not force and not _stale(LIB, deps):
         return LIB

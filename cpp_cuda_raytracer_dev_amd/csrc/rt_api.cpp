@@ -79,6 +79,16 @@ struct rt_camera {
     uint64_t order_gen = ~0ull;              // generation whose cost order d_order holds
     int rays = 16;                   // kOptRays: pixels per wave of kernel 3
     int items = 2;                   // kOptItems: items per lane per pool iteration
+    // shadow renders: the any-hit push order, fixed (kOptShadowOrder 0..3)
+    // or timed (-1): a round of trial frames runs each order kTuneReps times,
+    // interleaved, bracketed by events; the fastest is kept for kTunePeriod
+    // frames, then the next round starts (the view may have changed).
+    int shadow_order = -1;
+    int any_best = 1;
+    int tune_next = 0;               // next trial frame of the round; kTuneTrials = round queued
+    int tune_frames = 0;             // frames since the last round's result
+    bool tune_pending = false;
+    hipEvent_t tune_ev[2 * 12] = {};
 };
 
 namespace {
@@ -189,6 +199,8 @@ int ensure_order(rt_camera* c, const TraceParams& p) {
 }
 
 constexpr int kCostPeriod = 16;  // frames between cost samples (tile order 3)
+constexpr int kAnyOrders = 4, kTuneReps = 3, kTuneTrials = kAnyOrders * kTuneReps;
+constexpr int kTunePeriod = 2048;  // frames between timing rounds of the shadow push order
 
 // Buffers of tile order 3 for n fine tiles (allocated when the grid grows).
 int ensure_cost(rt_camera* c, int64_t n) {
@@ -737,6 +749,46 @@ extern "C" int rt_camera_add_object(rt_camera* c, rt_scene* s) {
     return prepare_camera_object(c);
 }
 
+// The any-hit push order of a shadow frame (TraceParams::any_order) and, on
+// a trial frame, its index in the round (else -1).  Never blocks: the round's
+// events are only queried, and nothing is timed while the stream is captured
+// or when counting (the counting walk does not stop at occluders).
+static int any_order_for(rt_camera* c, uint32_t flags, void* stream, int& trial) {
+    trial = -1;
+    if (!(flags & RT_FLAG_SHADOW)) return 0;
+    if (c->shadow_order >= 0) return c->shadow_order;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if ((flags & RT_FLAG_COUNT) ||
+        (hipStreamIsCapturing((hipStream_t)stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone))
+        return c->any_best;
+    if (c->tune_pending) {
+        if (hipEventQuery(c->tune_ev[2 * kTuneTrials - 1]) != hipSuccess) return c->any_best;
+        float best[kAnyOrders];
+        for (int o = 0; o < kAnyOrders; o++) best[o] = 1e30f;
+        for (int t = 0; t < kTuneTrials; t++) {
+            float ms = 0.0f;
+            if (hipEventElapsedTime(&ms, c->tune_ev[2 * t], c->tune_ev[2 * t + 1]) == hipSuccess)
+                best[t % kAnyOrders] = std::min(best[t % kAnyOrders], ms);
+        }
+        int b = 0;
+        for (int o = 1; o < kAnyOrders; o++)
+            if (best[o] < best[b]) b = o;
+        c->any_best = b;
+        c->tune_pending = false;
+        c->tune_frames = 0;
+        c->tune_next = kTuneTrials;
+        return c->any_best;
+    }
+    if (c->tune_next >= kTuneTrials) {
+        if (++c->tune_frames < kTunePeriod) return c->any_best;
+        c->tune_next = 0;
+    }
+    for (int k = 0; k < 2 * kTuneTrials; k++)
+        if (!c->tune_ev[k] && hipEventCreate(&c->tune_ev[k]) != hipSuccess) return c->any_best;
+    trial = c->tune_next++;
+    return trial % kAnyOrders;
+}
+
 // The trace launches of one frame: the coarse kernel, then the fine one, on
 // the caller's stream.  Debug bit 8 instead runs the coarse kernel on the
 // camera's side stream beside the fine one (forked after the caller's
@@ -787,7 +839,15 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
     }
     TraceParams p;
     if ((rc = fill_params(c, xform, tile, argb, hit, mode, p))) return rc;
+    int trial;
+    p.any_order = any_order_for(c, flags, stream, trial) | ((c->debug & 16) ? 4 : 0);
+    hipStream_t st = (hipStream_t)stream;
+    if (trial >= 0 && (rc = hip_check(hipEventRecord(c->tune_ev[2 * trial], st), "order trial start"))) return rc;
     if ((rc = launch_split(c, p, mode, flags, stream))) return rc;
+    if (trial >= 0) {
+        if ((rc = hip_check(hipEventRecord(c->tune_ev[2 * trial + 1], st), "order trial stop"))) return rc;
+        c->tune_pending = c->tune_next == kTuneTrials;
+    }
     return p.cost ? cost_feedback(c, p, stream) : RT_OK;
 }
 
@@ -901,6 +961,8 @@ extern "C" void rt_camera_destroy(rt_camera* c) {
     if (c->h_cost) (void)hipHostFree(c->h_cost);
     if (c->h_order) (void)hipHostFree(c->h_order);
     if (c->cost_ev) (void)hipEventDestroy(c->cost_ev);
+    for (hipEvent_t e : c->tune_ev)
+        if (e) (void)hipEventDestroy(e);
     if (c->order_ev) (void)hipEventDestroy(c->order_ev);
     if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
     if (c->join_ev) (void)hipEventDestroy(c->join_ev);
@@ -937,12 +999,32 @@ extern "C" int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value) {
     case kOptDebug:
         c->debug = value;
         return RT_OK;
+    case kOptShadowOrder:
+        if (value < -1 || value > 3) return fail(RT_ERR_INVALID, "shadow push order %d (-1 timed, 0..3)", value);
+        c->shadow_order = value;
+        c->tune_next = 0;
+        c->tune_frames = 0;
+        c->tune_pending = false;
+        return RT_OK;
     case kOptTileOrder:
         if (value < 0 || value > 4) return fail(RT_ERR_INVALID, "tile order %d (0..4)", value);
         c->tile_order = value;
         return RT_OK;
     default:
         return fail(RT_ERR_INVALID, "rt_camera_set_option: unknown key %d", key);
+    }
+}
+
+extern "C" int rt_camera_get_option(const rt_camera* c, int32_t key, int32_t* value) {
+    if (!c || !value) return fail(RT_ERR_INVALID, "rt_camera_get_option: null argument");
+    switch (key) {
+    case kOptKernel: *value = c->kernel_version; return RT_OK;
+    case kOptTileOrder: *value = c->tile_order; return RT_OK;
+    case kOptRays: *value = c->rays; return RT_OK;
+    case kOptItems: *value = c->items; return RT_OK;
+    case kOptCoarse: *value = c->coarse; return RT_OK;
+    case kOptShadowOrder: *value = c->shadow_order >= 0 ? c->shadow_order : c->any_best; return RT_OK;
+    default: return fail(RT_ERR_INVALID, "rt_camera_get_option: unknown key %d", key);
     }
 }
 

@@ -44,8 +44,10 @@ enum Option : int32_t {
     kOptRays = 3,       // kernel 3 pixels per wave: 64, 32, 16 or 8
     kOptItems = 4,      // kernel 3 items popped per lane per iteration: 1 or 2
     kOptCoarse = 5,     // kernel 3 coarse groups per wave outside the root box's rectangle (0 = off)
+    kOptShadowOrder = 6,  // kernel 3 any-hit push order 0..3, -1 = timed choice (default)
     kOptDebug = 100,    // diagnostics: 1 = skip traversal, 2 = per-wave timestamps, 4 = every group
-                        // coarse, 8 = coarse kernel on a side stream beside the fine one
+                        // coarse, 8 = coarse kernel on a side stream beside the fine one,
+                        // 16 = counted shadow walks stop at occluders (the timed walk's work)
     kOptPoolCap = 101,  // tests: shrink kernel 3's item pool (66..kPoolCap) to force its fallback
 };
 constexpr int kPoolCapMax = 640;
@@ -102,6 +104,7 @@ struct TraceParams {
     int32_t cg_x0, cg_x1;          // fine region in 8-px groups [x0, x1)
     int32_t cs0, cs1;              // fine region in slots [s0, s1)
     int32_t coarse_per_wave;       // coarse groups per wave
+    int32_t any_order;             // push order of any-hit (shadow) walks 0..3, +4: counted walks stop at occluders
     int32_t coarse_blocks;         // blocks of k_coarse_kd3
     int32_t fill_blocks;           // blocks after the fine grid filling far groups (fused mode)
     int64_t coarse_groups;         // total coarse groups

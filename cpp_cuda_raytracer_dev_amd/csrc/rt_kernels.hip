@@ -866,13 +866,37 @@ __device__ __forceinline__ void record_candidate(unsigned long long* s_key, uint
 }
 
 // Pushes one visited item's children (ballot compaction) at items[at...];
-// returns how many the wave pushed.
+// returns how many the wave pushed.  The order decides which items the next
+// pops take when the pool holds more than one pop.  Nearest-hit walks visit
+// every intersected node whatever the order; they push all lanes' first
+// children, then all second ones (0.084 ms at 1080p vs 0.092 for per-lane
+// pairs).  Any-hit (shadow) walks stop at the first occluder, and which order
+// reaches it soonest depends on the scene and resolution, so
+// it is a template choice of the launch (the host times the four and keeps
+// the fastest): 0 as nearest-hit, 1 per-lane pairs (first, second), 2 all
+// second children then all first ones (first children on top), 3 per-lane
+// pairs (second, first).  A runtime order costs scratch spills (measured).
+template <bool kAny, int any_order>
 __device__ __forceinline__ int push_children(uint4* items, int at, const Visit& v) {
     const unsigned long long m1 = __ballot(v.ka), m2 = __ballot(v.kb);
-    const int n1 = __builtin_popcountll(m1);
-    if (v.ka) items[at + (int)lanes_below(m1)] = v.ca;
-    if (v.kb) items[at + n1 + (int)lanes_below(m2)] = v.cb;
-    return n1 + __builtin_popcountll(m2);
+    const int n1 = __builtin_popcountll(m1), n2 = __builtin_popcountll(m2);
+    if (kAny && (any_order & 1)) {   // per-lane pairs
+        const int off = (int)(lanes_below(m1) + lanes_below(m2));
+        if (any_order == 1) {
+            if (v.ka) items[at + off] = v.ca;
+            if (v.kb) items[at + off + (v.ka ? 1 : 0)] = v.cb;
+        } else {
+            if (v.kb) items[at + off] = v.cb;
+            if (v.ka) items[at + off + (v.kb ? 1 : 0)] = v.ca;
+        }
+    } else if (kAny && any_order == 2) {
+        if (v.kb) items[at + (int)lanes_below(m2)] = v.cb;
+        if (v.ka) items[at + n2 + (int)lanes_below(m1)] = v.ca;
+    } else {
+        if (v.ka) items[at + (int)lanes_below(m1)] = v.ca;
+        if (v.kb) items[at + n1 + (int)lanes_below(m2)] = v.cb;
+    }
+    return n1 + n2;
 }
 
 // The pool walk of one wave.  kAny = false: nearest hit per ray, key[ray] =
@@ -881,7 +905,7 @@ __device__ __forceinline__ int push_children(uint4* items, int at, const Visit& 
 // key[ray] = 0; without counters the items of such rays are dropped.
 // Each lane pops up to P.items (1 or 2) items per iteration and fetches their
 // records together, so a lane keeps two memory round trips in flight.
-template <int kCap, int kVec, bool kTranslated, bool kCount, bool kAny>
+template <int kCap, int kVec, bool kTranslated, bool kCount, bool kAny, int kOrder = 0>
 __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, const float4* s_ray,
                                           unsigned long long* s_key, uint32_t* s_tri, int n, int lane,
                                           uint32_t& iters, uint32_t& popped, uint32_t& n_int, uint32_t& n_leaf,
@@ -911,8 +935,9 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
         const uint4 it1 = kTwo ? items[base + (act1 ? lane + 64 : 0)] : it0;
         __builtin_amdgcn_wave_barrier();
         // any-hit: a ray already shadowed needs no more visits (kept when
-        // counting, so the counters match the oracle's full walk)
-        if (kAny && !kCount) {
+        // counting, so the counters match the oracle's full walk, unless
+        // kOrder >= 4: counters of the walk a timed frame does)
+        if (kAny && (!kCount || kOrder >= 4)) {
             if (act0 && s_key[it0.w >> 26] == 0ull) act0 = false;
             if (act1 && s_key[it1.w >> 26] == 0ull) act1 = false;
         }
@@ -937,7 +962,7 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
                 visit_item<kVec, kTranslated, kCount, kAny>(s_ray + (size_t)(it0.w >> 26) * kVec, it0, a0, a1, a2, a3,
                                                             v0, n_int, n_leaf, n_acc, n_desc);
             record_candidate<kAny>(s_key, s_tri, it0, v0);
-            total += push_children(items, base + total, v0);
+            total += push_children<kAny, (kOrder & 3)>(items, base + total, v0);
         }
         {
             Visit v1;
@@ -946,7 +971,7 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
                 visit_item<kVec, kTranslated, kCount, kAny>(s_ray + (size_t)(it1.w >> 26) * kVec, it1, b0, b1, b2, b3,
                                                             v1, n_int, n_leaf, n_acc, n_desc);
             record_candidate<kAny>(s_key, s_tri, it1, v1);
-            total += push_children(items, base + total, v1);
+            total += push_children<kAny, (kOrder & 3)>(items, base + total, v1);
         }
         if (base + total > cap) {  // unreachable by the pop rule above; guard anyway
             if (lane == 0) atomicOr(P.err, 2);
@@ -998,7 +1023,7 @@ struct Counts {
 // One wave's unit of work: the kRays pixels (8 x kRays/8) of unit U.
 constexpr size_t kNoDbg = ~(size_t)0;
 constexpr int kCoarseMax = 32;  // coarse groups per wave (RT_OPT_COARSE <= 32)
-template <int kRays, int kCap, int kRayVec, bool kTranslated, bool kWriteHit, bool kCount, bool kShadow>
+template <int kRays, int kCap, int kRayVec, bool kTranslated, bool kWriteHit, bool kCount, int kShadow>
 __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, kCap, kRayVec>& S_, const Unit& U,
                                            int lane, size_t dbg_slot, uint32_t* cost, Counts& C) {
     uint4* items = S_.items;
@@ -1027,7 +1052,7 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
         best = kbest == ~0ull ? kMiss : S_.tri[lane];
     }
     bool shadowed = false;
-    if (kShadow) {
+    if constexpr (kShadow > 0) {
         // the shadow segment of each hit: from the light to H = d*r - od
         const bool sh_live = live && best != kMiss;
         Ray Sh;
@@ -1050,7 +1075,7 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
         }
         __builtin_amdgcn_wave_barrier();
         n = seed_root<kCount>(P, items, Sh, sh_live, lane, C.n_int, C.n_desc);
-        pool_walk<kCap, kRayVec, true, kCount, true>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters, popped, C.n_int,
+        pool_walk<kCap, kRayVec, true, kCount, true, kShadow - 1>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters, popped, C.n_int,
                                                     C.n_leaf, C.n_acc, C.n_desc);
         if (lane < kRays) shadowed = S_.key[lane] == 0ull;
     }
@@ -1209,7 +1234,7 @@ __device__ __forceinline__ unsigned long long coarse_root(const TraceParams& P, 
 #else
 #define RT_KD3_BOUNDS(threads) __launch_bounds__(threads)
 #endif
-template <int kRays, bool kTranslated, bool kWriteHit, bool kCount, bool kShadow>
+template <int kRays, bool kTranslated, bool kWriteHit, bool kCount, int kShadow>
 __global__ RT_KD3_BOUNDS(64 * kd3_waves(kRays)) void k_trace_kd3(TraceParams P) {
     constexpr int kWaves = kd3_waves(kRays);
     constexpr int kCap = pool_cap_for<kRays>();
@@ -1242,7 +1267,7 @@ __global__ RT_KD3_BOUNDS(64 * kd3_waves(kRays)) void k_trace_kd3(TraceParams P) 
 // The coarse groups (every 8x8 group of this rank outside the fine tiles),
 // P.coarse_per_wave (<= kCoarseMax) per wave.  A separate kernel: looping trace_unit inside
 // the fine kernel costs it a third of its occupancy (80 -> 113 VGPRs).
-template <int kRays, bool kTranslated, bool kWriteHit, bool kCount, bool kShadow>
+template <int kRays, bool kTranslated, bool kWriteHit, bool kCount, int kShadow>
 __global__ __launch_bounds__(128) void k_coarse_kd3(TraceParams P) {
     constexpr int kWaves = 2;
     constexpr int kCap = pool_cap_for<kRays>();
@@ -1484,7 +1509,7 @@ int launch_cam_nodes(const rt_kd_node* nodes, const int32_t* ids, const uint32_t
 
 using TraceFn = void (*)(TraceParams);
 
-template <bool T, bool H, bool C, bool S>
+template <bool T, bool H, bool C, int S>
 TraceFn kd3_kernel(int rays, bool coarse) {
     if (coarse) {
         if (rays == 8) return k_coarse_kd3<8, T, H, C, S>;
@@ -1498,11 +1523,32 @@ TraceFn kd3_kernel(int rays, bool coarse) {
     return k_trace_kd3<64, T, H, C, S>;
 }
 
+// shadow: -1 none, else the any-hit push order (0..3), + 4 for counting
+// walks that stop at occluders like a timed frame's (bench.py's roofline).
+// Other counting walks are not cut short, so the order does not change their
+// work: one instance serves them.
 template <bool T, bool H, bool C>
-TraceFn kd_kernel(int version, int rays, bool shadow, bool coarse) {
+TraceFn kd_kernel(int version, int rays, int shadow, bool coarse) {
     if (version == 1) return k_trace_kd<T, H, C>;
     if (version == 2) return k_trace_kd2<T, H, C>;
-    return shadow ? kd3_kernel<T, H, C, true>(rays, coarse) : kd3_kernel<T, H, C, false>(rays, coarse);
+    if (shadow < 0) return kd3_kernel<T, H, C, 0>(rays, coarse);
+    if constexpr (C) {
+        switch (shadow) {
+        case 4: return kd3_kernel<T, H, C, 5>(rays, coarse);
+        case 5: return kd3_kernel<T, H, C, 6>(rays, coarse);
+        case 6: return kd3_kernel<T, H, C, 7>(rays, coarse);
+        case 7: return kd3_kernel<T, H, C, 8>(rays, coarse);
+        default: return kd3_kernel<T, H, C, 1>(rays, coarse);
+        }
+    } else {
+        shadow &= 3;
+        switch (shadow) {
+        case 0: return kd3_kernel<T, H, C, 1>(rays, coarse);
+        case 1: return kd3_kernel<T, H, C, 2>(rays, coarse);
+        case 2: return kd3_kernel<T, H, C, 3>(rays, coarse);
+        default: return kd3_kernel<T, H, C, 4>(rays, coarse);
+        }
+    }
 }
 
 int launch_trace(const TraceParams& p, uint32_t mode, uint32_t flags, int kernel_version, void* stream, int part) {
@@ -1520,7 +1566,7 @@ int launch_trace(const TraceParams& p, uint32_t mode, uint32_t flags, int kernel
     }
     const bool tr = p.xf[3] != 0.0f || p.xf[7] != 0.0f || p.xf[11] != 0.0f;
     const int v = kernel_version, r = p.rays;
-    const bool sh = (flags & RT_FLAG_SHADOW) != 0;  // kernel 3 only (checked by the caller)
+    const int sh = (flags & RT_FLAG_SHADOW) ? p.any_order : -1;  // kernel 3 only (checked by the caller)
     for (int pass = 0; pass < 2; pass++) {
         // the coarse groups first, then the fine tiles (or just one of them)
         const bool coarse = pass == 0;

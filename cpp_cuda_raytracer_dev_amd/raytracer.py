@@ -6,8 +6,10 @@ Same names, argument meaning and error behaviour as the reference classes
 * ``read_ply``           TD/read_ply.cpp:13        -> rt_read_ply
 * ``Trixel``             TD/Trixel.h:39-478        -> rt_scene_* / rt_kd_build
 * ``Camera``             TD/Camera.h:15-97         -> rt_camera_*
-* ``Object``             TD/Object.h:10-19         -> Trixel + Quaternion
+* ``Object``             TD/Object.h:10-19         -> Trixel + Quaternion + motion
 * ``Quaternion``         TD/Quaternion.h:5-24      (rot_m only; identity)
+* ``Input``              TD/Input.h:3-15           (t_vec of a transform)
+* ``ObjectMotion``       TD/Camera.cu:254-335      -> rt_object_* (keyboard transforms)
 
 The frame semantics are the steady state of the reference's loop
 (TD/WinMain.cpp:212-237): ``Object.render`` runs the fused bg-fill ->
@@ -28,6 +30,11 @@ SET_COLOR_TAG = 1      # TD/Camera.h:13
 PHONG_COLOR_TAG = 2    # TD/Camera.h:14
 TRIXEL_OBJECT_TAG = 0  # TD/Object.h:3
 BACKGROUND_ARGB = 0x00F08200  # TD/Camera.cpp:72
+TRANSLATE_XYZ, TRANSLATE_X, TRANSLATE_Z = 30, 31, 32  # TD/platform_common.h:15-17
+ROTATE_TRI_PY, ROTATE_TRI_NY = 10, 11                 # TD/platform_common.h:19-20
+#: Held-key bits of ObjectMotion.tick / Object.key_tick (TD/WinMain.cpp:186-209).
+KEY_R, KEY_W, KEY_S, KEY_Q, KEY_E, KEY_T = 1, 2, 4, 8, 16, 32
+CAM_SPEED = np.float32(.005)  # TD/WinMain.cpp:170
 
 #: Material of every triangle in the reference demo (TD/WinMain.cpp:117-121).
 DEFAULT_RAD = (np.float32(0.1), np.float32(0.55), np.float32(0.2))
@@ -102,6 +109,62 @@ class Quaternion:
         return np.ascontiguousarray(self.rot_m, np.float32).reshape(12)
 
 
+class Input:
+    """TD/Input.h:3-15 without the Win32 buttons: ``set_quat`` stores the four
+    floats as the transform vector (TD/Input.cpp:16-19)."""
+
+    def __init__(self):
+        self.t_vec = np.zeros(4, np.float32)
+
+    def set_vec(self, x, y, z, w):
+        self.t_vec = np.array([x, y, z, w], np.float32)
+
+    def set_quat(self, x, y, z, w):
+        self.set_vec(x, y, z, w)
+
+
+class ObjectMotion:
+    """An object's motion state (quaternion, host and device rot_m,
+    init_face / cur_face) as Camera::add_object sets it up
+    (TD/Camera.cpp:131-134) and Object::transform updates it
+    (TD/Camera.cu:254-335).  ``xform()`` is the device rot_m the kernel reads."""
+
+    def __init__(self, cam_pos, cam_n, cam_u, cam_speed=CAM_SPEED):
+        # keep the arrays alive across the call (ptr() holds only the address)
+        p, n, u = (np.array(v, np.float32).reshape(3) for v in (cam_pos, cam_n, cam_u))
+        h = C.c_void_p()
+        _lib.call("rt_object_create", _lib.ptr(p), _lib.ptr(n), _lib.ptr(u), np.float32(cam_speed), C.byref(h))
+        self._h = h
+
+    def transform(self, t_vec, transform_select: int) -> None:
+        t = np.ascontiguousarray(t_vec, np.float32).reshape(4)
+        _lib.call("rt_object_transform", self._h, _lib.ptr(t), int(transform_select))
+
+    def tick(self, held_keys: int) -> None:
+        _lib.call("rt_object_tick", self._h, int(held_keys))
+
+    def xform(self) -> np.ndarray:
+        out = np.zeros(12, np.float32)
+        _lib.call("rt_object_xform", self._h, _lib.ptr(out))
+        return out
+
+    def state(self) -> dict:
+        q, r, i, c = (np.zeros(n, np.float32) for n in (4, 12, 4, 4))
+        _lib.call("rt_object_state", self._h, _lib.ptr(q), _lib.ptr(r), _lib.ptr(i), _lib.ptr(c))
+        return {"quat": q, "rot_m": r, "init_face": i, "cur_face": c}
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            _lib.lib().rt_object_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Trixel:
     """Triangles (+ KD tree) resident on one device (TD/Trixel.h:39-478)."""
 
@@ -171,6 +234,7 @@ class Object:
         self.object_tag = TRIXEL_OBJECT_TAG
         self.trixel_list = x
         self.quat = q if q is not None else Quaternion()
+        self.motion = None  # set by Camera.add_object
 
     def getTag(self) -> int:  # noqa: N802 (reference name)
         return self.object_tag
@@ -178,6 +242,26 @@ class Object:
     def render(self, c: "Camera", mode: int = RT_MODE_KD, flags: int = 0, stream=None) -> int:
         """Object::render (TD/Object.cpp:10-12)."""
         return self.trixel_list.intersect_trixels(c, self.quat, mode, flags, stream)
+
+    def _moved(self) -> int:
+        if self.motion is None:
+            raise _lib.RtError("Object.transform", -5, "add the object to a camera first")
+        self.quat.rot_m = self.motion.xform().reshape(3, 4)
+        return 0
+
+    def transform(self, dq: Input, transform_select: int) -> int:
+        """Object::transform (TD/Object.cpp:14-17); needs Camera.add_object first."""
+        if self.motion is None:
+            return self._moved()
+        self.motion.transform(dq.t_vec, transform_select)
+        return self._moved()
+
+    def key_tick(self, held_keys: int) -> int:
+        """One input tick of TD/WinMain.cpp:186-209 with KEY_* bits held."""
+        if self.motion is None:
+            return self._moved()
+        self.motion.tick(held_keys)
+        return self._moved()
 
 
 class Camera:
@@ -192,6 +276,7 @@ class Camera:
         self.device = device
         self.o_prop = camera_basis(r_w, r_h, f_w, f_h, fclen, self.pos, self.la, self.up)
         self.background_color = BACKGROUND_ARGB
+        self.cam_speed = CAM_SPEED
         self.object_list = []
         h = C.c_void_p()
         _lib.call("rt_camera_create", device, int(r_w), int(r_h), np.float32(f_w), np.float32(f_h),
@@ -211,6 +296,9 @@ class Camera:
         if new_object.getTag() != TRIXEL_OBJECT_TAG:
             return 0
         self.object_list.append(new_object)
+        # the object's transform state starts from the camera's (TD/Camera.cpp:131-134)
+        new_object.quat = Quaternion()
+        new_object.motion = ObjectMotion(self.pos, self.o_prop["n"], self.o_prop["u"], self.cam_speed)
         _lib.call("rt_camera_add_object", self._h, new_object.trixel_list._h)
         return 0
 
@@ -243,6 +331,11 @@ class Camera:
     def set_option(self, key: int, value: int) -> None:
         """Tuning knobs (_lib.RT_OPT_KERNEL, _lib.RT_OPT_TILE_ORDER); frames are identical."""
         _lib.call("rt_camera_set_option", self._h, key, value)
+
+    def get_option(self, key: int) -> int:
+        v = C.c_int32()
+        _lib.call("rt_camera_get_option", self._h, key, C.byref(v))
+        return v.value
 
     def counters(self, reset: bool = True) -> np.ndarray:
         out = np.zeros(5, np.uint64)

@@ -5,15 +5,17 @@
 //   read_ply            TD/read_ply.cpp:13        -> rt_read_ply
 //   Trixel              TD/Trixel.h:39-478        -> rt_scene_*, rt_kd_build
 //   Camera              TD/Camera.h:15-97         -> rt_camera_*
-//   Object              TD/Object.h:10-19
+//   Object              TD/Object.h:10-19         -> rt_object_* (motion)
 //   Quaternion          TD/Quaternion.h:5-24      (the rot_m the kernel reads)
+//   Input               TD/Input.h:3-15           (t_vec of a transform)
 //   Color               TD/Color.h:4-14
 //
 // The frame is the steady state of the reference's loop (TD/WinMain.cpp:
 // 212-237): Object::render runs the fused bg-fill -> intersect -> Phong
 // kernel; Camera::color_pixels copies it to h_mem.h_color.c (the D2H of
-// TD/Camera.cu:84).  Win32, keyboard input and quaternion animation are out of
-// scope; Object::set_transform takes a ready rot_m instead.
+// TD/Camera.cu:84).  Win32 is out of scope: the keyboard
+// loop's transforms are Object::transform / Object::key_tick (rt_object_*),
+// and Object::set_transform takes a ready rot_m.
 #pragma once
 
 #include <stdint.h>
@@ -36,6 +38,11 @@ typedef uint32_t u32;
 constexpr u8 SET_COLOR_TAG = 1;     // TD/Camera.h:13
 constexpr u8 PHONG_COLOR_TAG = 2;   // TD/Camera.h:14
 constexpr u8 TRIXEL_OBJECT_TAG = 0; // TD/Object.h:3
+constexpr u8 TRANSLATE_XYZ = RT_TRANSLATE_XYZ;  // TD/platform_common.h:15-20
+constexpr u8 TRANSLATE_X = RT_TRANSLATE_X;
+constexpr u8 TRANSLATE_Z = RT_TRANSLATE_Z;
+constexpr u8 ROTATE_TRI_PY = RT_ROTATE_PY;
+constexpr u8 ROTATE_TRI_NY = RT_ROTATE_NY;
 constexpr u32 RENDER_MODE_KD = RT_MODE_KD;
 constexpr u32 RENDER_MODE_FLAT = RT_MODE_FLAT;
 
@@ -64,6 +71,15 @@ public:
 class Quaternion {
 public:
     T_fp rot_m[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+};
+
+// TD/Input.h:3-15 without the Win32 buttons: set_quat stores the four floats
+// as the transform vector t_vec (TD/Input.cpp:16-19).
+class Input {
+public:
+    T_fp t_vec[4] = {0, 0, 0, 0};
+    void set_vec(T_fp x, T_fp y, T_fp z, T_fp w) { t_vec[0] = x; t_vec[1] = y; t_vec[2] = z; t_vec[3] = w; }
+    void set_quat(T_fp x, T_fp y, T_fp z, T_fp w) { set_vec(x, y, z, w); }
 };
 
 class Camera;
@@ -126,14 +142,37 @@ public:
 
     explicit Object(Trixel* x) : trixel_list(x), quat(&own_) {}
     Object(Trixel* x, Quaternion* q) : trixel_list(x), quat(&own_), own_(*q) {}
+    ~Object() { rt_object_destroy(motion_); }
+    Object(const Object&) = delete;
+    Object& operator=(const Object&) = delete;
     u8 getTag() const { return trixel_list->object_tag; }
     // Object::render (TD/Object.cpp:10-12)
     int render(Camera* c, u32 mode = RENDER_MODE_KD) { return trixel_list->intersect_trixels(c, quat, mode); }
-    // replaces Object::transform's keyboard-driven update with a ready matrix
+    // Object::transform (TD/Object.cpp:14-17): needs Camera::add_object first
+    int transform(Input* dq, u8 transform_select) {
+        if (!motion_) return RT_ERR_STATE;
+        int rc = rt_object_transform(motion_, dq->t_vec, transform_select);
+        return rc ? rc : rt_object_xform(motion_, own_.rot_m);
+    }
+    // one tick of TD/WinMain.cpp:186-209 with RT_KEY_* held
+    int key_tick(uint32_t held_keys) {
+        if (!motion_) return RT_ERR_STATE;
+        int rc = rt_object_tick(motion_, held_keys);
+        return rc ? rc : rt_object_xform(motion_, own_.rot_m);
+    }
+    // replaces the transform state with a ready matrix
     void set_transform(const T_fp rot_m[12]) { memcpy(own_.rot_m, rot_m, sizeof own_.rot_m); }
+    // Camera::add_object's init_face / cur_face / quat copy (TD/Camera.cpp:131-134)
+    int attach_motion(const float pos[3], const float n[3], const float u[3], T_fp cam_speed) {
+        rt_object_destroy(motion_);
+        motion_ = nullptr;
+        int rc = rt_object_create(pos, n, u, cam_speed, &motion_);
+        return rc ? rc : rt_object_xform(motion_, own_.rot_m);
+    }
 
 private:
     Quaternion own_;
+    rt_object* motion_ = nullptr;
 };
 
 class Camera {
@@ -155,6 +194,13 @@ public:
         f_prop.res.count = (uint64_t)r_w * (uint64_t)r_h;
         const float pos[3] = {p_x, p_y, p_z}, la[3] = {la_x, la_y, la_z}, up[3] = {up_x, up_y, up_z};
         status = rt_camera_create(dev, r_w, r_h, f_w, f_h, fclen, pos, la, up, &cam_);
+        memcpy(pos_, pos, sizeof pos_);
+        rt_camera_basis_t b;
+        if (status == RT_OK) status = rt_camera_basis(r_w, r_h, f_w, f_h, fclen, pos, la, up, &b);
+        if (status == RT_OK) {
+            memcpy(n_, b.n, sizeof n_);
+            memcpy(u_, b.u, sizeof u_);
+        }
         color_.assign(f_prop.res.count, 0u);
         rmi_.assign(f_prop.res.count, -1);
         h_mem.h_color.c = color_.data();
@@ -168,7 +214,8 @@ public:
     int add_object(Object* new_object) {
         if (new_object->getTag() != TRIXEL_OBJECT_TAG) return 0;
         objects_.push_back(new_object);
-        return rt_camera_add_object(cam_, new_object->trixel_list->handle());
+        int rc = new_object->attach_motion(pos_, n_, u_, cam_speed);
+        return rc ? rc : rt_camera_add_object(cam_, new_object->trixel_list->handle());
     }
 
     // Camera::color_pixels (TD/Camera.cpp:229): the frame to h_mem.h_color.c
@@ -183,9 +230,11 @@ public:
     }
     void keep_hit_buffer(bool on) { write_hit_ = on; }
     rt_camera* handle() const { return cam_; }
+    T_fp cam_speed = .005f;  // TD/WinMain.cpp:170
 
 private:
     rt_camera* cam_ = nullptr;
+    float pos_[3] = {0, 0, 0}, n_[3] = {0, 0, 1}, u_[3] = {1, 0, 0};
     std::vector<u32> color_;
     std::vector<s64> rmi_;
     std::vector<Object*> objects_;

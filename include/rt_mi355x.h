@@ -200,14 +200,57 @@ int rt_camera_info(const rt_camera* c, int32_t* w, int32_t* h, int32_t* max_dept
 #define RT_OPT_RAYS 3 /* kernel 3: pixels per wave (64, 32, 16 default, 8); the rest of the lanes help */
 #define RT_OPT_ITEMS 4 /* kernel 3: items each lane pops per iteration (1, 2 default) */
 #define RT_OPT_COARSE 5 /* kernel 3: 8x8 groups per wave outside the root box's screen rectangle (0..32, 8 default, 0 = off) */
+/* kernel 3, shadow rays: the order the any-hit walk pushes children in (0..3;
+ * -1 = timed, default: every 2048 shadow frames each order runs 3 frames
+ * bracketed by events and the fastest is kept; never blocks, skipped under
+ * stream capture).  Get returns the order in use. */
+#define RT_OPT_SHADOW_ORDER 6
 int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value);
+int rt_camera_get_option(const rt_camera* c, int32_t key, int32_t* value);
 
 /* Diagnostics (key 100 of rt_camera_set_option: 1 = skip traversal,
- * 2 = per-wave (start clock, end clock, max visits) records): copies up to
+ * 2 = per-wave (start clock, end clock, max visits) records, 16 = counted
+ * shadow walks stop at occluders like timed ones): copies up to
  * n u64 of the record buffer; returns the count or a negative status. */
 #define RT_OPT_DEBUG 100
 #define RT_OPT_POOL_CAP 101 /* tests: shrink the wave-cooperative kernel's item pool (86..640) */
 int64_t rt_camera_debug_read(rt_camera* c, uint64_t* out, int64_t n);
+
+/* Object motion: the reference's keyboard transform
+ * path, driven headlessly.  An rt_object is Object's motion state (its
+ * Quaternion, host rot_m, device d_rot_m, init_face/cur_face; TD/Object.h,
+ * TD/Camera.cpp:131-134).  rt_object_transform replaces Object::transform ->
+ * transform_camera_voxel_device_memory (TD/Object.cpp:14-17,
+ * TD/Camera.cu:254-335) with the reference's selector values
+ * (TD/platform_common.h:15-20); an unknown selector is RT_ERR_INVALID (the
+ * reference ignores it).  rt_object_tick applies one input tick's held keys
+ * in the order of TD/WinMain.cpp:186-209 (R, W, S, Q, E, T).
+ * rt_object_xform gives the device rot_m rows that rt_render's xform takes
+ * (what intersect_voxel_cuda reads, TD/Trixel.cu:60-66). */
+typedef struct rt_object rt_object;
+#define RT_TRANSLATE_XYZ 30
+#define RT_TRANSLATE_X 31
+#define RT_TRANSLATE_Z 32
+#define RT_ROTATE_PY 10
+#define RT_ROTATE_NY 11
+#define RT_KEY_R 1u   /* rotate +y: t_vec (0, 0.0995, 0, 0.995)  */
+#define RT_KEY_W 2u   /* forward:   (n, +speed), TRANSLATE_Z      */
+#define RT_KEY_S 4u   /* back:      (n, -speed)                   */
+#define RT_KEY_Q 8u   /* strafe:    (u, +speed), TRANSLATE_X      */
+#define RT_KEY_E 16u  /* strafe:    (u, -speed)                   */
+#define RT_KEY_T 32u  /* rotate -y: (0, -0.0995, 0, 0.995)        */
+#define RT_KEYS_ALL 63u
+/* cam_pos, cam_n, cam_u: the camera's o_prop.pos/n/u (rt_camera_basis);
+ * cam_speed: 0.005 in the reference (TD/WinMain.cpp:170). */
+int rt_object_create(const float cam_pos[3], const float cam_n[3], const float cam_u[3], float cam_speed,
+                     rt_object** out);
+int rt_object_transform(rt_object* o, const float t_vec[4], int32_t select);
+int rt_object_tick(rt_object* o, uint32_t held_keys);
+int rt_object_xform(const rt_object* o, float xform[12]);
+/* Host-side state for tests (any pointer may be NULL): quaternion (i j k w),
+ * host rot_m rows, init_face, cur_face. */
+int rt_object_state(const rt_object* o, float quat[4], float host_rot[12], float init_face[4], float cur_face[4]);
+void rt_object_destroy(rt_object* o);
 
 void rt_scene_destroy(rt_scene* s);
 void rt_camera_destroy(rt_camera* c);

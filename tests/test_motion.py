@@ -1,0 +1,116 @@
+"""Object motion, CPU only: the product's rt_object_*
+(csrc/motion.cpp) against oracle/motion.py, bit for bit, over key sequences
+of the reference's input loop (TD/WinMain.cpp:186-209).  Parity unpinned:
+no recorded reference motion exists."""
+import numpy as np
+import pytest
+
+from cpp_cuda_raytracer_dev_amd import _lib, raytracer as R
+from oracle import motion as M
+
+
+def _cam(w=160, h=120):
+    c = R.camera_basis(w, h, R.film_w(w, h), np.float32(.024), np.float32(.055), (0.0, 0.1, -1.0),
+                       (0.0, 0.1, 0.0), (0.0, 1.0, 0.0))
+    return np.array([0.0, 0.1, -1.0], np.float32), c["n"], c["u"]
+
+
+def _bits(a):
+    return np.asarray(a, np.float32).view(np.uint32)
+
+
+def _same(prod: R.ObjectMotion, ref: M.Motion):
+    st = prod.state()
+    assert (_bits(prod.xform()) == _bits(ref.xform())).all()
+    assert (_bits(st["rot_m"]) == _bits(ref.host_rot())).all()
+    assert (_bits(st["quat"]) == _bits(ref.q.as_list())).all()
+    assert (_bits(st["init_face"]) == _bits(ref.init_face.as_list())).all()
+    assert (_bits(st["cur_face"]) == _bits(ref.cur_face.as_list())).all()
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_random_key_ticks_match_oracle(seed):
+    pos, n, u = _cam()
+    prod, ref = R.ObjectMotion(pos, n, u), M.Motion(pos, n, u)
+    rng = np.random.default_rng(seed)
+    # mostly single keys, sometimes chords (the loop applies every held key)
+    for _ in range(300):
+        keys = int(rng.choice([1, 2, 4, 8, 16, 32])) if rng.random() < 0.7 else int(rng.integers(0, 64))
+        prod.tick(keys)
+        ref.tick(keys)
+        _same(prod, ref)
+
+
+def test_transform_selectors_and_vectors():
+    """Object::transform with arbitrary t_vec for every selector."""
+    pos, n, u = _cam()
+    prod, ref = R.ObjectMotion(pos, n, u, 0.02), M.Motion(pos, n, u, 0.02)
+    rng = np.random.default_rng(7)
+    for k in range(200):
+        sel = [M.TRANSLATE_XYZ, M.TRANSLATE_X, M.TRANSLATE_Z, M.ROTATE_TRI_PY, M.ROTATE_TRI_NY][k % 5]
+        if sel in (M.ROTATE_TRI_PY, M.ROTATE_TRI_NY):
+            axis = rng.normal(size=3)
+            axis /= np.linalg.norm(axis)
+            half = rng.uniform(-0.2, 0.2)
+            t = np.array([*(axis * np.sin(half)), np.cos(half)], np.float32)
+        else:
+            t = np.array([*rng.normal(size=3), rng.uniform(-0.05, 0.05)], np.float32)
+        prod.transform(t, sel)
+        ref.transform(t, sel)
+        _same(prod, ref)
+
+
+def test_device_column_drifts_from_host():
+    """The device translation column is fma-contracted, the host's is not:
+    after enough translates they differ, and a rotate copies host to device."""
+    pos, n, u = _cam()
+    ref = M.Motion(pos, n, u)
+    prod = R.ObjectMotion(pos, n, u)
+    differ = False
+    rng = np.random.default_rng(0)
+    for k in range(200):
+        keys = int(rng.choice([1, 2, 4, 8, 16, 32]))
+        ref.tick(keys)
+        prod.tick(keys)
+        differ |= bool((_bits(ref.xform()) != _bits(ref.host_rot())).any())
+    assert differ
+    _same(prod, ref)
+    while (_bits(ref.xform()) == _bits(ref.host_rot())).all():  # get them apart, then rotate
+        ref.tick(M.KEY_W)
+        prod.tick(M.KEY_W)
+    ref.tick(M.KEY_R)
+    prod.tick(M.KEY_R)
+    _same(prod, ref)
+    # right after a rotate the columns agree again (copy, then the same exact subtract)
+    assert (_bits(ref.xform()) == _bits(ref.host_rot())).all()
+
+
+def test_walk_moves_along_view_axis():
+    """W then S returns the translation column to (about) zero; R then T the rotation to identity."""
+    pos, n, u = _cam()
+    m = R.ObjectMotion(pos, n, u)
+    m.tick(R.KEY_W)
+    x = m.xform().reshape(3, 4)
+    # translate: w += speed * -(R n), R = I here
+    np.testing.assert_allclose(x[:, 3], -np.asarray(n) * 0.005, rtol=1e-6, atol=1e-9)
+    m.tick(R.KEY_S)
+    np.testing.assert_allclose(m.xform().reshape(3, 4)[:, 3], 0.0, atol=1e-8)
+    m.tick(R.KEY_R)
+    assert abs(m.xform().reshape(3, 4)[0, 2]) > 0.1
+    m.tick(R.KEY_T)
+    np.testing.assert_allclose(m.xform().reshape(3, 4)[:, :3], np.eye(3), atol=1e-6)
+
+
+def test_errors_and_object_api():
+    pos, n, u = _cam()
+    m = R.ObjectMotion(pos, n, u)
+    with pytest.raises(_lib.RtError):
+        m.transform([0, 0, 0, 1], 99)
+    with pytest.raises(_lib.RtError):
+        m.tick(64)
+    m.close()
+    # the Object API needs Camera.add_object first (it holds the camera basis)
+    obj = R.Object.__new__(R.Object)
+    obj.motion = None
+    with pytest.raises(_lib.RtError):
+        obj.key_tick(R.KEY_W)

@@ -12,7 +12,7 @@ for v in "$@"; do
     defs=${v#*:}
     [ "$defs" = "$v" ] && defs=""
     /opt/rocm/bin/hipcc $FLAGS $defs -shared -o "$ROOT/tools/variants/lib_$name.so" \
-        "$SRC/rt_kernels.hip" "$SRC/rt_api.cpp" "$SRC/scene_host.cpp" -lpthread &
+        "$SRC/rt_kernels.hip" "$SRC/rt_api.cpp" "$SRC/scene_host.cpp" "$SRC/motion.cpp" -lpthread &
 done
 wait
 ls -la "$ROOT/tools/variants"

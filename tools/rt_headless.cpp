@@ -1,8 +1,11 @@
 // rt_headless.cpp -- the headless frame loop that replaces WinMain
 // (TD/WinMain.cpp:44-249), written against the reference-shaped C++ facade.
 //
-//   rt_headless <mesh.ply> <mode 0|1|2> [w h frames out.ppm flat]
+//   rt_headless <mesh.ply> <mode 0|1|2> [w h frames out.ppm flat keys]
 //
+// keys: held keys per frame, cycled, one input tick per frame (WinMain ticks
+// at TICK_RATE, :173): letters of R W S Q E T, '+' joins keys held together,
+// '.' is a tick with none, e.g. "WWR+W.Q".
 // Same construction sequence as WinMain: Camera (:69-74), read_ply (:93),
 // Color (:114-121), Trixel + set_sorted_voxels + create_kd (:134-144), two
 // Objects added to the camera (:152-156), then render + color_pixels per
@@ -32,6 +35,21 @@ int main(int argc, char** argv) {
     const int frames = argc > 5 ? std::atoi(argv[5]) : 100;
     const char* out = argc > 6 ? argv[6] : nullptr;
     const u32 render_mode = (argc > 7 && std::atoi(argv[7])) ? RENDER_MODE_FLAT : RENDER_MODE_KD;
+    std::vector<uint32_t> ticks;  // held-key masks, one per frame
+    if (argc > 8) {
+        uint32_t m = 0;
+        for (const char* k = argv[8];; k++) {
+            const char c = *k;
+            if (c == '+') continue;
+            m |= c == 'R' ? RT_KEY_R : c == 'W' ? RT_KEY_W : c == 'S' ? RT_KEY_S : c == 'Q' ? RT_KEY_Q
+               : c == 'E' ? RT_KEY_E : c == 'T' ? RT_KEY_T : 0u;
+            if (c == '\0' || k[1] != '+') {
+                if (c != '\0' || m) ticks.push_back(m);
+                m = 0;
+            }
+            if (c == '\0') break;
+        }
+    }
 
     Camera* main_cam = new Camera(w, h, film_w(w, h), (T_fp).024, (T_fp).055, (T_fp)0.0, (T_fp)0.10, (T_fp)-1.0,
                                   (T_fp)0.00, (T_fp)0.100, (T_fp)0.00, (T_fp)0.0, (T_fp)1.0, (T_fp)0.0);
@@ -73,6 +91,10 @@ int main(int argc, char** argv) {
     main_cam->color_pixels(PHONG_COLOR_TAG);
     double t2 = now_s();
     for (int f = 0; f < frames; f++) {
+        if (!ticks.empty() && obj1->key_tick(ticks[(size_t)f % ticks.size()])) {
+            std::fprintf(stderr, "transform: %s\n", rt_last_error_string());
+            return 1;
+        }
         if (obj1->render(main_cam, render_mode)) { std::fprintf(stderr, "render: %s\n", rt_last_error_string()); return 1; }
         if (main_cam->color_pixels(PHONG_COLOR_TAG)) {
             std::fprintf(stderr, "color_pixels: %s\n", rt_last_error_string());
@@ -80,7 +102,8 @@ int main(int argc, char** argv) {
         }
     }
     const double dt = (now_s() - t2) / frames;
-    std::printf("Resolution: %d x %d\nFPS (render + D2H): %f\n", w, h, 1.0 / dt);
+    std::printf("Resolution: %d x %d\nFPS (%srender + D2H): %f\n", w, h, ticks.empty() ? "" : "key tick + ",
+                1.0 / dt);
 
     if (out) {
         FILE* fp = std::fopen(out, "wb");
