@@ -848,6 +848,9 @@ __device__ __forceinline__ void record_candidates(unsigned long long* s_key, uin
 #ifndef RT_MAX_ITEMS
 #define RT_MAX_ITEMS 2
 #endif
+#ifndef RT_NEAREST_ORDER
+#define RT_NEAREST_ORDER 0
+#endif
 
 // One visited item's candidate: any-hit marks the ray; nearest-hit takes the
 // 64-bit min of (w, path code) and the unique holder of the minimum records
@@ -880,16 +883,17 @@ template <bool kAny, int any_order>
 __device__ __forceinline__ int push_children(uint4* items, int at, const Visit& v) {
     const unsigned long long m1 = __ballot(v.ka), m2 = __ballot(v.kb);
     const int n1 = __builtin_popcountll(m1), n2 = __builtin_popcountll(m2);
-    if (kAny && (any_order & 1)) {   // per-lane pairs
+    constexpr int ord = kAny ? any_order : RT_NEAREST_ORDER;
+    if (ord & 1) {   // per-lane pairs
         const int off = (int)(lanes_below(m1) + lanes_below(m2));
-        if (any_order == 1) {
+        if (ord == 1) {
             if (v.ka) items[at + off] = v.ca;
             if (v.kb) items[at + off + (v.ka ? 1 : 0)] = v.cb;
         } else {
             if (v.kb) items[at + off] = v.cb;
             if (v.ka) items[at + off + (v.kb ? 1 : 0)] = v.ca;
         }
-    } else if (kAny && any_order == 2) {
+    } else if (ord == 2) {
         if (v.kb) items[at + (int)lanes_below(m2)] = v.cb;
         if (v.ka) items[at + n2 + (int)lanes_below(m1)] = v.ca;
     } else {

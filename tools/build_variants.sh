@@ -5,6 +5,7 @@
 set -eu
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 mkdir -p "$ROOT/tools/variants"
+rm -f "$ROOT"/tools/variants/lib_*.so  # only this build's variants travel
 FLAGS=$(python3 -c "import sys; sys.path.insert(0, '$ROOT'); from cpp_cuda_raytracer_dev_amd import build as B; print(' '.join(B.HIP_FLAGS))")
 SRC="$ROOT/cpp_cuda_raytracer_dev_amd/csrc"
 for v in "$@"; do

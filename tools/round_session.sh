@@ -34,6 +34,8 @@ for ctr in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
 done
 step bench_c3_960x540 300 python bench.py --steps 1000 --warmup 100 --width 960 --height 540 --no-cpu-baseline
 step bench_dragon_shadow 300 python bench.py --steps 500 --warmup 50 --shadow --no-cpu-baseline
+step bench_happy_shadow 300 python bench.py --steps 500 --warmup 50 --scene happy --shadow --no-cpu-baseline
+step bench_animate 300 python bench.py --steps 1000 --warmup 100 --animate "R+W.Q.T.W" --no-cpu-baseline
 step bench_c5_happy4k_shadow 400 python bench.py --steps 200 --warmup 20 --scene happy --width 3840 --height 2160 \
     --shadow --no-cpu-baseline
 echo "session done"
