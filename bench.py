@@ -43,7 +43,11 @@ def parse():
     ap.add_argument("--width", type=int, default=W)
     ap.add_argument("--height", type=int, default=H)
     ap.add_argument("--mode", type=int, default=0, help="0 KD, 1 flat list")
-    ap.add_argument("--collective", default="gather", choices=["gather", "allgather"])
+    ap.add_argument("--collective", default="rccl", choices=["rccl", "gather", "allgather"],
+                    help="N>1 frame gather: rccl = the library's own RCCL send/recv + unpack (rt_comm_*, "
+                         "pipelined); gather / allgather = torch.distributed collectives, one frame at a time")
+    ap.add_argument("--pipeline", type=int, default=2,
+                    help="rccl: buffer sets in flight (frame i+1 renders while frame i is gathered)")
     ap.add_argument("--kernel", type=int, default=3,
                     help="KD kernel: 1 per-lane DFS (own-box records), 2 per-lane DFS (child-box records), "
                          "3 wave-cooperative item pool")
@@ -176,7 +180,7 @@ def main():
     import torch
     import torch.distributed as dist
     from cpp_cuda_raytracer_dev_amd import raytracer as R
-    from cpp_cuda_raytracer_dev_amd.distributed import FrameGather
+    from cpp_cuda_raytracer_dev_amd.distributed import FrameGather, NativeFrameGather
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -244,7 +248,18 @@ def main():
     my_pix = int(np.count_nonzero(np.repeat(np.arange((h + 7) // 8) % world == rank, 8)[:h])) * w
     bytes_per_launch = B_INT * int(cnt[0]) + B_LEAF * int(cnt[1]) + B_HIT * int(cnt[2]) + B_PIX * my_pix
 
-    if world > 1:
+    ng = None
+    if world > 1 and a.collective == "rccl":
+        fg = None
+        ng = NativeFrameGather(dist, w, h, dev, nbuf=max(1, a.pipeline))
+        nbuf = len(ng.local)
+        cstream = torch.cuda.Stream(device=dev)
+        rendered = [torch.cuda.Event() for _ in range(nbuf)]
+        sent = [torch.cuda.Event() for _ in range(nbuf)]
+        for k in range(nbuf):
+            sent[k].record(cstream)
+        out = ng.local[0]
+    elif world > 1:
         def unpack(g, f):
             R.unpack_bands(local, w, h, world, g, f, stream=torch.cuda.current_stream(dev).cuda_stream)
         fg = FrameGather(dist, w, h, dev, a.collective, unpack=unpack)
@@ -257,6 +272,7 @@ def main():
     ev = {i: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for i in timed_frames}
 
     tick = [0]
+    seq = [0]
 
     def frame(i=None):
         nonlocal xf
@@ -264,6 +280,23 @@ def main():
             obj.key_tick(masks[tick[0] % len(masks)])
             tick[0] += 1
             xf = obj.quat.xform()
+        if ng is not None:
+            # frame j renders into buffer set j % nbuf once the gather that
+            # last read it is done, then is gathered on the comm stream while
+            # frame j + 1 renders
+            k = seq[0] % nbuf
+            seq[0] += 1
+            stream.wait_event(sent[k])
+            if i in ev:
+                ev[i][0].record(stream)
+            cam.render_into(ng.local[k], xform=xf, mode=a.mode, flags=sflag, tile=tile, stream=sptr)
+            if i in ev:
+                ev[i][1].record(stream)
+            rendered[k].record(stream)
+            cstream.wait_event(rendered[k])
+            ng.gather(k, cstream.cuda_stream)
+            sent[k].record(cstream)
+            return
         with torch.cuda.stream(stream):
             if i in ev:
                 ev[i][0].record(stream)
@@ -288,6 +321,14 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    frame_check = None
+    if world > 1 and rank == 0:
+        # the last gathered frame against a full frame rendered here (untimed)
+        got = ng.frames[(seq[0] - 1) % nbuf] if ng is not None else fg.frame
+        full = torch.zeros(w * h, dtype=torch.int32, device=dev)
+        cam.render_into(full, xform=xf, mode=a.mode, flags=sflag, stream=sptr)
+        torch.cuda.synchronize(dev)
+        frame_check = bool(torch.equal(got, full))
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev.values()]))
     full_walk = None
     if a.shadow and not masks:
@@ -349,7 +390,8 @@ def main():
                 "rays_per_frame": rays_per_frame,
                 "scene": f"synthetic {a.scene} stand-in, {len(pts)} triangles (seed 20221015)",
                 "resolution": [w, h],
-                "parallelism": f"screen bands x{world}" + (f" + RCCL {a.collective} to rank 0" if world > 1 else ""),
+                "parallelism": f"screen bands x{world}" + ((" + RCCL send/recv to rank 0, pipelined" if a.collective == "rccl"
+                                                         else f" + torch {a.collective} to rank 0") if world > 1 else ""),
             },
             "roofline": {
                 "bound": "hbm",
@@ -377,6 +419,9 @@ def main():
                 "bytes_model": "36*V_int + 40*V_leaf + 24*H + 4*P (SURVEY.md 8d)",
             },
         }
+        if frame_check is not None:
+            res["frame_check"] = {"gathered_equals_single_gpu_frame": frame_check,
+                                  "collective": a.collective + (f", {nbuf} buffer sets" if ng is not None else "")}
         if a.deliver and world == 1:
             res["delivery"] = delivery(cam, R, torch, dev, w, h, xf, a.mode, sflag, a.steps, a.warmup)
         if not a.no_cpu_baseline and world == 1:
@@ -387,6 +432,8 @@ def main():
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.barrier()
+        if ng is not None:
+            ng.close()
         dist.destroy_process_group()
     return 0
 

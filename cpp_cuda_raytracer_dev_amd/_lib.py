@@ -29,6 +29,7 @@ RT_OPT_COARSE = 5
 RT_OPT_SHADOW_ORDER = 6
 RT_OPT_DEBUG = 100
 RT_OPT_POOL_CAP = 101
+RT_COMM_ID_BYTES = 128
 
 LEAF_AABB_DTYPE = np.dtype([("x0", "<f4"), ("x1", "<f4"), ("y0", "<f4"), ("y1", "<f4"),
                             ("z0", "<f4"), ("z1", "<f4"), ("tri", "<i8")])
@@ -79,6 +80,12 @@ SIGNATURES = {
     "rt_render_into": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, C.POINTER(RtTile), _P, _P, _P]),
     "rt_tile_packed_pixels": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),
     "rt_unpack_bands": (C.c_int, [C.c_int, C.c_int32, C.c_int32, C.c_int32, _P, _P, _P]),
+    "rt_comm_available": (C.c_int, []),
+    "rt_comm_unique_id": (C.c_int, [_P]),
+    "rt_comm_create": (C.c_int, [C.c_int, C.c_int32, C.c_int32, _P, C.POINTER(_P)]),
+    "rt_comm_gather_frame": (C.c_int, [_P, C.c_int32, C.c_int32, _P, _P, _P, _P]),
+    "rt_comm_info": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "rt_comm_destroy": (None, [_P]),
     "rt_read_frame": (C.c_int, [_P, _P, _P]),
     "rt_camera_counters": (C.c_int, [_P, _P, C.c_int]),
     "rt_pinned_alloc": (C.c_int, [C.c_size_t, C.POINTER(_P)]),

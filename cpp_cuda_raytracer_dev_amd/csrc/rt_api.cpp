@@ -517,17 +517,13 @@ bool set_fine_region(rt_camera* c, TraceParams& p, int per_wave, bool fused) {
     return fused;
 }
 
-int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t* argb, int64_t* hit,
-                uint32_t mode, TraceParams& p) {
+// The launch geometry of one render: camera basis, transform, tiling, and
+// the fine / far split (set_fine_region).  Returns whether the far groups
+// are fused into the fine kernel (every pixel outside the fine region is
+// then provably background: a far wave that finds otherwise sets error 4).
+bool frame_geometry(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t mode, TraceParams& p) {
     static const float ident[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
     const rt_scene* s = c->obj;
-    p.inode = c->d_inode;
-    p.trec = c->d_trec;
-    p.shade = s->d_shade;
-    p.argb = argb;
-    p.hit = hit;
-    p.counters = c->d_counters;
-    p.err = c->d_err;
     for (int k = 0; k < 3; k++) {
         p.n_mod[k] = c->basis.n_mod[k];
         p.u_mod[k] = c->basis.u_mod[k];
@@ -551,16 +547,27 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
     p.tiles_x = (c->w + p.tile_w - 1) / p.tile_w;
     p.block_rows = ((nbands + p.nranks - 1) / p.nranks) * (kTileH / p.tile_h);
     camera_relative_box(s->root, c->pos, p.root_box);
-    {
-        static const float eye[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
-        p.plain_xf = 1;
-        for (int k = 0; k < 12; k++) p.plain_xf &= (p.xf[k] == eye[k]) ? 1 : 0;
-    }
+    p.plain_xf = 1;
+    for (int k = 0; k < 12; k++) p.plain_xf &= (p.xf[k] == ident[k]) ? 1 : 0;
     // Far groups go to the fine kernel's extra blocks when every coarse group
     // can be far (identity transform, interior root, no diagnostics);
     // otherwise to k_coarse_kd3.
     const bool fuse = kernel == 3 && p.plain_xf && !(s->root_ref & kLeafBit) && !(c->debug & (1 | 4 | 8));
-    set_fine_region(c, p, kernel == 3 ? c->coarse : 0, fuse);
+    return set_fine_region(c, p, kernel == 3 ? c->coarse : 0, fuse);
+}
+
+int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t* argb, int64_t* hit,
+                uint32_t mode, TraceParams& p) {
+    const rt_scene* s = c->obj;
+    p.inode = c->d_inode;
+    p.trec = c->d_trec;
+    p.shade = s->d_shade;
+    p.argb = argb;
+    p.hit = hit;
+    p.counters = c->d_counters;
+    p.err = c->d_err;
+    const int kernel = mode == RT_MODE_KD ? effective_kernel(c) : 0;
+    (void)frame_geometry(c, xform, tile, mode, p);
     p.root_ref = s->root_ref;
     p.ntri = s->ntri;
     p.max_depth = kMaxDepth;

@@ -1470,14 +1470,22 @@ __global__ void k_cam_nodes(const rt_kd_node* __restrict__ nodes, const int32_t*
 }
 
 // Rank 0's frame assembly after the gather: [rank][slot][8 rows][w] -> frame.
-__global__ void k_unpack(int32_t w, int32_t h, int32_t nranks, int32_t slots,
+// Every frame row is one contiguous row of the gathered buffer, so a block
+// copies one row (blockIdx.y) in 16-byte pieces when the rows are 16-byte
+// aligned (w % 4 == 0 and 16-byte aligned buffers: vec), else word by word.
+__global__ void k_unpack(int32_t w, int32_t h, int32_t nranks, int32_t slots, int32_t vec,
                          const uint32_t* __restrict__ g, uint32_t* __restrict__ frame) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)w * h) return;
-    const int32_t y = (int32_t)(i / w), x = (int32_t)(i - (int64_t)y * w);
+    const int32_t y = blockIdx.y;
     const int32_t band = y / kTileH, r = y - band * kTileH;
     const int32_t rank = band % nranks, slot = band / nranks;
-    frame[i] = g[(((int64_t)rank * slots + slot) * kTileH + r) * w + x];
+    const uint32_t* src = g + (((int64_t)rank * slots + slot) * kTileH + r) * w;
+    uint32_t* dst = frame + (int64_t)y * w;
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (vec) {
+        if (i < (w >> 2)) reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+    } else {
+        for (int32_t k = i; k < w; k += gridDim.x * blockDim.x) dst[k] = src[k];
+    }
 }
 
 template <class K>
@@ -1593,9 +1601,11 @@ int launch_unpack(int32_t w, int32_t h, int32_t nranks, const uint32_t* gathered
                   void* stream) {
     const int32_t nbands = (h + kTileH - 1) / kTileH;
     const int32_t slots = (nbands + nranks - 1) / nranks;
-    const int64_t n = (int64_t)w * h;
-    if (n == 0) return RT_OK;
-    k_unpack<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(w, h, nranks, slots, gathered, frame);
+    if ((int64_t)w * h == 0) return RT_OK;
+    const int32_t vec = (w & 3) == 0 && ((uintptr_t)gathered & 15) == 0 && ((uintptr_t)frame & 15) == 0;
+    const int32_t per_row = vec ? (w >> 2) : w;
+    const dim3 grid((unsigned)((per_row + 255) / 256), (unsigned)h);
+    k_unpack<<<grid, 256, 0, (hipStream_t)stream>>>(w, h, nranks, slots, vec, gathered, frame);
     return check_launch<void>("k_unpack");
 }
 

@@ -86,3 +86,59 @@ class FrameGather:
                 import torch
                 g = self.gathered.cpu().numpy().view(np.uint32)
                 self.frame.copy_(torch.from_numpy(unpack_bands_numpy(g, self.w, self.h, self.world).view(np.int32)))
+
+
+class NativeFrameGather:
+    """The gather through the library's own RCCL communicator (rt_comm_*).
+
+    One rt_comm_gather_frame call per frame enqueues, on the given stream, the
+    peers' ncclSend to rank 0, rank 0's N-1 ncclRecv into its gathered buffer
+    and the unpack kernel -- no Python collective per frame.  `nbuf` sets of
+    buffers let frame i+1 render while frame i is in flight (bench.py
+    pipelines them with events).  On rank 0 the local buffer of set k is slot
+    0 of gathered[k], so its own bands are rendered in place.  The 128-byte
+    RCCL id is broadcast with `dist` (any backend)."""
+
+    def __init__(self, dist, w: int, h: int, device, nbuf: int = 2):
+        import ctypes as C
+        import torch
+        from . import _lib
+        self.dist = dist
+        self.w, self.h = w, h
+        self.rank = dist.get_rank()
+        self.world = dist.get_world_size()
+        self.npk = packed_pixels(w, h, self.world)
+        self.device = device
+        if not _lib.lib().rt_comm_available():
+            raise RuntimeError("NativeFrameGather: librccl.so.1 not found (rt_comm_available() == 0)")
+        idb = (C.c_uint8 * _lib.RT_COMM_ID_BYTES)()
+        if self.rank == 0:
+            _lib.call("rt_comm_unique_id", C.cast(idb, C.c_void_p))
+        box = [bytes(idb)]
+        dist.broadcast_object_list(box, src=0)
+        idb = (C.c_uint8 * _lib.RT_COMM_ID_BYTES).from_buffer_copy(box[0])
+        self._h = C.c_void_p()
+        _lib.call("rt_comm_create", device.index, self.world, self.rank, C.cast(idb, C.c_void_p), C.byref(self._h))
+        if self.rank == 0:
+            self.gathered = [torch.zeros(self.world * self.npk, dtype=torch.int32, device=device) for _ in range(nbuf)]
+            self.local = [g[:self.npk] for g in self.gathered]
+            self.frames = [torch.zeros(w * h, dtype=torch.int32, device=device) for _ in range(nbuf)]
+        else:
+            self.gathered = [None] * nbuf
+            self.local = [torch.zeros(self.npk, dtype=torch.int32, device=device) for _ in range(nbuf)]
+            self.frames = [None] * nbuf
+
+    def gather(self, k: int, stream) -> None:
+        """Stream-ordered gather + unpack of buffer set k (stream: hipStream_t int)."""
+        from . import _lib
+        g = self.gathered[k]
+        f = self.frames[k]
+        _lib.call("rt_comm_gather_frame", self._h, self.w, self.h, _lib.ptr(self.local[k]),
+                  _lib.ptr(g) if g is not None else None, _lib.ptr(f) if f is not None else None,
+                  stream or None)
+
+    def close(self) -> None:
+        from . import _lib
+        if self._h:
+            _lib.lib().rt_comm_destroy(self._h)
+            self._h = None

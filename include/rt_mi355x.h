@@ -30,7 +30,8 @@ typedef enum rt_status {
     RT_ERR_NOMEM = -3,     /* host or device allocation failed         */
     RT_ERR_IO = -4,        /* file could not be read / parsed          */
     RT_ERR_STATE = -5,     /* call out of order (e.g. render w/o tree) */
-    RT_ERR_OVERFLOW = -6   /* traversal stack overflow flagged by GPU  */
+    RT_ERR_OVERFLOW = -6,  /* traversal stack overflow flagged by GPU  */
+    RT_ERR_COMM = -7       /* RCCL missing or a collective call failed */
 } rt_status;
 
 /* Render modes: KD traversal (intersect_voxel_cuda, TD/Trixel.cu:41-172) or
@@ -164,6 +165,27 @@ int64_t rt_tile_packed_pixels(int32_t w, int32_t h, int32_t nranks);
  * back -> d_frame (w*h).  Runs on `stream`. */
 int rt_unpack_bands(int device, int32_t w, int32_t h, int32_t nranks,
                     const uint32_t* d_gathered, uint32_t* d_frame, void* stream);
+
+/* Multi-GPU frame gather over RCCL (the reference is
+ * single-GPU, cudaSetDevice(0) at TD/Trixel.cu:213, so nothing is replaced).
+ * rt_comm_unique_id on rank 0, the 128 bytes broadcast by the caller (e.g.
+ * torch.distributed), then rt_comm_create on every rank (collective, like
+ * ncclCommInitRank).  rt_comm_gather_frame is stream-ordered on `stream`:
+ * ranks != 0 send their packed band buffer (rt_render_into with
+ * rt_tile{nranks, rank}) to rank 0; rank 0 receives the N-1 peers' buffers
+ * into slots 1..N-1 of d_gathered (N packed buffers), copies d_local into
+ * slot 0 unless d_local == d_gathered, and unpacks into d_frame (w*h).
+ * Every rank must call it once per frame.  RCCL is loaded at run time
+ * (librccl.so.1); rt_comm_available() says whether it was found. */
+#define RT_COMM_ID_BYTES 128
+typedef struct rt_comm rt_comm;
+int rt_comm_available(void);
+int rt_comm_unique_id(uint8_t id[RT_COMM_ID_BYTES]);
+int rt_comm_create(int device, int32_t nranks, int32_t rank, const uint8_t id[RT_COMM_ID_BYTES], rt_comm** out);
+int rt_comm_gather_frame(rt_comm* c, int32_t w, int32_t h, const uint32_t* d_local, uint32_t* d_gathered,
+                         uint32_t* d_frame, void* stream);
+int rt_comm_info(const rt_comm* c, int32_t* nranks, int32_t* rank);
+void rt_comm_destroy(rt_comm* c);
 
 /* The D2H copy of color_camera_device (TD/Camera.cu:84) and d_rmi.index.
  * Synchronises the device.  argb: w*h u32 0x00RRGGBB; hit may be NULL. */

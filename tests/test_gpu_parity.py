@@ -605,3 +605,63 @@ def test_shadow_counted_stop_at_occluder(order):
     argb2, hit2, cut = s.render(0, count=True, shadow=True)
     assert (argb == argb2).all() and (hit == hit2).all()
     assert cut[0] < full[0] and cut[1] <= full[1] and cut[3] == full[3]
+
+
+@pytest.mark.parametrize("w,h,nranks", [(81, 45, 3), (33, 9, 2), (64, 20, 8), (7, 130, 5)])
+def test_unpack_bands_shapes(w, h, nranks):
+    """k_unpack's row copy (16-byte pieces when w % 4 == 0, else words) against
+    the numpy inverse of the packing, on random words."""
+    import torch
+    from cpp_cuda_raytracer_dev_amd import raytracer as R, distributed as D
+    npk = R.packed_pixels(w, h, nranks)
+    rng = np.random.default_rng(w * 1000 + h)
+    g = rng.integers(0, 2**32, nranks * npk, dtype=np.uint64).astype(np.uint32)
+    dev = torch.device("cuda:0")
+    gathered = torch.from_numpy(g.view(np.int32)).to(dev)
+    frame = torch.full((w * h,), -1, dtype=torch.int32, device=dev)
+    R.unpack_bands(0, w, h, nranks, gathered, frame)
+    torch.cuda.synchronize()
+    assert (frame.cpu().numpy().view(np.uint32) == D.unpack_bands_numpy(g, w, h, nranks)).all()
+    # a misaligned frame pointer takes the word path
+    frame2 = torch.full((w * h + 1,), -1, dtype=torch.int32, device=dev)
+    R.unpack_bands(0, w, h, nranks, gathered, frame2[1:])
+    torch.cuda.synchronize()
+    assert (frame2[1:].cpu().numpy().view(np.uint32) == D.unpack_bands_numpy(g, w, h, nranks)).all()
+
+
+def test_native_comm_world1():
+    """rt_comm_* end to end in a one-rank group: RCCL resolved at run time, the
+    id broadcast, the communicator, and rt_comm_gather_frame's in-place slot 0
+    + unpack on a side stream, pipelined over two buffer sets."""
+    import os
+    import tempfile
+    import torch
+    import torch.distributed as dist
+    from cpp_cuda_raytracer_dev_amd import _lib
+    from cpp_cuda_raytracer_dev_amd.distributed import NativeFrameGather
+    assert _lib.lib().rt_comm_available() == 1
+    w, h = 320, 180
+    s = H.GpuScene("rabbit_70k", w, h)
+    full, _, _ = s.render(0)
+    fd, path = tempfile.mkstemp()
+    os.close(fd)
+    dist.init_process_group("gloo", init_method=f"file://{path}", rank=0, world_size=1)
+    try:
+        dev = torch.device("cuda:0")
+        ng = NativeFrameGather(dist, w, h, dev, nbuf=2)
+        cs = torch.cuda.Stream()
+        for j in range(4):
+            k = j % 2
+            s.cam.render_into(ng.local[k], mode=0)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream())
+            cs.wait_event(ev)
+            ng.gather(k, cs.cuda_stream)
+        torch.cuda.synchronize()
+        for k in range(2):
+            assert (ng.frames[k].cpu().numpy().view(np.uint32) == full).all()
+        ng.close()
+    finally:
+        dist.destroy_process_group()
+        if os.path.exists(path):  # the file store removes it itself
+            os.unlink(path)
