@@ -294,7 +294,7 @@ def main():
                 ev[i][1].record(stream)
             rendered[k].record(stream)
             cstream.wait_event(rendered[k])
-            ng.gather(k, cstream.cuda_stream)
+            ng.gather(k, cam, xf, a.mode, cstream.cuda_stream)
             sent[k].record(cstream)
             return
         with torch.cuda.stream(stream):

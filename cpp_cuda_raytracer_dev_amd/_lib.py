@@ -83,7 +83,11 @@ SIGNATURES = {
     "rt_comm_available": (C.c_int, []),
     "rt_comm_unique_id": (C.c_int, [_P]),
     "rt_comm_create": (C.c_int, [C.c_int, C.c_int32, C.c_int32, _P, C.POINTER(_P)]),
-    "rt_comm_gather_frame": (C.c_int, [_P, C.c_int32, C.c_int32, _P, _P, _P, _P]),
+    "rt_comm_gather_frame": (C.c_int, [_P, _P, _P, C.c_uint32, _P, _P, _P, _P]),
+    "rt_frame_rect": (C.c_int, [_P, _P, C.c_uint32, C.c_int32, _P]),
+    "rt_rect_pixels": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P]),
+    "rt_pack_rect": (C.c_int, [C.c_int, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, _P, _P, _P]),
+    "rt_unpack_rect": (C.c_int, [C.c_int, C.c_int32, C.c_int32, C.c_int32, _P, _P, _P, _P, _P]),
     "rt_comm_info": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "rt_comm_destroy": (None, [_P]),
     "rt_read_frame": (C.c_int, [_P, _P, _P]),

@@ -141,40 +141,44 @@ extern "C" int rt_comm_create(int device, int32_t nranks, int32_t rank, const ui
     return RT_OK;
 }
 
-extern "C" int rt_comm_gather_frame(rt_comm* c, int32_t w, int32_t h, const uint32_t* d_local,
-                                    uint32_t* d_gathered, uint32_t* d_frame, void* stream) {
-    if (!c || !d_local || w <= 0 || h <= 0) return fail(RT_ERR_INVALID, "rt_comm_gather_frame: bad argument");
-    if (c->rank == 0 && (!d_gathered || !d_frame))
-        return fail(RT_ERR_INVALID, "rt_comm_gather_frame: rank 0 needs the gathered and frame buffers");
+extern "C" int rt_comm_gather_frame(rt_comm* c, rt_camera* cam, const float* xform, uint32_t mode,
+                                    const uint32_t* d_local, uint32_t* d_scratch, uint32_t* d_frame, void* stream) {
+    if (!c || !cam || !d_local) return fail(RT_ERR_INVALID, "rt_comm_gather_frame: bad argument");
+    if ((c->rank == 0 && !d_frame) || (c->nranks > 1 && !d_scratch))
+        return fail(RT_ERR_INVALID, "rt_comm_gather_frame: missing scratch or frame buffer");
+    int32_t w, h, depth;
+    int rc;
+    if ((rc = rt_camera_info(cam, &w, &h, &depth))) return rc;
+    // the part of the frame that is not provably background: the same on
+    // every rank (same camera, transform and options), so sizes need no
+    // exchange
+    int32_t rect[4];
+    if ((rc = rt_frame_rect(cam, xform, mode, c->nranks, rect))) return rc;
     const Rccl* r = rccl();
-    const int64_t npk = rt_tile_packed_pixels(w, h, c->nranks);
     Guard g(c->device);
     if (!g.ok) return fail(RT_ERR_HIP, "rt_comm_gather_frame: hipSetDevice(%d) failed", c->device);
     hipStream_t s = (hipStream_t)stream;
-    int rc;
     if (c->rank == 0) {
-        // rank 0's own bands: rendered in place (d_local == slot 0) or copied there
-        if (d_local != d_gathered) {
-            hipError_t e = hipMemcpyAsync(d_gathered, d_local, (size_t)npk * 4, hipMemcpyDeviceToDevice, s);
-            if (e != hipSuccess) return fail(RT_ERR_HIP, "rt_comm_gather_frame: slot 0 copy: %s", hipGetErrorString(e));
-        }
         if (c->nranks > 1) {
             if ((rc = nccl_check(r, r->group_start(), "ncclGroupStart"))) return rc;
-            for (int p = 1; p < c->nranks; ++p) {
-                rc = nccl_check(r, r->recv(d_gathered + (int64_t)p * npk, (size_t)npk, kNcclUint32, p, c->comm, s),
-                                "ncclRecv");
-                if (rc) {
-                    (void)r->group_end();
-                    return rc;
-                }
+            int64_t off = 0;
+            for (int p = 1; p < c->nranks && !rc; ++p) {
+                const int64_t n = rt_rect_pixels(w, h, c->nranks, p, rect);
+                if (n > 0) rc = nccl_check(r, r->recv(d_scratch + off, (size_t)n, kNcclUint32, p, c->comm, s), "ncclRecv");
+                off += n;
             }
-            if ((rc = nccl_check(r, r->group_end(), "ncclGroupEnd"))) return rc;
+            const nres_t e = r->group_end();
+            if (rc) return rc;
+            if ((rc = nccl_check(r, e, "ncclGroupEnd"))) return rc;
         }
-        return launch_unpack(w, h, c->nranks, d_gathered, d_frame, stream);
+        return rt_unpack_rect(c->device, w, h, c->nranks, rect, d_local, d_scratch, d_frame, stream);
     }
+    const int64_t n = rt_rect_pixels(w, h, c->nranks, c->rank, rect);
+    if (n <= 0) return RT_OK;
+    if ((rc = rt_pack_rect(c->device, w, h, c->nranks, c->rank, rect, d_local, d_scratch, stream))) return rc;
     if ((rc = nccl_check(r, r->group_start(), "ncclGroupStart"))) return rc;
-    rc = nccl_check(r, r->send(d_local, (size_t)npk, kNcclUint32, 0, c->comm, s), "ncclSend");
-    nres_t e = r->group_end();
+    rc = nccl_check(r, r->send(d_scratch, (size_t)n, kNcclUint32, 0, c->comm, s), "ncclSend");
+    const nres_t e = r->group_end();
     if (rc) return rc;
     return nccl_check(r, e, "ncclGroupEnd");
 }

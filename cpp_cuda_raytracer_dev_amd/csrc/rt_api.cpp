@@ -885,6 +885,67 @@ extern "C" int rt_unpack_bands(int device, int32_t w, int32_t h, int32_t nranks,
     return launch_unpack(w, h, nranks, d_gathered, d_frame, stream);
 }
 
+extern "C" int rt_frame_rect(rt_camera* c, const float* xform, uint32_t mode, int32_t nranks, int32_t rect[4]) {
+    if (!c || !rect || nranks < 1) return fail(RT_ERR_INVALID, "rt_frame_rect: bad argument");
+    if (mode != RT_MODE_KD && mode != RT_MODE_FLAT) return fail(RT_ERR_INVALID, "rt_frame_rect: mode %u", mode);
+    DeviceGuard g(c->device);
+    int rc;
+    if ((rc = prepare_camera_object(c))) return rc;
+    const int32_t nbands = (c->h + kTileH - 1) / kTileH;
+    rect[0] = 0; rect[1] = c->w; rect[2] = 0; rect[3] = nbands;  // no proof: the whole frame
+    if (mode != RT_MODE_KD || !c->obj->d_nodes) return RT_OK;
+    int32_t x0 = INT32_MAX, x1 = INT32_MIN, b0 = INT32_MAX, b1 = INT32_MIN;
+    for (int32_t r = 0; r < nranks; r++) {
+        TraceParams p{};
+        const rt_tile t{nranks, r};
+        if (!frame_geometry(c, xform, &t, mode, p)) return RT_OK;  // a rank renders unfused
+        if (p.cs1 <= p.cs0 || p.cg_x1 <= p.cg_x0) continue;     // nothing fine on this rank
+        x0 = std::min(x0, p.cg_x0 * 8);
+        x1 = std::max(x1, std::min(p.cg_x1 * 8, c->w));
+        b0 = std::min(b0, r + p.cs0 * nranks);
+        b1 = std::max(b1, r + (p.cs1 - 1) * nranks + 1);
+    }
+    if (x0 >= x1 || b0 >= b1) {
+        rect[0] = rect[1] = rect[2] = rect[3] = 0;
+    } else {
+        rect[0] = x0; rect[1] = x1; rect[2] = b0; rect[3] = std::min(b1, nbands);
+    }
+    return RT_OK;
+}
+
+static int check_rect(int32_t w, int32_t h, int32_t nranks, const int32_t rect[4], const char* what) {
+    const int32_t nbands = (h + kTileH - 1) / kTileH;
+    if (w <= 0 || h <= 0 || nranks < 1 || !rect || rect[0] < 0 || rect[1] > w || rect[0] > rect[1] || rect[2] < 0 ||
+        rect[3] > nbands || rect[2] > rect[3])
+        return fail(RT_ERR_INVALID, "%s: bad frame geometry or rectangle", what);
+    return RT_OK;
+}
+
+extern "C" int64_t rt_rect_pixels(int32_t w, int32_t h, int32_t nranks, int32_t rank, const int32_t rect[4]) {
+    if (check_rect(w, h, nranks, rect, "rt_rect_pixels") || rank < 0 || rank >= nranks) return -1;
+    int32_t s0, s1;
+    rect_slots(rect[2], rect[3], nranks, rank, s0, s1);
+    return (int64_t)(s1 - s0) * kTileH * (rect[1] - rect[0]);
+}
+
+extern "C" int rt_pack_rect(int device, int32_t w, int32_t h, int32_t nranks, int32_t rank, const int32_t rect[4],
+                            const uint32_t* d_local, uint32_t* d_out, void* stream) {
+    int rc;
+    if ((rc = check_rect(w, h, nranks, rect, "rt_pack_rect"))) return rc;
+    if (rank < 0 || rank >= nranks || !d_local || !d_out) return fail(RT_ERR_INVALID, "rt_pack_rect: bad argument");
+    DeviceGuard g(device);
+    return launch_pack_rect(w, h, nranks, rank, rect, d_local, d_out, stream);
+}
+
+extern "C" int rt_unpack_rect(int device, int32_t w, int32_t h, int32_t nranks, const int32_t rect[4],
+                              const uint32_t* d_local0, const uint32_t* d_peers, uint32_t* d_frame, void* stream) {
+    int rc;
+    if ((rc = check_rect(w, h, nranks, rect, "rt_unpack_rect"))) return rc;
+    if (!d_local0 || !d_frame || (nranks > 1 && !d_peers)) return fail(RT_ERR_INVALID, "rt_unpack_rect: bad argument");
+    DeviceGuard g(device);
+    return launch_unpack_rect(w, h, nranks, rect, d_local0, d_peers, d_frame, stream);
+}
+
 extern "C" int rt_read_frame(rt_camera* c, uint32_t* argb, int64_t* hit) {
     if (!c || !argb) return fail(RT_ERR_INVALID, "rt_read_frame: null argument");
     DeviceGuard g(c->device);

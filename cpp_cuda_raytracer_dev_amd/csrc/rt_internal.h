@@ -144,4 +144,16 @@ int launch_trace(const TraceParams& p, uint32_t mode, uint32_t flags, int kernel
 void camera_relative_box(const rt_kd_node& nd, const float pos[3], float out[6]);
 int launch_unpack(int32_t w, int32_t h, int32_t nranks, const uint32_t* gathered,
                   uint32_t* frame, void* stream);
+// Slots s of `rank` whose band rank + s*nranks lies in [b0, b1): [s0, s1).
+__host__ __device__ inline void rect_slots(int32_t b0, int32_t b1, int32_t nranks, int32_t rank,
+                                           int32_t& s0, int32_t& s1) {
+    s0 = b0 <= rank ? 0 : (b0 - rank + nranks - 1) / nranks;
+    s1 = b1 <= rank ? 0 : (b1 - 1 - rank) / nranks + 1;
+    if (s1 < s0) s1 = s0;
+}
+// rect = (x0, x1, b0, b1): columns [x0, x1) of bands [b0, b1) (rt_frame_rect).
+int launch_pack_rect(int32_t w, int32_t h, int32_t nranks, int32_t rank, const int32_t rect[4],
+                     const uint32_t* local, uint32_t* out, void* stream);
+int launch_unpack_rect(int32_t w, int32_t h, int32_t nranks, const int32_t rect[4], const uint32_t* local0,
+                       const uint32_t* peers, uint32_t* frame, void* stream);
 }  // namespace rt

@@ -1488,6 +1488,48 @@ __global__ void k_unpack(int32_t w, int32_t h, int32_t nranks, int32_t slots, in
     }
 }
 
+// The rectangle gather (rt_frame_rect): outside columns [x0, x1) of bands
+// [b0, b1) every pixel is provably background, so a rank sends only its
+// slots' rows inside the rectangle.  Pack: row (s - s0)*8 + r of the
+// compact buffer <- columns [x0, x1) of packed row s*8 + r.
+__global__ void k_pack_rect(int32_t w, int32_t x0, int32_t cw, int32_t s0, const uint32_t* __restrict__ local,
+                            uint32_t* __restrict__ out) {
+    const int32_t row = blockIdx.y;
+    const int32_t x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= cw) return;
+    const int32_t s = s0 + row / kTileH, r = row - (row / kTileH) * kTileH;
+    out[(int64_t)row * cw + x] = local[((int64_t)s * kTileH + r) * w + x0 + x];
+}
+
+// Rank 0: frame row y (blockIdx.y) from rank 0's own packed buffer, a peer's
+// compact block (peers 1..N-1 back to back), or the background.
+__global__ void k_unpack_rect(int32_t w, int32_t nranks, int32_t x0, int32_t x1, int32_t b0, int32_t b1,
+                              const uint32_t* __restrict__ local0, const uint32_t* __restrict__ peers,
+                              uint32_t* __restrict__ frame) {
+    const int32_t y = blockIdx.y;
+    const int32_t x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= w) return;
+    const int32_t band = y / kTileH, r = y - band * kTileH;
+    const int32_t rank = band % nranks, slot = band / nranks;
+    uint32_t v = kBackground;
+    if (x >= x0 && x < x1 && band >= b0 && band < b1) {
+        if (rank == 0) {
+            v = local0[((int64_t)slot * kTileH + r) * w + x];
+        } else {
+            const int32_t cw = x1 - x0;
+            int64_t off = 0;
+            int32_t s0, s1;
+            for (int32_t q = 1; q < rank; q++) {
+                rect_slots(b0, b1, nranks, q, s0, s1);
+                off += (int64_t)(s1 - s0) * kTileH * cw;
+            }
+            rect_slots(b0, b1, nranks, rank, s0, s1);
+            v = peers[off + ((int64_t)(slot - s0) * kTileH + r) * cw + (x - x0)];
+        }
+    }
+    frame[(int64_t)y * w + x] = v;
+}
+
 template <class K>
 int check_launch(const char* what) {
     hipError_t e = hipGetLastError();
@@ -1607,6 +1649,27 @@ int launch_unpack(int32_t w, int32_t h, int32_t nranks, const uint32_t* gathered
     const dim3 grid((unsigned)((per_row + 255) / 256), (unsigned)h);
     k_unpack<<<grid, 256, 0, (hipStream_t)stream>>>(w, h, nranks, slots, vec, gathered, frame);
     return check_launch<void>("k_unpack");
+}
+
+int launch_pack_rect(int32_t w, int32_t h, int32_t nranks, int32_t rank, const int32_t rect[4],
+                     const uint32_t* local, uint32_t* out, void* stream) {
+    int32_t s0, s1;
+    rect_slots(rect[2], rect[3], nranks, rank, s0, s1);
+    const int32_t cw = rect[1] - rect[0];
+    if (cw <= 0 || s1 <= s0) return RT_OK;
+    (void)h;
+    const dim3 grid((unsigned)((cw + 255) / 256), (unsigned)((s1 - s0) * kTileH));
+    k_pack_rect<<<grid, 256, 0, (hipStream_t)stream>>>(w, rect[0], cw, s0, local, out);
+    return check_launch<void>("k_pack_rect");
+}
+
+int launch_unpack_rect(int32_t w, int32_t h, int32_t nranks, const int32_t rect[4], const uint32_t* local0,
+                       const uint32_t* peers, uint32_t* frame, void* stream) {
+    if ((int64_t)w * h == 0) return RT_OK;
+    const dim3 grid((unsigned)((w + 255) / 256), (unsigned)h);
+    k_unpack_rect<<<grid, 256, 0, (hipStream_t)stream>>>(w, nranks, rect[0], rect[1], rect[2], rect[3], local0,
+                                                         peers, frame);
+    return check_launch<void>("k_unpack_rect");
 }
 
 }  // namespace rt

@@ -119,23 +119,31 @@ class NativeFrameGather:
         idb = (C.c_uint8 * _lib.RT_COMM_ID_BYTES).from_buffer_copy(box[0])
         self._h = C.c_void_p()
         _lib.call("rt_comm_create", device.index, self.world, self.rank, C.cast(idb, C.c_void_p), C.byref(self._h))
-        if self.rank == 0:
-            self.gathered = [torch.zeros(self.world * self.npk, dtype=torch.int32, device=device) for _ in range(nbuf)]
-            self.local = [g[:self.npk] for g in self.gathered]
-            self.frames = [torch.zeros(w * h, dtype=torch.int32, device=device) for _ in range(nbuf)]
-        else:
-            self.gathered = [None] * nbuf
-            self.local = [torch.zeros(self.npk, dtype=torch.int32, device=device) for _ in range(nbuf)]
-            self.frames = [None] * nbuf
+        # scratch: the peers' rectangle parts on rank 0, the send staging elsewhere
+        nscr = max(1, (self.world - 1) * self.npk) if self.rank == 0 else self.npk
+        self.local = [torch.zeros(self.npk, dtype=torch.int32, device=device) for _ in range(nbuf)]
+        self.scratch = [torch.zeros(nscr, dtype=torch.int32, device=device) for _ in range(nbuf)]
+        self.frames = [torch.zeros(w * h, dtype=torch.int32, device=device) if self.rank == 0 else None
+                       for _ in range(nbuf)]
 
-    def gather(self, k: int, stream) -> None:
-        """Stream-ordered gather + unpack of buffer set k (stream: hipStream_t int)."""
+    def gather(self, k: int, cam, xform, mode: int, stream) -> None:
+        """Stream-ordered gather + assembly of buffer set k, rendered by `cam`
+        (raytracer.Camera) with (xform, mode); stream: hipStream_t int."""
+        import numpy as np
         from . import _lib
-        g = self.gathered[k]
+        xf = None if xform is None else np.ascontiguousarray(xform, np.float32)
         f = self.frames[k]
-        _lib.call("rt_comm_gather_frame", self._h, self.w, self.h, _lib.ptr(self.local[k]),
-                  _lib.ptr(g) if g is not None else None, _lib.ptr(f) if f is not None else None,
-                  stream or None)
+        _lib.call("rt_comm_gather_frame", self._h, cam._h, _lib.ptr(xf), mode, _lib.ptr(self.local[k]),
+                  _lib.ptr(self.scratch[k]), _lib.ptr(f) if f is not None else None, stream or None)
+
+    def frame_rect(self, cam, xform, mode: int):
+        """rt_frame_rect for this group's size: (x0, x1, b0, b1)."""
+        import numpy as np
+        from . import _lib
+        xf = None if xform is None else np.ascontiguousarray(xform, np.float32)
+        rect = np.zeros(4, np.int32)
+        _lib.call("rt_frame_rect", cam._h, _lib.ptr(xf), mode, self.world, _lib.ptr(rect))
+        return tuple(int(v) for v in rect)
 
     def close(self) -> None:
         from . import _lib

@@ -170,20 +170,39 @@ int rt_unpack_bands(int device, int32_t w, int32_t h, int32_t nranks,
  * single-GPU, cudaSetDevice(0) at TD/Trixel.cu:213, so nothing is replaced).
  * rt_comm_unique_id on rank 0, the 128 bytes broadcast by the caller (e.g.
  * torch.distributed), then rt_comm_create on every rank (collective, like
- * ncclCommInitRank).  rt_comm_gather_frame is stream-ordered on `stream`:
- * ranks != 0 send their packed band buffer (rt_render_into with
- * rt_tile{nranks, rank}) to rank 0; rank 0 receives the N-1 peers' buffers
- * into slots 1..N-1 of d_gathered (N packed buffers), copies d_local into
- * slot 0 unless d_local == d_gathered, and unpacks into d_frame (w*h).
- * Every rank must call it once per frame.  RCCL is loaded at run time
- * (librccl.so.1); rt_comm_available() says whether it was found. */
+ * ncclCommInitRank).  rt_comm_gather_frame is stream-ordered on `stream`,
+ * for the frame `cam` rendered with (xform, mode) into d_local (this rank's
+ * packed band buffer, rt_render_into with rt_tile{nranks, rank}): only the
+ * rectangle rt_frame_rect names travels -- ranks != 0 pack their part of it
+ * into d_scratch (rt_tile_packed_pixels u32) and send it to rank 0; rank 0
+ * receives the peers' parts into d_scratch ((N-1) * rt_tile_packed_pixels
+ * u32) and assembles d_frame (w*h) from them, its own d_local and the
+ * background.  Every rank must call it once per frame.  RCCL is loaded at
+ * run time (librccl.so.1); rt_comm_available() says whether it was found. */
 #define RT_COMM_ID_BYTES 128
 typedef struct rt_comm rt_comm;
 int rt_comm_available(void);
 int rt_comm_unique_id(uint8_t id[RT_COMM_ID_BYTES]);
 int rt_comm_create(int device, int32_t nranks, int32_t rank, const uint8_t id[RT_COMM_ID_BYTES], rt_comm** out);
-int rt_comm_gather_frame(rt_comm* c, int32_t w, int32_t h, const uint32_t* d_local, uint32_t* d_gathered,
-                         uint32_t* d_frame, void* stream);
+int rt_comm_gather_frame(rt_comm* c, rt_camera* cam, const float* xform, uint32_t mode, const uint32_t* d_local,
+                         uint32_t* d_scratch, uint32_t* d_frame, void* stream);
+/* The frame rectangle (x0, x1, b0, b1): columns [x0, x1) of 8-row bands
+ * [b0, b1).  Every pixel outside it is provably the background 0x00F08200
+ * for a render of `cam` with (xform, mode) split over nranks: each rank's
+ * far groups lie outside the root box's projected rectangle and are filled
+ * by the fused kernel, which flags (device error 4) any that is not.  When
+ * that does not hold for some rank (a transform, flat mode, options) the
+ * rectangle is the whole frame; an empty rectangle is (0, 0, 0, 0). */
+int rt_frame_rect(rt_camera* cam, const float* xform, uint32_t mode, int32_t nranks, int32_t rect[4]);
+/* Pixels of `rank`'s part of the rectangle (its slots inside it), or -1. */
+int64_t rt_rect_pixels(int32_t w, int32_t h, int32_t nranks, int32_t rank, const int32_t rect[4]);
+/* rank's packed buffer -> its part of the rectangle, contiguous. */
+int rt_pack_rect(int device, int32_t w, int32_t h, int32_t nranks, int32_t rank, const int32_t rect[4],
+                 const uint32_t* d_local, uint32_t* d_out, void* stream);
+/* Rank 0: the frame from its own packed buffer, the peers' parts (ranks
+ * 1..N-1 back to back) and the background. */
+int rt_unpack_rect(int device, int32_t w, int32_t h, int32_t nranks, const int32_t rect[4],
+                   const uint32_t* d_local0, const uint32_t* d_peers, uint32_t* d_frame, void* stream);
 int rt_comm_info(const rt_comm* c, int32_t* nranks, int32_t* rank);
 void rt_comm_destroy(rt_comm* c);
 

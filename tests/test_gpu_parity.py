@@ -629,6 +629,51 @@ def test_unpack_bands_shapes(w, h, nranks):
     assert (frame2[1:].cpu().numpy().view(np.uint32) == D.unpack_bands_numpy(g, w, h, nranks)).all()
 
 
+@pytest.mark.parametrize("scene,w,h,nranks,moved", [("dragon", 1920, 1080, 2, False), ("dragon", 1920, 1080, 8, False),
+                                                     ("rabbit_70k", 81, 45, 3, False), ("dragon", 960, 540, 4, True)])
+def test_rect_gather_single_gpu(scene, w, h, nranks, moved):
+    """The rectangle gather of rt_comm_gather_frame, every rank simulated on
+    one GPU: each rank's tile render -> rt_pack_rect -> (the peers' parts back
+    to back) -> rt_unpack_rect with rank 0's own buffer equals the full frame.
+    A moved object has no background proof: the rectangle is the whole frame."""
+    import ctypes as C
+    import torch
+    from cpp_cuda_raytracer_dev_amd import _lib, raytracer as R
+    s = H.GpuScene(scene, w, h)
+    xf = None
+    if moved:
+        xf = np.array([1, 0, 0, 0.01, 0, 1, 0, 0, 0, 0, 1, 0.02], np.float32)
+        s.obj.quat.rot_m = xf.reshape(3, 4)
+    full, _, _ = s.render(0, xform=xf)
+    rect = np.zeros(4, np.int32)
+    _lib.call("rt_frame_rect", s.cam._h, _lib.ptr(xf), 0, nranks, _lib.ptr(rect))
+    nbands = (h + 7) // 8
+    if moved:
+        assert tuple(rect) == (0, w, 0, nbands)
+    elif w >= 960:  # small frames: the widened projection may cover everything
+        assert 0 < (rect[1] - rect[0]) * (rect[3] - rect[2]) < w * nbands
+    npk = R.packed_pixels(w, h, nranks)
+    dev = torch.device("cuda:0")
+    locs = [torch.zeros(npk, dtype=torch.int32, device=dev) for _ in range(nranks)]
+    for r in range(nranks):
+        s.cam.render_into(locs[r], xform=xf, mode=0, tile=(nranks, r))
+    counts = [int(_lib.lib().rt_rect_pixels(w, h, nranks, r, _lib.ptr(rect))) for r in range(nranks)]
+    assert min(counts) >= 0
+    peers = torch.zeros(max(1, sum(counts[1:])), dtype=torch.int32, device=dev)
+    off = 0
+    for r in range(1, nranks):
+        if counts[r]:
+            _lib.call("rt_pack_rect", 0, w, h, nranks, r, _lib.ptr(rect), _lib.ptr(locs[r]),
+                      C.c_void_p(peers.data_ptr() + 4 * off), None)
+        off += counts[r]
+    frame = torch.full((w * h,), -1, dtype=torch.int32, device=dev)
+    _lib.call("rt_unpack_rect", 0, w, h, nranks, _lib.ptr(rect), _lib.ptr(locs[0]), _lib.ptr(peers),
+              _lib.ptr(frame), None)
+    torch.cuda.synchronize()
+    got = frame.cpu().numpy().view(np.uint32)
+    assert (got == full).all(), int((got != full).sum())
+
+
 def test_native_comm_world1():
     """rt_comm_* end to end in a one-rank group: RCCL resolved at run time, the
     id broadcast, the communicator, and rt_comm_gather_frame's in-place slot 0
@@ -656,10 +701,12 @@ def test_native_comm_world1():
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream())
             cs.wait_event(ev)
-            ng.gather(k, cs.cuda_stream)
+            ng.gather(k, s.cam, None, 0, cs.cuda_stream)
         torch.cuda.synchronize()
         for k in range(2):
             assert (ng.frames[k].cpu().numpy().view(np.uint32) == full).all()
+        x0, x1, b0, b1 = ng.frame_rect(s.cam, None, 0)
+        assert (x1 - x0) * (b1 - b0) * 8 < w * h  # the fused render proves part of the frame background
         ng.close()
     finally:
         dist.destroy_process_group()
