@@ -3,11 +3,12 @@
 // The reference is single-GPU (cudaSetDevice(0), TD/Trixel.cu:213); this is
 // new.  Each rank renders its interleaved 8-row bands into a packed buffer
 // (rt_render_into with an rt_tile); one rt_comm_gather_frame call then moves
-// every peer's packed buffer to rank 0 over xGMI and assembles the frame
-// there, all stream-ordered on the caller's stream:
-//   ncclGroupStart; rank != 0: ncclSend(local -> 0)
-//                   rank == 0: ncclRecv(gathered + r*npk <- r) for r = 1..N-1
-//   ncclGroupEnd;   rank == 0: k_unpack(gathered -> frame)
+// every peer's part of the frame to rank 0 over xGMI and assembles the frame
+// there, all stream-ordered on the caller's stream.  Only the rectangle
+// rt_frame_rect names travels: outside it every pixel is provably background.
+//   rank != 0: k_pack_rect(local -> scratch); ncclSend(scratch -> 0)
+//   rank == 0: ncclRecv(scratch + off_r <- r) for r = 1..N-1 (one group);
+//              k_unpack_rect(local, scratch, background -> frame)
 // i.e. N-1 point-to-point transfers, one xGMI link per peer, no ring.  The
 // host cost is a handful of enqueue calls, so a frame loop (or a captured
 // graph of frames) is not bound by the collective's Python path.

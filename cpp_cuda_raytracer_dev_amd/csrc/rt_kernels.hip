@@ -1503,18 +1503,23 @@ __global__ void k_pack_rect(int32_t w, int32_t x0, int32_t cw, int32_t s0, const
 
 // Rank 0: frame row y (blockIdx.y) from rank 0's own packed buffer, a peer's
 // compact block (peers 1..N-1 back to back), or the background.
-__global__ void k_unpack_rect(int32_t w, int32_t nranks, int32_t x0, int32_t x1, int32_t b0, int32_t b1,
+// Each thread writes `vec` (4 or 1) consecutive pixels of the row; rows
+// outside the rectangle are pure background stores.
+__global__ void k_unpack_rect(int32_t w, int32_t nranks, int32_t x0, int32_t x1, int32_t b0, int32_t b1, int32_t vec,
                               const uint32_t* __restrict__ local0, const uint32_t* __restrict__ peers,
                               uint32_t* __restrict__ frame) {
     const int32_t y = blockIdx.y;
-    const int32_t x = blockIdx.x * blockDim.x + threadIdx.x;
-    if (x >= w) return;
+    const int32_t xs = (blockIdx.x * blockDim.x + threadIdx.x) * vec;
+    if (xs >= w) return;
     const int32_t band = y / kTileH, r = y - band * kTileH;
     const int32_t rank = band % nranks, slot = band / nranks;
-    uint32_t v = kBackground;
-    if (x >= x0 && x < x1 && band >= b0 && band < b1) {
+    uint32_t v0 = kBackground, v1 = kBackground, v2 = kBackground, v3 = kBackground;
+    if (band >= b0 && band < b1 && xs + vec > x0 && xs < x1) {
+        const uint32_t* src;
+        int32_t sx;  // source index of column x: src[x - sx]
         if (rank == 0) {
-            v = local0[((int64_t)slot * kTileH + r) * w + x];
+            src = local0 + ((int64_t)slot * kTileH + r) * w;
+            sx = 0;
         } else {
             const int32_t cw = x1 - x0;
             int64_t off = 0;
@@ -1524,10 +1529,23 @@ __global__ void k_unpack_rect(int32_t w, int32_t nranks, int32_t x0, int32_t x1,
                 off += (int64_t)(s1 - s0) * kTileH * cw;
             }
             rect_slots(b0, b1, nranks, rank, s0, s1);
-            v = peers[off + ((int64_t)(slot - s0) * kTileH + r) * cw + (x - x0)];
+            src = peers + off + ((int64_t)(slot - s0) * kTileH + r) * cw;
+            sx = x0;
+        }
+        // straight-line per pixel (an indexed array would live in scratch)
+        if (xs >= x0 && xs < x1) v0 = src[xs - sx];
+        if (vec == 4) {
+            if (xs + 1 >= x0 && xs + 1 < x1) v1 = src[xs + 1 - sx];
+            if (xs + 2 >= x0 && xs + 2 < x1) v2 = src[xs + 2 - sx];
+            if (xs + 3 >= x0 && xs + 3 < x1) v3 = src[xs + 3 - sx];
         }
     }
-    frame[(int64_t)y * w + x] = v;
+    uint32_t* dst = frame + (int64_t)y * w + xs;
+    if (vec == 4) {
+        *reinterpret_cast<uint4*>(dst) = make_uint4(v0, v1, v2, v3);
+    } else {
+        dst[0] = v0;
+    }
 }
 
 template <class K>
@@ -1666,8 +1684,10 @@ int launch_pack_rect(int32_t w, int32_t h, int32_t nranks, int32_t rank, const i
 int launch_unpack_rect(int32_t w, int32_t h, int32_t nranks, const int32_t rect[4], const uint32_t* local0,
                        const uint32_t* peers, uint32_t* frame, void* stream) {
     if ((int64_t)w * h == 0) return RT_OK;
-    const dim3 grid((unsigned)((w + 255) / 256), (unsigned)h);
-    k_unpack_rect<<<grid, 256, 0, (hipStream_t)stream>>>(w, nranks, rect[0], rect[1], rect[2], rect[3], local0,
+    const int32_t vec = ((w & 3) == 0 && ((uintptr_t)frame & 15) == 0) ? 4 : 1;
+    const int32_t per_row = w / vec;
+    const dim3 grid((unsigned)((per_row + 255) / 256), (unsigned)h);
+    k_unpack_rect<<<grid, 256, 0, (hipStream_t)stream>>>(w, nranks, rect[0], rect[1], rect[2], rect[3], vec, local0,
                                                          peers, frame);
     return check_launch<void>("k_unpack_rect");
 }

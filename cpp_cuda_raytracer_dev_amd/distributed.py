@@ -92,12 +92,12 @@ class NativeFrameGather:
     """The gather through the library's own RCCL communicator (rt_comm_*).
 
     One rt_comm_gather_frame call per frame enqueues, on the given stream, the
-    peers' ncclSend to rank 0, rank 0's N-1 ncclRecv into its gathered buffer
-    and the unpack kernel -- no Python collective per frame.  `nbuf` sets of
-    buffers let frame i+1 render while frame i is in flight (bench.py
-    pipelines them with events).  On rank 0 the local buffer of set k is slot
-    0 of gathered[k], so its own bands are rendered in place.  The 128-byte
-    RCCL id is broadcast with `dist` (any backend)."""
+    peers' pack kernel and ncclSend to rank 0, rank 0's N-1 ncclRecv and the
+    assembly kernel -- no Python collective per frame.  Only the rectangle
+    rt_frame_rect names travels (outside it the frame is provably
+    background).  `nbuf` sets of buffers let frame i+1 render while frame i
+    is in flight (bench.py pipelines them with events).  The 128-byte RCCL id
+    is broadcast with `dist` (any backend)."""
 
     def __init__(self, dist, w: int, h: int, device, nbuf: int = 2):
         import ctypes as C
