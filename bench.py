@@ -8,8 +8,9 @@ KD traversal, 1..N MI355X GPUs (BASELINE.json metric; configs C3/C4).
 
 A step is one frame: bg fill -> primary rays -> KD traversal -> Moller-
 Trumbore -> Phong into the u32 frame (one fused kernel), plus, for N > 1,
-the RCCL gather of every rank's screen bands to rank 0 and the unpack
-kernel there.  Frames are fixed-size (1920x1080), so N > 1 is strong
+the RCCL gather to rank 0 of every rank's screen bands (the part of them
+not provably background) and the frame assembly kernel there, pipelined
+with the next frame's render.  Frames are fixed-size (1920x1080), so N > 1 is strong
 scaling.  The scene is the seeded synthetic stand-in for
 dragon_vrip_mod.ply (missing from the reference; 871,414 triangles).
 Rank 0 prints one JSON line.
@@ -57,9 +58,10 @@ def parse():
     ap.add_argument("--items", type=int, default=2, help="kernel 3: items each lane pops per iteration (1, 2)")
     ap.add_argument("--coarse", type=int, default=8,
                     help="kernel 3: 8x8 groups per wave outside the root box's screen rectangle (0 = off)")
-    ap.add_argument("--event-every", type=int, default=1,
+    ap.add_argument("--event-every", type=int, default=0,
                     help="bracket every Nth timed frame with HIP events for the kernel time (each pair costs "
-                         "queue time, so N > 1 keeps the frame rate closer to the uninstrumented one)")
+                         "queue time, so N > 1 keeps the frame rate closer to the uninstrumented one); 0 = every frame "
+                         "at one GPU, every 8th with more, where a frame is a few tens of microseconds")
     ap.add_argument("--side-coarse", action="store_true",
                     help="kernel 3: run the coarse kernel beside the fine one on a side stream (default: before it)")
     ap.add_argument("--deliver", action="store_true",
@@ -268,6 +270,8 @@ def main():
         fg = None
         out = torch.zeros(w * h, dtype=torch.int32, device=dev)
 
+    if a.event_every <= 0:
+        a.event_every = 1 if world == 1 else 8
     timed_frames = list(range(0, a.steps, max(1, a.event_every)))
     ev = {i: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for i in timed_frames}
 
