@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--collective", default="rccl", choices=["rccl", "gather", "allgather"],
                     help="N>1 frame gather: rccl = the library's own RCCL send/recv + unpack (rt_comm_*, "
                          "pipelined); gather / allgather = torch.distributed collectives, one frame at a time")
+    ap.add_argument("--rehearse-gather", action="store_true",
+                    help="one process: run the N>1 frame loop (process group, gather, frame check) with one rank, "
+                         "to rehearse the multi-GPU path on a one-GPU machine; not a bench line")
     ap.add_argument("--pipeline", type=int, default=2,
                     help="rccl: buffer sets in flight (frame i+1 renders while frame i is gathered)")
     ap.add_argument("--kernel", type=int, default=3,
@@ -193,8 +196,14 @@ def main():
             return 2
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    multi = world > 1 or a.rehearse_gather
+    if multi:
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29531")
+            dist.init_process_group("nccl", device_id=dev, rank=0, world_size=1)
+        else:
+            dist.init_process_group("nccl", device_id=dev)
     w, h = a.width, a.height
 
     pts, leafs, nodes = build_scene(a.scene)
@@ -214,7 +223,7 @@ def main():
     tile = (world, rank)
 
     # Algorithmic counts of this rank's tiles (one untimed counting frame).
-    npk = R.packed_pixels(w, h, world) if world > 1 else w * h
+    npk = R.packed_pixels(w, h, world) if multi else w * h
     scratch = torch.zeros(npk, dtype=torch.int32, device=dev)
     sflag = R.RT_FLAG_SHADOW if a.shadow else 0
     masks = key_masks(a.animate) if a.animate else []
@@ -227,13 +236,13 @@ def main():
             mo.tick(masks[i % len(masks)])
             if i >= a.warmup:
                 cam.render_into(scratch, xform=mo.xform(), mode=a.mode, flags=R.RT_FLAG_COUNT | sflag,
-                                tile=tile if world > 1 else None, stream=sptr)
+                                tile=tile if multi else None, stream=sptr)
                 torch.cuda.synchronize(dev)
                 acc += cam.counters(reset=True)
         mo.close()
         cnt = acc / a.steps  # mean per frame
     else:
-        cam.render_into(scratch, mode=a.mode, flags=R.RT_FLAG_COUNT | sflag, tile=tile if world > 1 else None,
+        cam.render_into(scratch, mode=a.mode, flags=R.RT_FLAG_COUNT | sflag, tile=tile if multi else None,
                         stream=sptr)
         torch.cuda.synchronize(dev)
         cnt = cam.counters(reset=True)
@@ -244,14 +253,14 @@ def main():
     cam.set_option(_lib.RT_OPT_SHADOW_ORDER, a.shadow_order)
     if a.side_coarse:
         cam.set_option(_lib.RT_OPT_DEBUG, 8)
-    cam.render_into(scratch, mode=a.mode, flags=sflag, tile=tile if world > 1 else None,
+    cam.render_into(scratch, mode=a.mode, flags=sflag, tile=tile if multi else None,
                     stream=sptr)  # re-prepares layout
     torch.cuda.synchronize(dev)
     my_pix = int(np.count_nonzero(np.repeat(np.arange((h + 7) // 8) % world == rank, 8)[:h])) * w
     bytes_per_launch = B_INT * int(cnt[0]) + B_LEAF * int(cnt[1]) + B_HIT * int(cnt[2]) + B_PIX * my_pix
 
     ng = None
-    if world > 1 and a.collective == "rccl":
+    if multi and a.collective == "rccl":
         fg = None
         ng = NativeFrameGather(dist, w, h, dev, nbuf=max(1, a.pipeline))
         nbuf = len(ng.local)
@@ -261,7 +270,7 @@ def main():
         for k in range(nbuf):
             sent[k].record(cstream)
         out = ng.local[0]
-    elif world > 1:
+    elif multi:
         def unpack(g, f):
             R.unpack_bands(local, w, h, world, g, f, stream=torch.cuda.current_stream(dev).cuda_stream)
         fg = FrameGather(dist, w, h, dev, a.collective, unpack=unpack)
@@ -271,7 +280,7 @@ def main():
         out = torch.zeros(w * h, dtype=torch.int32, device=dev)
 
     if a.event_every <= 0:
-        a.event_every = 1 if world == 1 else 8
+        a.event_every = 8 if multi else 1
     timed_frames = list(range(0, a.steps, max(1, a.event_every)))
     ev = {i: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for i in timed_frames}
 
@@ -304,7 +313,7 @@ def main():
         with torch.cuda.stream(stream):
             if i in ev:
                 ev[i][0].record(stream)
-            cam.render_into(out, xform=xf, mode=a.mode, flags=sflag, tile=tile if world > 1 else None,
+            cam.render_into(out, xform=xf, mode=a.mode, flags=sflag, tile=tile if multi else None,
                             stream=sptr)
             if i in ev:
                 ev[i][1].record(stream)
@@ -314,19 +323,19 @@ def main():
     for _ in range(a.warmup):
         frame()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if multi:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(a.steps):
         frame(i)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if multi:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     frame_check = None
-    if world > 1 and rank == 0:
+    if multi and rank == 0:
         # the last gathered frame against a full frame rendered here (untimed)
         got = ng.frames[(seq[0] - 1) % nbuf] if ng is not None else fg.frame
         full = torch.zeros(w * h, dtype=torch.int32, device=dev)
@@ -342,11 +351,11 @@ def main():
         full_walk = cnt
         cam.set_option(_lib.RT_OPT_DEBUG, 16 | (8 if a.side_coarse else 0))
         cam.render_into(scratch, xform=xf, mode=a.mode, flags=R.RT_FLAG_COUNT | sflag,
-                        tile=tile if world > 1 else None, stream=sptr)
+                        tile=tile if multi else None, stream=sptr)
         torch.cuda.synchronize(dev)
         cnt = cam.counters(reset=True)
         bytes_per_launch = B_INT * int(cnt[0]) + B_LEAF * int(cnt[1]) + B_HIT * int(cnt[2]) + B_PIX * my_pix
-    if world > 1:
+    if multi:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms_max = float(t[0]), float(t[1])
@@ -395,7 +404,7 @@ def main():
                 "scene": f"synthetic {a.scene} stand-in, {len(pts)} triangles (seed 20221015)",
                 "resolution": [w, h],
                 "parallelism": f"screen bands x{world}" + ((" + RCCL send/recv to rank 0, pipelined" if a.collective == "rccl"
-                                                         else f" + torch {a.collective} to rank 0") if world > 1 else ""),
+                                                         else f" + torch {a.collective} to rank 0") if multi else ""),
             },
             "roofline": {
                 "bound": "hbm",
@@ -434,7 +443,7 @@ def main():
         else:
             res["cpu_baseline"] = None
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if multi:
         dist.barrier()
         if ng is not None:
             ng.close()
