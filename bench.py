@@ -14,6 +14,19 @@ with the next frame's render.  Frames are fixed-size (1920x1080), so N > 1 is st
 scaling.  The scene is the seeded synthetic stand-in for
 dragon_vrip_mod.ply (missing from the reference; 871,414 triangles).
 Rank 0 prints one JSON line.
+
+The other BASELINE configs are selected with flags:
+    C1  --cpu-only --scene tester --width 320 --height 180   (CPU path, no GPU)
+    C2  --scene rabbit_70k --width 960 --height 540 --mode 1  (flat list, VALU roofline)
+    C3  --width 960 --height 540
+    C5  --scene happy --width 3840 --height 2160 --shadow
+and README.md:19's high-coverage view with --view fill.
+
+After the timed frames every line carries `device_err` (the camera's device
+error word; the run exits non-zero when it is set) and, at N = 1, a
+`frame_check`: the last timed frame against the oracle's committed full-frame
+hash (tests/golden/frame_hashes.json), or against an oracle render on this
+host when no hash matches.
 """
 from __future__ import annotations
 
@@ -31,6 +44,14 @@ sys.path.insert(0, ROOT)
 METRIC = "frames/sec + Mray/s at 1920×1080, Stanford dragon 800k tris, 1/2/4/8 GPU"
 W, H = 1920, 1080
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# FP32 vector peak (MI355X_MICROARCH.md): 256 CU x 128 lanes x 2.4 GHz = 78.6e12
+# instructions/s, x2 for packed v_pk_* = 157.3 TFLOP/s (the spec counts an FMA
+# as 2; with contraction off every flop is its own operation, so 157.3 is the
+# most a packed non-FMA stream can reach, 78.6 the unpacked one)
+VALU_PEAK_TFLOPS, VALU_PEAK_UNPACKED_TFLOPS = 157.3, 78.6
+# 28 FP32 flops + one correctly rounded divide per flat test
+FLOPS_PER_TEST = 28
+HASHES = os.path.join(ROOT, "tests", "golden", "frame_hashes.json")
 # bytes per interior visit, leaf visit, accepted hit, pixel
 B_INT, B_LEAF, B_HIT, B_PIX = 36, 40, 24, 4
 
@@ -40,7 +61,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--scene", default="dragon", choices=["dragon", "happy"])
+    ap.add_argument("--scene", default="dragon", choices=["dragon", "happy", "rabbit_70k", "tester"],
+                    help="dragon / happy: seeded stand-ins for the missing meshes; rabbit_70k / tester: the "
+                         "reference's own meshes")
+    ap.add_argument("--view", default="default", choices=["default", "fill"],
+                    help="default: WinMain's camera; fill: the object over >= 90%% of the pixels (README.md:19)")
+    ap.add_argument("--cpu-only", action="store_true",
+                    help="config C1: the CPU path only (the oracle), no GPU; value = its frames/s")
     ap.add_argument("--width", type=int, default=W)
     ap.add_argument("--height", type=int, default=H)
     ap.add_argument("--mode", type=int, default=0, help="0 KD, 1 flat list")
@@ -77,33 +104,95 @@ def parse():
                          "a tick with none; one input tick (TD/WinMain.cpp:186-209) before each frame, timed")
     ap.add_argument("--shadow", action="store_true",
                     help="one shadow ray per hit (config C5: --scene happy --width 3840 --height 2160 --shadow)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0,
+                    help="CPU baseline sample length, for each of the 1-thread and all-thread runs")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (0: OMP_NUM_THREADS, else the CPUs this process may use)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
 
 def build_scene(name):
+    """(points9, leafs, nodes, timings): read_ply's face assembly and the KD
+    build (a11) on this host, the build timed with all threads and one."""
     from cpp_cuda_raytracer_dev_amd import raytracer as R, scenes
-    v, f = scenes.standin(name)
-    pts, n, leafs = R.assemble_mesh(v, f)
+    v, arity, idx = scenes.mesh_arrays(name)
+    pts, n, leafs = R.assemble_mesh(v, scenes.faces_of(arity, idx))
+    t0 = time.perf_counter()
     nodes = R.kd_build(leafs)
-    return pts, leafs, nodes
+    t1 = time.perf_counter()
+    R.kd_build(leafs, nthreads=1)
+    t2 = time.perf_counter()
+    return pts, leafs, nodes, {"kd_build_s": round(t1 - t0, 4), "kd_build_s_1thread": round(t2 - t1, 4)}
 
 
-def cpu_baseline(pts, nodes, w, h, seconds, threads, mode, shadow=False, rays_per_frame=None):
-    """The oracle (C restatement, -O2, OpenMP over rows) on the same frame,
-    repeated for ~`seconds`.  Test infrastructure: the checker, timed beside
-    the GPU; never part of the product path."""
+def cpu_threads(requested: int) -> int:
+    if requested > 0:
+        return requested
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        return int(env)
+    return len(os.sched_getaffinity(0))
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as fp:
+            for line in fp:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def data_label(scene: str) -> str:
+    from cpp_cuda_raytracer_dev_amd import scenes
+    return "synthetic" if scene in scenes.STANDINS else f"{scene}.ply from the reference (TD/), parsed with strtof"
+
+
+def frame_key(scene, w, h, mode, shadow, view):
+    return f"{scene}_{w}x{h}_m{mode}" + ("_shadow" if shadow else "") + ("" if view == "default" else f"_{view}")
+
+
+def reference_frame(scene, w, h, mode, shadow, view):
+    """The committed oracle entry for this frame (tests/golden/frame_hashes.json)
+    when its mesh bytes equal this host's, else None."""
+    from cpp_cuda_raytracer_dev_amd import scenes
+    try:
+        with open(HASHES) as fp:
+            ent = json.load(fp)["frames"].get(frame_key(scene, w, h, mode, shadow, view))
+    except (OSError, ValueError, KeyError):
+        return None
+    if ent is None or ent.get("mesh_sha") != scenes.mesh_sha(scene):
+        return None
+    return ent
+
+
+def frame_check_n1(argb: np.ndarray, pts, nodes, cam_kw, a, xform=None):
+    """The last timed frame against the oracle: its committed full-frame hash,
+    or (no hash for this frame / mesh, or a moved object) an oracle render
+    here (KD mode)."""
+    import hashlib
+    got = hashlib.sha256(np.ascontiguousarray(argb).tobytes()).hexdigest()
+    ent = None if a.animate else reference_frame(a.scene, a.width, a.height, a.mode, a.shadow, a.view)
+    if ent is not None:
+        return {"matches_oracle": got == ent["argb_sha"], "method": "sha256 vs tests/golden/frame_hashes.json "
+                f"[{frame_key(a.scene, a.width, a.height, a.mode, a.shadow, a.view)}]"}
+    if a.mode != 0:
+        return {"matches_oracle": None, "method": "no committed hash; the flat oracle is too slow to run here"}
     from oracle import _oracle as O
     on = np.zeros(len(nodes), O.NODE_DTYPE)
     for k in nodes.dtype.names:
         on[k] = nodes[k]
-    s = O.Scene(pts, O.default_rad(len(pts)), on if mode == 0 else None, O.camera(w, h))
-    rows = (0, h)
-    if mode == 1:  # flat list is O(npix*ntri): sample a band of rows
-        rows = (h // 2 - 4, h // 2 + 4)
+    s = O.Scene(pts, O.default_rad(len(pts)), on, O.camera(a.width, a.height, **cam_kw))
+    ref, _, _ = s.render(0, xform=xform, nthreads=cpu_threads(a.cpu_threads), want_hit=False, shadow=a.shadow)
+    s.close()
+    return {"matches_oracle": bool(np.array_equal(ref, argb)), "method": "oracle render on this host"}
+
+
+def _oracle_fps(s, mode, rows, h, seconds, threads, shadow):
     frames, t0 = 0, time.perf_counter()
     while True:
         s.render(mode, rows=rows, nthreads=threads, want_hit=False, shadow=shadow)
@@ -111,13 +200,85 @@ def cpu_baseline(pts, nodes, w, h, seconds, threads, mode, shadow=False, rays_pe
         if time.perf_counter() - t0 >= seconds and frames >= 2:
             break
     dt = time.perf_counter() - t0
+    return frames * (rows[1] - rows[0]) / h / dt, frames, dt
+
+
+def cpu_baseline(pts, nodes, w, h, seconds, threads, mode, shadow=False, rays_per_frame=None, cam_kw=None,
+                 build_times=None):
+    """The oracle (C restatement, gcc -O3 -ffp-contract=off, OpenMP over rows)
+    on the same frame, repeated for ~`seconds` with all `threads` and with
+    one.  The reference has no CPU intersect path, so this
+    restatement is the CPU baseline (kind "port").  Test infrastructure: the
+    checker, timed beside the GPU; never part of the product path."""
+    from oracle import _oracle as O
+    on = np.zeros(len(nodes), O.NODE_DTYPE)
+    for k in nodes.dtype.names:
+        on[k] = nodes[k]
+    s = O.Scene(pts, O.default_rad(len(pts)), on if mode == 0 else None, O.camera(w, h, **(cam_kw or {})))
+    rows = (0, h)
+    if mode == 1:  # flat list is O(npix*ntri): sample a band of rows through the object
+        rows = (h // 2 - 4, h // 2 + 4)
+    fps, frames, dt = _oracle_fps(s, mode, rows, h, seconds, threads, shadow)
+    rows1 = rows if mode == 1 else (h // 2 - h // 16, h // 2 + h // 16)  # one thread: the middle eighth
+    fps1, frames1, dt1 = _oracle_fps(s, mode, rows1, h, seconds, 1, shadow)
     s.close()
-    frac = (rows[1] - rows[0]) / h
-    fps = frames * frac / dt
-    return {"value": round(fps, 3), "unit": "frames/s", "cores": threads, "kind": "port",
-            "mray_per_s": round(fps * (rays_per_frame or w * h) / 1e6, 3),
-            "sample": f"{frames} x rows {rows[0]}-{rows[1]} of the same {w}x{h} frame, oracle/oracle.c "
-                      f"(-O2 -ffp-contract=off, OpenMP {threads} threads), {dt:.1f} s"}
+    rpf = rays_per_frame or w * h
+    out = {"value": round(fps, 3), "unit": "frames/s", "cores": threads, "kind": "port",
+           "mray_per_s": round(fps * rpf / 1e6, 3),
+           "value_1thread": round(fps1, 3), "mray_per_s_1thread": round(fps1 * rpf / 1e6, 3),
+           "nproc": os.cpu_count(), "cpus_allowed": len(os.sched_getaffinity(0)), "cpu_model": cpu_model(),
+           "sample": f"{frames} x rows {rows[0]}-{rows[1]} of the same {w}x{h} frame with {threads} threads "
+                     f"({dt:.1f} s), {frames1} x rows {rows1[0]}-{rows1[1]} with 1 thread ({dt1:.1f} s); "
+                     "oracle/oracle.c (gcc -O3 -ffp-contract=off, OpenMP over rows)"}
+    if build_times:
+        out["kd_build"] = {**build_times, "what": "rt_kd_build (a11, TD/Trixel.h:135-473) on this host, "
+                                                  "all threads / 1 thread"}
+    return out
+
+
+def cpu_only(a):
+    """Config C1: the CPU path alone (no GPU): the oracle's full frames."""
+    from cpp_cuda_raytracer_dev_amd import scenes
+    from oracle import _oracle as O
+    import hashlib
+    w, h = a.width, a.height
+    pts, leafs, nodes, bt = build_scene(a.scene)
+    on = np.zeros(len(nodes), O.NODE_DTYPE)
+    for k in nodes.dtype.names:
+        on[k] = nodes[k]
+    cam_kw = scenes.view(a.scene, a.view)
+    s = O.Scene(pts, O.default_rad(len(pts)), on if a.mode == 0 else None, O.camera(w, h, **cam_kw))
+    threads = cpu_threads(a.cpu_threads)
+    argb, hit, cnt = s.render(a.mode, nthreads=threads, shadow=a.shadow)
+    fps, frames, dt = _oracle_fps(s, a.mode, (0, h), h, a.cpu_seconds, threads, a.shadow)
+    fps1, frames1, dt1 = _oracle_fps(s, a.mode, (0, h), h, a.cpu_seconds, 1, a.shadow)
+    s.close()
+    ent = reference_frame(a.scene, w, h, a.mode, a.shadow, a.view)
+    got = hashlib.sha256(argb.tobytes()).hexdigest()
+    rpf = w * h + (int((hit >= 0).sum()) if a.shadow else 0)
+    res = {
+        "metric": METRIC, "value": round(fps, 2), "unit": "frames/s", "mray_per_s": round(fps * rpf / 1e6, 3),
+        "n_gpus": 0, "steps": frames, "warmup": 1, "ms_per_step": round(1e3 * dt / frames, 4),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+        "data": data_label(a.scene),
+        "config": {"workload": f"{a.scene} {w}x{h}, CPU-only intersect path ({'KD traversal' if a.mode == 0 else 'flat list'}"
+                               " + Phong, u32 frame), config C1",
+                   "scene": f"{a.scene} ({len(pts)} triangles)", "resolution": [w, h], "view": a.view,
+                   "coverage": round(float((hit >= 0).mean()), 4), "parallelism": f"OpenMP x{threads}"},
+        "roofline": None,
+        "frame_check": {"matches_oracle": (got == ent["argb_sha"]) if ent else None,
+                        "method": "sha256 vs tests/golden/frame_hashes.json" if ent else "no committed hash"},
+        "cpu_baseline": {"value": round(fps, 3), "unit": "frames/s", "cores": threads, "kind": "port",
+                         "value_1thread": round(fps1, 3), "nproc": os.cpu_count(),
+                         "cpus_allowed": len(os.sched_getaffinity(0)), "cpu_model": cpu_model(),
+                         "kd_build": bt,
+                         "sample": f"{frames} full frames with {threads} threads ({dt:.1f} s), {frames1} with 1 thread "
+                                   f"({dt1:.1f} s); oracle/oracle.c (gcc -O3 -ffp-contract=off)"},
+        "note": "C1 is the CPU path (BASELINE.json configs[0]): the reference has no CPU intersect path, so this is "
+                "the build's C restatement (oracle/oracle.c); no GPU kernel runs, so there is no roofline",
+    }
+    print(json.dumps(res), flush=True)
+    return 0 if res["frame_check"]["matches_oracle"] is not False else 1
 
 
 def delivery(cam, R, torch, dev, w, h, xf, mode, sflag, steps, warmup):
@@ -182,6 +343,8 @@ def key_masks(spec: str) -> list:
 
 def main():
     a = parse()
+    if a.cpu_only:
+        return cpu_only(a)
     import torch
     import torch.distributed as dist
     from cpp_cuda_raytracer_dev_amd import raytracer as R
@@ -206,10 +369,13 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
     w, h = a.width, a.height
 
-    pts, leafs, nodes = build_scene(a.scene)
+    from cpp_cuda_raytracer_dev_amd import scenes
+    pts, leafs, nodes, build_times = build_scene(a.scene)
     trixel = R.Trixel(len(pts), pts, device=local)
     trixel.set_kd_nodes(nodes)
-    cam = R.Camera.default(w, h, device=local)
+    cam_kw = scenes.view(a.scene, a.view)
+    cam = R.Camera(w, h, R.film_w(w, h), np.float32(.024), np.float32(.055), *cam_kw["pos"], *cam_kw["look_at"],
+                   0.0, 1.0, 0.0, device=local)
     from cpp_cuda_raytracer_dev_amd import _lib
     # the counting frame runs the reference's DFS order (kernel 2); shadow
     # walks exist in kernel 3 only, whose accept count is the candidate count
@@ -334,14 +500,21 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    # the device error word of this rank's timed frames (stack / pool
+    # overflow, a far-group proof that failed): reported, and fatal below
+    dev_err = cam.device_error(reset=True)
     frame_check = None
+    if not multi and rank == 0:
+        frame_check = frame_check_n1(out.cpu().numpy().view(np.uint32), pts, nodes, cam_kw, a,
+                                     xform=xf if masks else None)
     if multi and rank == 0:
         # the last gathered frame against a full frame rendered here (untimed)
         got = ng.frames[(seq[0] - 1) % nbuf] if ng is not None else fg.frame
         full = torch.zeros(w * h, dtype=torch.int32, device=dev)
         cam.render_into(full, xform=xf, mode=a.mode, flags=sflag, stream=sptr)
         torch.cuda.synchronize(dev)
-        frame_check = bool(torch.equal(got, full))
+        frame_check = {"gathered_equals_single_gpu_frame": bool(torch.equal(got, full)),
+                       "collective": a.collective + (f", {nbuf} buffer sets" if ng is not None else "")}
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev.values()]))
     full_walk = None
     if a.shadow and not masks:
@@ -355,7 +528,11 @@ def main():
         torch.cuda.synchronize(dev)
         cnt = cam.counters(reset=True)
         bytes_per_launch = B_INT * int(cnt[0]) + B_LEAF * int(cnt[1]) + B_HIT * int(cnt[2]) + B_PIX * my_pix
+    errs = [dev_err]
     if multi:
+        te = torch.zeros(world, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(te, torch.tensor([dev_err], dtype=torch.int64, device=dev))
+        errs = [int(x) for x in te.cpu()]
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms_max = float(t[0]), float(t[1])
@@ -370,9 +547,12 @@ def main():
     # rays per frame: every pixel's primary ray, plus a shadow ray per hit
     rays_per_frame = w * h + (hits_all if a.shadow else 0)
 
+    rc = 0
     if rank == 0:
         fps = a.steps / elapsed
         achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+        tests = w * h * len(pts)  # flat list: every ray against every triangle
+        tflops = FLOPS_PER_TEST * tests / (kern_ms * 1e-3) / 1e12
         traffic = None
         if os.path.exists(a.traffic_json):
             try:
@@ -394,19 +574,43 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic",
+            "data": data_label(a.scene),
             "config": {
-                "workload": f"{a.scene} stand-in {w}x{h}, {'KD traversal' if a.mode == 0 else 'flat list'}, "
+                "workload": f"{a.scene}{' stand-in' if a.scene in scenes.STANDINS else ''} {w}x{h}"
+                            + ("" if a.view == "default" else f" ({a.view} view)")
+                            + f", {'KD traversal' if a.mode == 0 else 'flat list'}, "
                             + ("primary + one shadow ray per hit" if a.shadow else "primary rays")
                             + " + Phong, u32 frame on GPU 0"
                             + (f", object moved by keys {a.animate!r} (one tick per frame)" if masks else ""),
                 "rays_per_frame": rays_per_frame,
-                "scene": f"synthetic {a.scene} stand-in, {len(pts)} triangles (seed 20221015)",
+                "scene": (f"synthetic {a.scene} stand-in, {len(pts)} triangles (seed 20221015)"
+                          if a.scene in scenes.STANDINS else f"{a.scene}.ply (the reference's mesh), {len(pts)} triangles"),
                 "resolution": [w, h],
+                "view": {"name": a.view, **cam_kw},
+                "coverage": round(hits_all / (w * h), 5),
                 "parallelism": f"screen bands x{world}" + ((" + RCCL send/recv to rank 0, pipelined" if a.collective == "rccl"
                                                          else f" + torch {a.collective} to rank 0") if multi else ""),
             },
-            "roofline": {
+            "roofline": ({
+                "bound": "valu",
+                "achieved": round(tflops, 2),
+                "peak": VALU_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": round(tflops / VALU_PEAK_TFLOPS, 4),
+                "traffic": None,
+                "kernel": "k_trace_flat",
+                "kernel_ms_avg": round(kern_ms, 5),
+                "kernel_ms_frames": f"{len(ev)} of {a.steps} timed frames (every {max(1, a.event_every)})",
+                "kernel_ms_avg_max_rank": round(kern_ms_max, 5),
+                "tests_per_launch": tests,
+                "flops_per_launch": FLOPS_PER_TEST * tests,
+                "divides_per_launch": tests,
+                "peak_unpacked": VALU_PEAK_UNPACKED_TFLOPS,
+                "flops_model": "28 FP32 flops + 1 divide per ray-triangle test x npix x ntri (SURVEY.md 8d, "
+                               "TD/Trixel.cu:173-209); peak = FP32 vector spec (packed issue), 78.6 unpacked",
+                "counts_per_launch": {"leaf_tests": int(cnt[1]), "accept": int(cnt[2]), "hit_pixels": int(cnt[3]),
+                                      "pixels": my_pix},
+            } if a.mode == 1 else {
                 "bound": "hbm",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
@@ -430,25 +634,33 @@ def main():
                 **({"counts_full_shadow_walk": {"interior": int(full_walk[0]), "leaf": int(full_walk[1]),
                                                 "accept": int(full_walk[2])}} if full_walk is not None else {}),
                 "bytes_model": "36*V_int + 40*V_leaf + 24*H + 4*P (SURVEY.md 8d)",
-            },
+            }),
+            "device_err": errs if multi else dev_err,
         }
         if frame_check is not None:
-            res["frame_check"] = {"gathered_equals_single_gpu_frame": frame_check,
-                                  "collective": a.collective + (f", {nbuf} buffer sets" if ng is not None else "")}
+            res["frame_check"] = frame_check
         if a.deliver and world == 1:
             res["delivery"] = delivery(cam, R, torch, dev, w, h, xf, a.mode, sflag, a.steps, a.warmup)
         if not a.no_cpu_baseline and world == 1:
-            res["cpu_baseline"] = cpu_baseline(pts, nodes, w, h, a.cpu_seconds, a.cpu_threads, a.mode, a.shadow,
-                                              rays_per_frame)
+            res["cpu_baseline"] = cpu_baseline(pts, nodes, w, h, a.cpu_seconds, cpu_threads(a.cpu_threads), a.mode,
+                                              a.shadow, rays_per_frame, cam_kw, build_times)
         else:
             res["cpu_baseline"] = None
         print(json.dumps(res), flush=True)
+        bad = [e for e in errs if e]
+        fc = (frame_check or {}).get("matches_oracle", (frame_check or {}).get("gathered_equals_single_gpu_frame"))
+        if bad:
+            print(f"bench.py: device error word {errs} after the timed frames", file=sys.stderr)
+            rc = 3
+        elif fc is False:
+            print("bench.py: frame_check failed", file=sys.stderr)
+            rc = 4
     if multi:
         dist.barrier()
         if ng is not None:
             ng.close()
         dist.destroy_process_group()
-    return 0
+    return rc
 
 
 if __name__ == "__main__":

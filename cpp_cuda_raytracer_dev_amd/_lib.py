@@ -101,6 +101,7 @@ SIGNATURES = {
     "rt_object_xform": (C.c_int, [_P, _P]),
     "rt_object_state": (C.c_int, [_P, _P, _P, _P, _P]),
     "rt_object_destroy": (None, [_P]),
+    "rt_camera_error": (C.c_int, [_P, C.POINTER(C.c_int32), C.c_int]),
     "rt_camera_info": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "rt_camera_set_option": (C.c_int, [_P, C.c_int32, C.c_int32]),
     "rt_camera_get_option": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_int32)]),

@@ -995,6 +995,16 @@ extern "C" int rt_camera_counters(rt_camera* c, uint64_t out[5], int reset) {
     return RT_OK;
 }
 
+extern "C" int rt_camera_error(rt_camera* c, int32_t* err, int reset) {
+    if (!c || !err) return fail(RT_ERR_INVALID, "rt_camera_error: null argument");
+    DeviceGuard g(c->device);
+    int rc;
+    if ((rc = hip_check(hipDeviceSynchronize(), "rt_camera_error sync"))) return rc;
+    if ((rc = hip_check(hipMemcpy(err, c->d_err, sizeof *err, hipMemcpyDeviceToHost), "D2H err"))) return rc;
+    if (reset && (rc = hip_check(hipMemset(c->d_err, 0, sizeof(int32_t)), "reset err"))) return rc;
+    return RT_OK;
+}
+
 extern "C" int rt_camera_info(const rt_camera* c, int32_t* w, int32_t* h, int32_t* max_depth) {
     if (!c) return fail(RT_ERR_INVALID, "rt_camera_info: null camera");
     if (w) *w = c->w;

@@ -342,6 +342,13 @@ class Camera:
         _lib.call("rt_camera_counters", self._h, _lib.ptr(out), int(reset))
         return out
 
+    def device_error(self, reset: bool = False) -> int:
+        """The device error word every render ORs into (rt_camera_error):
+        1 stack overflow, 2 item-pool overflow, 4 far-group proof failed."""
+        e = C.c_int32()
+        _lib.call("rt_camera_error", self._h, C.byref(e), int(reset))
+        return e.value
+
     def frame(self) -> np.ndarray:
         """h_color as [h, w] u32, row 0 = bottom (the DIB is bottom-up)."""
         w, h = self.res

@@ -29,6 +29,29 @@ STANDINS = {
 }
 STANDIN_SEED = 20221015
 
+#: WinMain's camera (TD/WinMain.cpp:69-74): every view keeps its film and
+#: focal length; only the position and look-at point change.
+DEFAULT_VIEW = {"pos": (0.0, 0.1, -1.0), "look_at": (0.0, 0.1, 0.0)}
+#: "fill" views put the object over >= 90 % of the pixels (README.md:19 quotes
+#: "25 FPS at 90%+ pixel coverage" beside the default view's ~100 FPS): the
+#: camera looks along +z at the object's box centre from closer in.  Found by
+#: rendering the oracle at 192x108; the coverage at each resolution is
+#: recorded with the frame hashes (tests/golden/frame_hashes.json).
+FILL_VIEWS = {
+    "dragon": {"pos": (-0.0097, 0.1309, -0.2312), "look_at": (-0.0097, 0.1309, -0.0061)},   # ~94 %
+    "rabbit_70k": {"pos": (-0.0068, 0.0902, -0.1419), "look_at": (-0.0068, 0.0902, -0.0015)},  # ~95 %
+    "happy": {"pos": (-0.0037, 0.1512, -0.1147), "look_at": (-0.0037, 0.1512, 0.0061)},
+}
+
+
+def view(scene: str, name: str = "default") -> dict:
+    """Camera position / look-at of a named view ("default" or "fill")."""
+    if name == "default":
+        return dict(DEFAULT_VIEW)
+    if name == "fill":
+        return dict(FILL_VIEWS[scene])
+    raise KeyError(f"unknown view {name!r} (default, fill)")
+
 
 def fixture_mesh(name: str):
     """(verts [nv,3] f32, arity [nf] i32, idx [sum arity] i32) of a reference mesh."""
@@ -87,6 +110,36 @@ def standin(name: str):
     faces = np.concatenate([f, f2 + len(body)]).astype(np.int32)
     assert len(faces) == ntri, (name, len(faces))
     return verts, faces
+
+
+def mesh_arrays(name: str):
+    """(verts [nv,3] f32, arity [nf] i32, idx i32) of a reference fixture or a
+    stand-in, the input of read_ply's face assembly."""
+    if name in STANDINS:
+        v, f = standin(name)
+        return v, np.full(len(f), 3, np.int32), np.ascontiguousarray(f, np.int32).reshape(-1)
+    return fixture_mesh(name)
+
+
+def faces_of(arity: np.ndarray, idx: np.ndarray):
+    """Faces for raytracer.assemble_mesh: an [nf, k] array when every face has
+    k vertices, else a list of per-face index lists."""
+    if len(arity) and arity.min() == arity.max():
+        return np.asarray(idx, np.int32).reshape(len(arity), -1)
+    starts = np.r_[0, np.cumsum(arity)[:-1]]
+    return [list(idx[s:s + k]) for s, k in zip(starts, arity)]
+
+
+def mesh_sha(name: str) -> str:
+    """SHA-256 of a mesh's vertex and face arrays: frame hashes recorded for a
+    stand-in hold only where its (numpy-generated) vertices are the same."""
+    import hashlib
+    v, a, ix = mesh_arrays(name)
+    h = hashlib.sha256()
+    for arr in (np.ascontiguousarray(v, np.float32), np.ascontiguousarray(a, np.int32),
+                np.ascontiguousarray(ix, np.int32)):
+        h.update(arr.tobytes())
+    return h.hexdigest()
 
 
 def write_ply(path: str, verts: np.ndarray, faces: np.ndarray) -> None:

@@ -226,6 +226,15 @@ int rt_frame_copy_async(int device, const uint32_t* d_argb, uint32_t* h_argb, in
  * that descended.  reset != 0 zeroes them after reading.  Synchronises. */
 int rt_camera_counters(rt_camera* c, uint64_t out[5], int reset);
 
+/* The camera's device error word, which every render ORs into: 1 = DFS
+ * stack overflow (kernels 1-2), 2 = item pool overflow (kernel 3), 4 = a
+ * fused far group that was not provably background (kernel 3; the gathered
+ * frame's background then is not the rendered one).  The reference has no
+ * equivalent (its status is the last sync, TD/Trixel.cu:227-240).
+ * Synchronises the device; *err receives the word; reset != 0 clears it.
+ * Returns RT_OK even when *err is non-zero (the word is the report). */
+int rt_camera_error(rt_camera* c, int32_t* err, int reset);
+
 /* Kernel launch geometry and the traversal stack depth in use. */
 int rt_camera_info(const rt_camera* c, int32_t* w, int32_t* h, int32_t* max_depth);
 

@@ -4,7 +4,7 @@
  * TEST INFRASTRUCTURE ONLY (see oracle.h): the parity checker and the timed
  * CPU baseline ("kind": "port").  Never linked into the product library.
  *
- * Built with -O2 -ffp-contract=off on x86-64 (SSE scalar float, no x87), so
+ * Built with -O3 -ffp-contract=off on x86-64 (SSE scalar float, no x87), so
  * every float expression below is evaluated in IEEE single precision in the
  * written order, and every expression the reference promotes to double
  * (1e-16 epsilons, `.6*`, `*.3`, `1.0/f`) is evaluated in double (SURVEY.md

@@ -8,6 +8,7 @@ from cpp_cuda_raytracer_dev_amd import raytracer as R, scenes
 from oracle import _oracle as O
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "golden_frames.npz")
+HASHES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "frame_hashes.json")
 ORACLE_THREADS = int(os.environ.get("RT_ORACLE_THREADS", "16"))
 
 
@@ -100,3 +101,34 @@ class GpuScene:
 
 def golden():
     return np.load(GOLDEN, allow_pickle=False)
+
+
+_hashes = None
+
+
+def frame_hashes() -> dict:
+    """tests/golden/frame_hashes.json "frames": key -> oracle full-frame entry."""
+    global _hashes
+    if _hashes is None:
+        import json
+        with open(HASHES) as fp:
+            _hashes = json.load(fp)["frames"]
+    return _hashes
+
+
+def hash_keys():
+    return sorted(frame_hashes())
+
+
+def view_kw(ent) -> dict:
+    return {"pos": tuple(ent["camera"]["pos"]), "look_at": tuple(ent["camera"]["look_at"])}
+
+
+_mesh_sha = {}
+
+
+def mesh_matches(ent) -> bool:
+    """Whether this host generates the mesh the hash was recorded for."""
+    if ent["scene"] not in _mesh_sha:
+        _mesh_sha[ent["scene"]] = scenes.mesh_sha(ent["scene"])
+    return _mesh_sha[ent["scene"]] == ent["mesh_sha"]
