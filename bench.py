@@ -86,6 +86,9 @@ def parse():
                     help="0 XCD-contiguous, 1 natural, 2 centre-out, 3 by the cost an earlier frame measured")
     ap.add_argument("--rays", type=int, default=16, help="kernel 3: pixels per wave (64, 32, 16, 8)")
     ap.add_argument("--items", type=int, default=2, help="kernel 3: items each lane pops per iteration (1, 2)")
+    ap.add_argument("--flat", type=int, default=-1,
+                    help="flat-list kernel form: 0 one triangle per iteration, 1 pairs, 2 packed float2 pairs "
+                         "(-1: the library default)")
     ap.add_argument("--coarse", type=int, default=8,
                     help="kernel 3: 8x8 groups per wave outside the root box's screen rectangle (0 = off)")
     ap.add_argument("--event-every", type=int, default=0,
@@ -417,6 +420,8 @@ def main():
     cam.set_option(_lib.RT_OPT_ITEMS, a.items)
     cam.set_option(_lib.RT_OPT_COARSE, a.coarse)
     cam.set_option(_lib.RT_OPT_SHADOW_ORDER, a.shadow_order)
+    if a.flat >= 0:
+        cam.set_option(_lib.RT_OPT_FLAT, a.flat)
     if a.side_coarse:
         cam.set_option(_lib.RT_OPT_DEBUG, 8)
     cam.render_into(scratch, mode=a.mode, flags=sflag, tile=tile if multi else None,
@@ -599,6 +604,7 @@ def main():
                 "frac": round(tflops / VALU_PEAK_TFLOPS, 4),
                 "traffic": None,
                 "kernel": "k_trace_flat",
+                "kernel_form": cam.get_option(_lib.RT_OPT_FLAT),
                 "kernel_ms_avg": round(kern_ms, 5),
                 "kernel_ms_frames": f"{len(ev)} of {a.steps} timed frames (every {max(1, a.event_every)})",
                 "kernel_ms_avg_max_rank": round(kern_ms_max, 5),

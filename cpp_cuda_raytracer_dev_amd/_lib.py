@@ -27,6 +27,7 @@ RT_OPT_RAYS = 3
 RT_OPT_ITEMS = 4
 RT_OPT_COARSE = 5
 RT_OPT_SHADOW_ORDER = 6
+RT_OPT_FLAT = 7
 RT_OPT_DEBUG = 100
 RT_OPT_POOL_CAP = 101
 RT_COMM_ID_BYTES = 128

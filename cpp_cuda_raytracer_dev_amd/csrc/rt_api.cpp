@@ -43,6 +43,7 @@ struct rt_camera {
     uint64_t prepared_version = 0;
     float4* d_trec = nullptr;        // camera-relative triangle records
     float4* d_inode = nullptr;       // camera-relative interior nodes
+    float4* d_tpair = nullptr;       // flat variant 2: camera-relative triangle pairs
     uint32_t trec_cap = 0;
     int64_t inode_cap = 0;           // in float4
     int prepared_layout = 0;         // interior record layout of d_inode (1 or 2)
@@ -79,6 +80,7 @@ struct rt_camera {
     uint64_t order_gen = ~0ull;              // generation whose cost order d_order holds
     int rays = 16;                   // kOptRays: pixels per wave of kernel 3
     int items = 2;                   // kOptItems: items per lane per pool iteration
+    int flat_variant = 2;            // kOptFlat: flat-list kernel form
     // shadow renders: the any-hit push order, fixed (kOptShadowOrder 0..3)
     // or timed (-1): a round of trial frames runs each order kTuneReps times,
     // interleaved, bracketed by events; the fastest is kept for kTunePeriod
@@ -140,11 +142,17 @@ int prepare_camera_object(rt_camera* c) {
     int rc;
     if (c->trec_cap < s->ntri) {
         dev_free(c->d_trec);
-        if ((rc = dev_alloc(&c->d_trec, (size_t)s->ntri * 4, "hipMalloc(trec)"))) return rc;
+        dev_free(c->d_tpair);
+        if ((rc = dev_alloc(&c->d_trec, (size_t)s->ntri * 4, "hipMalloc(trec)")) ||
+            (rc = dev_alloc(&c->d_tpair, (size_t)((s->ntri + 1) / 2) * 8, "hipMalloc(tpair)")))
+            return rc;
         c->trec_cap = s->ntri;
     }
-    // init_camera_trixel_device_memory (TD/Trixel.cu:244-264)
-    if ((rc = launch_cam_tri(s->d_tri_world, s->ntri, c->pos, c->d_trec, nullptr))) return rc;
+    // init_camera_trixel_device_memory (TD/Trixel.cu:244-264), plus its pair
+    // layout for the packed flat-list kernel
+    if ((rc = launch_cam_tri(s->d_tri_world, s->ntri, c->pos, c->d_trec, nullptr)) ||
+        (rc = launch_pair_tri(c->d_trec, s->ntri, c->d_tpair, nullptr)))
+        return rc;
     if (s->d_nodes) {
         const int64_t need = std::max<int64_t>(s->ninterior, 1) * (layout == 1 ? 3 : 4);
         if (c->inode_cap < need) {
@@ -561,6 +569,8 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
     const rt_scene* s = c->obj;
     p.inode = c->d_inode;
     p.trec = c->d_trec;
+    p.tpair = c->d_tpair;
+    p.flat_variant = c->flat_variant;
     p.shade = s->d_shade;
     p.argb = argb;
     p.hit = hit;
@@ -1033,6 +1043,7 @@ extern "C" void rt_camera_destroy(rt_camera* c) {
     dev_free(c->d_err);
     dev_free(c->d_trec);
     dev_free(c->d_inode);
+    dev_free(c->d_tpair);
     dev_free(c->d_order);
     dev_free(c->d_dbg);
     dev_free(c->d_cost);
@@ -1084,6 +1095,10 @@ extern "C" int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value) {
         c->tune_frames = 0;
         c->tune_pending = false;
         return RT_OK;
+    case kOptFlat:
+        if (value < 0 || value > 2) return fail(RT_ERR_INVALID, "flat kernel form %d (0..2)", value);
+        c->flat_variant = value;
+        return RT_OK;
     case kOptTileOrder:
         if (value < 0 || value > 4) return fail(RT_ERR_INVALID, "tile order %d (0..4)", value);
         c->tile_order = value;
@@ -1101,6 +1116,7 @@ extern "C" int rt_camera_get_option(const rt_camera* c, int32_t key, int32_t* va
     case kOptRays: *value = c->rays; return RT_OK;
     case kOptItems: *value = c->items; return RT_OK;
     case kOptCoarse: *value = c->coarse; return RT_OK;
+    case kOptFlat: *value = c->flat_variant; return RT_OK;
     case kOptShadowOrder: *value = c->shadow_order >= 0 ? c->shadow_order : c->any_best; return RT_OK;
     default: return fail(RT_ERR_INVALID, "rt_camera_get_option: unknown key %d", key);
     }

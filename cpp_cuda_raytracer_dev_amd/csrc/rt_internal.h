@@ -45,6 +45,7 @@ enum Option : int32_t {
     kOptItems = 4,      // kernel 3 items popped per lane per iteration: 1 or 2
     kOptCoarse = 5,     // kernel 3 coarse groups per wave outside the root box's rectangle (0 = off)
     kOptShadowOrder = 6,  // kernel 3 any-hit push order 0..3, -1 = timed choice (default)
+    kOptFlat = 7,       // flat-list kernel: 0 one triangle per iteration, 1 pairs, 2 packed pairs
     kOptDebug = 100,    // diagnostics: 1 = skip traversal, 2 = per-wave timestamps, 4 = every group
                         // coarse, 8 = coarse kernel on a side stream beside the fine one,
                         // 16 = counted shadow walks stop at occluders (the timed walk's work)
@@ -84,6 +85,7 @@ constexpr int kCostSlots = 4;   // kernel 3 items per wave (peak measured <= 440
 struct TraceParams {
     const float4* inode;
     const float4* trec;
+    const float4* tpair;           // flat variant 2: triangle pairs (k_pair_tri), or null
     const float4* shade;
     uint32_t* argb;
     int64_t* hit;
@@ -123,6 +125,7 @@ struct TraceParams {
     uint32_t root_ref;
     uint32_t ntri;
     int32_t max_depth;
+    int32_t flat_variant;          // Option kOptFlat: flat-list kernel form (0, 1, 2)
 };
 
 }  // namespace rt
@@ -133,6 +136,7 @@ int launch_tri_world(const float* points9, const float* rad3, uint32_t ntri,
                      float4* tri_world, float4* shade, void* stream);
 int launch_cam_tri(const float4* tri_world, uint32_t ntri, const float pos[3],
                    float4* trec, void* stream);
+int launch_pair_tri(const float4* trec, uint32_t ntri, float4* tpair, void* stream);
 int launch_cam_nodes(const rt_kd_node* nodes, const int32_t* interior_ids,
                      const uint32_t* node_ref, int64_t ninterior, const float pos[3],
                      float4* inode, int version, void* stream);

@@ -1315,10 +1315,49 @@ __global__ __launch_bounds__(128) void k_coarse_kd3(TraceParams P) {
 // -------------------------------------------------------------- flat trace
 
 // intersect_trixel_cuda (TD/Trixel.cu:173-209) fused with the shading.  The
-// triangle loop index is wave-uniform, so its 64-B records arrive through the
-// scalar data cache into SGPRs; the exact sign tests below skip the division
-// for the (common) rays that cannot pass u >= eps, v >= eps or w >= eps.
-template <bool kWriteHit, bool kCount>
+// triangle loop index is wave-uniform, so its records arrive through the
+// scalar data cache into SGPRs; an exact sign screen skips the division for
+// the (common) rays that cannot pass u >= eps, v >= eps or w >= eps.
+//
+// The screen.  u = pe1*U, v = pe1*V, w = pe1*W with sign(pe1) = sign(f), so
+// with U, V, W sign-flipped when f is negative (an XOR of f's sign bit), a
+// flipped value <= 0 makes u, v or w <= 0 < eps: rejected.  min3 ignores NaN
+// (IEEE minNum), so a NaN U, V or W never rejects by itself (the full test
+// decides); f = +-0 or NaN makes the full test reject anyway (|f| < eps, or
+// NaN w fails w < d).  A ray passes the screen iff !(min3 <= 0).
+__device__ __forceinline__ float flip_by(float x, float f) {
+    return __uint_as_float(__float_as_uint(x) ^ (__float_as_uint(f) & 0x80000000u));
+}
+__device__ __forceinline__ bool flat_screen(float f, float U, float V, float W) {
+    const float m = fminf(fminf(flip_by(U, f), flip_by(V, f)), flip_by(W, f));
+    return !(m <= 0.0f);
+}
+
+// The rest of one flat test (TD/Trixel.cu:185-205) for a ray that passed
+// the screen: strict w < d, so among equal w the lowest index wins.
+__device__ __forceinline__ void flat_accept(float f, float U, float V, float W, uint32_t t, float& d,
+                                            uint32_t& best, uint32_t& n_acc) {
+    if (!(f < kEpsF && f > -kEpsF)) {
+        const float pe1 = 1.0f / f;   // == (float)(1.0 / (double)f)
+        const float u = pe1 * U;
+        const float v = pe1 * V;
+        const float w = pe1 * W;
+        if ((w < d) && !((u < kEpsF) || (v < kEpsF) || ((u + v) > 1.0f) || (w < kEpsF))) {
+            d = w;
+            best = t;
+            n_acc++;
+        }
+    }
+}
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// kVariant 0: one triangle per iteration, the 64-B camera-relative record
+// (the first form).  1: two triangles per iteration, both records loaded
+// before either is tested, branch-free screen.  2: the same pair as packed
+// float2 arithmetic (v_pk_mul_f32 / v_pk_add_f32, one IEEE rounding per half,
+// so every value is the unpacked one) over the pair layout P.tpair.
+template <bool kWriteHit, bool kCount, int kVariant>
 __global__ __launch_bounds__(kTileWFlat * kTileH) void k_trace_flat(TraceParams P) {
     Pixel px;
     if (!pixel_of_thread(P, px)) return;
@@ -1330,31 +1369,76 @@ __global__ __launch_bounds__(kTileWFlat * kTileH) void k_trace_flat(TraceParams 
     uint32_t n_acc = 0;
     const float4* __restrict__ T = P.trec;
     const uint32_t ntri = P.ntri;
-    for (uint32_t t = 0; t < ntri; t++) {
-        const float4 A = T[4 * (size_t)t];
-        const float4 B = T[4 * (size_t)t + 1];
-        const float4 Cq = T[4 * (size_t)t + 2];
-        const float4 D = T[4 * (size_t)t + 3];
-        float qpx, qpy, qpz;
-        cross3(qpx, qpy, qpz, rx, ry, rz, A.w, B.x, B.y);
-        const float f = dot3(qpx, qpy, qpz, A.x, A.y, A.z);
-        const float U = dot3(qpx, qpy, qpz, B.z, B.w, Cq.x);
-        const float V = dot3(rx, ry, rz, Cq.y, Cq.z, Cq.w);
-        const float W = D.x;
-        // u = pe1*U with sign(pe1) = sign(f): a zero or wrong-signed U makes
-        // u <= 0 < eps (NaN is never rejected here), likewise V and W.
-        const bool pos = f > 0;
-        const bool reject = (pos ? (U <= 0 || V <= 0 || W <= 0) : (U >= 0 || V >= 0 || W >= 0));
-        if (reject) continue;
-        if (!(f < kEpsF && f > -kEpsF)) {
-            const float pe1 = 1.0f / f;
-            const float u = pe1 * U;
-            const float v = pe1 * V;
-            const float w = pe1 * W;
-            if ((w < d) && !((u < kEpsF) || (v < kEpsF) || ((u + v) > 1.0f) || (w < kEpsF))) {
-                d = w;
-                best = t;
-                if (kCount) n_acc++;
+    if (kVariant == 0) {
+        for (uint32_t t = 0; t < ntri; t++) {
+            const float4 A = T[4 * (size_t)t];
+            const float4 B = T[4 * (size_t)t + 1];
+            const float4 Cq = T[4 * (size_t)t + 2];
+            const float4 D = T[4 * (size_t)t + 3];
+            float qpx, qpy, qpz;
+            cross3(qpx, qpy, qpz, rx, ry, rz, A.w, B.x, B.y);
+            const float f = dot3(qpx, qpy, qpz, A.x, A.y, A.z);
+            const float U = dot3(qpx, qpy, qpz, B.z, B.w, Cq.x);
+            const float V = dot3(rx, ry, rz, Cq.y, Cq.z, Cq.w);
+            const float W = D.x;
+            const bool pos = f > 0;
+            const bool reject = (pos ? (U <= 0 || V <= 0 || W <= 0) : (U >= 0 || V >= 0 || W >= 0));
+            if (reject) continue;
+            flat_accept(f, U, V, W, t, d, best, n_acc);
+        }
+    } else if (kVariant == 1) {
+        uint32_t t = 0;
+        for (; t + 1 < ntri; t += 2) {
+            const float4 A0 = T[4 * (size_t)t], B0 = T[4 * (size_t)t + 1], C0 = T[4 * (size_t)t + 2],
+                         D0 = T[4 * (size_t)t + 3];
+            const float4 A1 = T[4 * (size_t)t + 4], B1 = T[4 * (size_t)t + 5], C1 = T[4 * (size_t)t + 6],
+                         D1 = T[4 * (size_t)t + 7];
+            float q0x, q0y, q0z, q1x, q1y, q1z;
+            cross3(q0x, q0y, q0z, rx, ry, rz, A0.w, B0.x, B0.y);
+            cross3(q1x, q1y, q1z, rx, ry, rz, A1.w, B1.x, B1.y);
+            const float f0 = dot3(q0x, q0y, q0z, A0.x, A0.y, A0.z);
+            const float f1 = dot3(q1x, q1y, q1z, A1.x, A1.y, A1.z);
+            const float U0 = dot3(q0x, q0y, q0z, B0.z, B0.w, C0.x);
+            const float U1 = dot3(q1x, q1y, q1z, B1.z, B1.w, C1.x);
+            const float V0 = dot3(rx, ry, rz, C0.y, C0.z, C0.w);
+            const float V1 = dot3(rx, ry, rz, C1.y, C1.z, C1.w);
+            const bool c0 = flat_screen(f0, U0, V0, D0.x), c1 = flat_screen(f1, U1, V1, D1.x);
+            if (c0 || c1) {
+                if (c0) flat_accept(f0, U0, V0, D0.x, t, d, best, n_acc);
+                if (c1) flat_accept(f1, U1, V1, D1.x, t + 1, d, best, n_acc);
+            }
+        }
+        if (t < ntri) {
+            const float4 A = T[4 * (size_t)t], B = T[4 * (size_t)t + 1], Cq = T[4 * (size_t)t + 2],
+                         D = T[4 * (size_t)t + 3];
+            float qpx, qpy, qpz;
+            cross3(qpx, qpy, qpz, rx, ry, rz, A.w, B.x, B.y);
+            const float f = dot3(qpx, qpy, qpz, A.x, A.y, A.z);
+            const float U = dot3(qpx, qpy, qpz, B.z, B.w, Cq.x);
+            const float V = dot3(rx, ry, rz, Cq.y, Cq.z, Cq.w);
+            if (flat_screen(f, U, V, D.x)) flat_accept(f, U, V, D.x, t, d, best, n_acc);
+        }
+    } else {
+        // pair p = triangles (2p, 2p+1): 13 float2 (e1, e2, d_t, d_q, d_w), 128 B;
+        // an odd count's last pair holds a dead twin (d_w = 0: never accepted)
+        const f2v* __restrict__ Q = reinterpret_cast<const f2v*>(P.tpair);
+        const f2v X = {rx, rx}, Y = {ry, ry}, Z = {rz, rz};
+        const uint32_t npair = (ntri + 1) >> 1;
+        for (uint32_t p = 0; p < npair; p++) {
+            const f2v* q = Q + 16 * (size_t)p;
+            const f2v e1x = q[0], e1y = q[1], e1z = q[2], e2x = q[3], e2y = q[4], e2z = q[5];
+            const f2v tx = q[6], ty = q[7], tz = q[8], dqx = q[9], dqy = q[10], dqz = q[11], dw = q[12];
+            // device_cross(rmd, e2) then the dots, TD/Trixel.cu:180-186, per half
+            const f2v qx = Y * e2z - Z * e2y;
+            const f2v qy = Z * e2x - X * e2z;
+            const f2v qz = X * e2y - Y * e2x;
+            const f2v f = (qx * e1x + qy * e1y) + qz * e1z;
+            const f2v U = (qx * tx + qy * ty) + qz * tz;
+            const f2v V = (X * dqx + Y * dqy) + Z * dqz;
+            const bool c0 = flat_screen(f.x, U.x, V.x, dw.x), c1 = flat_screen(f.y, U.y, V.y, dw.y);
+            if (c0 || c1) {
+                if (c0) flat_accept(f.x, U.x, V.x, dw.x, 2 * p, d, best, n_acc);
+                if (c1) flat_accept(f.y, U.y, V.y, dw.y, 2 * p + 1, d, best, n_acc);
             }
         }
     }
@@ -1374,6 +1458,38 @@ __global__ __launch_bounds__(kTileWFlat * kTileH) void k_trace_flat(TraceParams 
         wave_count_add(&P.counters[2], n_acc);
         wave_count_add(&P.counters[3], best != kMiss ? 1u : 0u);
     }
+}
+
+// The flat kernel's pair layout: pair p <- camera-relative records 2p, 2p+1,
+// each field as (value of 2p, value of 2p+1); a missing twin is dead (all
+// zero: d_w = 0 fails the screen, and its full test gives w = 0 < eps).
+__global__ void k_pair_tri(const float4* __restrict__ trec, uint32_t ntri, float4* __restrict__ tpair) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t npair = (ntri + 1) >> 1;
+    if (p >= npair) return;
+    float a[13], b[13];
+    const uint32_t t0 = 2 * p, t1 = 2 * p + 1;
+    const float4* r0 = trec + 4 * (size_t)t0;
+    const float4 A0 = r0[0], B0 = r0[1], C0 = r0[2], D0 = r0[3];
+    a[0] = A0.x; a[1] = A0.y; a[2] = A0.z; a[3] = A0.w; a[4] = B0.x; a[5] = B0.y; a[6] = B0.z; a[7] = B0.w;
+    a[8] = C0.x; a[9] = C0.y; a[10] = C0.z; a[11] = C0.w; a[12] = D0.x;
+    for (int k = 0; k < 13; k++) b[k] = 0.0f;
+    if (t1 < ntri) {
+        const float4* r1 = trec + 4 * (size_t)t1;
+        const float4 A1 = r1[0], B1 = r1[1], C1 = r1[2], D1 = r1[3];
+        b[0] = A1.x; b[1] = A1.y; b[2] = A1.z; b[3] = A1.w; b[4] = B1.x; b[5] = B1.y; b[6] = B1.z; b[7] = B1.w;
+        b[8] = C1.x; b[9] = C1.y; b[10] = C1.z; b[11] = C1.w; b[12] = D1.x;
+    }
+    // field order of the kernel: e1 (3), e2 (3), d_t (3), d_q (3), d_w
+    float4* o = tpair + 8 * (size_t)p;
+    o[0] = make_float4(a[0], b[0], a[1], b[1]);
+    o[1] = make_float4(a[2], b[2], a[3], b[3]);
+    o[2] = make_float4(a[4], b[4], a[5], b[5]);
+    o[3] = make_float4(a[6], b[6], a[7], b[7]);
+    o[4] = make_float4(a[8], b[8], a[9], b[9]);
+    o[5] = make_float4(a[10], b[10], a[11], b[11]);
+    o[6] = make_float4(a[12], b[12], 0.0f, 0.0f);
+    o[7] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 }
 
 // ------------------------------------------------------------------ prep
@@ -1581,6 +1697,25 @@ int launch_cam_nodes(const rt_kd_node* nodes, const int32_t* ids, const uint32_t
 
 using TraceFn = void (*)(TraceParams);
 
+template <int V>
+TraceFn flat_kernel_v(bool wh, bool cnt) {
+    return wh ? (cnt ? k_trace_flat<true, true, V> : k_trace_flat<true, false, V>)
+              : (cnt ? k_trace_flat<false, true, V> : k_trace_flat<false, false, V>);
+}
+
+TraceFn flat_kernel(bool wh, bool cnt, int variant) {
+    if (variant == 0) return flat_kernel_v<0>(wh, cnt);
+    if (variant == 1) return flat_kernel_v<1>(wh, cnt);
+    return flat_kernel_v<2>(wh, cnt);
+}
+
+int launch_pair_tri(const float4* trec, uint32_t ntri, float4* tpair, void* stream) {
+    if (ntri == 0) return RT_OK;
+    const uint32_t npair = (ntri + 1) >> 1;
+    k_pair_tri<<<(npair + 255) / 256, 256, 0, (hipStream_t)stream>>>(trec, ntri, tpair);
+    return check_launch<void>("k_pair_tri");
+}
+
 template <bool T, bool H, bool C, int S>
 TraceFn kd3_kernel(int rays, bool coarse) {
     if (coarse) {
@@ -1631,8 +1766,7 @@ int launch_trace(const TraceParams& p, uint32_t mode, uint32_t flags, int kernel
     const unsigned threads = (unsigned)((p.tile_w / 8) * (p.tile_h / (p.rays / 8)) * 64);
     if (mode == RT_MODE_FLAT) {
         if (fine == 0) return RT_OK;
-        TraceFn fn = wh ? (cnt ? k_trace_flat<true, true> : k_trace_flat<true, false>)
-                        : (cnt ? k_trace_flat<false, true> : k_trace_flat<false, false>);
+        TraceFn fn = flat_kernel(wh, cnt, p.flat_variant);
         fn<<<fine, threads, 0, s>>>(p);
         return check_launch<void>("k_trace_flat");
     }

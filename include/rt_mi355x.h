@@ -255,6 +255,9 @@ int rt_camera_info(const rt_camera* c, int32_t* w, int32_t* h, int32_t* max_dept
  * bracketed by events and the fastest is kept; never blocks, skipped under
  * stream capture).  Get returns the order in use. */
 #define RT_OPT_SHADOW_ORDER 6
+/* Flat-list kernel form (same frame): 0 one triangle per iteration, 1 two
+ * per iteration, 2 two per iteration as packed float2 arithmetic (default). */
+#define RT_OPT_FLAT 7
 int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value);
 int rt_camera_get_option(const rt_camera* c, int32_t key, int32_t* value);
 
