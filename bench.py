@@ -86,6 +86,9 @@ def parse():
                     help="0 XCD-contiguous, 1 natural, 2 centre-out, 3 by the cost an earlier frame measured")
     ap.add_argument("--rays", type=int, default=16, help="kernel 3: pixels per wave (64, 32, 16, 8)")
     ap.add_argument("--items", type=int, default=2, help="kernel 3: items each lane pops per iteration (1, 2)")
+    ap.add_argument("--order", type=int, default=-1,
+                    help="interior record order: 0 BFS, 1 DFS preorder, 2 treelets (-1: the library default)")
+    ap.add_argument("--treelet", type=int, default=0, help="treelet height for --order 2 (0: library default)")
     ap.add_argument("--flat", type=int, default=-1,
                     help="flat-list kernel form: 0 one triangle per iteration, 1 pairs, 2 packed float2 pairs "
                          "(-1: the library default)")
@@ -148,6 +151,11 @@ def cpu_model() -> str:
     except OSError:
         pass
     return "unknown"
+
+
+def _lib_mod():
+    from cpp_cuda_raytracer_dev_amd import _lib
+    return _lib
 
 
 def data_label(scene: str) -> str:
@@ -376,6 +384,10 @@ def main():
     pts, leafs, nodes, build_times = build_scene(a.scene)
     trixel = R.Trixel(len(pts), pts, device=local)
     trixel.set_kd_nodes(nodes)
+    if a.treelet > 0:
+        trixel.set_option(_lib_mod().RT_SCENE_TREELET_HEIGHT, a.treelet)
+    if a.order >= 0:
+        trixel.set_option(_lib_mod().RT_SCENE_ORDER, a.order)
     cam_kw = scenes.view(a.scene, a.view)
     cam = R.Camera(w, h, R.film_w(w, h), np.float32(.024), np.float32(.055), *cam_kw["pos"], *cam_kw["look_at"],
                    0.0, 1.0, 0.0, device=local)
@@ -626,6 +638,8 @@ def main():
                 "kernel": {1: "k_trace_kd", 2: "k_trace_kd2", 3: "k_trace_kd3"}[a.kernel] if a.mode == 0
                           else "k_trace_flat",
                 "kernel_options": {"kernel": a.kernel, "tile_order": a.tile_order, "rays_per_wave": a.rays,
+                                   "record_order": trixel.get_option(_lib.RT_SCENE_ORDER),
+                                   "treelet_height": trixel.get_option(_lib.RT_SCENE_TREELET_HEIGHT),
                                    "items_per_lane": a.items, "coarse_groups_per_wave": a.coarse,
                                    "shadow": a.shadow,
                                    **({"shadow_push_order": cam.get_option(_lib.RT_OPT_SHADOW_ORDER),

@@ -28,6 +28,8 @@ RT_OPT_ITEMS = 4
 RT_OPT_COARSE = 5
 RT_OPT_SHADOW_ORDER = 6
 RT_OPT_FLAT = 7
+RT_SCENE_ORDER = 1
+RT_SCENE_TREELET_HEIGHT = 2
 RT_OPT_DEBUG = 100
 RT_OPT_POOL_CAP = 101
 RT_COMM_ID_BYTES = 128
@@ -74,6 +76,8 @@ SIGNATURES = {
     "rt_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "rt_scene_create": (C.c_int, [C.c_int, _P, _P, C.c_uint32, C.POINTER(_P)]),
     "rt_scene_set_kd": (C.c_int, [_P, _P, C.c_uint64]),
+    "rt_scene_set_option": (C.c_int, [_P, C.c_int32, C.c_int32]),
+    "rt_scene_get_option": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_int32)]),
     "rt_camera_create": (C.c_int, [C.c_int, C.c_int32, C.c_int32, C.c_float, C.c_float, C.c_float, _P, _P, _P,
                                    C.POINTER(_P)]),
     "rt_camera_add_object": (C.c_int, [_P, _P]),

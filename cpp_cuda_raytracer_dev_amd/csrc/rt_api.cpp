@@ -28,6 +28,12 @@ struct rt_scene {
     int32_t height = 0;
     uint64_t tree_version = 0;
     rt_kd_node root{};               // host copy of node 0 (root box)
+    // host shape of the tree (left child or -1 for a leaf, leaf triangle),
+    // kept to re-lay the interior records out (rt_scene_set_option)
+    std::vector<int32_t> h_left;
+    std::vector<uint32_t> h_tri;
+    int record_order = 0;            // RT_SCENE_ORDER: 0 BFS, 1 DFS preorder, 2 treelets
+    int treelet_height = 3;          // RT_SCENE_TREELET_HEIGHT
 };
 
 struct rt_camera {
@@ -663,6 +669,84 @@ extern "C" int rt_scene_create(int device, const float* points9, const float* ra
     return RT_OK;
 }
 
+namespace {
+
+// The order of the dense interior records.  Internal: a record names its
+// children by position, the traversal's tie rule uses DFS path codes, so the
+// frame never depends on it; only the cache locality of the walk does.
+//   0  BFS (node index order, as the reference stores kd_tree_node)
+//   1  DFS preorder, left child first: a node's first child is the next record
+//   2  treelets of height H: a node and its descendants down to H-1 levels
+//      below it are consecutive (BFS inside), treelets in DFS order
+std::vector<int32_t> interior_order(const std::vector<int32_t>& left, int order, int h) {
+    std::vector<int32_t> ids;
+    const int64_t n = (int64_t)left.size();
+    if (n == 0 || left[0] < 0) return ids;
+    ids.reserve((size_t)(n / 2));
+    if (order == 0) {
+        for (int64_t i = 0; i < n; i++)
+            if (left[(size_t)i] >= 0) ids.push_back((int32_t)i);
+        return ids;
+    }
+    if (order == 1) {
+        std::vector<int32_t> st{0};
+        while (!st.empty()) {
+            const int32_t i = st.back();
+            st.pop_back();
+            if (left[(size_t)i] < 0) continue;
+            ids.push_back(i);
+            st.push_back(left[(size_t)i] + 1);
+            st.push_back(left[(size_t)i]);
+        }
+        return ids;
+    }
+    std::vector<int32_t> roots{0}, level, next, below;
+    while (!roots.empty()) {
+        const int32_t r = roots.back();
+        roots.pop_back();
+        level.assign(1, r);
+        below.clear();
+        for (int d = 0; d < h && !level.empty(); d++) {
+            next.clear();
+            for (int32_t i : level) {
+                ids.push_back(i);
+                for (int32_t c : {left[(size_t)i], left[(size_t)i] + 1})
+                    if (left[(size_t)c] >= 0) (d + 1 < h ? next : below).push_back(c);
+            }
+            level.swap(next);
+        }
+        // child treelets left to right: push in reverse so the leftmost pops first
+        for (auto it = below.rbegin(); it != below.rend(); ++it) roots.push_back(*it);
+    }
+    return ids;
+}
+
+// (Re)builds the interior record order, the node -> ref table and uploads them.
+int relabel(rt_scene* s) {
+    const int64_t n = (int64_t)s->h_left.size();
+    const std::vector<int32_t> ids = interior_order(s->h_left, s->record_order, s->treelet_height);
+    std::vector<uint32_t> ref((size_t)n);
+    for (int64_t i = 0; i < n; i++)
+        if (s->h_left[(size_t)i] < 0) ref[(size_t)i] = kLeafBit | s->h_tri[(size_t)i];
+    for (size_t k = 0; k < ids.size(); k++) ref[(size_t)ids[k]] = (uint32_t)k;
+    DeviceGuard g(s->device);
+    dev_free(s->d_interior_ids);
+    dev_free(s->d_node_ref);
+    int rc;
+    if ((rc = dev_alloc(&s->d_interior_ids, ids.size(), "hipMalloc(ids)")) ||
+        (rc = dev_alloc(&s->d_node_ref, (size_t)n, "hipMalloc(node_ref)")) ||
+        (rc = hip_check(hipMemcpy(s->d_node_ref, ref.data(), sizeof(uint32_t) * (size_t)n, hipMemcpyHostToDevice), "H2D refs")) ||
+        (!ids.empty() && (rc = hip_check(hipMemcpy(s->d_interior_ids, ids.data(), sizeof(int32_t) * ids.size(),
+                                                   hipMemcpyHostToDevice), "H2D ids"))))
+        return rc;
+    s->ninterior = (int64_t)ids.size();
+    s->root_ref = ref[0];
+    s->tree_version++;
+    return RT_OK;
+}
+
+}  // namespace
+
 extern "C" int rt_scene_set_kd(rt_scene* s, const rt_kd_node* nodes, uint64_t nnode) {
     if (!s || !nodes) return fail(RT_ERR_INVALID, "rt_scene_set_kd: null argument");
     const int64_t n = (int64_t)nnode;
@@ -670,11 +754,10 @@ extern "C" int rt_scene_set_kd(rt_scene* s, const rt_kd_node* nodes, uint64_t nn
         return fail(RT_ERR_INVALID, "rt_scene_set_kd: %lld nodes for %u triangles", (long long)n, s->ntri);
     // Validate: BFS order with right = left + 1 (so every DFS terminates),
     // leaves cover every triangle exactly once, bounded height.
-    std::vector<uint32_t> ref((size_t)n);
-    std::vector<int32_t> ids;
+    std::vector<int32_t> left((size_t)n, -1);
+    std::vector<uint32_t> tri((size_t)n, 0);
     std::vector<uint8_t> seen(s->ntri, 0);
     std::vector<int32_t> depth((size_t)n, 0);
-    int64_t ninterior = 0;
     int32_t height = 0;
     for (int64_t i = 0; i < n; i++) {
         const rt_kd_node& nd = nodes[i];
@@ -682,7 +765,7 @@ extern "C" int rt_scene_set_kd(rt_scene* s, const rt_kd_node* nodes, uint64_t nn
             if (nd.tri_index < 0 || nd.tri_index >= (int64_t)s->ntri || seen[(size_t)nd.tri_index])
                 return fail(RT_ERR_INVALID, "rt_scene_set_kd: leaf %lld has bad/duplicate triangle", (long long)i);
             seen[(size_t)nd.tri_index] = 1;
-            ref[(size_t)i] = kLeafBit | (uint32_t)nd.tri_index;
+            tri[(size_t)i] = (uint32_t)nd.tri_index;
         } else {
             if (nd.left <= i || nd.right != nd.left + 1 || nd.right >= n)
                 return fail(RT_ERR_INVALID, "rt_scene_set_kd: node %lld children %lld/%lld not BFS", (long long)i,
@@ -692,34 +775,55 @@ extern "C" int rt_scene_set_kd(rt_scene* s, const rt_kd_node* nodes, uint64_t nn
             depth[(size_t)nd.left] = depth[(size_t)i] + 1;
             depth[(size_t)nd.right] = depth[(size_t)i] + 1;
             height = std::max(height, depth[(size_t)i] + 1);
-            ref[(size_t)i] = (uint32_t)ninterior++;
-            ids.push_back((int32_t)i);
+            left[(size_t)i] = (int32_t)nd.left;
         }
     }
     if (height > kMaxDepth)
         return fail(RT_ERR_INVALID, "rt_scene_set_kd: tree height %d exceeds the %d-entry LDS stack", height, kMaxDepth);
     DeviceGuard g(s->device);
     dev_free(s->d_nodes);
-    dev_free(s->d_interior_ids);
-    dev_free(s->d_node_ref);
     int rc;
     if ((rc = dev_alloc(&s->d_nodes, (size_t)n, "hipMalloc(nodes)")) ||
-        (rc = dev_alloc(&s->d_interior_ids, ids.size(), "hipMalloc(ids)")) ||
-        (rc = dev_alloc(&s->d_node_ref, (size_t)n, "hipMalloc(node_ref)")) ||
-        (rc = hip_check(hipMemcpy(s->d_nodes, nodes, sizeof(rt_kd_node) * (size_t)n, hipMemcpyHostToDevice), "H2D nodes")) ||
-        (rc = hip_check(hipMemcpy(s->d_node_ref, ref.data(), sizeof(uint32_t) * (size_t)n, hipMemcpyHostToDevice), "H2D refs")) ||
-        (!ids.empty() && (rc = hip_check(hipMemcpy(s->d_interior_ids, ids.data(), sizeof(int32_t) * ids.size(),
-                                                   hipMemcpyHostToDevice), "H2D ids")))) {
+        (rc = hip_check(hipMemcpy(s->d_nodes, nodes, sizeof(rt_kd_node) * (size_t)n, hipMemcpyHostToDevice), "H2D nodes"))) {
         dev_free(s->d_nodes);
         return rc;
     }
     s->nnode = n;
     s->root = nodes[0];
-    s->ninterior = ninterior;
-    s->root_ref = ref[0];
     s->height = height;
-    s->tree_version++;
+    s->h_left.swap(left);
+    s->h_tri.swap(tri);
+    if ((rc = relabel(s))) {
+        dev_free(s->d_nodes);
+        return rc;
+    }
     return RT_OK;
+}
+
+extern "C" int rt_scene_set_option(rt_scene* s, int32_t key, int32_t value) {
+    if (!s) return fail(RT_ERR_INVALID, "rt_scene_set_option: null scene");
+    switch (key) {
+    case RT_SCENE_ORDER:
+        if (value < 0 || value > 2) return fail(RT_ERR_INVALID, "interior record order %d (0..2)", value);
+        s->record_order = value;
+        break;
+    case RT_SCENE_TREELET_HEIGHT:
+        if (value < 1 || value > 12) return fail(RT_ERR_INVALID, "treelet height %d (1..12)", value);
+        s->treelet_height = value;
+        break;
+    default:
+        return fail(RT_ERR_INVALID, "rt_scene_set_option: unknown key %d", key);
+    }
+    return s->h_left.empty() ? RT_OK : relabel(s);
+}
+
+extern "C" int rt_scene_get_option(const rt_scene* s, int32_t key, int32_t* value) {
+    if (!s || !value) return fail(RT_ERR_INVALID, "rt_scene_get_option: null argument");
+    switch (key) {
+    case RT_SCENE_ORDER: *value = s->record_order; return RT_OK;
+    case RT_SCENE_TREELET_HEIGHT: *value = s->treelet_height; return RT_OK;
+    default: return fail(RT_ERR_INVALID, "rt_scene_get_option: unknown key %d", key);
+    }
 }
 
 extern "C" int rt_camera_create(int device, int32_t w, int32_t h, float f_w, float f_h, float focal,

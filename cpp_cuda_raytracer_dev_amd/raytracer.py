@@ -210,6 +210,15 @@ class Trixel:
         _lib.call("rt_scene_set_kd", self._h, _lib.ptr(self.h_nodes), len(self.h_nodes))
         return 0
 
+    def set_option(self, key: int, value: int) -> None:
+        """Scene layout knobs (_lib.RT_SCENE_ORDER, _lib.RT_SCENE_TREELET_HEIGHT); frames are identical."""
+        _lib.call("rt_scene_set_option", self._h, key, value)
+
+    def get_option(self, key: int) -> int:
+        v = C.c_int32()
+        _lib.call("rt_scene_get_option", self._h, key, C.byref(v))
+        return v.value
+
     def intersect_trixels(self, c: "Camera", q: Quaternion = None, m: int = RT_MODE_KD, flags: int = 0,
                           stream=None) -> int:
         """TD/Trixel.h:474-476.  Unlike the reference, ``m`` selects KD (0) or flat (1)."""

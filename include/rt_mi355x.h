@@ -130,6 +130,16 @@ int rt_scene_create(int device, const float* points9, const float* rad3,
  * the tree (BFS order, 2*ntri-1 nodes, leaves cover every triangle once). */
 int rt_scene_set_kd(rt_scene* s, const rt_kd_node* nodes, uint64_t nnode);
 
+/* Layout knobs of a scene (not in the reference; every setting renders the
+ * identical frame): RT_SCENE_ORDER = the order of the dense interior records
+ * the KD kernels read (0: BFS, the reference's kd_tree_node order; 1: DFS
+ * preorder; 2: treelets of RT_SCENE_TREELET_HEIGHT levels, consecutive, in
+ * DFS order).  Takes effect at once (cameras re-derive their records). */
+#define RT_SCENE_ORDER 1
+#define RT_SCENE_TREELET_HEIGHT 2
+int rt_scene_set_option(rt_scene* s, int32_t key, int32_t value);
+int rt_scene_get_option(const rt_scene* s, int32_t key, int32_t* value);
+
 /* Camera::Camera + init_camera_device_memory (TD/Camera.cpp:5-117,
  * TD/Camera.cu:112-136). */
 int rt_camera_create(int device, int32_t w, int32_t h, float f_w, float f_h,

@@ -97,6 +97,25 @@ def test_rabbit_960x540_flat_band():
     assert (khit[sl] == hit[sl]).all()
 
 
+@pytest.mark.parametrize("order,height", [(0, 3), (1, 3), (2, 2), (2, 3), (2, 5)])
+@pytest.mark.parametrize("kernel", [1, 2, 3])
+@pytest.mark.parametrize("shadow", [False, True])
+def test_interior_record_orders(order, height, kernel, shadow):
+    """The interior records' order (BFS, DFS preorder, treelets) is internal:
+    every kernel renders the oracle's frame and counters with each."""
+    from cpp_cuda_raytracer_dev_amd import _lib
+    if shadow and kernel != 3:
+        pytest.skip("shadow rays run in kernel 3")
+    s = H.GpuScene("dragon", 960, 540, kernel=kernel)
+    s.trixel.set_option(_lib.RT_SCENE_TREELET_HEIGHT, height)
+    s.trixel.set_option(_lib.RT_SCENE_ORDER, order)
+    assert s.trixel.get_option(_lib.RT_SCENE_ORDER) == order
+    argb, hit, cnt = s.render(0, count=True, shadow=shadow)
+    oargb, ohit, ocnt = H.oracle_render("dragon", 960, 540, 0, shadow=shadow)
+    _assert_same((argb, hit), (oargb, ohit), f"order {order}/{height} kernel {kernel}")
+    _counters_match(cnt, ocnt, kernel)
+
+
 @pytest.mark.parametrize("variant", [0, 1, 2])
 @pytest.mark.parametrize("name,w,h", [("dump_test", 64, 36), ("tester", 80, 45), ("dump", 48, 27),
                                       ("tester", 33, 9)])
