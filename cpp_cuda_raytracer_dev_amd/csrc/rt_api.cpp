@@ -53,7 +53,7 @@ struct rt_camera {
     uint32_t trec_cap = 0;
     int64_t inode_cap = 0;           // in float4
     int prepared_layout = 0;         // interior record layout of d_inode (1 or 2)
-    int kernel_version = 3;          // kOptKernel (3 falls back to 2 on trees taller than 21)
+    int kernel_version = 3;          // kOptKernel
     int tile_order = 3;              // kOptTileOrder
     int debug = 0;                   // kOptDebug (diagnostics)
     int pool_cap = kPoolCapMax;      // kOptPoolCap
@@ -131,12 +131,10 @@ void dev_free(T*& p) {
     p = nullptr;
 }
 
-// The KD kernel a render runs: the wave-cooperative kernel (3) encodes DFS
-// path codes in 21 bits, so taller trees use the per-lane DFS kernel (2).
-int effective_kernel(const rt_camera* c) {
-    if (c->kernel_version == 3 && c->obj && c->obj->height > 21) return 2;
-    return c->kernel_version;
-}
+// The KD kernel a render runs.  Every kernel handles any tree the LDS stack
+// admits (height <= kMaxDepth; rt_scene_set_kd rejects taller ones): kernel
+// 3's marked path codes take height + 1 <= 25 bits.
+int effective_kernel(const rt_camera* c) { return c->kernel_version; }
 
 int record_layout(int kernel) { return kernel == 1 ? 1 : 2; }
 
@@ -955,8 +953,8 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
     if (flags & RT_FLAG_SHADOW) {
         if (mode != RT_MODE_KD) return fail(RT_ERR_INVALID, "rt_render: RT_FLAG_SHADOW needs RT_MODE_KD");
         if (effective_kernel(c) != 3)
-            return fail(RT_ERR_STATE, "rt_render: shadow rays run in the wave-cooperative kernel (3); kernel %d%s",
-                        effective_kernel(c), c->obj->height > 21 ? " (tree height > 21)" : "");
+            return fail(RT_ERR_STATE, "rt_render: shadow rays run in the wave-cooperative kernel (3); kernel %d",
+                        effective_kernel(c));
     }
     TraceParams p;
     if ((rc = fill_params(c, xform, tile, argb, hit, mode, p))) return rc;
@@ -1184,9 +1182,9 @@ extern "C" int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value) {
         c->coarse = value;
         return RT_OK;
     case kOptPoolCap:
-        // the 64 root items plus a DFS run of height <= 21 must fit
-        if (value < 64 + 22 || value > kPoolCapMax)
-            return fail(RT_ERR_INVALID, "pool cap %d (86..%d)", value, kPoolCapMax);
+        // the 64 root items plus a DFS run of height <= 24 must fit
+        if (value < 64 + kMaxDepth + 1 || value > kPoolCapMax)
+            return fail(RT_ERR_INVALID, "pool cap %d (%d..%d)", value, 64 + kMaxDepth + 1, kPoolCapMax);
         c->pool_cap = value;
         return RT_OK;
     case kOptDebug:
@@ -1200,7 +1198,7 @@ extern "C" int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value) {
         c->tune_pending = false;
         return RT_OK;
     case kOptFlat:
-        if (value < 0 || value > 2) return fail(RT_ERR_INVALID, "flat kernel form %d (0..2)", value);
+        if (value < 0 || value > 3) return fail(RT_ERR_INVALID, "flat kernel form %d (0..3)", value);
         c->flat_variant = value;
         return RT_OK;
     case kOptTileOrder:

@@ -594,21 +594,33 @@ __global__ __launch_bounds__(kTileWKd * kTileH) void k_trace_kd2(TraceParams P) 
 // the (ray, node) work items of its 64 rays in one LDS stack and every lane
 // takes an item per iteration, whatever ray it belongs to: the wave runs
 // ~sum(visits)/64 iterations instead of max(visits).  Each item carries its
-// DFS path code (bit = "second child popped" at each level, left aligned), so
-// the lexicographic minimum of (w, code) -- one 64-bit LDS atomic min per
-// candidate -- is exactly the reference's winner.
+// DFS path code (bit = "second child popped" at each level), so the
+// lexicographic minimum of (w, code left-aligned) -- one 64-bit LDS atomic
+// min per candidate -- is exactly the reference's winner.
+//
+// The path code is stored with a leading marker bit: the root is 1, a node
+// with code m has children 2m (popped first) and 2m + 1, so its depth is the
+// position of the marker and any tree the LDS stack admits (height <=
+// kMaxDepth = 24: 25 bits) fits beside the 6-bit ray index.
 constexpr int kPoolCap = kPoolCapMax;
-constexpr int kCodeBits = 21;         // path code bits: trees of height <= 21
-constexpr uint32_t kCodeMask = (1u << kCodeBits) - 1;
+constexpr int kCodeBits = kMaxDepth;       // left-aligned code width in the key
+constexpr uint32_t kCodeMarkMask = (1u << 26) - 1;
+constexpr int kPoolSlack = kMaxDepth + 1;  // a DFS run's growth: height + 1
 
 struct Item {
     uint32_t ref;      // node ref (kLeafBit | tri, or interior index)
     float t0, t1;      // the node's (maxt0, mint1) for interior refs
-    uint32_t meta;     // ray << 26 | depth << 21 | code
+    uint32_t meta;     // ray << 26 | marked path code
 };
 
+// The key bits of a marked path code: the code left-aligned in kCodeBits.
+__device__ __forceinline__ uint32_t code_key(uint32_t marked) {
+    const uint32_t depth = 31u - (uint32_t)__builtin_clz(marked);
+    return (marked ^ (1u << depth)) << (kCodeBits - depth);
+}
+
 // Pool capacity per wave for kRays rays (the DFS fallback keeps any
-// capacity >= 86 correct; these cover the measured peaks with margin).
+// capacity >= 89 correct; these cover the measured peaks with margin).
 #ifndef RT_POOL_CAP_R32
 #define RT_POOL_CAP_R32 448
 #endif
@@ -694,7 +706,7 @@ __device__ __forceinline__ int seed_root(const TraceParams& P, uint4* items, con
     const bool has = root_pass<kCount>(P, R, live, r0t0, r0t1, n_int, n_desc);
     const unsigned long long b = __ballot(has);
     const uint32_t off = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
-    if (has) items[off] = make_uint4(P.root_ref, __float_as_uint(r0t0), __float_as_uint(r0t1), (uint32_t)lane << 26);
+    if (has) items[off] = make_uint4(P.root_ref, __float_as_uint(r0t0), __float_as_uint(r0t1), ((uint32_t)lane << 26) | 1u);
     __builtin_amdgcn_wave_barrier();
     return __builtin_popcountll(b);
 }
@@ -738,14 +750,13 @@ __device__ __forceinline__ void visit_leaf(const float4* rd, uint4 it, float4 r0
     Ray Q;
     float4 q2, q3, q4;
     ray_of<kTranslated>(rd, Q, q2, q3, q4);
-    const uint32_t code = it.w & kCodeMask;
     if (kCount) n_leaf++;
     float d = kAny ? q4.z : kDrawDistance;
     uint32_t best = kMiss;
     if (leaf_test_rec(Q, r0, r1, r2, it.x & ~kLeafBit, d, best) && (!kAny || best != __float_as_uint(q4.w))) {
         o.cand = true;
         o.ctri = best;
-        o.key = kAny ? 0ull : ((unsigned long long)__float_as_uint(d) << 32) | code;
+        o.key = kAny ? 0ull : ((unsigned long long)__float_as_uint(d) << 32) | code_key(it.w & kCodeMarkMask);
         if (kCount) n_acc++;
     }
 }
@@ -759,7 +770,7 @@ __device__ __forceinline__ void visit_interior(const float4* rd, uint4 it, float
     float4 q2, q3, q4;
     ray_of<kTranslated>(rd, Q, q2, q3, q4);
     const uint32_t ray = it.w >> 26;
-    const uint32_t depth = (it.w >> kCodeBits) & 31u, code = it.w & kCodeMask;
+    const uint32_t marked = it.w & kCodeMarkMask;
     const uint32_t lw = __float_as_uint(r3.z);
     const uint32_t axis = (lw >> kAxisShift) & 3u;
     const uint32_t L = lw & ~(3u << kAxisShift), Rr = __float_as_uint(r3.w);
@@ -795,10 +806,8 @@ __device__ __forceinline__ void visit_interior(const float4* rd, uint4 it, float
         n_int += (first_leaf ? 0u : 1u) + ((push_second && !second_leaf) ? 1u : 0u);
         n_desc += ((!first_leaf && keep_first) ? 1u : 0u) + ((push_second && !second_leaf && keep_second) ? 1u : 0u);
     }
-    const uint32_t cd = depth + 1;
-    const uint32_t bit = 1u << (kCodeBits - cd);
-    const uint32_t meta_first = (ray << 26) | (cd << kCodeBits) | code;
-    const uint32_t meta_second = meta_first | bit;
+    const uint32_t meta_first = (ray << 26) | (marked << 1);
+    const uint32_t meta_second = meta_first | 1u;
     const float f0 = left_first ? lt0 : rt0, f1 = left_first ? lt1 : rt1;
     const float g0 = left_first ? rt0 : lt0, g1 = left_first ? rt1 : lt1;
     const uint4 A = make_uint4(first, __float_as_uint(f0), __float_as_uint(f1), meta_first);
@@ -922,10 +931,10 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
         // Pop as many items as the pool has room for the children of plus
         // the DFS slack below; a single (DFS-like) pop when there is none.
         // Popping k items pushes at most 2k, so a parallel pop leaves
-        // n <= cap - 22; a run of single pops starting at n0 never holds
-        // more than n0 + height items (height <= 21), so the pool never
-        // overflows.
-        int take = min(min(n, per), cap - kCodeBits - 1 - n);
+        // n <= cap - kPoolSlack; a run of single pops starting at n0 never
+        // holds more than n0 + height + 1 items (height <= 24), so the pool
+        // never overflows.
+        int take = min(min(n, per), cap - kPoolSlack - n);
         if (take < 1) take = 1;
         iters++;
         popped += (uint32_t)take;
@@ -1352,11 +1361,47 @@ __device__ __forceinline__ void flat_accept(float f, float U, float V, float W, 
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 
+// One pair of the flat kernel's pair layout in registers (SGPRs: the loop
+// index is wave-uniform) and its two tests as packed float2 arithmetic.
+struct FlatPair {
+    f2v e1x, e1y, e1z, e2x, e2y, e2z, tx, ty, tz, dqx, dqy, dqz, dw;
+    __device__ __forceinline__ void load(const f2v* q) {
+        e1x = q[0]; e1y = q[1]; e1z = q[2]; e2x = q[3]; e2y = q[4]; e2z = q[5];
+        tx = q[6]; ty = q[7]; tz = q[8]; dqx = q[9]; dqy = q[10]; dqz = q[11]; dw = q[12];
+    }
+    // Loads pair `pair` of Q only after `prev`'s values have arrived: the
+    // index is made to depend on one of them through `zero`, a run-time 0
+    // the compiler cannot fold (an asm barrier would make the loads vector
+    // loads), so waiting for prev never waits for this pair's loads.
+    __device__ __forceinline__ void load_after(const f2v* __restrict__ Q, uint32_t pair, const FlatPair& prev,
+                                               uint32_t zero) {
+        pair ^= __float_as_uint(prev.dw.y) & zero;
+        load(Q + 16 * (size_t)pair);
+    }
+    // device_cross(rmd, e2) then the dots (TD/Trixel.cu:180-186) per half;
+    // triangle t then t + 1, so equal w keeps the lower index.
+    __device__ __forceinline__ void test(const f2v X, const f2v Y, const f2v Z, uint32_t t, float& d, uint32_t& best,
+                                         uint32_t& n_acc) const {
+        const f2v qx = Y * e2z - Z * e2y;
+        const f2v qy = Z * e2x - X * e2z;
+        const f2v qz = X * e2y - Y * e2x;
+        const f2v f = (qx * e1x + qy * e1y) + qz * e1z;
+        const f2v U = (qx * tx + qy * ty) + qz * tz;
+        const f2v V = (X * dqx + Y * dqy) + Z * dqz;
+        const bool c0 = flat_screen(f.x, U.x, V.x, dw.x), c1 = flat_screen(f.y, U.y, V.y, dw.y);
+        if (c0 || c1) {
+            if (c0) flat_accept(f.x, U.x, V.x, dw.x, t, d, best, n_acc);
+            if (c1) flat_accept(f.y, U.y, V.y, dw.y, t + 1, d, best, n_acc);
+        }
+    }
+};
+
 // kVariant 0: one triangle per iteration, the 64-B camera-relative record
 // (the first form).  1: two triangles per iteration, both records loaded
 // before either is tested, branch-free screen.  2: the same pair as packed
 // float2 arithmetic (v_pk_mul_f32 / v_pk_add_f32, one IEEE rounding per half,
-// so every value is the unpacked one) over the pair layout P.tpair.
+// so every value is the unpacked one) over the pair layout P.tpair.  3: 2,
+// software pipelined (the next pair's loads in flight during a pair's tests).
 template <bool kWriteHit, bool kCount, int kVariant>
 __global__ __launch_bounds__(kTileWFlat * kTileH) void k_trace_flat(TraceParams P) {
     Pixel px;
@@ -1424,22 +1469,27 @@ __global__ __launch_bounds__(kTileWFlat * kTileH) void k_trace_flat(TraceParams 
         const f2v* __restrict__ Q = reinterpret_cast<const f2v*>(P.tpair);
         const f2v X = {rx, rx}, Y = {ry, ry}, Z = {rz, rz};
         const uint32_t npair = (ntri + 1) >> 1;
-        for (uint32_t p = 0; p < npair; p++) {
-            const f2v* q = Q + 16 * (size_t)p;
-            const f2v e1x = q[0], e1y = q[1], e1z = q[2], e2x = q[3], e2y = q[4], e2z = q[5];
-            const f2v tx = q[6], ty = q[7], tz = q[8], dqx = q[9], dqy = q[10], dqz = q[11], dw = q[12];
-            // device_cross(rmd, e2) then the dots, TD/Trixel.cu:180-186, per half
-            const f2v qx = Y * e2z - Z * e2y;
-            const f2v qy = Z * e2x - X * e2z;
-            const f2v qz = X * e2y - Y * e2x;
-            const f2v f = (qx * e1x + qy * e1y) + qz * e1z;
-            const f2v U = (qx * tx + qy * ty) + qz * tz;
-            const f2v V = (X * dqx + Y * dqy) + Z * dqz;
-            const bool c0 = flat_screen(f.x, U.x, V.x, dw.x), c1 = flat_screen(f.y, U.y, V.y, dw.y);
-            if (c0 || c1) {
-                if (c0) flat_accept(f.x, U.x, V.x, dw.x, 2 * p, d, best, n_acc);
-                if (c1) flat_accept(f.y, U.y, V.y, dw.y, 2 * p + 1, d, best, n_acc);
+        if (kVariant == 2) {
+            for (uint32_t p = 0; p < npair; p++) {
+                FlatPair c;
+                c.load(Q + 16 * (size_t)p);
+                c.test(X, Y, Z, 2 * p, d, best, n_acc);
             }
+        } else {
+            // software pipelined: pair p + 1's scalar loads are issued once
+            // pair p's have arrived (scalar loads return out of order, so a
+            // wait is always for all of them) and overlap pair p's tests
+            const uint32_t zero = ntri >> 31;  // 0: scenes hold < 2^29 triangles
+            FlatPair a, b;
+            a.load(Q);
+            uint32_t p = 0;
+            for (; p + 1 < npair; p += 2) {
+                b.load_after(Q, p + 1, a, zero);
+                a.test(X, Y, Z, 2 * p, d, best, n_acc);
+                a.load_after(Q, min(p + 2, npair - 1), b, zero);
+                b.test(X, Y, Z, 2 * p + 2, d, best, n_acc);
+            }
+            if (p < npair) a.test(X, Y, Z, 2 * p, d, best, n_acc);
         }
     }
     uint32_t argb = kBackground;
@@ -1706,7 +1756,8 @@ TraceFn flat_kernel_v(bool wh, bool cnt) {
 TraceFn flat_kernel(bool wh, bool cnt, int variant) {
     if (variant == 0) return flat_kernel_v<0>(wh, cnt);
     if (variant == 1) return flat_kernel_v<1>(wh, cnt);
-    return flat_kernel_v<2>(wh, cnt);
+    if (variant == 2) return flat_kernel_v<2>(wh, cnt);
+    return flat_kernel_v<3>(wh, cnt);
 }
 
 int launch_pair_tri(const float4* trec, uint32_t ntri, float4* tpair, void* stream) {

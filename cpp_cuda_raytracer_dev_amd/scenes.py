@@ -26,6 +26,9 @@ STANDINS = {
     # name: (triangles, bbox lo, bbox hi, (U, V) main blob, (U, V) small blob)
     "dragon": (871_414, (-0.112, 0.052, -0.067), (0.093, 0.199, 0.054), (640, 681), (39, 14)),
     "happy": (1_087_716, (-0.047, 0.055, -0.037), (0.044, 0.248, 0.047), (720, 756), (43, 7)),
+    # not a reference mesh: > 2^21 triangles, so its median tree is 22 levels
+    # tall (kernel 3's former path-code limit was 21); dragon-sized box
+    "big": (3_146_328, (-0.112, 0.052, -0.067), (0.093, 0.199, 0.054), (1536, 1025), (60, 6)),
 }
 STANDIN_SEED = 20221015
 
@@ -96,7 +99,7 @@ def _displace(v: np.ndarray, rng: np.random.Generator, octaves: int, amp: float)
 def standin(name: str):
     """Synthetic stand-in mesh: (verts [nv,3] f32, faces [nf,3] i32)."""
     ntri, lo, hi, (U, V), (u2, v2) = STANDINS[name]
-    rng = np.random.default_rng(STANDIN_SEED if name == "dragon" else STANDIN_SEED + 1)
+    rng = np.random.default_rng(STANDIN_SEED + {"dragon": 0, "happy": 1, "big": 2}[name])
     lo, hi = np.asarray(lo), np.asarray(hi)
     c, half = (lo + hi) / 2, (hi - lo) / 2
     v, f = _uv_sphere(U, V)

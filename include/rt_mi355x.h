@@ -46,7 +46,7 @@ typedef enum rt_status {
  * at TD/Camera.cu:28-34).  The segment from the light (2,2,2) to the hit is
  * walked with the reference's traversal rules; a pixel with an occluder
  * (any triangle but its own, w < 0.999*|segment|) is 0x00000000.  KD mode and
- * the wave-cooperative kernel only (tree height <= 21); the shadow rays'
+ * the wave-cooperative kernel only; the shadow rays'
  * visits are added to the same counters. */
 #define RT_FLAG_SHADOW 4u
 
@@ -276,7 +276,7 @@ int rt_camera_get_option(const rt_camera* c, int32_t key, int32_t* value);
  * shadow walks stop at occluders like timed ones): copies up to
  * n u64 of the record buffer; returns the count or a negative status. */
 #define RT_OPT_DEBUG 100
-#define RT_OPT_POOL_CAP 101 /* tests: shrink the wave-cooperative kernel's item pool (86..640) */
+#define RT_OPT_POOL_CAP 101 /* tests: shrink the wave-cooperative kernel's item pool (89..640) */
 int64_t rt_camera_debug_read(rt_camera* c, uint64_t* out, int64_t n);
 
 /* Object motion: the reference's keyboard transform

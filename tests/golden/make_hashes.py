@@ -42,6 +42,8 @@ FRAMES = [
     ("happy", 1920, 1080, 0, True, "default"),
     ("happy", 3840, 2160, 0, False, "default"),
     ("happy", 3840, 2160, 0, True, "default"),      # C5
+    ("big", 1920, 1080, 0, False, "default"),       # 3.1M triangles: a 22-level tree in kernel 3
+    ("big", 1920, 1080, 0, True, "default"),
 ]
 
 

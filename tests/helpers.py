@@ -40,16 +40,27 @@ def mesh(name):
 _tree_cache = {}
 
 
+def product_tree(name):
+    """rt_kd_build's node array (the product's builder)."""
+    if (name, 0) not in _tree_cache:
+        _tree_cache[(name, 0)] = R.kd_build(mesh(name)[1])
+    return _tree_cache[(name, 0)]
+
+
+def oracle_tree(name):
+    """The oracle's literal create_kd restatement (slow for millions of triangles)."""
+    if (name, 1) not in _tree_cache:
+        _tree_cache[(name, 1)] = O.build_kd(mesh(name)[2])
+    return _tree_cache[(name, 1)]
+
+
 def trees(name):
-    if name not in _tree_cache:
-        pts, leafs, oleafs = mesh(name)
-        _tree_cache[name] = (R.kd_build(leafs), O.build_kd(oleafs))
-    return _tree_cache[name]
+    return product_tree(name), oracle_tree(name)
 
 
 def oracle_render(name, w, h, mode=0, xform=None, rows=None, cam_kw=None, shadow=False):
     pts, _, _ = mesh(name)
-    onodes = trees(name)[1] if mode == 0 else None
+    onodes = oracle_tree(name) if mode == 0 else None
     cam = O.camera(w, h, **(cam_kw or {}))
     s = O.Scene(pts, O.default_rad(len(pts)), onodes, cam)
     try:
@@ -65,7 +76,7 @@ class GpuScene:
                  coarse=None, debug=None):
         pts, leafs, _ = mesh(name)
         self.trixel = R.Trixel(len(pts), pts, device=device)
-        self.trixel.set_kd_nodes(trees(name)[0])
+        self.trixel.set_kd_nodes(product_tree(name))
         if cam_kw:
             kw = dict(f_w=R.film_w(w, h), f_h=np.float32(.024), focal=np.float32(.055), pos=(0.0, 0.1, -1.0),
                       look_at=(0.0, 0.1, 0.0), up=(0.0, 1.0, 0.0)) | cam_kw
