@@ -44,11 +44,12 @@ sys.path.insert(0, ROOT)
 METRIC = "frames/sec + Mray/s at 1920×1080, Stanford dragon 800k tris, 1/2/4/8 GPU"
 W, H = 1920, 1080
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# FP32 vector peak (MI355X_MICROARCH.md): 256 CU x 128 lanes x 2.4 GHz = 78.6e12
-# instructions/s, x2 for packed v_pk_* = 157.3 TFLOP/s (the spec counts an FMA
-# as 2; with contraction off every flop is its own operation, so 157.3 is the
-# most a packed non-FMA stream can reach, 78.6 the unpacked one)
-VALU_PEAK_TFLOPS, VALU_PEAK_UNPACKED_TFLOPS = 157.3, 78.6
+# FP32 vector peak without FMA: the spec's 157.3 TFLOP/s (MI355X_MICROARCH.md)
+# counts a packed FMA as 4 flops per lane; with contraction off every flop is
+# its own operation, so the ceiling is 157.3 / 2 = 78.6 TFLOP/s with packed
+# v_pk_mul_f32 / v_pk_add_f32 and 39.3 unpacked.  tools/ubench_pk.hip measured
+# 64.8 (packed) and 34.6 (unpacked) T mul+add/s: 82 % and 88 % of those.
+VALU_PEAK_TFLOPS, VALU_PEAK_UNPACKED_TFLOPS = 78.6, 39.3
 # 28 FP32 flops + one correctly rounded divide per flat test
 FLOPS_PER_TEST = 28
 HASHES = os.path.join(ROOT, "tests", "golden", "frame_hashes.json")
@@ -61,8 +62,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--scene", default="dragon", choices=["dragon", "happy", "rabbit_70k", "tester"],
-                    help="dragon / happy: seeded stand-ins for the missing meshes; rabbit_70k / tester: the "
+    ap.add_argument("--scene", default="dragon", choices=["dragon", "happy", "rabbit_70k", "tester", "big"],
+                    help="dragon / happy: seeded stand-ins for the missing meshes (big: a 3.1M-triangle one); rabbit_70k / tester: the "
                          "reference's own meshes")
     ap.add_argument("--view", default="default", choices=["default", "fill"],
                     help="default: WinMain's camera; fill: the object over >= 90%% of the pixels (README.md:19)")
@@ -84,7 +85,8 @@ def parse():
                          "3 wave-cooperative item pool")
     ap.add_argument("--tile-order", type=int, default=3,
                     help="0 XCD-contiguous, 1 natural, 2 centre-out, 3 by the cost an earlier frame measured")
-    ap.add_argument("--rays", type=int, default=16, help="kernel 3: pixels per wave (64, 32, 16, 8)")
+    ap.add_argument("--rays", type=int, default=0,
+                    help="kernel 3: pixels per wave (64, 32, 16, 8; 0 = the library's automatic choice)")
     ap.add_argument("--items", type=int, default=2, help="kernel 3: items each lane pops per iteration (1, 2)")
     ap.add_argument("--order", type=int, default=-1,
                     help="interior record order: 0 BFS, 1 DFS preorder, 2 treelets (-1: the library default)")
@@ -625,7 +627,8 @@ def main():
                 "divides_per_launch": tests,
                 "peak_unpacked": VALU_PEAK_UNPACKED_TFLOPS,
                 "flops_model": "28 FP32 flops + 1 divide per ray-triangle test x npix x ntri (SURVEY.md 8d, "
-                               "TD/Trixel.cu:173-209); peak = FP32 vector spec (packed issue), 78.6 unpacked",
+                               "TD/Trixel.cu:173-209); peak = non-FMA FP32 issue with packed v_pk_* "
+                               "(157.3 TF FMA spec / 2), 39.3 unpacked",
                 "counts_per_launch": {"leaf_tests": int(cnt[1]), "accept": int(cnt[2]), "hit_pixels": int(cnt[3]),
                                       "pixels": my_pix},
             } if a.mode == 1 else {
@@ -637,7 +640,9 @@ def main():
                 "traffic": traffic,
                 "kernel": {1: "k_trace_kd", 2: "k_trace_kd2", 3: "k_trace_kd3"}[a.kernel] if a.mode == 0
                           else "k_trace_flat",
-                "kernel_options": {"kernel": a.kernel, "tile_order": a.tile_order, "rays_per_wave": a.rays,
+                "kernel_options": {"kernel": a.kernel, "tile_order": a.tile_order,
+                                   "rays_per_wave": cam.get_option(_lib.RT_OPT_RAYS_USED),
+                                   "rays_per_wave_option": a.rays,
                                    "record_order": trixel.get_option(_lib.RT_SCENE_ORDER),
                                    "treelet_height": trixel.get_option(_lib.RT_SCENE_TREELET_HEIGHT),
                                    "items_per_lane": a.items, "coarse_groups_per_wave": a.coarse,

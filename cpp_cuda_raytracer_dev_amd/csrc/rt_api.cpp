@@ -84,7 +84,8 @@ struct rt_camera {
     int frames_since = 0;
     uint64_t layout_gen = 0, cost_gen = 0;   // fine-grid generation, and the one h_cost was read for
     uint64_t order_gen = ~0ull;              // generation whose cost order d_order holds
-    int rays = 16;                   // kOptRays: pixels per wave of kernel 3
+    int rays = 0;                    // kOptRays: pixels per wave of kernel 3 (0: auto_rays)
+    int last_rays = 0;               // the pixels per wave the last kernel-3 render used
     int items = 2;                   // kOptItems: items per lane per pool iteration
     int flat_variant = 2;            // kOptFlat: flat-list kernel form
     // shadow renders: the any-hit push order, fixed (kOptShadowOrder 0..3)
@@ -533,6 +534,24 @@ bool set_fine_region(rt_camera* c, TraceParams& p, int per_wave, bool fused) {
 // the fine / far split (set_fine_region).  Returns whether the far groups
 // are fused into the fine kernel (every pixel outside the fine region is
 // then provably background: a far wave that finds otherwise sets error 4).
+// Kernel 3's pixels per wave when RT_OPT_RAYS is 0 (auto): 16, unless this
+// rank's fine region (the root box's screen rectangle) holds too few 16-ray
+// units to fill the GPU -- then 8, which doubles the waves and halves the
+// heaviest unit's pool chain.  Measured on the dragon stand-in (one GPU):
+// 960x540 (3.4k 16-ray units) 67.7 -> 52.7 us with 8 rays, 1920x1080 (13.4k
+// units) 88 -> 130 us.
+constexpr int64_t kAutoRaysMinUnits = 8192;
+
+int auto_rays(const rt_camera* c, const TraceParams& p) {
+    double r[4];
+    if (!root_rect(c, p, r)) return 16;  // no bounded rectangle: the whole frame is fine
+    const double x0 = std::max(r[0] - 2, 0.0), x1 = std::min(r[1] + 2, (double)c->w - 1);
+    const double y0 = std::max(r[2] - 2, 0.0), y1 = std::min(r[3] + 2, (double)c->h - 1);
+    if (x1 < x0 || y1 < y0) return 16;
+    const double px = (x1 - x0 + 1) * (y1 - y0 + 1) / p.nranks;
+    return px / 16 < (double)kAutoRaysMinUnits ? 8 : 16;
+}
+
 bool frame_geometry(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t mode, TraceParams& p) {
     static const float ident[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
     const rt_scene* s = c->obj;
@@ -546,9 +565,10 @@ bool frame_geometry(rt_camera* c, const float* xform, const rt_tile* tile, uint3
     p.h = c->h;
     p.nranks = tile ? tile->nranks : 1;
     p.rank = tile ? tile->rank : 0;
+    camera_relative_box(s->root, c->pos, p.root_box);
     const int32_t nbands = (c->h + kTileH - 1) / kTileH;
     const int kernel = mode == RT_MODE_KD ? effective_kernel(c) : 0;
-    p.rays = kernel == 3 ? c->rays : 64;
+    p.rays = kernel == 3 ? (c->rays > 0 ? c->rays : auto_rays(c, p)) : 64;
     if (kernel == 0 || kernel == 1) {        // flat / v1: 32x8 tiles, four 8x8 waves
         p.tile_w = kTileWFlat; p.tile_h = kTileH;
     } else if (p.rays == 64) {               // v2 / v3: 16x8 tiles, two 8x8 waves
@@ -558,7 +578,6 @@ bool frame_geometry(rt_camera* c, const float* xform, const rt_tile* tile, uint3
     }
     p.tiles_x = (c->w + p.tile_w - 1) / p.tile_w;
     p.block_rows = ((nbands + p.nranks - 1) / p.nranks) * (kTileH / p.tile_h);
-    camera_relative_box(s->root, c->pos, p.root_box);
     p.plain_xf = 1;
     for (int k = 0; k < 12; k++) p.plain_xf &= (p.xf[k] == ident[k]) ? 1 : 0;
     // Far groups go to the fine kernel's extra blocks when every coarse group
@@ -958,6 +977,7 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
     }
     TraceParams p;
     if ((rc = fill_params(c, xform, tile, argb, hit, mode, p))) return rc;
+    if (mode == RT_MODE_KD && effective_kernel(c) == 3) c->last_rays = p.rays;
     int trial;
     p.any_order = any_order_for(c, flags, stream, trial) | ((c->debug & 16) ? 4 : 0);
     hipStream_t st = (hipStream_t)stream;
@@ -1169,8 +1189,8 @@ extern "C" int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value) {
         c->kernel_version = value;
         return RT_OK;
     case kOptRays:
-        if (value != 8 && value != 16 && value != 32 && value != 64)
-            return fail(RT_ERR_INVALID, "rays per wave %d (8, 16, 32, 64)", value);
+        if (value != 0 && value != 8 && value != 16 && value != 32 && value != 64)
+            return fail(RT_ERR_INVALID, "rays per wave %d (0 auto, 8, 16, 32, 64)", value);
         c->rays = value;
         return RT_OK;
     case kOptItems:
@@ -1219,6 +1239,7 @@ extern "C" int rt_camera_get_option(const rt_camera* c, int32_t key, int32_t* va
     case kOptItems: *value = c->items; return RT_OK;
     case kOptCoarse: *value = c->coarse; return RT_OK;
     case kOptFlat: *value = c->flat_variant; return RT_OK;
+    case kOptRaysUsed: *value = c->last_rays; return RT_OK;
     case kOptShadowOrder: *value = c->shadow_order >= 0 ? c->shadow_order : c->any_best; return RT_OK;
     default: return fail(RT_ERR_INVALID, "rt_camera_get_option: unknown key %d", key);
     }

@@ -45,7 +45,8 @@ enum Option : int32_t {
     kOptItems = 4,      // kernel 3 items popped per lane per iteration: 1 or 2
     kOptCoarse = 5,     // kernel 3 coarse groups per wave outside the root box's rectangle (0 = off)
     kOptShadowOrder = 6,  // kernel 3 any-hit push order 0..3, -1 = timed choice (default)
-    kOptFlat = 7,       // flat-list kernel: 0 one triangle per iteration, 1 pairs, 2 packed pairs
+    kOptFlat = 7,       // flat-list kernel: 0 one triangle per iteration, 1 pairs, 2 packed pairs, 3 pipelined
+    kOptRaysUsed = 8,   // get only: pixels per wave of the last kernel-3 render
     kOptDebug = 100,    // diagnostics: 1 = skip traversal, 2 = per-wave timestamps, 4 = every group
                         // coarse, 8 = coarse kernel on a side stream beside the fine one,
                         // 16 = counted shadow walks stop at occluders (the timed walk's work)

@@ -257,7 +257,8 @@ int rt_camera_info(const rt_camera* c, int32_t* w, int32_t* h, int32_t* max_dept
  * Every setting renders the identical frame. */
 #define RT_OPT_KERNEL 1
 #define RT_OPT_TILE_ORDER 2
-#define RT_OPT_RAYS 3 /* kernel 3: pixels per wave (64, 32, 16 default, 8); the rest of the lanes help */
+#define RT_OPT_RAYS 3 /* kernel 3: pixels per wave (64, 32, 16, 8; 0 = auto, default: 8 when this rank's
+                         share of the object's screen rectangle is too small to fill the GPU with 16) */
 #define RT_OPT_ITEMS 4 /* kernel 3: items each lane pops per iteration (1, 2 default) */
 #define RT_OPT_COARSE 5 /* kernel 3: 8x8 groups per wave outside the root box's screen rectangle (0..32, 8 default, 0 = off) */
 /* kernel 3, shadow rays: the order the any-hit walk pushes children in (0..3;
@@ -266,8 +267,10 @@ int rt_camera_info(const rt_camera* c, int32_t* w, int32_t* h, int32_t* max_dept
  * stream capture).  Get returns the order in use. */
 #define RT_OPT_SHADOW_ORDER 6
 /* Flat-list kernel form (same frame): 0 one triangle per iteration, 1 two
- * per iteration, 2 two per iteration as packed float2 arithmetic (default). */
+ * per iteration, 2 two per iteration as packed float2 arithmetic (default),
+ * 3 = 2 software pipelined. */
 #define RT_OPT_FLAT 7
+#define RT_OPT_RAYS_USED 8 /* get only: the pixels per wave the last kernel-3 render used */
 int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value);
 int rt_camera_get_option(const rt_camera* c, int32_t key, int32_t* value);
 

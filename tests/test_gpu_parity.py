@@ -45,7 +45,7 @@ def test_small_frames_vs_golden(name, w, h, mode):
 
 
 KERNELS = [(1, 0, 64), (2, 2, 64), (2, 1, 64), (3, 1, 64), (3, 2, 32), (3, 1, 32), (3, 2, 16), (3, 2, 8), (3, 3, 16),
-           (3, 3, 8), (3, 4, 16)]  # (KD kernel, tile order, rays/wave)
+           (3, 3, 8), (3, 4, 16), (3, 3, 0)]  # (KD kernel, tile order, rays/wave; 0 = automatic)
 
 
 def _counters_match(cnt, ocnt, kernel):
@@ -95,6 +95,16 @@ def test_rabbit_960x540_flat_band():
     # the flat and KD results agree on this scene (no boundary-pruned hits here)
     kargb, khit, _ = s.render(0)
     assert (khit[sl] == hit[sl]).all()
+
+
+def test_auto_rays_choice():
+    """RT_OPT_RAYS 0 (default): 8 pixels per wave when the object's screen
+    rectangle holds few 16-ray units (dragon 960x540), else 16 (1080p)."""
+    from cpp_cuda_raytracer_dev_amd import _lib
+    for (w, h), want in (((960, 540), 8), ((1920, 1080), 16)):
+        s = H.GpuScene("dragon", w, h)
+        s.render(0)
+        assert s.cam.get_option(_lib.RT_OPT_RAYS_USED) == want, (w, h)
 
 
 @pytest.mark.parametrize("shadow", [False, True])
