@@ -65,7 +65,7 @@ int resolve_threads(int nthreads) {
 
 // ------------------------------------------------------------- PLY input
 
-// windows.h min/max as used by TD/read_ply.cpp:142-195 (order matters only
+// windows.h min/max as used by TD/read_ply.cpp:82-89,104-111,128-135 (order matters only
 // for the sign of zero, which is kept identical anyway).
 inline float wmin(float a, float b) { return (a < b) ? a : b; }
 inline float wmax(float a, float b) { return (a > b) ? a : b; }
@@ -135,7 +135,7 @@ extern "C" int rt_mesh_assemble(const float* verts, int64_t nvert, const int32_t
                 free(pts); free(lf);
                 return fail(RT_ERR_INVALID, "rt_mesh_assemble: face %lld index out of range", (long long)f);
             }
-        if (a == 4) {  // TD/read_ply.cpp:130-185: ABCD -> (A,B,C), (A,C,D)
+        if (a == 4) {  // TD/read_ply.cpp:70-125: ABCD -> (A,B,C), (A,C,D)
             const float* A = verts + 3 * (int64_t)idx[k];
             const float* B = verts + 3 * (int64_t)idx[k + 1];
             const float* Cv = verts + 3 * (int64_t)idx[k + 2];
@@ -144,7 +144,7 @@ extern "C" int rt_mesh_assemble(const float* verts, int64_t nvert, const int32_t
             put(t, 0, A); put(t, 1, B); put(t, 2, Cv); t++;
             aabb3(lf[t], A, D, Cv); lf[t].tri = t;
             put(t, 0, A); put(t, 1, Cv); put(t, 2, D); t++;
-        } else {       // TD/read_ply.cpp:187-209: P1P2P3 stored as (P3,P1,P2)
+        } else {       // TD/read_ply.cpp:127-149: P1P2P3 stored as (P3,P1,P2)
             const float* P1 = verts + 3 * (int64_t)idx[k];
             const float* P2 = verts + 3 * (int64_t)idx[k + 1];
             const float* P3 = verts + 3 * (int64_t)idx[k + 2];

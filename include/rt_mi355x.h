@@ -94,7 +94,7 @@ typedef struct rt_camera rt_camera; /* Camera: rays, frame, camera-relative obje
 int rt_read_ply(const char* path, int mode, float** points9, uint32_t* ntri,
                 rt_leaf_aabb** leafs);
 
-/* The face-assembly half of read_ply (TD/read_ply.cpp:128-210) on an indexed
+/* The face-assembly half of read_ply (TD/read_ply.cpp:67-149) on an indexed
  * mesh: arity[f] in {3,4}, idx = concatenated face indices. */
 int rt_mesh_assemble(const float* verts, int64_t nvert, const int32_t* arity,
                      const int32_t* idx, int64_t nface, float** points9,

@@ -89,7 +89,7 @@ def primary_ray(cam, ix, iy):
 # ----------------------------------------------------------- mesh + KD (a11)
 
 def assemble(verts, arity, idx):
-    """TD/read_ply.cpp:128-210."""
+    """TD/read_ply.cpp:67-149."""
     mn = lambda a, b: a if a < b else b  # noqa: E731
     mx = lambda a, b: a if a > b else b  # noqa: E731
     pts, boxes = [], []

@@ -89,7 +89,7 @@ static uint32_t to_u8(float t) {
 
 /* -------------------------------------------------------------- PLY input */
 
-/* min/max macros of windows.h as used in TD/read_ply.cpp:142-195 */
+/* min/max macros of windows.h as used in TD/read_ply.cpp:82-89,104-111,128-135 */
 static float wmin(float a, float b) { return (a < b) ? a : b; }
 static float wmax(float a, float b) { return (a > b) ? a : b; }
 
@@ -102,7 +102,7 @@ static void set_aabb(orc_leaf* lf, const float* a, const float* b, const float* 
 
 static void put3(float* dst, const float* v) { dst[0] = v[0]; dst[1] = v[1]; dst[2] = v[2]; }
 
-/* Face assembly of TD/read_ply.cpp:128-210 (H8): a 4-gon ABCD becomes
+/* Face assembly of TD/read_ply.cpp:67-149 (H8): a 4-gon ABCD becomes
  * (A,B,C),(A,C,D) with AABBs over {A,B,C} and {A,D,C}; a 3-gon P1P2P3 is
  * stored (P3,P1,P2) with its AABB over {P1,P2,P3}. */
 int orc_assemble(const float* verts, int64_t nvert, const int32_t* arity,
@@ -231,7 +231,7 @@ int orc_read_ply(const char* path, int mode, float** points9, uint32_t* ntri,
             if (j < 3) verts[3 * i + j] = v;
         }
     }
-    /* TD/read_ply.cpp:128: `for (i = 0; i < num_tri*3;)` with num_tri bumped
+    /* TD/read_ply.cpp:68: `for (i = 0; i < num_tri*3;)` with num_tri bumped
      * per quad reads exactly nf faces. */
     long k = 0;
     for (long f = 0; f < nf; f++) {
