@@ -244,8 +244,8 @@ def cpu_baseline(pts, nodes, w, h, seconds, threads, mode, shadow=False, rays_pe
                      f"({dt:.1f} s), {frames1} x rows {rows1[0]}-{rows1[1]} with 1 thread ({dt1:.1f} s); "
                      "oracle/oracle.c (gcc -O3 -ffp-contract=off, OpenMP over rows)"}
     if build_times:
-        out["kd_build"] = {**build_times, "what": "rt_kd_build (a11, TD/Trixel.h:135-473) on this host, "
-                                                  "all threads / 1 thread"}
+        out["kd_build"] = {**build_times, "what": "rt_kd_build (a11, TD/Trixel.h:135-473) on this host, all "
+                                                  "threads / 1 thread; rt_kd_build_gpu on the GPU (host in/out)"}
     return out
 
 
@@ -384,6 +384,17 @@ def main():
 
     from cpp_cuda_raytracer_dev_amd import scenes
     pts, leafs, nodes, build_times = build_scene(a.scene)
+    # the same tree built on this GPU (rt_kd_build_gpu):
+    # first call (allocations included) and a warm one, byte-checked
+    gb = []
+    for _ in range(2):
+        t0 = time.perf_counter()
+        gnodes = R.kd_build_gpu(leafs, device=local)
+        gb.append(time.perf_counter() - t0)
+    build_times["kd_build_gpu_s"] = round(gb[1], 4)
+    build_times["kd_build_gpu_s_first"] = round(gb[0], 4)
+    build_times["kd_build_gpu_equals_host"] = gnodes.tobytes() == nodes.tobytes()
+    del gnodes
     trixel = R.Trixel(len(pts), pts, device=local)
     trixel.set_kd_nodes(nodes)
     if a.treelet > 0:
@@ -661,6 +672,7 @@ def main():
                 "bytes_model": "36*V_int + 40*V_leaf + 24*H + 4*P (SURVEY.md 8d)",
             }),
             "device_err": errs if multi else dev_err,
+            "kd_build": build_times,
         }
         if frame_check is not None:
             res["frame_check"] = frame_check

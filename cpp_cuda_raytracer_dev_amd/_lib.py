@@ -71,6 +71,9 @@ SIGNATURES = {
                                    C.POINTER(_P)]),
     "rt_host_free": (None, [_P]),
     "rt_kd_build": (C.c_int, [_P, C.c_uint32, _P, C.c_int]),
+    "rt_kd_build_gpu": (C.c_int, [C.c_int, _P, C.c_uint32, _P, _P]),
+    "rt_scene_build_kd": (C.c_int, [_P, _P, C.c_uint32, _P]),
+    "rt_scene_read_kd": (C.c_int, [_P, _P, C.c_uint64]),
     "rt_camera_basis": (C.c_int, [C.c_int32, C.c_int32, C.c_float, C.c_float, C.c_float, _P, _P, _P,
                                   C.POINTER(RtCameraBasis)]),
     "rt_film_w": (C.c_float, [C.c_int32, C.c_int32]),

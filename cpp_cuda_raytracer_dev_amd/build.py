@@ -21,7 +21,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "librt_mi355x.so")
 ARCH = os.environ.get("RT_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["rt_kernels.hip", "rt_api.cpp", "scene_host.cpp", "motion.cpp", "comm.cpp"]
+SOURCES = ["rt_kernels.hip", "kd_build_gpu.hip", "rt_api.cpp", "scene_host.cpp", "motion.cpp", "comm.cpp"]
 OBJ = os.path.join(PKG, "_obj")  # per-source objects (git- and gpurun-ignored)
 # -fno-slp-vectorize: hipcc's packed-math (v_pk_*) SLP pairs cost more register
 # moves than they save in the traversal loop (0.0851 vs 0.0871 ms per 1080p

@@ -28,10 +28,9 @@ struct rt_scene {
     int32_t height = 0;
     uint64_t tree_version = 0;
     rt_kd_node root{};               // host copy of node 0 (root box)
-    // host shape of the tree (left child or -1 for a leaf, leaf triangle),
-    // kept to re-lay the interior records out (rt_scene_set_option)
+    // host shape of the tree (left child or -1 for a leaf), kept to re-lay
+    // the interior records out (rt_scene_set_option)
     std::vector<int32_t> h_left;
-    std::vector<uint32_t> h_tri;
     int record_order = 0;            // RT_SCENE_ORDER: 0 BFS, 1 DFS preorder, 2 treelets
     int treelet_height = 3;          // RT_SCENE_TREELET_HEIGHT
 };
@@ -738,26 +737,23 @@ std::vector<int32_t> interior_order(const std::vector<int32_t>& left, int order,
     return ids;
 }
 
-// (Re)builds the interior record order, the node -> ref table and uploads them.
+// (Re)builds the interior record order and the node -> ref table (on the
+// device, from the uploaded nodes).
 int relabel(rt_scene* s) {
     const int64_t n = (int64_t)s->h_left.size();
     const std::vector<int32_t> ids = interior_order(s->h_left, s->record_order, s->treelet_height);
-    std::vector<uint32_t> ref((size_t)n);
-    for (int64_t i = 0; i < n; i++)
-        if (s->h_left[(size_t)i] < 0) ref[(size_t)i] = kLeafBit | s->h_tri[(size_t)i];
-    for (size_t k = 0; k < ids.size(); k++) ref[(size_t)ids[k]] = (uint32_t)k;
     DeviceGuard g(s->device);
     dev_free(s->d_interior_ids);
     dev_free(s->d_node_ref);
     int rc;
     if ((rc = dev_alloc(&s->d_interior_ids, ids.size(), "hipMalloc(ids)")) ||
         (rc = dev_alloc(&s->d_node_ref, (size_t)n, "hipMalloc(node_ref)")) ||
-        (rc = hip_check(hipMemcpy(s->d_node_ref, ref.data(), sizeof(uint32_t) * (size_t)n, hipMemcpyHostToDevice), "H2D refs")) ||
         (!ids.empty() && (rc = hip_check(hipMemcpy(s->d_interior_ids, ids.data(), sizeof(int32_t) * ids.size(),
-                                                   hipMemcpyHostToDevice), "H2D ids"))))
+                                                   hipMemcpyHostToDevice), "H2D ids"))) ||
+        (rc = launch_node_ref(s->d_nodes, n, s->d_interior_ids, (int64_t)ids.size(), s->d_node_ref, nullptr)) ||
+        (rc = hip_check(hipMemcpy(&s->root_ref, s->d_node_ref, sizeof(uint32_t), hipMemcpyDeviceToHost), "D2H root ref")))
         return rc;
     s->ninterior = (int64_t)ids.size();
-    s->root_ref = ref[0];
     s->tree_version++;
     return RT_OK;
 }
@@ -772,7 +768,6 @@ extern "C" int rt_scene_set_kd(rt_scene* s, const rt_kd_node* nodes, uint64_t nn
     // Validate: BFS order with right = left + 1 (so every DFS terminates),
     // leaves cover every triangle exactly once, bounded height.
     std::vector<int32_t> left((size_t)n, -1);
-    std::vector<uint32_t> tri((size_t)n, 0);
     std::vector<uint8_t> seen(s->ntri, 0);
     std::vector<int32_t> depth((size_t)n, 0);
     int32_t height = 0;
@@ -782,7 +777,6 @@ extern "C" int rt_scene_set_kd(rt_scene* s, const rt_kd_node* nodes, uint64_t nn
             if (nd.tri_index < 0 || nd.tri_index >= (int64_t)s->ntri || seen[(size_t)nd.tri_index])
                 return fail(RT_ERR_INVALID, "rt_scene_set_kd: leaf %lld has bad/duplicate triangle", (long long)i);
             seen[(size_t)nd.tri_index] = 1;
-            tri[(size_t)i] = (uint32_t)nd.tri_index;
         } else {
             if (nd.left <= i || nd.right != nd.left + 1 || nd.right >= n)
                 return fail(RT_ERR_INVALID, "rt_scene_set_kd: node %lld children %lld/%lld not BFS", (long long)i,
@@ -809,12 +803,68 @@ extern "C" int rt_scene_set_kd(rt_scene* s, const rt_kd_node* nodes, uint64_t nn
     s->root = nodes[0];
     s->height = height;
     s->h_left.swap(left);
-    s->h_tri.swap(tri);
     if ((rc = relabel(s))) {
         dev_free(s->d_nodes);
         return rc;
     }
     return RT_OK;
+}
+
+extern "C" int rt_kd_build_gpu(int device, const rt_leaf_aabb* leafs, uint32_t ntri, rt_kd_node* nodes, void* stream) {
+    if (!nodes) return fail(RT_ERR_INVALID, "rt_kd_build_gpu: null nodes");
+    int rc = validate_leafs(leafs, ntri, "rt_kd_build_gpu");
+    if (rc) return rc;
+    DeviceGuard g(device);
+    if (!g.ok) return fail(RT_ERR_HIP, "rt_kd_build_gpu: hipSetDevice(%d) failed", device);
+    KdShape shape;
+    kd_shape(ntri, shape);
+    const int64_t nnode = 2 * (int64_t)ntri - 1;
+    rt_kd_node* d = nullptr;
+    if ((rc = dev_alloc(&d, (size_t)nnode, "hipMalloc(kd nodes)"))) return rc;
+    rc = kd_build_device(leafs, ntri, shape, d, stream);
+    if (!rc)
+        rc = hip_check(hipMemcpy(nodes, d, sizeof(rt_kd_node) * (size_t)nnode, hipMemcpyDeviceToHost), "D2H kd nodes");
+    dev_free(d);
+    return rc;
+}
+
+extern "C" int rt_scene_build_kd(rt_scene* s, const rt_leaf_aabb* leafs, uint32_t ntri, void* stream) {
+    if (!s) return fail(RT_ERR_INVALID, "rt_scene_build_kd: null scene");
+    if (ntri != s->ntri)
+        return fail(RT_ERR_INVALID, "rt_scene_build_kd: %u leaf boxes for %u triangles", ntri, s->ntri);
+    int rc = validate_leafs(leafs, ntri, "rt_scene_build_kd");
+    if (rc) return rc;
+    KdShape shape;
+    kd_shape(ntri, shape);
+    if (shape.height > kMaxDepth)
+        return fail(RT_ERR_INVALID, "rt_scene_build_kd: tree height %d exceeds the %d-entry LDS stack", shape.height,
+                    kMaxDepth);
+    DeviceGuard g(s->device);
+    const int64_t nnode = 2 * (int64_t)ntri - 1;
+    dev_free(s->d_nodes);
+    if ((rc = dev_alloc(&s->d_nodes, (size_t)nnode, "hipMalloc(nodes)")) ||
+        (rc = kd_build_device(leafs, ntri, shape, s->d_nodes, stream)) ||
+        (rc = hip_check(hipMemcpy(&s->root, s->d_nodes, sizeof(rt_kd_node), hipMemcpyDeviceToHost), "D2H root"))) {
+        dev_free(s->d_nodes);
+        return rc;
+    }
+    s->nnode = nnode;
+    s->height = shape.height;
+    s->h_left.swap(shape.left);
+    if ((rc = relabel(s))) {
+        dev_free(s->d_nodes);
+        return rc;
+    }
+    return RT_OK;
+}
+
+extern "C" int rt_scene_read_kd(rt_scene* s, rt_kd_node* nodes, uint64_t nnode) {
+    if (!s || !nodes) return fail(RT_ERR_INVALID, "rt_scene_read_kd: null argument");
+    if (!s->d_nodes || (int64_t)nnode != s->nnode)
+        return fail(RT_ERR_INVALID, "rt_scene_read_kd: scene has %lld nodes, %llu requested", (long long)s->nnode,
+                    (unsigned long long)nnode);
+    DeviceGuard g(s->device);
+    return hip_check(hipMemcpy(nodes, s->d_nodes, sizeof(rt_kd_node) * (size_t)nnode, hipMemcpyDeviceToHost), "D2H nodes");
 }
 
 extern "C" int rt_scene_set_option(rt_scene* s, int32_t key, int32_t value) {

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "../../include/rt_mi355x.h"
 
 namespace rt {
@@ -147,6 +149,23 @@ int launch_trace(const TraceParams& p, uint32_t mode, uint32_t flags, int kernel
                  void* stream, int part);
 // Camera-relative box of one world node, exactly as init_cam_voxel_mem_cuda.
 void camera_relative_box(const rt_kd_node& nd, const float pos[3], float out[6]);
+// KD build on the GPU (kd_build_gpu.hip).  The median tree's shape depends
+// on the triangle count alone: per node its position range [l, r], median m,
+// first child (-1 for a leaf) and parent; level k = nodes [level[k], level[k+1]).
+struct KdShape {
+    std::vector<int32_t> l, m, r, left, parent;
+    std::vector<int64_t> level;
+    int32_t height = 0;
+};
+void kd_shape(uint32_t n, KdShape& out);
+// The node array of rt_kd_build, built on the current device into d_nodes
+// (2n-1 entries); synchronises `stream`.
+int kd_build_device(const rt_leaf_aabb* h_leafs, uint32_t n, const KdShape& shape, rt_kd_node* d_nodes, void* stream);
+// Traversal refs: kLeafBit | tri for leaves, record position for interior ids.
+int launch_node_ref(const rt_kd_node* d_nodes, int64_t nnode, const int32_t* d_ids, int64_t ninterior,
+                    uint32_t* d_ref, void* stream);
+// rt_kd_build's input checks: tri indices a permutation of [0, n), no NaN bound.
+int validate_leafs(const rt_leaf_aabb* leafs, uint32_t n, const char* what);
 int launch_unpack(int32_t w, int32_t h, int32_t nranks, const uint32_t* gathered,
                   uint32_t* frame, void* stream);
 // Slots s of `rank` whose band rank + s*nranks lies in [b0, b1): [s0, s1).

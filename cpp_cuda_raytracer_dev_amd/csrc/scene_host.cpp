@@ -474,20 +474,28 @@ struct Range { int64_t l, m, r; };
 
 }  // namespace
 
-extern "C" int rt_kd_build(const rt_leaf_aabb* leafs, uint32_t n, rt_kd_node* nodes, int nthreads) {
-    if (!leafs || !nodes || n == 0) return fail(RT_ERR_INVALID, "rt_kd_build: empty input");
-    if (n >= kLeafBit) return fail(RT_ERR_INVALID, "rt_kd_build: too many triangles");
-    const int T = resolve_threads(nthreads);
-    {   // tri_list_index must be a permutation (set_sorted_voxels indexes by it)
-        std::vector<uint8_t> seen(n, 0);
-        for (uint32_t i = 0; i < n; i++) {
-            int64_t t = leafs[i].tri;
-            if (t < 0 || t >= (int64_t)n || seen[(size_t)t]) return fail(RT_ERR_INVALID, "rt_kd_build: tri indices are not a permutation");
-            seen[(size_t)t] = 1;
-            for (int k = 0; k < 6; k++)
-                if (isnan(list_key(leafs[i], k))) return fail(RT_ERR_INVALID, "rt_kd_build: NaN bound at %u", i);
-        }
+namespace rt {
+int validate_leafs(const rt_leaf_aabb* leafs, uint32_t n, const char* what) {
+    if (!leafs || n == 0) return fail(RT_ERR_INVALID, "%s: empty input", what);
+    if (n >= kLeafBit) return fail(RT_ERR_INVALID, "%s: too many triangles", what);
+    // tri_list_index must be a permutation (set_sorted_voxels indexes by it)
+    std::vector<uint8_t> seen(n, 0);
+    for (uint32_t i = 0; i < n; i++) {
+        int64_t t = leafs[i].tri;
+        if (t < 0 || t >= (int64_t)n || seen[(size_t)t]) return fail(RT_ERR_INVALID, "%s: tri indices are not a permutation", what);
+        seen[(size_t)t] = 1;
+        for (int k = 0; k < 6; k++)
+            if (isnan(list_key(leafs[i], k))) return fail(RT_ERR_INVALID, "%s: NaN bound at %u", what, i);
     }
+    return RT_OK;
+}
+}  // namespace rt
+
+extern "C" int rt_kd_build(const rt_leaf_aabb* leafs, uint32_t n, rt_kd_node* nodes, int nthreads) {
+    if (!nodes) return fail(RT_ERR_INVALID, "rt_kd_build: null nodes");
+    int vrc = validate_leafs(leafs, n, "rt_kd_build");
+    if (vrc) return vrc;
+    const int T = resolve_threads(nthreads);
     // Six sorted position lists.  merge_sort (TD/sort.h:25-60) takes the right
     // run on ties, so equal keys end up in descending input position: sort by
     // (key ascending, position descending).

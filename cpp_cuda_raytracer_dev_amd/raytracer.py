@@ -80,6 +80,15 @@ def kd_build(kd_leafs: np.ndarray, nthreads: int = 0) -> np.ndarray:
     return nodes
 
 
+def kd_build_gpu(kd_leafs: np.ndarray, device: int = 0, stream=None) -> np.ndarray:
+    """rt_kd_build_gpu: the same node array as ``kd_build``, built on a GPU."""
+    leafs = np.ascontiguousarray(kd_leafs, LEAF_AABB_DTYPE)
+    nodes = np.zeros(max(2 * len(leafs) - 1, 1), KD_NODE_DTYPE)
+    s = C.c_void_p(stream) if isinstance(stream, int) else C.c_void_p(None)
+    _lib.call("rt_kd_build_gpu", device, _lib.ptr(leafs), len(leafs), _lib.ptr(nodes), s)
+    return nodes
+
+
 def film_w(w: int, h: int) -> float:
     """WinMain's film width ((float)w/h)*.024f (TD/WinMain.cpp:29,69-70)."""
     return float(np.float32(_lib.lib().rt_film_w(w, h)))
@@ -195,14 +204,25 @@ class Trixel:
         self._leafs = np.ascontiguousarray(voxel_list, LEAF_AABB_DTYPE)[:num_leaf_voxels].copy()
         return 0
 
-    def create_kd(self, nthreads: int = 0) -> int:
-        """TD/Trixel.h:135-385: -12 if set_sorted_voxels was not called."""
+    def create_kd(self, nthreads: int = 0, on_device: bool = False) -> int:
+        """TD/Trixel.h:135-385: -12 if set_sorted_voxels was not called.
+        on_device: build on the scene's GPU (rt_scene_build_kd; same nodes)."""
         if self._leafs is None:
             return -12
-        self.h_nodes = kd_build(self._leafs, nthreads)
-        _lib.call("rt_scene_set_kd", self._h, _lib.ptr(self.h_nodes), len(self.h_nodes))
+        if on_device:
+            _lib.call("rt_scene_build_kd", self._h, _lib.ptr(self._leafs), len(self._leafs), None)
+            self.h_nodes = None
+        else:
+            self.h_nodes = kd_build(self._leafs, nthreads)
+            _lib.call("rt_scene_set_kd", self._h, _lib.ptr(self.h_nodes), len(self.h_nodes))
         self._leafs = None  # the reference frees the sorted lists (TD/Trixel.h:381-383)
         return 0
+
+    def read_kd_nodes(self) -> np.ndarray:
+        """The scene's node array, copied back from the device."""
+        nodes = np.zeros(2 * self.num_trixels - 1, KD_NODE_DTYPE)
+        _lib.call("rt_scene_read_kd", self._h, _lib.ptr(nodes), len(nodes))
+        return nodes
 
     def set_kd_nodes(self, nodes: np.ndarray) -> int:
         """Upload an already built node array (e.g. cached on disk)."""

@@ -108,6 +108,14 @@ void rt_host_free(void* p);
 int rt_kd_build(const rt_leaf_aabb* leafs, uint32_t ntri, rt_kd_node* nodes,
                 int nthreads);
 
+/* The same build on a GPU: byte-identical nodes.  The
+ * six merge sorts are stable radix sorts fed in descending position order
+ * (merge_sort's tie order, TD/sort.h:25-60), each BFS level's stable
+ * partitions (TD/Trixel.h:214-327) one scan and one scatter over all six
+ * lists.  leafs/nodes are host arrays; the device work runs on `stream`
+ * (hipStream_t or NULL) of `device` and is synchronised before returning. */
+int rt_kd_build_gpu(int device, const rt_leaf_aabb* leafs, uint32_t ntri, rt_kd_node* nodes, void* stream);
+
 /* Camera::Camera basis (TD/Camera.cpp:5-67). */
 int rt_camera_basis(int32_t w, int32_t h, float f_w, float f_h, float focal,
                     const float pos[3], const float look_at[3], const float up[3],
@@ -129,6 +137,13 @@ int rt_scene_create(int device, const float* points9, const float* rad3,
 /* The H2D copy at the end of Trixel::create_kd (TD/Trixel.h:380).  Validates
  * the tree (BFS order, 2*ntri-1 nodes, leaves cover every triangle once). */
 int rt_scene_set_kd(rt_scene* s, const rt_kd_node* nodes, uint64_t nnode);
+
+/* Trixel::set_sorted_voxels + create_kd + the H2D copy (TD/Trixel.h:135-473)
+ * in one call, built on the scene's device (rt_kd_build_gpu) and left there:
+ * no node array crosses PCIe.  Equivalent to rt_kd_build + rt_scene_set_kd. */
+int rt_scene_build_kd(rt_scene* s, const rt_leaf_aabb* leafs, uint32_t ntri, void* stream);
+/* Copies the scene's node array (2*ntri-1 rt_kd_node) to the host. */
+int rt_scene_read_kd(rt_scene* s, rt_kd_node* nodes, uint64_t nnode);
 
 /* Layout knobs of a scene (not in the reference; every setting renders the
  * identical frame): RT_SCENE_ORDER = the order of the dense interior records
