@@ -21,7 +21,13 @@ CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "librt_mi355x.so")
 ARCH = os.environ.get("RT_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["rt_kernels.hip", "kd_build_gpu.hip", "rt_api.cpp", "scene_host.cpp", "motion.cpp", "comm.cpp"]
+# (source, object name, extra flags): rt_kd_dispatch.hip is compiled once per
+# (translated, write-hit, count) combination, so the KD kernels' template
+# instances build in parallel
+SOURCES = [("rt_kernels.hip", "rt_kernels", [])] + [
+    ("rt_kd_dispatch.hip", f"rt_kd_{t}{h}{c}", [f"-DRT_KD_T={t}", f"-DRT_KD_H={h}", f"-DRT_KD_C={c}"])
+    for t in (0, 1) for h in (0, 1) for c in (0, 1)] + [
+    (f, os.path.splitext(f)[0], []) for f in ("kd_build_gpu.hip", "rt_api.cpp", "scene_host.cpp", "motion.cpp", "comm.cpp")]
 OBJ = os.path.join(PKG, "_obj")  # per-source objects (git- and gpurun-ignored)
 # -fno-slp-vectorize: hipcc's packed-math (v_pk_*) SLP pairs cost more register
 # moves than they save in the traversal loop (0.0851 vs 0.0871 ms per 1080p
@@ -44,32 +50,45 @@ def _stale(target: str, deps) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_lib(force: bool = False, verbose: bool = False) -> str:
-    """Compile each source to its own object (only the stale ones), then link."""
-    headers = [os.path.join(CSRC, "rt_internal.h"), os.path.join(CSRC, "rt_predicates.h"),
-               os.path.join(ROOT, "include", "rt_mi355x.h")]
-    os.makedirs(OBJ, exist_ok=True)
-    objs, relink = [], force or not os.path.exists(LIB)
-    for src in SOURCES:
+def build_lib(force: bool = False, verbose: bool = False, jobs: int = 0, out: str = LIB, defs=(),
+              objdir: str = OBJ) -> str:
+    """Compile each source to its own object (only the stale ones, in
+    parallel), then link.  out / defs / objdir: an experiment variant (extra
+    -D flags, its own objects), e.g. tools/build_variants.sh."""
+    from concurrent.futures import ThreadPoolExecutor
+    headers = [os.path.join(CSRC, h) for h in ("rt_internal.h", "rt_predicates.h", "rt_kernels_impl.h")] + [
+        os.path.join(ROOT, "include", "rt_mi355x.h")]
+    os.makedirs(objdir, exist_ok=True)
+    objs, todo = [], []
+    relink = force or not os.path.exists(out)
+    for src, name, extra in SOURCES:
         path = os.path.join(CSRC, src)
-        obj = os.path.join(OBJ, os.path.splitext(src)[0] + ".o")
+        obj = os.path.join(objdir, name + ".o")
         objs.append(obj)
         if force or _stale(obj, [path, *headers, __file__]):
-            cmd = [hipcc(), *HIP_FLAGS, "-c", "-o", obj + ".tmp", path]
-            if verbose:
-                print(" ".join(cmd), flush=True)
-            subprocess.run(cmd, check=True)
-            os.replace(obj + ".tmp", obj)
-            relink = True
-    if not relink and not _stale(LIB, objs):
-        return LIB
-    tmp = LIB + ".tmp"
+            todo.append(([hipcc(), *HIP_FLAGS, *defs, *extra, "-c", "-o", obj + ".tmp", path], obj))
+
+    def compile_one(job):
+        cmd, obj = job
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        os.replace(obj + ".tmp", obj)
+
+    if todo:
+        n = jobs or min(len(todo), max(1, len(os.sched_getaffinity(0))), 16)
+        with ThreadPoolExecutor(n) as ex:
+            list(ex.map(compile_one, todo))
+        relink = True
+    if not relink and not _stale(out, objs):
+        return out
+    tmp = out + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-o", tmp, *objs, "-lpthread", "-ldl"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, out)
+    return out
 
 
 def build_driver(verbose: bool = False) -> str:
@@ -91,7 +110,14 @@ def main(argv=None) -> int:
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--driver", action="store_true")
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--variant", default="", help="experiment build: tools/variants/lib_<name>.so")
+    ap.add_argument("--defs", default="", help="extra compile flags of the variant, e.g. '-DRT_POOL_CAP_R16=384'")
     a = ap.parse_args(argv)
+    if a.variant:
+        vdir = os.path.join(ROOT, "tools", "variants")
+        print(build_lib(a.force, a.verbose, out=os.path.join(vdir, f"lib_{a.variant}.so"), defs=a.defs.split(),
+                        objdir=os.path.join(vdir, "_obj_" + a.variant)))
+        return 0
     print(build_lib(a.force, a.verbose))
     if a.driver:
         print(build_driver(a.verbose))

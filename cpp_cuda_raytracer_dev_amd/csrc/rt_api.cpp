@@ -603,6 +603,7 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
     p.root_ref = s->root_ref;
     p.ntri = s->ntri;
     p.max_depth = kMaxDepth;
+    p.tree_height = s->height;
     p.tile_order = c->tile_order;
     p.order = nullptr;
     p.debug = c->debug;

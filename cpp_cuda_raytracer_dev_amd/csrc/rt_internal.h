@@ -128,6 +128,7 @@ struct TraceParams {
     uint32_t root_ref;
     uint32_t ntri;
     int32_t max_depth;
+    int32_t tree_height;           // the scene tree's height (kernel 3's pool slack is height + 1)
     int32_t flat_variant;          // Option kOptFlat: flat-list kernel form (0, 1, 2)
 };
 

@@ -1,0 +1,1773 @@
+// rt_kernels_impl.h -- gfx950 kernels of the per-pixel ray-cast hot path
+// (included by rt_kernels.hip and, once per (translated, write-hit, count)
+// combination, by rt_kd_dispatch.hip, so the KD kernels' many template
+// instances compile in parallel translation units).
+//
+// One fused kernel per frame: primary ray -> object transform -> KD-tree DFS
+// (or the flat triangle list) -> Moller-Trumbore -> Phong -> u32 0x00RRGGBB.
+// One ray per lane; a block is a 32x8 pixel tile (four 8x8 wave64 tiles), so
+// a wave's rays are spatially coherent and walk the same upper tree.  The DFS
+// stack lives in LDS (per-lane columns of a [depth][256] array) with its top
+// entry in a register.  Blocks are remapped so each XCD's L2 serves a
+// contiguous band of screen tiles.
+//
+// Arithmetic follows the reference expression by expression (SURVEY.md §5
+// H1-H16): single precision with contraction off (-ffp-contract=off), the
+// reference's double-promoted epsilons evaluated in double, correctly
+// rounded float division (equal to the reference's (float)(1.0/f)), the
+// 21-step fast inverse square root, and the deterministic pow5 shared with the
+// oracle.  Every kernel cites the reference code it replaces.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+
+#include "rt_internal.h"
+#include "rt_predicates.h"
+
+namespace rt {
+namespace {
+
+constexpr double kEps = 1e-16;                  // TD/vector.cuh:10-11 (double literals)
+// Smallest float >= 1e-16: for a float x, (double)x < 1e-16 <=> x < kEpsF and
+// (double)x > -1e-16 <=> x > -kEpsF (1e-16 is not a float).  Checked in tests.
+constexpr float kEpsF = __builtin_bit_cast(float, 0x24e69595u);
+constexpr float kDrawDistance = 400.0f;         // TD/Trixel.cu:47
+constexpr uint32_t kBackground = 0x00F08200u;   // VEC4<T_uint>(240,130,0,0), TD/Camera.cpp:72
+constexpr uint32_t kMiss = 0xFFFFFFFFu;
+
+// The wave's index in its block, as a scalar (the compiler cannot see that
+// threadIdx.x >> 6 is wave-uniform and would keep it, and everything derived
+// from it, in vector registers).
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6); }
+
+// device_inverse_sqrt, TD/vector.cuh:79-95 (seed from bits(s/2), 21 steps).
+__device__ __forceinline__ float rsqrt21(float x, float y, float z) {
+    float s = (x * x) + (y * y) + (z * z);
+    const float half = 0.5f * s;
+    uint32_t i = 0x5f375a86u - (__float_as_uint(half) >> 1);
+    float r = __uint_as_float(i);
+#pragma unroll
+    for (int k = 0; k < 21; k++) r = r * (1.5f - half * r * r);
+    return r;
+}
+
+// device_cross / device_dot, TD/vector.cuh:72-77,121-124
+__device__ __forceinline__ void cross3(float& cx, float& cy, float& cz, float ax, float ay,
+                                       float az, float bx, float by, float bz) {
+    cx = ay * bz - az * by;
+    cy = az * bx - ax * bz;
+    cz = ax * by - ay * bx;
+}
+__device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, float by, float bz) {
+    return (ax * bx) + (ay * by) + (az * bz);
+}
+
+// powf(|x|, 5) of TD/Camera.cu:45 as one deterministic rounding (H5).
+__device__ __forceinline__ float pow5(float x) {
+    double d = (double)x;
+    double d2 = d * d;
+    double d4 = d2 * d2;
+    return (float)(d4 * d);
+}
+
+// (u8)(float) with NaN -> 0 (H14).
+__device__ __forceinline__ uint32_t to_u8(float t) {
+    if (!(t >= 0.0f)) return 0u;
+    if (t >= 256.0f) return 255u;
+    return (uint32_t)(int)t;
+}
+
+// color_cam_cuda, TD/Camera.cu:27-60 (norm.x used twice in the dot, H1).
+__device__ __forceinline__ uint32_t phong(const float pnt[3], const float nrm[3], const float rmd[3],
+                          const float rad[3]) {
+    float sdx = 2 - pnt[0], sdy = 2 - pnt[1], sdz = 2 - pnt[2];
+    const float r = rsqrt21(sdx, sdy, sdz);
+    sdx *= r; sdy *= r; sdz *= r;
+    const float dot_r_n = dot3(sdx, sdy, sdz, nrm[0], nrm[0], nrm[2]);
+    const float rx = (sdx - (2 * dot_r_n * nrm[0])) * rmd[0];
+    const float ry = (sdy - (2 * dot_r_n * nrm[1])) * rmd[1];
+    const float rz = (sdz - (2 * dot_r_n * nrm[2])) * rmd[2];
+    const float diff = (float)(.6 * (double)fabsf(dot_r_n));
+    const float spec = (float)((double)pow5(fabsf((rx + ry + rz))) * .3);
+    float pr = 0.0f, pg = 0.0f, pb = 0.0f;
+    pr += (rad[0] * diff) + (1 * spec);
+    pg += (rad[1] * diff) + (1 * spec);
+    pb += (rad[2] * diff) + (1 * spec);
+    const float mx = fmaxf(fmaxf(pr, pg), pb);
+    return (to_u8((pr / mx) * 255) << 16) | (to_u8((pg / mx) * 255) << 8) | to_u8((pb / mx) * 255);
+}
+
+// Block -> (tile_x, slot).  Order 0: blocks b and b+8 share an XCD, so give
+// each XCD a contiguous run of tiles (bijective for any grid size); order 1:
+// natural (neighbouring tiles on different XCDs); order 2: the host's
+// centre-out permutation, so the heavy centre tiles are dispatched first;
+// order 3: the host's permutation by the tiles' measured cost in an earlier
+// frame, heaviest first (centre-out until costs arrive); order 4: the same
+// per XCD over 8 screen regions of equal cost.
+__device__ __forceinline__ int32_t tile_index(const TraceParams& P, int32_t b) {
+    const int32_t nblocks = P.tiles_x * P.block_rows;
+    if (P.tile_order == 0) {
+        const int32_t q = nblocks >> 3, rem = nblocks & 7;
+        const int32_t xcd = b & 7, k = b >> 3;
+        return (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + k;
+    }
+    if (P.tile_order >= 2 && P.order) return P.order[b];  // orders 2-4: host permutation
+    return b;
+}
+
+__device__ __forceinline__ void tile_of(const TraceParams& P, int32_t b, int32_t& tx, int32_t& slot) {
+    const int32_t t = tile_index(P, b);
+    slot = t / P.tiles_x;
+    tx = t - slot * P.tiles_x;
+    tx += P.fine_tx0;
+    slot += P.fine_s0 * (kTileH / P.tile_h);
+}
+
+struct Pixel {
+    int32_t x, y;      // frame coordinates (row 0 = bottom, TD/WinMain.cpp:32)
+    int64_t out;       // index into the (packed) output buffer
+};
+
+// Tile b covers tile_w x tile_h pixels of one 8-row band; wave `wave` of it
+// owns an 8 x (rays/8) sub-tile (side by side when tile_w > 8, stacked
+// otherwise).  Lanes >= rays own no pixel (the wave-cooperative kernel's
+// helper lanes).
+// A wave's unit of pixels: 8 columns from x0, rows yin.. of band slot `slot`.
+struct Unit {
+    int32_t x0, slot, yin;
+};
+
+// Lane `lane`'s pixel of a unit (8 pixels per row, row-major); lanes >= rows*8
+// own no pixel.
+__device__ __forceinline__ bool unit_pixel(const TraceParams& P, const Unit& u, int32_t rows, int32_t lane,
+                                           Pixel& px) {
+    const int32_t band = P.rank + u.slot * P.nranks;
+    const int32_t ly = u.yin + (lane >> 3);
+    px.x = u.x0 + (lane & 7);
+    px.y = band * kTileH + ly;
+    px.out = (int64_t)(u.slot * kTileH + ly) * P.w + px.x;
+    return lane < rows * 8 && px.x < P.w && px.y < P.h;
+}
+
+// Sub-tile `wave` of fine tile b.
+__device__ __forceinline__ Unit unit_of(const TraceParams& P, int32_t b, int32_t wave) {
+    int32_t tx, row;
+    tile_of(P, b, tx, row);
+    const int32_t per_band = kTileH / P.tile_h;
+    const int32_t slot = row / per_band, yin = (row - slot * per_band) * P.tile_h;
+    const int32_t wrows = P.rays >> 3;
+    const int32_t wx = P.tile_w > 8 ? wave * 8 : 0, wy = P.tile_w > 8 ? 0 : wave * wrows;
+    return Unit{tx * P.tile_w + wx, slot, yin + wy};
+}
+
+__device__ __forceinline__ bool pixel_of(const TraceParams& P, int32_t b, int32_t wave, Pixel& px) {
+    return unit_pixel(P, unit_of(P, b, wave), P.rays >> 3, (int32_t)threadIdx.x & 63, px);
+}
+
+// Coarse group j (row-major over this rank's slots and 8-px columns, skipping
+// the fine region) -> its 8x8 unit.  32-bit arithmetic: the host keeps
+// coarse_groups below 2^31 (64-bit division is a long software sequence).
+__device__ __forceinline__ Unit coarse_unit(const TraceParams& P, int32_t j) {
+    const int32_t gx = P.groups_x;
+    const int32_t before = P.cs0 * gx;
+    int32_t slot, col;
+    if (j < before) {
+        slot = j / gx;
+        col = j - slot * gx;
+    } else {
+        j -= before;
+        const int32_t m = gx - (P.cg_x1 - P.cg_x0);
+        const int32_t mid = (P.cs1 - P.cs0) * m;
+        if (j < mid) {
+            const int32_t r = j / m;
+            slot = P.cs0 + r;
+            col = j - r * m;
+            if (col >= P.cg_x0) col += P.cg_x1 - P.cg_x0;
+        } else {
+            j -= mid;
+            const int32_t r = j / gx;
+            slot = P.cs1 + r;
+            col = j - r * gx;
+        }
+    }
+    return Unit{col * 8, slot, 0};
+}
+
+// One tile per block (blockIdx), one sub-tile per wave.
+__device__ __forceinline__ bool pixel_of_thread(const TraceParams& P, Pixel& px) {
+    return pixel_of(P, (int32_t)blockIdx.x, wave_id(), px);
+}
+
+// init_cam_mem_cuda, TD/Camera.cu:103-104: rmd = n + u*ix + v*iy, normalised.
+__device__ __forceinline__ void primary_ray(const TraceParams& P, int32_t ix, int32_t iy,
+                                            float rmd[3]) {
+    // (float)ix of the reference's unsigned pixel index: exact and equal for any ix < 2^32
+    const float fx = (float)(uint32_t)ix, fy = (float)(uint32_t)iy;
+    float x = P.n_mod[0] + P.u_mod[0] * fx + P.v_mod[0] * fy;
+    float y = P.n_mod[1] + P.u_mod[1] * fx + P.v_mod[1] * fy;
+    float z = P.n_mod[2] + P.u_mod[2] * fx + P.v_mod[2] * fy;
+    const float r = rsqrt21(x, y, z);
+    rmd[0] = x * r; rmd[1] = y * r; rmd[2] = z * r;
+}
+
+__device__ __forceinline__ void wave_count_add(unsigned long long* dst, uint32_t v) {
+    // counting builds only; the compiler's atomic optimizer folds the active
+    // lanes of a wave into one atomic (lanes of edge tiles may have exited)
+    if (v) atomicAdd(dst, (unsigned long long)v);
+}
+
+// ---------------------------------------------------------------- KD trace
+
+// intersect_voxel_cuda (TD/Trixel.cu:41-172) fused with set_cam_cuda +
+// color_cam_cuda (TD/Camera.cu:12-69).
+template <bool kTranslated, bool kWriteHit, bool kCount>
+__global__ __launch_bounds__(kTileWFlat * kTileH) void k_trace_kd(TraceParams P) {
+    constexpr int kBlock = kTileWFlat * kTileH;
+    __shared__ uint32_t stack[kMaxDepth * kBlock];
+    Pixel px;
+    const bool live = pixel_of_thread(P, px);
+    if (!live) return;  // no barriers in this kernel
+
+    float cam[3];
+    primary_ray(P, px.x, px.y, cam);
+    const float* X = P.xf;
+    // object transform of the ray, TD/Trixel.cu:60-66 (identity in every config)
+    const float odx = X[3], ody = X[7], odz = X[11];
+    const float rx = -1 * (X[0] * -cam[0] + X[1] * -cam[1] + X[2] * -cam[2]);
+    const float ry = -1 * (X[4] * -cam[0] + X[5] * -cam[1] + X[6] * -cam[2]);
+    const float rz = -1 * (X[8] * -cam[0] + X[9] * -cam[1] + X[10] * -cam[2]);
+    // per-ray invariants of the slab test (TD/Trixel.cu:76-95)
+    const float ix = 1 / rx, iy = 1 / ry, iz = 1 / rz;
+    const float ox = odx / rx, oy = ody / ry, oz = odz / rz;
+    const bool sx = rx > 0, sy = ry > 0, sz = rz > 0;
+    // dir and ds for each one-hot cut axis (TD/Trixel.cu:88-90)
+    const float dir_a[3] = {(rx * 1.0f) + (ry * 0.0f) + (rz * 0.0f),
+                            (rx * 0.0f) + (ry * 1.0f) + (rz * 0.0f),
+                            (rx * 0.0f) + (ry * 0.0f) + (rz * 1.0f)};
+    const float ds_a[3] = {(odx * 1.0f) + (ody * 0.0f) + (odz * 0.0f),
+                           (odx * 0.0f) + (ody * 1.0f) + (odz * 0.0f),
+                           (odx * 0.0f) + (ody * 0.0f) + (odz * 1.0f)};
+
+    float d = kDrawDistance;
+    uint32_t best = kMiss;
+    uint32_t n_int = 0, n_leaf = 0, n_acc = 0, n_desc = 0;
+    uint32_t* stk = stack + threadIdx.x;   // column of this lane: stk[k * kBlock]
+    int sp = 0;
+    uint32_t ref = P.root_ref;
+    for (;;) {
+        if (ref & kLeafBit) {
+            // Moller-Trumbore at a leaf, TD/Trixel.cu:98-145
+            const uint32_t t = ref & ~kLeafBit;
+            if (kCount) n_leaf++;
+            const float4 A = P.trec[4 * (size_t)t];
+            const float4 B = P.trec[4 * (size_t)t + 1];
+            const float4 Cq = P.trec[4 * (size_t)t + 2];
+            const float e1x = A.x, e1y = A.y, e1z = A.z;
+            const float e2x = A.w, e2y = B.x, e2z = B.y;
+            const float dtx = B.z, dty = B.w, dtz = Cq.x;
+            float qpx, qpy, qpz;
+            cross3(qpx, qpy, qpz, rx, ry, rz, e2x, e2y, e2z);
+            const float f = dot3(qpx, qpy, qpz, e1x, e1y, e1z);
+            if (!(f < kEpsF && f > -kEpsF)) {
+                const float pe1 = 1.0f / f;   // == (float)(1.0 / (double)f)
+                const float tx = dtx - odx, ty = dty - ody, tz = dtz - odz;
+                const float u = pe1 * dot3(qpx, qpy, qpz, tx, ty, tz);
+                float qx, qy, qz;
+                cross3(qx, qy, qz, tx, ty, tz, e1x, e1y, e1z);
+                const float v = pe1 * dot3(rx, ry, rz, qx, qy, qz);
+                const float w = pe1 * dot3(e2x, e2y, e2z, qx, qy, qz);
+                // (u+v) > 1 + 1e-16 is (u+v) > 1.0 in double
+                if ((w < d) && !((u < kEpsF) || (v < kEpsF) || ((u + v) > 1.0f) || (w < kEpsF))) {
+                    d = w;
+                    best = t;
+                    if (kCount) n_acc++;
+                }
+            }
+            if (sp == 0) break;
+            ref = stk[(--sp) * kBlock];
+            continue;
+        }
+        // interior node: slab test and split-plane child order, TD/Trixel.cu:76-95,146-168
+        if (kCount) n_int++;
+        const float4 a = P.inode[3 * (size_t)ref];
+        const float4 b = P.inode[3 * (size_t)ref + 1];
+        const uint4 c = reinterpret_cast<const uint4*>(P.inode)[3 * (size_t)ref + 2];
+        const float t0x = sx ? a.x * ix : a.y * ix;
+        const float t1x = sx ? a.y * ix : a.x * ix;
+        const float t0y = sy ? a.z * iy : a.w * iy;
+        const float t1y = sy ? a.w * iy : a.z * iy;
+        const float t0z = sz ? b.x * iz : b.y * iz;
+        const float t1z = sz ? b.y * iz : b.x * iz;
+        float maxt0 = fmaxf(t0z + oz, fmaxf(t0x + ox, t0y + oy));
+        float mint1 = fminf(t1z + oz, fminf(t1x + ox, t1y + oy));
+        if (pred::enter(maxt0, mint1)) {
+            if (kCount) n_desc++;
+            const uint32_t axis = c.z;
+            const float dir = axis == 0 ? dir_a[0] : axis == 1 ? dir_a[1] : dir_a[2];
+            maxt0 *= dir;
+            mint1 *= dir;
+            float s1, s2;
+            if (kTranslated) {
+                const float ds = axis == 0 ? ds_a[0] : axis == 1 ? ds_a[1] : ds_a[2];
+                s1 = (float)((double)b.z + kEps + (double)ds);
+                s2 = b.w + ds;
+            } else {
+                s1 = __uint_as_float(c.w);   // (float)((double)s1 + 1e-16), ds == 0
+                s2 = b.w;
+            }
+            const uint32_t L = c.x, R = c.y;
+            if (pred::lt_eps(maxt0, s2)) {
+                // pushes right (if) then left: left is popped first
+                if (pred::gt_eps(mint1, s2)) {
+                    if (sp >= P.max_depth) { atomicOr(P.err, 1); break; }
+                    stk[(sp++) * kBlock] = R;
+                }
+                ref = L;
+            } else {
+                // pushes left (if) then right: right is popped first
+                if (mint1 < s1 || maxt0 < s1) {
+                    if (sp >= P.max_depth) { atomicOr(P.err, 1); break; }
+                    stk[(sp++) * kBlock] = L;
+                }
+                ref = R;
+            }
+            continue;
+        }
+        if (sp == 0) break;
+        ref = stk[(--sp) * kBlock];
+    }
+
+    uint32_t argb = kBackground;
+    if (best != kMiss) {
+        // nearest-hit writes of TD/Trixel.cu:128-140, done once for the final hit
+        const float4 N = P.shade[2 * (size_t)best];
+        const float4 M = P.shade[2 * (size_t)best + 1];
+        const float pnt[3] = {d * rx + odx, d * ry + ody, d * rz + odz};
+        // norm.device_rotate(rot_m, i, -1), TD/vector.cuh:23-33
+        const float ax = -1 * N.x, ay = -1 * N.y, az = -1 * N.z;
+        const float nrm[3] = {(ax * X[0] + ay * X[1] + az * X[2]) * -1,
+                              (ax * X[4] + ay * X[5] + az * X[6]) * -1,
+                              (ax * X[8] + ay * X[9] + az * X[10]) * -1};
+        const float rad[3] = {M.x, M.y, M.z};
+        argb = phong(pnt, nrm, cam, rad);
+    }
+    P.argb[px.out] = argb;
+    if (kWriteHit) P.hit[px.out] = best == kMiss ? (int64_t)-1 : (int64_t)best;
+    if (kCount) {
+        wave_count_add(&P.counters[0], n_int);
+        wave_count_add(&P.counters[1], n_leaf);
+        wave_count_add(&P.counters[2], n_acc);
+        wave_count_add(&P.counters[3], best != kMiss ? 1u : 0u);
+        wave_count_add(&P.counters[4], n_desc);
+    }
+}
+
+// ------------------------------------------------------------- KD trace v2
+
+// Issues the four dwordx4 loads of a 64-B record together and consumes them
+// before any branch, so a visit costs one memory round trip (left to itself
+// hipcc sinks the conditionally used loads into the branches: three
+// dependent round trips per visit).
+__device__ __forceinline__ void load_record(const float4* __restrict__ p, float4& r0, float4& r1,
+                                            float4& r2, float4& r3) {
+    r0 = p[0]; r1 = p[1]; r2 = p[2]; r3 = p[3];
+    asm volatile("" ::"v"(r0.x), "v"(r0.y), "v"(r0.z), "v"(r0.w), "v"(r1.x), "v"(r1.y), "v"(r1.z),
+                 "v"(r1.w), "v"(r2.x), "v"(r2.y), "v"(r2.z), "v"(r2.w), "v"(r3.x), "v"(r3.y), "v"(r3.z),
+                 "v"(r3.w));
+}
+
+struct Ray {
+    float rx, ry, rz;          // object-space direction, TD/Trixel.cu:64-66
+    float odx, ody, odz;       // object translation, TD/Trixel.cu:60-62
+    float ix, iy, iz;          // 1 / r
+    float ox, oy, oz;          // od / r
+    bool sx, sy, sz;           // r > 0
+};
+
+// Slab test of one node, TD/Trixel.cu:76-95,146: entry/exit parameters and
+// whether the reference descends into the node.
+__device__ __forceinline__ bool slab(const Ray& R, float lx, float hx, float ly, float hy, float lz,
+                                     float hz, float& maxt0, float& mint1) {
+    const float t0x = R.sx ? lx * R.ix : hx * R.ix;
+    const float t1x = R.sx ? hx * R.ix : lx * R.ix;
+    const float t0y = R.sy ? ly * R.iy : hy * R.iy;
+    const float t1y = R.sy ? hy * R.iy : ly * R.iy;
+    const float t0z = R.sz ? lz * R.iz : hz * R.iz;
+    const float t1z = R.sz ? hz * R.iz : lz * R.iz;
+    maxt0 = fmaxf(t0z + R.oz, fmaxf(t0x + R.ox, t0y + R.oy));
+    mint1 = fminf(t1z + R.oz, fminf(t1x + R.ox, t1y + R.oy));
+    return pred::enter(maxt0, mint1);
+}
+
+// Moller-Trumbore at a leaf, TD/Trixel.cu:98-145; updates (d, best) on a
+// strictly nearer accepted hit.
+__device__ __forceinline__ bool leaf_test_rec(const Ray& R, const float4 A, const float4 B, const float4 Cq,
+                                              uint32_t t, float& d, uint32_t& best) {
+    const float e1x = A.x, e1y = A.y, e1z = A.z;
+    const float e2x = A.w, e2y = B.x, e2z = B.y;
+    const float dtx = B.z, dty = B.w, dtz = Cq.x;
+    float qpx, qpy, qpz;
+    cross3(qpx, qpy, qpz, R.rx, R.ry, R.rz, e2x, e2y, e2z);
+    const float f = dot3(qpx, qpy, qpz, e1x, e1y, e1z);
+    if (!(f < kEpsF && f > -kEpsF)) {
+        const float pe1 = 1.0f / f;   // == (float)(1.0 / (double)f)
+        const float tx = dtx - R.odx, ty = dty - R.ody, tz = dtz - R.odz;
+        const float u = pe1 * dot3(qpx, qpy, qpz, tx, ty, tz);
+        float qx, qy, qz;
+        cross3(qx, qy, qz, tx, ty, tz, e1x, e1y, e1z);
+        const float v = pe1 * dot3(R.rx, R.ry, R.rz, qx, qy, qz);
+        const float w = pe1 * dot3(e2x, e2y, e2z, qx, qy, qz);
+        // (u+v) > 1 + 1e-16 is (u+v) > 1.0 in double
+        if ((w < d) && !((u < kEpsF) || (v < kEpsF) || ((u + v) > 1.0f) || (w < kEpsF))) {
+            d = w;
+            best = t;
+            return true;
+        }
+    }
+    return false;
+}
+
+__device__ __forceinline__ bool leaf_test(const Ray& R, const float4* __restrict__ trec, uint32_t t,
+                                          float& d, uint32_t& best) {
+    return leaf_test_rec(R, trec[4 * (size_t)t], trec[4 * (size_t)t + 1], trec[4 * (size_t)t + 2], t, d, best);
+}
+
+// intersect_voxel_cuda (TD/Trixel.cu:41-172) fused with set_cam_cuda +
+// color_cam_cuda (TD/Camera.cu:12-69), v2 layout.  A node's record carries its
+// children's boxes, so a child's slab test runs when the parent decides to
+// push it: children that the reference would pop and reject are never
+// fetched, the deferred sibling keeps its (maxt0, mint1) in LDS, and every
+// effectful visit happens in the reference's DFS order.
+template <bool kTranslated, bool kWriteHit, bool kCount>
+__global__ __launch_bounds__(kTileWKd * kTileH) void k_trace_kd2(TraceParams P) {
+    constexpr int kB = kTileWKd * kTileH;
+    __shared__ uint32_t s_ref[kMaxDepth * kB];
+    __shared__ float s_t0[kMaxDepth * kB];
+    __shared__ float s_t1[kMaxDepth * kB];
+    Pixel px;
+    if (!pixel_of_thread(P, px)) return;  // no barriers in this kernel
+    const unsigned long long t_start = P.dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
+
+    float cam[3];
+    primary_ray(P, px.x, px.y, cam);
+    const float* X = P.xf;
+    Ray R;
+    R.odx = X[3]; R.ody = X[7]; R.odz = X[11];
+    R.rx = -1 * (X[0] * -cam[0] + X[1] * -cam[1] + X[2] * -cam[2]);
+    R.ry = -1 * (X[4] * -cam[0] + X[5] * -cam[1] + X[6] * -cam[2]);
+    R.rz = -1 * (X[8] * -cam[0] + X[9] * -cam[1] + X[10] * -cam[2]);
+    R.ix = 1 / R.rx; R.iy = 1 / R.ry; R.iz = 1 / R.rz;
+    R.ox = R.odx / R.rx; R.oy = R.ody / R.ry; R.oz = R.odz / R.rz;
+    R.sx = R.rx > 0; R.sy = R.ry > 0; R.sz = R.rz > 0;
+    // dir and ds for each one-hot cut axis (TD/Trixel.cu:88-90)
+    const float dir_a[3] = {(R.rx * 1.0f) + (R.ry * 0.0f) + (R.rz * 0.0f),
+                            (R.rx * 0.0f) + (R.ry * 1.0f) + (R.rz * 0.0f),
+                            (R.rx * 0.0f) + (R.ry * 0.0f) + (R.rz * 1.0f)};
+    const float ds_a[3] = {(R.odx * 1.0f) + (R.ody * 0.0f) + (R.odz * 0.0f),
+                           (R.odx * 0.0f) + (R.ody * 1.0f) + (R.odz * 0.0f),
+                           (R.odx * 0.0f) + (R.ody * 0.0f) + (R.odz * 1.0f)};
+
+    float d = kDrawDistance;
+    uint32_t best = kMiss;
+    uint32_t n_int = 0, n_leaf = 0, n_acc = 0, n_desc = 0;
+    const int lane_col = (int)threadIdx.x;
+    int sp = 0;
+    uint32_t ref = P.root_ref;
+    float cmax = 0.0f, cmin = 0.0f;
+    bool have = true;
+    if (!(ref & kLeafBit)) {
+        if (kCount) n_int++;
+        have = slab(R, P.root_box[0], P.root_box[1], P.root_box[2], P.root_box[3], P.root_box[4],
+                    P.root_box[5], cmax, cmin);
+        if (kCount && have) n_desc++;
+    }
+    if (P.debug & 1) have = false;
+    uint32_t n_visit = 0;
+    while (have) {
+        if (P.dbg) n_visit++;
+        if (ref & kLeafBit) {
+            if (kCount) n_leaf++;
+            const bool acc = leaf_test(R, P.trec, ref & ~kLeafBit, d, best);
+            if (kCount && acc) n_acc++;
+        } else {
+            float4 r0, r1, r2, r3;
+            load_record(P.inode + 4 * (size_t)ref, r0, r1, r2, r3);
+            const uint32_t lw = __float_as_uint(r3.z);
+            const uint32_t axis = (lw >> kAxisShift) & 3u;
+            const uint32_t L = lw & ~(3u << kAxisShift), Rr = __float_as_uint(r3.w);
+            const float dir = axis == 0 ? dir_a[0] : axis == 1 ? dir_a[1] : dir_a[2];
+            const float mx = cmax * dir, mn = cmin * dir;
+            float s1, s2;
+            if (kTranslated) {
+                const float ds = axis == 0 ? ds_a[0] : axis == 1 ? ds_a[1] : ds_a[2];
+                s1 = (float)((double)r3.x + kEps + (double)ds);
+                s2 = r3.y + ds;
+            } else {  // ds == 0: the same values without the +0
+                s1 = pred::add_eps(r3.x);
+                s2 = r3.y;
+            }
+            // Push order of TD/Trixel.cu:155-168.  `first` is popped next,
+            // `second` (if pushed) after first's subtree.
+            bool left_first, push_second;
+            if (pred::lt_eps(mx, s2)) {
+                left_first = true;
+                push_second = pred::gt_eps(mn, s2);
+            } else {
+                left_first = false;
+                push_second = (mn < s1 || mx < s1);
+            }
+            const uint32_t first = left_first ? L : Rr;
+            const uint32_t second = left_first ? Rr : L;
+            // slab tests of the children that would be popped (boxes in r0..r2)
+            float f0 = 0.0f, f1 = 0.0f, g0 = 0.0f, g1 = 0.0f;
+            bool keep_first = true, keep_second = push_second;
+            if (!(first & kLeafBit)) {
+                if (kCount) n_int++;
+                keep_first = left_first ? slab(R, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, f0, f1)
+                                        : slab(R, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w, f0, f1);
+                if (kCount && keep_first) n_desc++;
+            }
+            if (push_second && !(second & kLeafBit)) {
+                if (kCount) n_int++;
+                keep_second = left_first ? slab(R, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w, g0, g1)
+                                         : slab(R, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, g0, g1);
+                if (kCount && keep_second) n_desc++;
+            }
+            if (keep_first) {
+                if (keep_second) {
+                    if (sp >= P.max_depth) { atomicOr(P.err, 1); break; }
+                    const int k = sp * kB + lane_col;
+                    s_ref[k] = second; s_t0[k] = g0; s_t1[k] = g1;
+                    sp++;
+                }
+                ref = first; cmax = f0; cmin = f1;
+                continue;
+            }
+            if (keep_second) {
+                ref = second; cmax = g0; cmin = g1;
+                continue;
+            }
+        }
+        if (sp == 0) break;
+        sp--;
+        const int k = sp * kB + lane_col;
+        ref = s_ref[k]; cmax = s_t0[k]; cmin = s_t1[k];
+    }
+
+    uint32_t argb = kBackground;
+    if (best != kMiss) {
+        // nearest-hit writes of TD/Trixel.cu:128-140, done once for the final hit
+        const float4 N = P.shade[2 * (size_t)best];
+        const float4 M = P.shade[2 * (size_t)best + 1];
+        const float pnt[3] = {d * R.rx + R.odx, d * R.ry + R.ody, d * R.rz + R.odz};
+        // norm.device_rotate(rot_m, i, -1), TD/vector.cuh:23-33
+        const float ax = -1 * N.x, ay = -1 * N.y, az = -1 * N.z;
+        const float nrm[3] = {(ax * X[0] + ay * X[1] + az * X[2]) * -1,
+                              (ax * X[4] + ay * X[5] + az * X[6]) * -1,
+                              (ax * X[8] + ay * X[9] + az * X[10]) * -1};
+        const float rad[3] = {M.x, M.y, M.z};
+        argb = phong(pnt, nrm, cam, rad);
+    }
+    P.argb[px.out] = argb;
+    if (kWriteHit) P.hit[px.out] = best == kMiss ? (int64_t)-1 : (int64_t)best;
+    if (kCount) {
+        wave_count_add(&P.counters[0], n_int);
+        wave_count_add(&P.counters[1], n_leaf);
+        wave_count_add(&P.counters[2], n_acc);
+        wave_count_add(&P.counters[3], best != kMiss ? 1u : 0u);
+        wave_count_add(&P.counters[4], n_desc);
+    }
+    if (P.dbg) {  // diagnostic build: wave start/end clock and its max visits
+        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+        const size_t wv = (size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+        atomicMax(&P.dbg[3 * wv + 2], (unsigned long long)n_visit);
+        if (((int)threadIdx.x & 63) == __builtin_amdgcn_readfirstlane((int)threadIdx.x & 63)) {
+            P.dbg[3 * wv] = t_start;
+            P.dbg[3 * wv + 1] = t_end;
+        }
+    }
+}
+
+// ------------------------------------------------------------- KD trace v3
+
+// Wave-cooperative traversal.  With no early termination the SET of nodes a
+// ray visits does not depend on the order of the visits, and the reference's
+// result is the accepted candidate with the smallest w, ties going to the one
+// its DFS visits first (strict `w < d`, TD/Trixel.cu:127).  So a wave pools
+// the (ray, node) work items of its 64 rays in one LDS stack and every lane
+// takes an item per iteration, whatever ray it belongs to: the wave runs
+// ~sum(visits)/64 iterations instead of max(visits).  Each item carries its
+// DFS path code (bit = "second child popped" at each level), so the
+// lexicographic minimum of (w, code left-aligned) -- one 64-bit LDS atomic
+// min per candidate -- is exactly the reference's winner.
+//
+// The path code is stored with a leading marker bit: the root is 1, a node
+// with code m has children 2m (popped first) and 2m + 1, so its depth is the
+// position of the marker and any tree the LDS stack admits (height <=
+// kMaxDepth = 24: 25 bits) fits beside the 6-bit ray index.
+constexpr int kPoolCap = kPoolCapMax;
+constexpr int kCodeBits = kMaxDepth;       // left-aligned code width in the key
+constexpr uint32_t kCodeMarkMask = (1u << 26) - 1;
+
+struct Item {
+    uint32_t ref;      // node ref (kLeafBit | tri, or interior index)
+    float t0, t1;      // the node's (maxt0, mint1) for interior refs
+    uint32_t meta;     // ray << 26 | marked path code
+};
+
+// The key bits of a marked path code: the code left-aligned in kCodeBits.
+__device__ __forceinline__ uint32_t code_key(uint32_t marked) {
+    const uint32_t depth = 31u - (uint32_t)__builtin_clz(marked);
+    return (marked ^ (1u << depth)) << (kCodeBits - depth);
+}
+
+// Pool capacity per wave for kRays rays (the DFS fallback keeps any
+// capacity >= 89 correct; these cover the measured peaks with margin).
+#ifndef RT_POOL_CAP_R32
+#define RT_POOL_CAP_R32 448
+#endif
+#ifndef RT_POOL_CAP_R16
+#define RT_POOL_CAP_R16 352
+#endif
+#ifndef RT_POOL_CAP_R8
+#define RT_POOL_CAP_R8 256
+#endif
+template <int kRays>
+constexpr int pool_cap_for() {
+    return kRays == 64 ? kPoolCap : kRays == 32 ? RT_POOL_CAP_R32 : kRays == 16 ? RT_POOL_CAP_R16 : RT_POOL_CAP_R8;
+}
+
+// Per-ray data of the pool walk in LDS: rd[0] = (rx, ry, rz, 1/rx),
+// rd[1] = (1/ry, 1/rz, odx/rx, ody/ry), rd[2] = (odz/rz, dir per cut axis),
+// translated walks add rd[3] = (od, ds of axis 0), rd[4] = (ds of axes 1-2,
+// shadow walks: Lmax, hit triangle).
+__device__ __forceinline__ void store_ray(float4* rd, const Ray& R, bool translated, float lmax, uint32_t self) {
+    // dir and ds for each one-hot cut axis (TD/Trixel.cu:88-90)
+    const float d0 = (R.rx * 1.0f) + (R.ry * 0.0f) + (R.rz * 0.0f);
+    const float d1 = (R.rx * 0.0f) + (R.ry * 1.0f) + (R.rz * 0.0f);
+    const float d2 = (R.rx * 0.0f) + (R.ry * 0.0f) + (R.rz * 1.0f);
+    rd[0] = make_float4(R.rx, R.ry, R.rz, R.ix);
+    rd[1] = make_float4(R.iy, R.iz, R.ox, R.oy);
+    rd[2] = make_float4(R.oz, d0, d1, d2);
+    if (translated) {
+        const float e0 = (R.odx * 1.0f) + (R.ody * 0.0f) + (R.odz * 0.0f);
+        const float e1 = (R.odx * 0.0f) + (R.ody * 1.0f) + (R.odz * 0.0f);
+        const float e2 = (R.odx * 0.0f) + (R.ody * 0.0f) + (R.odz * 1.0f);
+        rd[3] = make_float4(R.odx, R.ody, R.odz, e0);
+        rd[4] = make_float4(e1, e2, lmax, __uint_as_float(self));
+    }
+}
+
+// Derived fields of a ray whose direction and translation are set.
+__device__ __forceinline__ void finish_ray(Ray& R) {
+    R.ix = 1 / R.rx; R.iy = 1 / R.ry; R.iz = 1 / R.rz;
+    R.ox = R.odx / R.rx; R.oy = R.ody / R.ry; R.oz = R.odz / R.rz;
+    R.sx = R.rx > 0; R.sy = R.ry > 0; R.sz = R.rz > 0;
+}
+
+// The primary ray of a pixel (TD/Camera.cu:103-104) and its object-space form
+// (TD/Trixel.cu:60-66); dead lanes get a harmless +z ray.
+__device__ __forceinline__ void camera_ray(const TraceParams& P, const Pixel& px, bool live, float cam[3], Ray& R) {
+    cam[0] = 0.0f; cam[1] = 0.0f; cam[2] = 1.0f;
+    if (live) primary_ray(P, px.x, px.y, cam);
+    const float* X = P.xf;
+    R.odx = X[3]; R.ody = X[7]; R.odz = X[11];
+    R.rx = -1 * (X[0] * -cam[0] + X[1] * -cam[1] + X[2] * -cam[2]);
+    R.ry = -1 * (X[4] * -cam[0] + X[5] * -cam[1] + X[6] * -cam[2]);
+    R.rz = -1 * (X[8] * -cam[0] + X[9] * -cam[1] + X[10] * -cam[2]);
+    finish_ray(R);
+}
+
+// The reference's root visit (TD/Trixel.cu:53,71-95): a leaf root is always
+// visited, an interior root when its slab test passes.
+template <bool kCount>
+__device__ __forceinline__ bool root_pass(const TraceParams& P, const Ray& R, bool live, float& t0, float& t1,
+                                          uint32_t& n_int, uint32_t& n_desc) {
+    bool has = false;
+    t0 = 0.0f; t1 = 0.0f;
+    if (live) {
+        if (P.root_ref & kLeafBit) {
+            has = true;
+        } else {
+            if (kCount) n_int++;
+            has = slab(R, P.root_box[0], P.root_box[1], P.root_box[2], P.root_box[3], P.root_box[4],
+                       P.root_box[5], t0, t1);
+            if (kCount && has) n_desc++;
+        }
+    }
+    if (P.debug & 1) has = false;
+    return has;
+}
+
+// Seeds the pool with the root item of every lane whose root test passes (or
+// a leaf root); returns the item count.
+template <bool kCount>
+__device__ __forceinline__ int seed_root(const TraceParams& P, uint4* items, const Ray& R, bool live, int lane,
+                                         uint32_t& n_int, uint32_t& n_desc) {
+    float r0t0, r0t1;
+    const bool has = root_pass<kCount>(P, R, live, r0t0, r0t1, n_int, n_desc);
+    const unsigned long long b = __ballot(has);
+    const uint32_t off = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+    if (has) items[off] = make_uint4(P.root_ref, __float_as_uint(r0t0), __float_as_uint(r0t1), ((uint32_t)lane << 26) | 1u);
+    __builtin_amdgcn_wave_barrier();
+    return __builtin_popcountll(b);
+}
+
+// One popped item's outcome: up to two children and a candidate hit.
+struct Visit {
+    uint4 ca, cb;      // the first and second child items (TD/Trixel.cu:155-168 order)
+    bool ka, kb;       // whether each is pushed
+    bool cand;
+    unsigned long long key;
+    uint32_t ctri;
+};
+
+// The 64-B record of an item: a node's child-box record, or a leaf's
+// triangle record (tri_world relative to the camera).
+__device__ __forceinline__ const float4* record_of(const TraceParams& P, uint32_t ref) {
+    return (ref & kLeafBit) ? P.trec + 4 * (size_t)(ref & ~kLeafBit) : P.inode + 4 * (size_t)ref;
+}
+
+// The per-ray data of an item's ray from LDS (see store_ray).
+template <bool kTranslated>
+__device__ __forceinline__ void ray_of(const float4* rd, Ray& Q, float4& q2, float4& q3, float4& q4) {
+    const float4 q0 = rd[0], q1 = rd[1];
+    q2 = rd[2];
+    q3 = kTranslated ? rd[3] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    q4 = kTranslated ? rd[4] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    Q.rx = q0.x; Q.ry = q0.y; Q.rz = q0.z; Q.ix = q0.w;
+    Q.iy = q1.x; Q.iz = q1.y; Q.ox = q1.z; Q.oy = q1.w;
+    Q.oz = q2.x;
+    // object translation (exact zeros when untranslated, as X[3], X[7], X[11] are)
+    Q.odx = kTranslated ? q3.x : 0.0f; Q.ody = kTranslated ? q3.y : 0.0f; Q.odz = kTranslated ? q3.z : 0.0f;
+    Q.sx = Q.rx > 0; Q.sy = Q.ry > 0; Q.sz = Q.rz > 0;
+}
+
+// A leaf item whose triangle record (r0..r2) has arrived: the MT test of
+// TD/Trixel.cu:98-145.  kAny: shadow walk (Lmax and the hit triangle come
+// from rd[4]).
+template <bool kTranslated, bool kCount, bool kAny>
+__device__ __forceinline__ void visit_leaf(const float4* rd, uint4 it, float4 r0, float4 r1, float4 r2, Visit& o,
+                                           uint32_t& n_leaf, uint32_t& n_acc) {
+    Ray Q;
+    float4 q2, q3, q4;
+    ray_of<kTranslated>(rd, Q, q2, q3, q4);
+    if (kCount) n_leaf++;
+    float d = kAny ? q4.z : kDrawDistance;
+    uint32_t best = kMiss;
+    if (leaf_test_rec(Q, r0, r1, r2, it.x & ~kLeafBit, d, best) && (!kAny || best != __float_as_uint(q4.w))) {
+        o.cand = true;
+        o.ctri = best;
+        o.key = kAny ? 0ull : ((unsigned long long)__float_as_uint(d) << 32) | code_key(it.w & kCodeMarkMask);
+        if (kCount) n_acc++;
+    }
+}
+
+// An interior item whose child-box record (r0..r3) has arrived: the node's
+// child ordering (TD/Trixel.cu:146-170) and the children's slab tests.
+template <bool kTranslated, bool kCount>
+__device__ __forceinline__ void visit_interior(const float4* rd, uint4 it, float4 r0, float4 r1, float4 r2,
+                                               float4 r3, Visit& o, uint32_t& n_int, uint32_t& n_desc) {
+    Ray Q;
+    float4 q2, q3, q4;
+    ray_of<kTranslated>(rd, Q, q2, q3, q4);
+    const uint32_t ray = it.w >> 26;
+    const uint32_t marked = it.w & kCodeMarkMask;
+    const uint32_t lw = __float_as_uint(r3.z);
+    const uint32_t axis = (lw >> kAxisShift) & 3u;
+    const uint32_t L = lw & ~(3u << kAxisShift), Rr = __float_as_uint(r3.w);
+    const float dir = axis == 0 ? q2.y : axis == 1 ? q2.z : q2.w;
+    const float mx = __uint_as_float(it.y) * dir, mn = __uint_as_float(it.z) * dir;
+    float s1, s2;
+    if (kTranslated) {
+        const float ds = axis == 0 ? q3.w : axis == 1 ? q4.x : q4.y;
+        s1 = (float)((double)r3.x + kEps + (double)ds);
+        s2 = r3.y + ds;
+    } else {
+        s1 = pred::add_eps(r3.x);
+        s2 = r3.y;
+    }
+    bool left_first, push_second;
+    if (pred::lt_eps(mx, s2)) {
+        left_first = true;
+        push_second = pred::gt_eps(mn, s2);
+    } else {
+        left_first = false;
+        push_second = (mn < s1 || mx < s1);
+    }
+    const uint32_t first = left_first ? L : Rr;
+    const uint32_t second = left_first ? Rr : L;
+    // children's slab tests from the boxes in this record
+    float lt0, lt1, rt0, rt1;
+    const bool lpass = slab(Q, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, lt0, lt1);
+    const bool rpass = slab(Q, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w, rt0, rt1);
+    const bool first_leaf = (first & kLeafBit) != 0, second_leaf = (second & kLeafBit) != 0;
+    const bool keep_first = first_leaf || (left_first ? lpass : rpass);
+    const bool keep_second = push_second && (second_leaf || (left_first ? rpass : lpass));
+    if (kCount) {
+        n_int += (first_leaf ? 0u : 1u) + ((push_second && !second_leaf) ? 1u : 0u);
+        n_desc += ((!first_leaf && keep_first) ? 1u : 0u) + ((push_second && !second_leaf && keep_second) ? 1u : 0u);
+    }
+    const uint32_t meta_first = (ray << 26) | (marked << 1);
+    const uint32_t meta_second = meta_first | 1u;
+    const float f0 = left_first ? lt0 : rt0, f1 = left_first ? lt1 : rt1;
+    const float g0 = left_first ? rt0 : lt0, g1 = left_first ? rt1 : lt1;
+    const uint4 A = make_uint4(first, __float_as_uint(f0), __float_as_uint(f1), meta_first);
+    const uint4 B = make_uint4(second, __float_as_uint(g0), __float_as_uint(g1), meta_second);
+    o.ca = A;
+    o.cb = B;
+    o.ka = keep_first;
+    o.kb = keep_second;
+}
+
+// Visits one item whose record has arrived: a leaf's MT test or an interior
+// node's child ordering and slab tests.
+template <int kVec, bool kTranslated, bool kCount, bool kAny>
+__device__ __forceinline__ void visit_item(const float4* rd, uint4 it, float4 r0, float4 r1, float4 r2, float4 r3,
+                                           Visit& o, uint32_t& n_int, uint32_t& n_leaf, uint32_t& n_acc,
+                                           uint32_t& n_desc) {
+    if (it.x & kLeafBit) visit_leaf<kTranslated, kCount, kAny>(rd, it, r0, r1, r2, o, n_leaf, n_acc);
+    else visit_interior<kTranslated, kCount>(rd, it, r0, r1, r2, r3, o, n_int, n_desc);
+}
+
+__device__ __forceinline__ uint32_t lanes_below(unsigned long long b) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+}
+
+// Nearest-candidate / any-hit bookkeeping of two visited items.
+template <bool kAny>
+__device__ __forceinline__ void record_candidates(unsigned long long* s_key, uint32_t* s_tri, const uint4& it0,
+                                                  const uint4& it1, const Visit& v0, const Visit& v1) {
+    const uint32_t ray0 = it0.w >> 26, ray1 = it1.w >> 26;
+    if (kAny) {
+        if (v0.cand) s_key[ray0] = 0ull;
+        if (v1.cand) s_key[ray1] = 0ull;
+    } else {
+        // nearest candidate per ray: 64-bit min of (w, path code), then the
+        // unique item holding the minimum records its triangle
+        if (v0.cand) atomicMin(&s_key[ray0], v0.key);
+        if (v1.cand) atomicMin(&s_key[ray1], v1.key);
+        __builtin_amdgcn_wave_barrier();
+        if (v0.cand && s_key[ray0] == v0.key) s_tri[ray0] = v0.ctri;
+        if (v1.cand && s_key[ray1] == v1.key) s_tri[ray1] = v1.ctri;
+    }
+}
+
+#ifndef RT_SEQ_PUSH
+#define RT_SEQ_PUSH 1
+#endif
+#ifndef RT_MAX_ITEMS
+#define RT_MAX_ITEMS 2
+#endif
+#ifndef RT_NEAREST_ORDER
+#define RT_NEAREST_ORDER 0
+#endif
+
+// One visited item's candidate: any-hit marks the ray; nearest-hit takes the
+// 64-bit min of (w, path code) and the unique holder of the minimum records
+// its triangle.
+template <bool kAny>
+__device__ __forceinline__ void record_candidate(unsigned long long* s_key, uint32_t* s_tri, const uint4& it,
+                                                 const Visit& v) {
+    const uint32_t ray = it.w >> 26;
+    if (kAny) {
+        if (v.cand) s_key[ray] = 0ull;
+    } else {
+        if (v.cand) atomicMin(&s_key[ray], v.key);
+        __builtin_amdgcn_wave_barrier();
+        if (v.cand && s_key[ray] == v.key) s_tri[ray] = v.ctri;
+    }
+}
+
+// Pushes one visited item's children (ballot compaction) at items[at...];
+// returns how many the wave pushed.  The order decides which items the next
+// pops take when the pool holds more than one pop.  Nearest-hit walks visit
+// every intersected node whatever the order; they push all lanes' first
+// children, then all second ones (0.084 ms at 1080p vs 0.092 for per-lane
+// pairs).  Any-hit (shadow) walks stop at the first occluder, and which order
+// reaches it soonest depends on the scene and resolution, so
+// it is a template choice of the launch (the host times the four and keeps
+// the fastest): 0 as nearest-hit, 1 per-lane pairs (first, second), 2 all
+// second children then all first ones (first children on top), 3 per-lane
+// pairs (second, first).  A runtime order costs scratch spills (measured).
+template <bool kAny, int any_order>
+__device__ __forceinline__ int push_children(uint4* items, int at, const Visit& v) {
+    const unsigned long long m1 = __ballot(v.ka), m2 = __ballot(v.kb);
+    const int n1 = __builtin_popcountll(m1), n2 = __builtin_popcountll(m2);
+    constexpr int ord = kAny ? any_order : RT_NEAREST_ORDER;
+    if (ord & 1) {   // per-lane pairs
+        const int off = (int)(lanes_below(m1) + lanes_below(m2));
+        if (ord == 1) {
+            if (v.ka) items[at + off] = v.ca;
+            if (v.kb) items[at + off + (v.ka ? 1 : 0)] = v.cb;
+        } else {
+            if (v.kb) items[at + off] = v.cb;
+            if (v.ka) items[at + off + (v.kb ? 1 : 0)] = v.ca;
+        }
+    } else if (ord == 2) {
+        if (v.kb) items[at + (int)lanes_below(m2)] = v.cb;
+        if (v.ka) items[at + n2 + (int)lanes_below(m1)] = v.ca;
+    } else {
+        if (v.ka) items[at + (int)lanes_below(m1)] = v.ca;
+        if (v.kb) items[at + n1 + (int)lanes_below(m2)] = v.cb;
+    }
+    return n1 + n2;
+}
+
+// The pool walk of one wave.  kAny = false: nearest hit per ray, key[ray] =
+// min (w, path code), tri[ray] = its triangle.  kAny = true (shadow rays): any
+// accepted leaf with w < Lmax other than the ray's own hit triangle sets
+// key[ray] = 0; without counters the items of such rays are dropped.
+// Each lane pops up to P.items (1 or 2) items per iteration and fetches their
+// records together, so a lane keeps two memory round trips in flight.
+template <int kCap, int kVec, bool kTranslated, bool kCount, bool kAny, int kOrder = 0>
+__device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, const float4* s_ray,
+                                          unsigned long long* s_key, uint32_t* s_tri, int n, int lane,
+                                          uint32_t& iters, uint32_t& popped, uint32_t& n_int, uint32_t& n_leaf,
+                                          uint32_t& n_acc,
+                                          uint32_t& n_desc) {
+    const int cap = min(P.pool_cap, kCap);
+    const int slack = P.tree_height + 1;
+    constexpr bool kTwo = RT_MAX_ITEMS > 1;  // compile-time: one-item builds drop item 1's registers
+    const int per = kTwo && P.items > 1 ? 128 : 64;
+    while (n > 0) {
+        // Pop as many items as the pool has room for the children of plus
+        // the DFS slack below; a single (DFS-like) pop when there is none.
+        // Popping k items pushes at most 2k, so a parallel pop leaves
+        // n <= cap - slack; a run of single pops starting at n0 is a DFS of
+        // the top item's subtree and never holds more than n0 + height items
+        // (slack = height + 1, height <= 24), so the pool never overflows.
+        int take = min(min(n, per), cap - slack - n);
+        if (take < 1) take = 1;
+        iters++;
+        popped += (uint32_t)take;
+        const int base = n - take;
+        // Both items and both records are read unconditionally (idle lanes
+        // re-read item `base`, a live item, whose record is a valid address):
+        // with guarded loads hipcc zero-fills the registers of the idle path
+        // and waits for the first record before issuing the second.
+        bool act0 = lane < take, act1 = kTwo && lane + 64 < take;
+        const uint4 it0 = items[base + (act0 ? lane : 0)];
+        const uint4 it1 = kTwo ? items[base + (act1 ? lane + 64 : 0)] : it0;
+        __builtin_amdgcn_wave_barrier();
+        // any-hit: a ray already shadowed needs no more visits (kept when
+        // counting, so the counters match the oracle's full walk, unless
+        // kOrder >= 4: counters of the walk a timed frame does)
+        if (kAny && (!kCount || kOrder >= 4)) {
+            if (act0 && s_key[it0.w >> 26] == 0ull) act0 = false;
+            if (act1 && s_key[it1.w >> 26] == 0ull) act1 = false;
+        }
+        // both records in flight before either is consumed
+        const float4* p0 = record_of(P, it0.x);
+        const float4* p1 = record_of(P, it1.x);
+        const float4 a0 = p0[0], a1 = p0[1], a2 = p0[2], a3 = p0[3];
+        const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        const float4 b0 = kTwo ? p1[0] : z, b1 = kTwo ? p1[1] : z, b2 = kTwo ? p1[2] : z, b3 = kTwo ? p1[3] : z;
+        asm volatile("" ::"v"(a0.x), "v"(a0.y), "v"(a0.z), "v"(a0.w), "v"(a1.x), "v"(a1.y), "v"(a1.z), "v"(a1.w),
+                     "v"(a2.x), "v"(a2.y), "v"(a2.z), "v"(a2.w), "v"(a3.x), "v"(a3.y), "v"(a3.z), "v"(a3.w));
+        asm volatile("" ::"v"(b0.x), "v"(b0.y), "v"(b0.z), "v"(b0.w), "v"(b1.x), "v"(b1.y), "v"(b1.z), "v"(b1.w),
+                     "v"(b2.x), "v"(b2.y), "v"(b2.z), "v"(b2.w), "v"(b3.x), "v"(b3.y), "v"(b3.z), "v"(b3.w));
+#if RT_SEQ_PUSH
+        // item 0 is visited, recorded and pushed before item 1 is visited, so
+        // its results die before item 1's are made (fewer live VGPRs)
+        int total = 0;
+        {
+            Visit v0;
+            v0.ka = v0.kb = false; v0.cand = false;
+            if (act0)
+                visit_item<kVec, kTranslated, kCount, kAny>(s_ray + (size_t)(it0.w >> 26) * kVec, it0, a0, a1, a2, a3,
+                                                            v0, n_int, n_leaf, n_acc, n_desc);
+            record_candidate<kAny>(s_key, s_tri, it0, v0);
+            total += push_children<kAny, (kOrder & 3)>(items, base + total, v0);
+        }
+        {
+            Visit v1;
+            v1.ka = v1.kb = false; v1.cand = false;
+            if (act1)
+                visit_item<kVec, kTranslated, kCount, kAny>(s_ray + (size_t)(it1.w >> 26) * kVec, it1, b0, b1, b2, b3,
+                                                            v1, n_int, n_leaf, n_acc, n_desc);
+            record_candidate<kAny>(s_key, s_tri, it1, v1);
+            total += push_children<kAny, (kOrder & 3)>(items, base + total, v1);
+        }
+        if (base + total > cap) {  // unreachable by the pop rule above; guard anyway
+            if (lane == 0) atomicOr(P.err, 2);
+            break;
+        }
+#else
+        Visit v0, v1;  // children / key fields are read only where nk / cand say so
+        v0.ka = v0.kb = false; v0.cand = false;
+        v1.ka = v1.kb = false; v1.cand = false;
+        if (act0)
+            visit_item<kVec, kTranslated, kCount, kAny>(s_ray + (size_t)(it0.w >> 26) * kVec, it0, a0, a1, a2, a3, v0,
+                                                        n_int, n_leaf, n_acc, n_desc);
+        if (act1)
+            visit_item<kVec, kTranslated, kCount, kAny>(s_ray + (size_t)(it1.w >> 26) * kVec, it1, b0, b1, b2, b3, v1,
+                                                        n_int, n_leaf, n_acc, n_desc);
+        record_candidates<kAny>(s_key, s_tri, it0, it1, v0, v1);
+        // push the children (all first children of item 0, all second ones, then item 1's): ballot compaction
+        const unsigned long long m1 = __ballot(v0.ka), m2 = __ballot(v0.kb);
+        const unsigned long long m3 = __ballot(v1.ka), m4 = __ballot(v1.kb);
+        const int n1 = __builtin_popcountll(m1), n2 = __builtin_popcountll(m2), n3 = __builtin_popcountll(m3);
+        const int total = n1 + n2 + n3 + __builtin_popcountll(m4);
+        if (base + total > cap) {  // unreachable by the pop rule above; guard anyway
+            if (lane == 0) atomicOr(P.err, 2);
+            break;
+        }
+        if (v0.ka) items[base + (int)lanes_below(m1)] = v0.ca;
+        if (v0.kb) items[base + n1 + (int)lanes_below(m2)] = v0.cb;
+        if (v1.ka) items[base + n1 + n2 + (int)lanes_below(m3)] = v1.ca;
+        if (v1.kb) items[base + n1 + n2 + n3 + (int)lanes_below(m4)] = v1.cb;
+#endif
+        n = base + total;
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// Per-wave LDS of the wave-cooperative kernel.
+template <int kRays, int kCap, int kRayVec>
+struct WaveLds {
+    uint4 items[kCap];
+    float4 ray[kRays * kRayVec];
+    unsigned long long key[kRays];
+    uint32_t tri[kRays];
+};
+
+struct Counts {
+    uint32_t n_int = 0, n_leaf = 0, n_acc = 0, n_desc = 0, n_hit = 0;
+};
+
+// One wave's unit of work: the kRays pixels (8 x kRays/8) of unit U.
+constexpr size_t kNoDbg = ~(size_t)0;
+constexpr int kCoarseMax = 32;  // coarse groups per wave (RT_OPT_COARSE <= 32)
+template <int kRays, int kCap, int kRayVec, bool kTranslated, bool kWriteHit, bool kCount, int kShadow>
+__device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, kCap, kRayVec>& S_, const Unit& U,
+                                           int lane, size_t dbg_slot, uint32_t* cost, Counts& C) {
+    uint4* items = S_.items;
+    Pixel px;
+    const bool live = unit_pixel(P, U, kRays / 8, lane, px);  // every lane stays for the ballots
+    const unsigned long long t_start = P.dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    uint32_t iters = 0, popped = 0;
+
+    float cam[3];
+    Ray R;
+    camera_ray(P, px, live, cam, R);
+    const float* X = P.xf;
+    if (lane < kRays) {
+        store_ray(&S_.ray[lane * kRayVec], R, kTranslated, 0.0f, 0u);
+        S_.key[lane] = ~0ull;
+        S_.tri[lane] = kMiss;
+    }
+
+    int n = seed_root<kCount>(P, items, R, live, lane, C.n_int, C.n_desc);
+    pool_walk<kCap, kRayVec, kTranslated, kCount, false>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters, popped, C.n_int,
+                                                        C.n_leaf, C.n_acc, C.n_desc);
+    unsigned long long kbest = ~0ull;
+    uint32_t best = kMiss;
+    if (lane < kRays) {
+        kbest = S_.key[lane];
+        best = kbest == ~0ull ? kMiss : S_.tri[lane];
+    }
+    bool shadowed = false;
+    if constexpr (kShadow > 0) {
+        // the shadow segment of each hit: from the light to H = d*r - od
+        const bool sh_live = live && best != kMiss;
+        Ray Sh;
+        Sh.odx = -2.0f; Sh.ody = -2.0f; Sh.odz = -2.0f;
+        Sh.rx = 1.0f; Sh.ry = 1.0f; Sh.rz = 1.0f;
+        float lmax = 0.0f;
+        if (sh_live) {
+            const float d = __uint_as_float((uint32_t)(kbest >> 32));
+            float sx = ((d * R.rx) - R.odx) - 2;
+            float sy = ((d * R.ry) - R.ody) - 2;
+            float sz = ((d * R.rz) - R.odz) - 2;
+            lmax = sqrtf((sx * sx) + (sy * sy) + (sz * sz)) * 0.9990234375f;  // correctly rounded sqrt
+            const float r = rsqrt21(sx, sy, sz);
+            Sh.rx = sx * r; Sh.ry = sy * r; Sh.rz = sz * r;
+        }
+        finish_ray(Sh);
+        if (lane < kRays) {
+            store_ray(&S_.ray[lane * kRayVec], Sh, true, lmax, best);
+            S_.key[lane] = ~0ull;
+        }
+        __builtin_amdgcn_wave_barrier();
+        n = seed_root<kCount>(P, items, Sh, sh_live, lane, C.n_int, C.n_desc);
+        pool_walk<kCap, kRayVec, true, kCount, true, kShadow - 1>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters, popped, C.n_int,
+                                                    C.n_leaf, C.n_acc, C.n_desc);
+        if (lane < kRays) shadowed = S_.key[lane] == 0ull;
+    }
+    if (P.dbg && lane == 0 && dbg_slot != kNoDbg) {  // diagnostics: the unit's start/end clock (100 MHz) and pool iterations
+        P.dbg[3 * dbg_slot] = t_start;
+        P.dbg[3 * dbg_slot + 1] = __builtin_amdgcn_s_memrealtime();
+        P.dbg[3 * dbg_slot + 2] = iters | ((unsigned long long)popped << 32);
+    }
+    if (cost && lane == 0) *cost = iters;  // tile order 3: this unit's pool iterations
+    __builtin_amdgcn_wave_barrier();  // LDS of this unit is read; the next unit may overwrite it
+    if (!live) return;
+    uint32_t argb = kBackground;
+    if (shadowed) {
+        argb = 0x00000000u;  // point_rad stays 0: 0/0 -> (u8)NaN = 0 (H14)
+    } else if (best != kMiss) {
+        const float d = __uint_as_float((uint32_t)(kbest >> 32));
+        const float4 N = P.shade[2 * (size_t)best];
+        const float4 M = P.shade[2 * (size_t)best + 1];
+        const float pnt[3] = {d * R.rx + R.odx, d * R.ry + R.ody, d * R.rz + R.odz};
+        // norm.device_rotate(rot_m, i, -1), TD/vector.cuh:23-33
+        const float ax = -1 * N.x, ay = -1 * N.y, az = -1 * N.z;
+        const float nrm[3] = {(ax * X[0] + ay * X[1] + az * X[2]) * -1,
+                              (ax * X[4] + ay * X[5] + az * X[6]) * -1,
+                              (ax * X[8] + ay * X[9] + az * X[10]) * -1};
+        const float rad[3] = {M.x, M.y, M.z};
+        argb = phong(pnt, nrm, cam, rad);
+    }
+    P.argb[px.out] = argb;
+    if (kWriteHit) P.hit[px.out] = best == kMiss ? (int64_t)-1 : (int64_t)best;
+    if (kCount && best != kMiss) C.n_hit++;
+}
+
+__device__ __forceinline__ void count_flush(const TraceParams& P, const Counts& C) {
+    // every lane (also those past the frame edge) processed pool items;
+    // counter [2] counts valid candidates here (>= the DFS's accept events)
+    wave_count_add(&P.counters[0], C.n_int);
+    wave_count_add(&P.counters[1], C.n_leaf);
+    wave_count_add(&P.counters[2], C.n_acc);
+    wave_count_add(&P.counters[3], C.n_hit);
+    wave_count_add(&P.counters[4], C.n_desc);
+}
+
+// Root test of one coarse 8x8 group (all 64 lanes): returns the ballot of
+// lanes whose root test passes; lanes whose kRays-pixel sub-tile has no
+// passing ray write the background now.  The sub-tiles with a passing ray are
+// traced by trace_unit, which repeats the same root test, so a coarse group's
+// pixels are exactly what fine units would produce; only the packing of work
+// into waves differs.
+//
+// With the identity object transform (P.plain_xf) a group first tries a
+// cheap test: the ray normalised by the hardware rsqrt / rcp instead of the
+// 21-step Newton loop and correctly rounded divisions.  Its slab parameters
+// are within ~1e-6 (relative) of the exact ones, so a pixel whose test fails
+// by a 1e-3 relative margin (or whose entry lies behind the eye by more than
+// 1e-12) fails the exact test too; rays with a zero or tiny component, a NaN,
+// or any doubt take the exact test.  When every pixel of the group is such a
+// certain miss the group is background without the exact rays.
+__device__ __forceinline__ bool root_certain_miss(const TraceParams& P, int32_t ix, int32_t iy) {
+    // (float)ix of the reference's unsigned pixel index: exact and equal for any ix < 2^32
+    const float fx = (float)(uint32_t)ix, fy = (float)(uint32_t)iy;
+    const float x = P.n_mod[0] + P.u_mod[0] * fx + P.v_mod[0] * fy;
+    const float y = P.n_mod[1] + P.u_mod[1] * fx + P.v_mod[1] * fy;
+    const float z = P.n_mod[2] + P.u_mod[2] * fx + P.v_mod[2] * fy;
+    const float r = __builtin_amdgcn_rsqf((x * x) + (y * y) + (z * z));
+    const float dx = x * r, dy = y * r, dz = z * r;
+    if (!(fabsf(dx) > 1e-6f && fabsf(dy) > 1e-6f && fabsf(dz) > 1e-6f)) return false;
+    const float ix_ = __builtin_amdgcn_rcpf(dx), iy_ = __builtin_amdgcn_rcpf(dy), iz_ = __builtin_amdgcn_rcpf(dz);
+    const float* b = P.root_box;
+    const float t0x = (dx > 0 ? b[0] : b[1]) * ix_, t1x = (dx > 0 ? b[1] : b[0]) * ix_;
+    const float t0y = (dy > 0 ? b[2] : b[3]) * iy_, t1y = (dy > 0 ? b[3] : b[2]) * iy_;
+    const float t0z = (dz > 0 ? b[4] : b[5]) * iz_, t1z = (dz > 0 ? b[5] : b[4]) * iz_;
+    const float maxt0 = fmaxf(t0z, fmaxf(t0x, t0y)), mint1 = fminf(t1z, fminf(t1x, t1y));
+    if (!(fabsf(maxt0) < 1e30f && fabsf(mint1) < 1e30f)) return false;  // NaN or huge: exact test
+    const float tol = 1e-3f * (fabsf(maxt0) + fabsf(mint1));
+    return mint1 < maxt0 - tol || (maxt0 < -tol && maxt0 < -1e-12f);
+}
+
+//
+// Groups at least 2 pixels outside the root box's screen rectangle
+// (P.far_rect, identity transform only) skip even that: the rectangle is the
+// box's exact projection (in double, from the same float basis), a pixel's
+// float ray deviates from its exact direction by ~1e-6 rad against the
+// ~1e-3 rad of two pixels, and with a zero object offset the slab parameters
+// are single roundings of bound / D, so the test fails -- unless a component
+// of the ray is zero (0/0 = NaN drops that axis from the test) or tiny,
+// which each pixel checks.
+__device__ __forceinline__ bool far_group(const TraceParams& P, const Unit& G) {
+    const int32_t y0 = (P.rank + G.slot * P.nranks) * kTileH;
+    return G.x0 + 7 < P.far_rect[0] || G.x0 > P.far_rect[1] || y0 + 7 < P.far_rect[2] || y0 > P.far_rect[3];
+}
+
+__device__ __forceinline__ bool ray_has_tiny_component(const TraceParams& P, int32_t ix, int32_t iy) {
+    const float fx = (float)(uint32_t)ix, fy = (float)(uint32_t)iy;
+    const float x = P.n_mod[0] + P.u_mod[0] * fx + P.v_mod[0] * fy;
+    const float y = P.n_mod[1] + P.u_mod[1] * fx + P.v_mod[1] * fy;
+    const float z = P.n_mod[2] + P.u_mod[2] * fx + P.v_mod[2] * fy;
+    return !(fabsf(x) > 1e-30f && fabsf(y) > 1e-30f && fabsf(z) > 1e-30f);
+}
+
+// A far group (see above) whose rays have no tiny component is background:
+// writes it and returns true; otherwise returns false and writes nothing.
+template <bool kWriteHit, bool kCount>
+__device__ __forceinline__ bool fill_far(const TraceParams& P, const Unit& G, int lane, Counts& C) {
+    if (!far_group(P, G)) return false;
+    Pixel px;
+    const bool live = unit_pixel(P, G, 8, lane, px);
+    if (__ballot(live && ray_has_tiny_component(P, px.x, px.y)) != 0ull) return false;
+    if (live) {
+        P.argb[px.out] = kBackground;
+        if (kWriteHit) P.hit[px.out] = (int64_t)-1;
+        if (kCount) C.n_int += 1u;  // the root visit, which fails
+    }
+    return true;
+}
+
+template <int kRays, bool kWriteHit, bool kCount>
+__device__ __forceinline__ unsigned long long coarse_root(const TraceParams& P, const Unit& G, int lane, Counts& C) {
+    Pixel px;
+    const bool live = unit_pixel(P, G, 8, lane, px);
+    if (P.plain_xf && !(P.root_ref & kLeafBit) && !(P.debug & 1)) {
+        const bool sure = !live || root_certain_miss(P, px.x, px.y);
+        if (__ballot(!sure) == 0ull) {
+            if (live) {
+                P.argb[px.out] = kBackground;
+                if (kWriteHit) P.hit[px.out] = (int64_t)-1;
+                if (kCount) C.n_int += 1u;  // the root visit, which fails
+            }
+            return 0ull;
+        }
+    }
+    float cam[3], t0, t1;
+    Ray R;
+    camera_ray(P, px, live, cam, R);
+    uint32_t ni = 0, nd = 0;
+    const bool has = root_pass<kCount>(P, R, live, t0, t1, ni, nd);
+    const unsigned long long b = __ballot(has);
+    constexpr unsigned long long kSub = kRays == 64 ? ~0ull : ((1ull << (kRays & 63)) - 1);
+    const bool traced = ((b >> ((lane / kRays) * kRays)) & kSub) != 0;
+    if (live && !traced) {
+        P.argb[px.out] = kBackground;
+        if (kWriteHit) P.hit[px.out] = (int64_t)-1;
+        if (kCount) C.n_int += ni;  // the root visit; no root test passed in this sub-tile
+    }
+    return b;
+}
+
+// kRays pixels per wave (64: 8x8; 32: 8x4; 16: 8x2; 8: 8x1): fewer rays per wave
+// spread a heavy tile's items over more SIMDs, the other lanes only help.
+// kShadow: a second pool walk traces one shadow ray per hit (SURVEY.md §8a
+// a12; definition in oracle/oracle.c trace_shadow): the segment from the light
+// (2,2,2) to the hit, walked from the light with the reference's rules.
+// One fine tile per block (the tiles covering the root box's screen
+// rectangle, or the whole frame), one unit per wave.
+#ifdef RT_KD3_WAVES_PER_SIMD
+#define RT_KD3_BOUNDS(threads) __launch_bounds__(threads, RT_KD3_WAVES_PER_SIMD)
+#else
+#define RT_KD3_BOUNDS(threads) __launch_bounds__(threads)
+#endif
+template <int kRays, bool kTranslated, bool kWriteHit, bool kCount, int kShadow>
+__global__ RT_KD3_BOUNDS(64 * kd3_waves(kRays)) void k_trace_kd3(TraceParams P) {
+    constexpr int kWaves = kd3_waves(kRays);
+    constexpr int kCap = pool_cap_for<kRays>();
+    constexpr int kRayVec = (kTranslated || kShadow) ? 5 : 3;  // float4s of per-ray data in LDS
+    __shared__ WaveLds<kRays, kCap, kRayVec> s_lds[kWaves];
+    const int wv = wave_id(), lane = (int)threadIdx.x & 63;
+    Counts C;
+    const int32_t b = (int32_t)blockIdx.x;
+    if (b >= P.tiles_x * P.block_rows) {
+        // fused far fill: blocks after the fine tiles write the coarse groups,
+        // all far by construction (set_fine_region); unrolled as in k_coarse_kd3
+        const int32_t j0 = ((b - P.tiles_x * P.block_rows) * kWaves + wv) * P.coarse_per_wave;
+        const int32_t j1 = min(j0 + P.coarse_per_wave, (int32_t)P.coarse_groups);
+        bool ok = true;
+#pragma unroll 8
+        for (int g = 0; g < kCoarseMax; g++) {
+            const int32_t j = j0 + g;
+            if (j < j1) ok = fill_far<kWriteHit, kCount>(P, coarse_unit(P, j), lane, C) && ok;
+        }
+        if (!ok && lane == 0) atomicOr(P.err, 4);  // a group the host promised far was not
+        if (kCount) count_flush(P, C);
+        return;
+    }
+    uint32_t* cost = P.cost ? P.cost + kCostSlots * (size_t)tile_index(P, b) + wv : nullptr;
+    trace_unit<kRays, kCap, kRayVec, kTranslated, kWriteHit, kCount, kShadow>(P, s_lds[wv], unit_of(P, b, wv), lane,
+                                                                             (size_t)b * kWaves + wv, cost, C);
+    if (kCount) count_flush(P, C);
+}
+
+// The coarse groups (every 8x8 group of this rank outside the fine tiles),
+// P.coarse_per_wave (<= kCoarseMax) per wave.  A separate kernel: looping trace_unit inside
+// the fine kernel costs it a third of its occupancy (80 -> 113 VGPRs).
+template <int kRays, bool kTranslated, bool kWriteHit, bool kCount, int kShadow>
+__global__ __launch_bounds__(128) void k_coarse_kd3(TraceParams P) {
+    constexpr int kWaves = 2;
+    constexpr int kCap = pool_cap_for<kRays>();
+    constexpr int kRayVec = (kTranslated || kShadow) ? 5 : 3;
+    constexpr unsigned long long kSub = kRays == 64 ? ~0ull : ((1ull << (kRays & 63)) - 1);
+    __shared__ WaveLds<kRays, kCap, kRayVec> s_lds[kWaves];
+    const int wv = wave_id(), lane = (int)threadIdx.x & 63;
+    Counts C;
+    const unsigned long long t_start = P.dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    const int32_t cw = (int32_t)blockIdx.x * kWaves + wv;
+    const int32_t j0 = cw * P.coarse_per_wave;
+    const int32_t j1 = min(j0 + P.coarse_per_wave, (int32_t)P.coarse_groups);
+    // Far groups first, unrolled so their short independent chains overlap
+    // (one after another they cost ~1 us each in latency); the rest after.
+    const bool far_ok = P.plain_xf && !(P.root_ref & kLeafBit) && !(P.debug & 1);
+    uint32_t pending = 0;
+#pragma unroll 8
+    for (int g = 0; g < kCoarseMax; g++) {
+        const int32_t j = j0 + g;
+        if (j < j1 && !(far_ok && fill_far<kWriteHit, kCount>(P, coarse_unit(P, j), lane, C))) pending |= 1u << g;
+    }
+    while (pending) {
+        const int32_t j = j0 + __builtin_ctz(pending);
+        pending &= pending - 1;
+        const Unit G = coarse_unit(P, j);
+        const unsigned long long gmask = coarse_root<kRays, kWriteHit, kCount>(P, G, lane, C);
+        for (int k = 0; k < 64 / kRays; k++)
+            if ((gmask >> (k * kRays)) & kSub)
+                trace_unit<kRays, kCap, kRayVec, kTranslated, kWriteHit, kCount, kShadow>(
+                    P, s_lds[wv], Unit{G.x0, G.slot, k * (kRays / 8)}, lane, kNoDbg, nullptr, C);
+    }
+    if (P.dbg && lane == 0) {  // after the fine kernel's slots
+        const size_t slot = (size_t)(P.tiles_x * P.block_rows + blockIdx.x) * kWaves + wv;
+        P.dbg[3 * slot] = t_start;
+        P.dbg[3 * slot + 1] = __builtin_amdgcn_s_memrealtime();
+        P.dbg[3 * slot + 2] = 0xFFFFFFFFull;  // marks a coarse wave
+    }
+    if (kCount) count_flush(P, C);
+}
+
+// -------------------------------------------------------------- flat trace
+
+// intersect_trixel_cuda (TD/Trixel.cu:173-209) fused with the shading.  The
+// triangle loop index is wave-uniform, so its records arrive through the
+// scalar data cache into SGPRs; an exact sign screen skips the division for
+// the (common) rays that cannot pass u >= eps, v >= eps or w >= eps.
+//
+// The screen.  u = pe1*U, v = pe1*V, w = pe1*W with sign(pe1) = sign(f), so
+// with U, V, W sign-flipped when f is negative (an XOR of f's sign bit), a
+// flipped value <= 0 makes u, v or w <= 0 < eps: rejected.  min3 ignores NaN
+// (IEEE minNum), so a NaN U, V or W never rejects by itself (the full test
+// decides); f = +-0 or NaN makes the full test reject anyway (|f| < eps, or
+// NaN w fails w < d).  A ray passes the screen iff !(min3 <= 0).
+__device__ __forceinline__ float flip_by(float x, float f) {
+    return __uint_as_float(__float_as_uint(x) ^ (__float_as_uint(f) & 0x80000000u));
+}
+__device__ __forceinline__ bool flat_screen(float f, float U, float V, float W) {
+    const float m = fminf(fminf(flip_by(U, f), flip_by(V, f)), flip_by(W, f));
+    return !(m <= 0.0f);
+}
+
+// The rest of one flat test (TD/Trixel.cu:185-205) for a ray that passed
+// the screen: strict w < d, so among equal w the lowest index wins.
+__device__ __forceinline__ void flat_accept(float f, float U, float V, float W, uint32_t t, float& d,
+                                            uint32_t& best, uint32_t& n_acc) {
+    if (!(f < kEpsF && f > -kEpsF)) {
+        const float pe1 = 1.0f / f;   // == (float)(1.0 / (double)f)
+        const float u = pe1 * U;
+        const float v = pe1 * V;
+        const float w = pe1 * W;
+        if ((w < d) && !((u < kEpsF) || (v < kEpsF) || ((u + v) > 1.0f) || (w < kEpsF))) {
+            d = w;
+            best = t;
+            n_acc++;
+        }
+    }
+}
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// One pair of the flat kernel's pair layout in registers (SGPRs: the loop
+// index is wave-uniform) and its two tests as packed float2 arithmetic.
+struct FlatPair {
+    f2v e1x, e1y, e1z, e2x, e2y, e2z, tx, ty, tz, dqx, dqy, dqz, dw;
+    __device__ __forceinline__ void load(const f2v* q) {
+        e1x = q[0]; e1y = q[1]; e1z = q[2]; e2x = q[3]; e2y = q[4]; e2z = q[5];
+        tx = q[6]; ty = q[7]; tz = q[8]; dqx = q[9]; dqy = q[10]; dqz = q[11]; dw = q[12];
+    }
+    // Loads pair `pair` of Q only after `prev`'s values have arrived: the
+    // index is made to depend on one of them through `zero`, a run-time 0
+    // the compiler cannot fold (an asm barrier would make the loads vector
+    // loads), so waiting for prev never waits for this pair's loads.
+    __device__ __forceinline__ void load_after(const f2v* __restrict__ Q, uint32_t pair, const FlatPair& prev,
+                                               uint32_t zero) {
+        pair ^= __float_as_uint(prev.dw.y) & zero;
+        load(Q + 16 * (size_t)pair);
+    }
+    // device_cross(rmd, e2) then the dots (TD/Trixel.cu:180-186) per half;
+    // triangle t then t + 1, so equal w keeps the lower index.
+    __device__ __forceinline__ void test(const f2v X, const f2v Y, const f2v Z, uint32_t t, float& d, uint32_t& best,
+                                         uint32_t& n_acc) const {
+        const f2v qx = Y * e2z - Z * e2y;
+        const f2v qy = Z * e2x - X * e2z;
+        const f2v qz = X * e2y - Y * e2x;
+        const f2v f = (qx * e1x + qy * e1y) + qz * e1z;
+        const f2v U = (qx * tx + qy * ty) + qz * tz;
+        const f2v V = (X * dqx + Y * dqy) + Z * dqz;
+        const bool c0 = flat_screen(f.x, U.x, V.x, dw.x), c1 = flat_screen(f.y, U.y, V.y, dw.y);
+        if (c0 || c1) {
+            if (c0) flat_accept(f.x, U.x, V.x, dw.x, t, d, best, n_acc);
+            if (c1) flat_accept(f.y, U.y, V.y, dw.y, t + 1, d, best, n_acc);
+        }
+    }
+};
+
+// kVariant 0: one triangle per iteration, the 64-B camera-relative record
+// (the first form).  1: two triangles per iteration, both records loaded
+// before either is tested, branch-free screen.  2: the same pair as packed
+// float2 arithmetic (v_pk_mul_f32 / v_pk_add_f32, one IEEE rounding per half,
+// so every value is the unpacked one) over the pair layout P.tpair.  3: 2,
+// software pipelined (the next pair's loads in flight during a pair's tests).
+template <bool kWriteHit, bool kCount, int kVariant>
+__global__ __launch_bounds__(kTileWFlat * kTileH) void k_trace_flat(TraceParams P) {
+    Pixel px;
+    if (!pixel_of_thread(P, px)) return;
+    float rmd[3];
+    primary_ray(P, px.x, px.y, rmd);
+    const float rx = rmd[0], ry = rmd[1], rz = rmd[2];
+    float d = kDrawDistance;
+    uint32_t best = kMiss;
+    uint32_t n_acc = 0;
+    const float4* __restrict__ T = P.trec;
+    const uint32_t ntri = P.ntri;
+    if (kVariant == 0) {
+        for (uint32_t t = 0; t < ntri; t++) {
+            const float4 A = T[4 * (size_t)t];
+            const float4 B = T[4 * (size_t)t + 1];
+            const float4 Cq = T[4 * (size_t)t + 2];
+            const float4 D = T[4 * (size_t)t + 3];
+            float qpx, qpy, qpz;
+            cross3(qpx, qpy, qpz, rx, ry, rz, A.w, B.x, B.y);
+            const float f = dot3(qpx, qpy, qpz, A.x, A.y, A.z);
+            const float U = dot3(qpx, qpy, qpz, B.z, B.w, Cq.x);
+            const float V = dot3(rx, ry, rz, Cq.y, Cq.z, Cq.w);
+            const float W = D.x;
+            const bool pos = f > 0;
+            const bool reject = (pos ? (U <= 0 || V <= 0 || W <= 0) : (U >= 0 || V >= 0 || W >= 0));
+            if (reject) continue;
+            flat_accept(f, U, V, W, t, d, best, n_acc);
+        }
+    } else if (kVariant == 1) {
+        uint32_t t = 0;
+        for (; t + 1 < ntri; t += 2) {
+            const float4 A0 = T[4 * (size_t)t], B0 = T[4 * (size_t)t + 1], C0 = T[4 * (size_t)t + 2],
+                         D0 = T[4 * (size_t)t + 3];
+            const float4 A1 = T[4 * (size_t)t + 4], B1 = T[4 * (size_t)t + 5], C1 = T[4 * (size_t)t + 6],
+                         D1 = T[4 * (size_t)t + 7];
+            float q0x, q0y, q0z, q1x, q1y, q1z;
+            cross3(q0x, q0y, q0z, rx, ry, rz, A0.w, B0.x, B0.y);
+            cross3(q1x, q1y, q1z, rx, ry, rz, A1.w, B1.x, B1.y);
+            const float f0 = dot3(q0x, q0y, q0z, A0.x, A0.y, A0.z);
+            const float f1 = dot3(q1x, q1y, q1z, A1.x, A1.y, A1.z);
+            const float U0 = dot3(q0x, q0y, q0z, B0.z, B0.w, C0.x);
+            const float U1 = dot3(q1x, q1y, q1z, B1.z, B1.w, C1.x);
+            const float V0 = dot3(rx, ry, rz, C0.y, C0.z, C0.w);
+            const float V1 = dot3(rx, ry, rz, C1.y, C1.z, C1.w);
+            const bool c0 = flat_screen(f0, U0, V0, D0.x), c1 = flat_screen(f1, U1, V1, D1.x);
+            if (c0 || c1) {
+                if (c0) flat_accept(f0, U0, V0, D0.x, t, d, best, n_acc);
+                if (c1) flat_accept(f1, U1, V1, D1.x, t + 1, d, best, n_acc);
+            }
+        }
+        if (t < ntri) {
+            const float4 A = T[4 * (size_t)t], B = T[4 * (size_t)t + 1], Cq = T[4 * (size_t)t + 2],
+                         D = T[4 * (size_t)t + 3];
+            float qpx, qpy, qpz;
+            cross3(qpx, qpy, qpz, rx, ry, rz, A.w, B.x, B.y);
+            const float f = dot3(qpx, qpy, qpz, A.x, A.y, A.z);
+            const float U = dot3(qpx, qpy, qpz, B.z, B.w, Cq.x);
+            const float V = dot3(rx, ry, rz, Cq.y, Cq.z, Cq.w);
+            if (flat_screen(f, U, V, D.x)) flat_accept(f, U, V, D.x, t, d, best, n_acc);
+        }
+    } else {
+        // pair p = triangles (2p, 2p+1): 13 float2 (e1, e2, d_t, d_q, d_w), 128 B;
+        // an odd count's last pair holds a dead twin (d_w = 0: never accepted)
+        const f2v* __restrict__ Q = reinterpret_cast<const f2v*>(P.tpair);
+        const f2v X = {rx, rx}, Y = {ry, ry}, Z = {rz, rz};
+        const uint32_t npair = (ntri + 1) >> 1;
+        if (kVariant == 2) {
+            for (uint32_t p = 0; p < npair; p++) {
+                FlatPair c;
+                c.load(Q + 16 * (size_t)p);
+                c.test(X, Y, Z, 2 * p, d, best, n_acc);
+            }
+        } else {
+            // software pipelined: pair p + 1's scalar loads are issued once
+            // pair p's have arrived (scalar loads return out of order, so a
+            // wait is always for all of them) and overlap pair p's tests
+            const uint32_t zero = ntri >> 31;  // 0: scenes hold < 2^29 triangles
+            FlatPair a, b;
+            a.load(Q);
+            uint32_t p = 0;
+            for (; p + 1 < npair; p += 2) {
+                b.load_after(Q, p + 1, a, zero);
+                a.test(X, Y, Z, 2 * p, d, best, n_acc);
+                a.load_after(Q, min(p + 2, npair - 1), b, zero);
+                b.test(X, Y, Z, 2 * p + 2, d, best, n_acc);
+            }
+            if (p < npair) a.test(X, Y, Z, 2 * p, d, best, n_acc);
+        }
+    }
+    uint32_t argb = kBackground;
+    if (best != kMiss) {
+        const float4 N = P.shade[2 * (size_t)best];
+        const float4 M = P.shade[2 * (size_t)best + 1];
+        const float pnt[3] = {d * rx, d * ry, d * rz};
+        const float nrm[3] = {N.x, N.y, N.z};
+        const float rad[3] = {M.x, M.y, M.z};
+        argb = phong(pnt, nrm, rmd, rad);
+    }
+    P.argb[px.out] = argb;
+    if (kWriteHit) P.hit[px.out] = best == kMiss ? (int64_t)-1 : (int64_t)best;
+    if (kCount) {
+        wave_count_add(&P.counters[1], ntri);
+        wave_count_add(&P.counters[2], n_acc);
+        wave_count_add(&P.counters[3], best != kMiss ? 1u : 0u);
+    }
+}
+
+// The flat kernel's pair layout: pair p <- camera-relative records 2p, 2p+1,
+// each field as (value of 2p, value of 2p+1); a missing twin is dead (all
+// zero: d_w = 0 fails the screen, and its full test gives w = 0 < eps).
+__global__ void k_pair_tri(const float4* __restrict__ trec, uint32_t ntri, float4* __restrict__ tpair) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t npair = (ntri + 1) >> 1;
+    if (p >= npair) return;
+    float a[13], b[13];
+    const uint32_t t0 = 2 * p, t1 = 2 * p + 1;
+    const float4* r0 = trec + 4 * (size_t)t0;
+    const float4 A0 = r0[0], B0 = r0[1], C0 = r0[2], D0 = r0[3];
+    a[0] = A0.x; a[1] = A0.y; a[2] = A0.z; a[3] = A0.w; a[4] = B0.x; a[5] = B0.y; a[6] = B0.z; a[7] = B0.w;
+    a[8] = C0.x; a[9] = C0.y; a[10] = C0.z; a[11] = C0.w; a[12] = D0.x;
+    for (int k = 0; k < 13; k++) b[k] = 0.0f;
+    if (t1 < ntri) {
+        const float4* r1 = trec + 4 * (size_t)t1;
+        const float4 A1 = r1[0], B1 = r1[1], C1 = r1[2], D1 = r1[3];
+        b[0] = A1.x; b[1] = A1.y; b[2] = A1.z; b[3] = A1.w; b[4] = B1.x; b[5] = B1.y; b[6] = B1.z; b[7] = B1.w;
+        b[8] = C1.x; b[9] = C1.y; b[10] = C1.z; b[11] = C1.w; b[12] = D1.x;
+    }
+    // field order of the kernel: e1 (3), e2 (3), d_t (3), d_q (3), d_w
+    float4* o = tpair + 8 * (size_t)p;
+    o[0] = make_float4(a[0], b[0], a[1], b[1]);
+    o[1] = make_float4(a[2], b[2], a[3], b[3]);
+    o[2] = make_float4(a[4], b[4], a[5], b[5]);
+    o[3] = make_float4(a[6], b[6], a[7], b[7]);
+    o[4] = make_float4(a[8], b[8], a[9], b[9]);
+    o[5] = make_float4(a[10], b[10], a[11], b[11]);
+    o[6] = make_float4(a[12], b[12], 0.0f, 0.0f);
+    o[7] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+}
+
+// ------------------------------------------------------------------ prep
+
+// init_tri_mem_cuda, TD/Trixel.cu:11-27, plus the Color::rad copy.
+// tri_world = (p1.xyz, e1.x) (e1.yz, e2.xy) (e2.z, n.xyz); shade = (n, 0) (rad, 0)
+__global__ void k_tri_world(const float* __restrict__ pts, const float* __restrict__ rad,
+                            uint32_t ntri, float4* __restrict__ tw, float4* __restrict__ shade) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ntri) return;
+    const float* P = pts + 9 * (size_t)i;
+    const float e1x = P[3] - P[0], e1y = P[4] - P[1], e1z = P[5] - P[2];
+    const float e2x = P[6] - P[0], e2y = P[7] - P[1], e2z = P[8] - P[2];
+    float nx, ny, nz;
+    cross3(nx, ny, nz, e1x, e1y, e1z, e2x, e2y, e2z);
+    const float r = rsqrt21(nx, ny, nz);
+    nx *= r; ny *= r; nz *= r;
+    tw[3 * (size_t)i] = make_float4(P[0], P[1], P[2], e1x);
+    tw[3 * (size_t)i + 1] = make_float4(e1y, e1z, e2x, e2y);
+    tw[3 * (size_t)i + 2] = make_float4(e2z, nx, ny, nz);
+    shade[2 * (size_t)i] = make_float4(nx, ny, nz, 0.0f);
+    shade[2 * (size_t)i + 1] = make_float4(rad[3 * (size_t)i], rad[3 * (size_t)i + 1], rad[3 * (size_t)i + 2], 0.0f);
+}
+
+// init_cam_tri_mem_cuda, TD/Trixel.cu:29-36: d_t = cam - p1, d_q = d_t x e1, d_w = d_q . e2
+__global__ void k_cam_tri(const float4* __restrict__ tw, uint32_t ntri, float cx, float cy,
+                          float cz, float4* __restrict__ trec) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ntri) return;
+    const float4 A = tw[3 * (size_t)i], B = tw[3 * (size_t)i + 1], Cq = tw[3 * (size_t)i + 2];
+    const float e1x = A.w, e1y = B.x, e1z = B.y, e2x = B.z, e2y = B.w, e2z = Cq.x;
+    const float dtx = cx - A.x, dty = cy - A.y, dtz = cz - A.z;
+    float qx, qy, qz;
+    cross3(qx, qy, qz, dtx, dty, dtz, e1x, e1y, e1z);
+    const float dw = dot3(qx, qy, qz, e2x, e2y, e2z);
+    trec[4 * (size_t)i] = make_float4(e1x, e1y, e1z, e2x);
+    trec[4 * (size_t)i + 1] = make_float4(e2y, e2z, dtx, dty);
+    trec[4 * (size_t)i + 2] = make_float4(dtz, qx, qy, qz);
+    trec[4 * (size_t)i + 3] = make_float4(dw, 0.0f, 0.0f, 0.0f);
+}
+
+// Camera-relative box of a world node, init_cam_voxel_mem_cuda
+// (TD/Camera.cu:142-147); obj_center is 0 (TD/Camera.cpp:167-170).
+__device__ __forceinline__ void rel_box(const rt_kd_node& nd, float cx, float cy, float cz, float b[6]) {
+    const float oc = 0.0f;
+    b[0] = nd.x0 - cx + oc; b[1] = nd.x1 - cx + oc;
+    b[2] = nd.y0 - cy + oc; b[3] = nd.y1 - cy + oc;
+    b[4] = nd.z0 - cz + oc; b[5] = nd.z1 - cz + oc;
+}
+
+// Split planes minus the camera on the cut axis, TD/Camera.cu:155-160 (the
+// reference's obj_center.x typo on the z term of s2 is kept; it is 0).
+__device__ __forceinline__ void rel_split(const rt_kd_node& nd, float cx, float cy, float cz, float& s1,
+                                          float& s2, uint32_t& axis) {
+    const float ocx = 0.0f, ocy = 0.0f, ocz = 0.0f;
+    const int cd = nd.cut_flag;
+    const float fx = (cd == 0 || cd == 3) ? 1.0f : 0.0f;
+    const float fy = (cd == 1 || cd == 4) ? 1.0f : 0.0f;
+    const float fz = (cd == 2 || cd == 5) ? 1.0f : 0.0f;
+    s1 = nd.s1 - (((cx + ocx) * fx) + ((cy + ocy) * fy) + ((cz + ocz) * fz));
+    s2 = nd.s2 - (((cx + ocx) * fx) + ((cy + ocy) * fy) + ((cz + ocx) * fz));
+    axis = fx != 0.0f ? 0u : fy != 0.0f ? 1u : 2u;
+}
+
+// init_cam_voxel_mem_cuda (TD/Camera.cu:137-162) into the dense interior
+// record layouts of rt_internal.h (v1: own box, 48 B; v2: children's boxes, 64 B).
+__global__ void k_cam_nodes(const rt_kd_node* __restrict__ nodes, const int32_t* __restrict__ ids,
+                            const uint32_t* __restrict__ node_ref, int64_t ninterior, float cx,
+                            float cy, float cz, float4* __restrict__ out, int version) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= ninterior) return;
+    const rt_kd_node nd = nodes[ids[k]];
+    float s1, s2;
+    uint32_t axis;
+    rel_split(nd, cx, cy, cz, s1, s2, axis);
+    if (version == 1) {
+        float b[6];
+        rel_box(nd, cx, cy, cz, b);
+        const float s1e = (float)((double)s1 + kEps);
+        out[3 * k] = make_float4(b[0], b[1], b[2], b[3]);
+        out[3 * k + 1] = make_float4(b[4], b[5], s1, s2);
+        out[3 * k + 2] = make_float4(__uint_as_float(node_ref[nd.left]), __uint_as_float(node_ref[nd.right]),
+                                     __uint_as_float(axis), s1e);
+        return;
+    }
+    float lb[6], rb[6];
+    rel_box(nodes[nd.left], cx, cy, cz, lb);
+    rel_box(nodes[nd.right], cx, cy, cz, rb);
+    out[4 * k] = make_float4(lb[0], lb[1], lb[2], lb[3]);
+    out[4 * k + 1] = make_float4(lb[4], lb[5], rb[0], rb[1]);
+    out[4 * k + 2] = make_float4(rb[2], rb[3], rb[4], rb[5]);
+    out[4 * k + 3] = make_float4(s1, s2, __uint_as_float(node_ref[nd.left] | (axis << kAxisShift)),
+                                 __uint_as_float(node_ref[nd.right]));
+}
+
+// Rank 0's frame assembly after the gather: [rank][slot][8 rows][w] -> frame.
+// Every frame row is one contiguous row of the gathered buffer, so a block
+// copies one row (blockIdx.y) in 16-byte pieces when the rows are 16-byte
+// aligned (w % 4 == 0 and 16-byte aligned buffers: vec), else word by word.
+__global__ void k_unpack(int32_t w, int32_t h, int32_t nranks, int32_t slots, int32_t vec,
+                         const uint32_t* __restrict__ g, uint32_t* __restrict__ frame) {
+    const int32_t y = blockIdx.y;
+    const int32_t band = y / kTileH, r = y - band * kTileH;
+    const int32_t rank = band % nranks, slot = band / nranks;
+    const uint32_t* src = g + (((int64_t)rank * slots + slot) * kTileH + r) * w;
+    uint32_t* dst = frame + (int64_t)y * w;
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (vec) {
+        if (i < (w >> 2)) reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+    } else {
+        for (int32_t k = i; k < w; k += gridDim.x * blockDim.x) dst[k] = src[k];
+    }
+}
+
+// The rectangle gather (rt_frame_rect): outside columns [x0, x1) of bands
+// [b0, b1) every pixel is provably background, so a rank sends only its
+// slots' rows inside the rectangle.  Pack: row (s - s0)*8 + r of the
+// compact buffer <- columns [x0, x1) of packed row s*8 + r.
+__global__ void k_pack_rect(int32_t w, int32_t x0, int32_t cw, int32_t s0, const uint32_t* __restrict__ local,
+                            uint32_t* __restrict__ out) {
+    const int32_t row = blockIdx.y;
+    const int32_t x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= cw) return;
+    const int32_t s = s0 + row / kTileH, r = row - (row / kTileH) * kTileH;
+    out[(int64_t)row * cw + x] = local[((int64_t)s * kTileH + r) * w + x0 + x];
+}
+
+// Rank 0: frame row y (blockIdx.y) from rank 0's own packed buffer, a peer's
+// compact block (peers 1..N-1 back to back), or the background.
+// Each thread writes `vec` (4 or 1) consecutive pixels of the row; rows
+// outside the rectangle are pure background stores.
+__global__ void k_unpack_rect(int32_t w, int32_t nranks, int32_t x0, int32_t x1, int32_t b0, int32_t b1, int32_t vec,
+                              const uint32_t* __restrict__ local0, const uint32_t* __restrict__ peers,
+                              uint32_t* __restrict__ frame) {
+    const int32_t y = blockIdx.y;
+    const int32_t xs = (blockIdx.x * blockDim.x + threadIdx.x) * vec;
+    if (xs >= w) return;
+    const int32_t band = y / kTileH, r = y - band * kTileH;
+    const int32_t rank = band % nranks, slot = band / nranks;
+    uint32_t v0 = kBackground, v1 = kBackground, v2 = kBackground, v3 = kBackground;
+    if (band >= b0 && band < b1 && xs + vec > x0 && xs < x1) {
+        const uint32_t* src;
+        int32_t sx;  // source index of column x: src[x - sx]
+        if (rank == 0) {
+            src = local0 + ((int64_t)slot * kTileH + r) * w;
+            sx = 0;
+        } else {
+            const int32_t cw = x1 - x0;
+            int64_t off = 0;
+            int32_t s0, s1;
+            for (int32_t q = 1; q < rank; q++) {
+                rect_slots(b0, b1, nranks, q, s0, s1);
+                off += (int64_t)(s1 - s0) * kTileH * cw;
+            }
+            rect_slots(b0, b1, nranks, rank, s0, s1);
+            src = peers + off + ((int64_t)(slot - s0) * kTileH + r) * cw;
+            sx = x0;
+        }
+        // straight-line per pixel (an indexed array would live in scratch)
+        if (xs >= x0 && xs < x1) v0 = src[xs - sx];
+        if (vec == 4) {
+            if (xs + 1 >= x0 && xs + 1 < x1) v1 = src[xs + 1 - sx];
+            if (xs + 2 >= x0 && xs + 2 < x1) v2 = src[xs + 2 - sx];
+            if (xs + 3 >= x0 && xs + 3 < x1) v3 = src[xs + 3 - sx];
+        }
+    }
+    uint32_t* dst = frame + (int64_t)y * w + xs;
+    if (vec == 4) {
+        *reinterpret_cast<uint4*>(dst) = make_uint4(v0, v1, v2, v3);
+    } else {
+        dst[0] = v0;
+    }
+}
+
+template <class K>
+int check_launch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(RT_ERR_HIP, "%s launch failed: %s", what, hipGetErrorString(e));
+    return RT_OK;
+}
+
+using TraceFn = void (*)(TraceParams);
+
+template <bool T, bool H, bool C, int S>
+TraceFn kd3_kernel(int rays, bool coarse) {
+    if (coarse) {
+        if (rays == 8) return k_coarse_kd3<8, T, H, C, S>;
+        if (rays == 16) return k_coarse_kd3<16, T, H, C, S>;
+        if (rays == 32) return k_coarse_kd3<32, T, H, C, S>;
+        return k_coarse_kd3<64, T, H, C, S>;
+    }
+    if (rays == 8) return k_trace_kd3<8, T, H, C, S>;
+    if (rays == 16) return k_trace_kd3<16, T, H, C, S>;
+    if (rays == 32) return k_trace_kd3<32, T, H, C, S>;
+    return k_trace_kd3<64, T, H, C, S>;
+}
+
+// shadow: -1 none, else the any-hit push order (0..3), + 4 for counting
+// walks that stop at occluders like a timed frame's (bench.py's roofline).
+// Other counting walks are not cut short, so the order does not change their
+// work: one instance serves them.
+template <bool T, bool H, bool C>
+TraceFn kd_kernel(int version, int rays, int shadow, bool coarse) {
+    if (version == 1) return k_trace_kd<T, H, C>;
+    if (version == 2) return k_trace_kd2<T, H, C>;
+    if (shadow < 0) return kd3_kernel<T, H, C, 0>(rays, coarse);
+    if constexpr (C) {
+        switch (shadow) {
+        case 4: return kd3_kernel<T, H, C, 5>(rays, coarse);
+        case 5: return kd3_kernel<T, H, C, 6>(rays, coarse);
+        case 6: return kd3_kernel<T, H, C, 7>(rays, coarse);
+        case 7: return kd3_kernel<T, H, C, 8>(rays, coarse);
+        default: return kd3_kernel<T, H, C, 1>(rays, coarse);
+        }
+    } else {
+        shadow &= 3;
+        switch (shadow) {
+        case 0: return kd3_kernel<T, H, C, 1>(rays, coarse);
+        case 1: return kd3_kernel<T, H, C, 2>(rays, coarse);
+        case 2: return kd3_kernel<T, H, C, 3>(rays, coarse);
+        default: return kd3_kernel<T, H, C, 4>(rays, coarse);
+        }
+    }
+}
+
+}  // namespace
+}  // namespace rt

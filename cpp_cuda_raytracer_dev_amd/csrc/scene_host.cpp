@@ -7,6 +7,7 @@
 // comparison sorts with the merge sort's tie order, and the per-level
 // partitions run in parallel because sibling ranges are disjoint.
 #include <math.h>
+#include <sched.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -57,9 +58,21 @@ void parallel_for(int64_t n, int threads, F&& body) {
     for (auto& th : pool) th.join();
 }
 
+// nthreads <= 0: the CPUs this process may run on (its affinity mask, and
+// OMP_NUM_THREADS when set lower), at most 64.  hardware_concurrency() counts
+// the whole machine, which oversubscribes a container's CPU share.
 int resolve_threads(int nthreads) {
     if (nthreads > 0) return nthreads;
     unsigned hc = std::thread::hardware_concurrency();
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) == 0) {
+        const int c = CPU_COUNT(&set);
+        if (c > 0) hc = std::min(hc ? hc : (unsigned)c, (unsigned)c);
+    }
+    if (const char* e = getenv("OMP_NUM_THREADS")) {
+        const int v = atoi(e);
+        if (v > 0) hc = std::min(hc ? hc : (unsigned)v, (unsigned)v);
+    }
     return hc ? (int)std::min(hc, 64u) : 4;
 }
 
