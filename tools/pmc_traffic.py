@@ -47,6 +47,24 @@ def main():
     if "TCC_HIT_sum" in counters and "TCC_MISS_sum" in counters:
         h, m = counters["TCC_HIT_sum"], counters["TCC_MISS_sum"]
         entry["l2_hit_rate"] = h / (h + m) if h + m else None
+    c = counters
+    if c.get("SQ_WAVE_CYCLES"):
+        wc = c["SQ_WAVE_CYCLES"]
+        # share of the waves' lifetime: waiting on anything, waiting for an
+        # instruction's operands, issuing (any, VALU, LDS, scalar)
+        entry["wave_time_split"] = {k: round(c[n] / wc, 4) for k, n in (
+            ("wait_any", "SQ_WAIT_ANY"), ("wait_inst_any", "SQ_WAIT_INST_ANY"), ("active_any", "SQ_ACTIVE_INST_ANY"),
+            ("active_valu", "SQ_ACTIVE_INST_VALU"), ("active_lds", "SQ_ACTIVE_INST_LDS"),
+            ("wait_inst_lds", "SQ_WAIT_INST_LDS"), ("active_scalar", "SQ_ACTIVE_INST_SCA")) if n in c}
+    if c.get("TCP_TCC_READ_REQ_sum"):
+        entry["l1_miss_latency_cycles"] = c.get("TCP_TCC_READ_REQ_LATENCY_sum", 0.0) / c["TCP_TCC_READ_REQ_sum"]
+        if c.get("TCP_TOTAL_CACHE_ACCESSES_sum"):
+            entry["l1_miss_rate"] = c["TCP_TCC_READ_REQ_sum"] / c["TCP_TOTAL_CACHE_ACCESSES_sum"]
+    if c.get("SQ_WAVES"):
+        entry["per_wave"] = {k: round(c[n] / c["SQ_WAVES"], 2) for k, n in (
+            ("valu_insts", "SQ_INSTS_VALU"), ("lds_insts", "SQ_INSTS_LDS"), ("salu_insts", "SQ_INSTS_SALU"),
+            ("vmem_rd_insts", "SQ_INSTS_VMEM_RD"), ("branch_insts", "SQ_INSTS_BRANCH"),
+            ("lds_bank_conflict_cycles", "SQ_LDS_BANK_CONFLICT")) if n in c}
     data[key] = entry
     json.dump(data, open(out_path, "w"), indent=1, sort_keys=True)
     print(json.dumps({key: entry}))
