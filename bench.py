@@ -78,6 +78,9 @@ def parse():
     ap.add_argument("--rehearse-gather", action="store_true",
                     help="one process: run the N>1 frame loop (process group, gather, frame check) with one rank, "
                          "to rehearse the multi-GPU path on a one-GPU machine; not a bench line")
+    ap.add_argument("--loop", default="native", choices=["native", "python"],
+                    help="frame loop: native = rt_run_frames (C++, the render + RCCL gather enqueued per frame "
+                         "without Python), python = the same calls from Python (torch collectives, --animate)")
     ap.add_argument("--pipeline", type=int, default=2,
                     help="rccl: buffer sets in flight (frame i+1 renders while frame i is gathered)")
     ap.add_argument("--kernel", type=int, default=3,
@@ -455,81 +458,143 @@ def main():
     my_pix = int(np.count_nonzero(np.repeat(np.arange((h + 7) // 8) % world == rank, 8)[:h])) * w
     bytes_per_launch = B_INT * int(cnt[0]) + B_LEAF * int(cnt[1]) + B_HIT * int(cnt[2]) + B_PIX * my_pix
 
-    ng = None
-    if multi and a.collective == "rccl":
-        fg = None
-        ng = NativeFrameGather(dist, w, h, dev, nbuf=max(1, a.pipeline))
-        nbuf = len(ng.local)
-        cstream = torch.cuda.Stream(device=dev)
-        rendered = [torch.cuda.Event() for _ in range(nbuf)]
-        sent = [torch.cuda.Event() for _ in range(nbuf)]
-        for k in range(nbuf):
-            sent[k].record(cstream)
-        out = ng.local[0]
-    elif multi:
-        def unpack(g, f):
-            R.unpack_bands(local, w, h, world, g, f, stream=torch.cuda.current_stream(dev).cuda_stream)
-        fg = FrameGather(dist, w, h, dev, a.collective, unpack=unpack)
-        out = fg.local
-    else:
-        fg = None
-        out = torch.zeros(w * h, dtype=torch.int32, device=dev)
-
     if a.event_every <= 0:
         a.event_every = 8 if multi else 1
-    timed_frames = list(range(0, a.steps, max(1, a.event_every)))
-    ev = {i: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for i in timed_frames}
+    collective = a.collective
+    loop_kind = a.loop if not masks else "python"  # a moving object ticks per frame in Python
+    gather_note = None
 
-    tick = [0]
-    seq = [0]
+    def make_gather(kind):
+        """(NativeFrameGather or None, FrameGather or None, render target)."""
+        if multi and kind == "rccl":
+            g = NativeFrameGather(dist, w, h, dev, nbuf=max(1, min(a.pipeline, 4)))
+            # every rank must derive the same rectangle and options, or the
+            # receive sizes would not match the sends (ADVICE r01)
+            g.verify(cam, xf, a.mode)
+            return g, None, g.local[0]
+        if multi:
+            def unpack(g, f):
+                R.unpack_bands(local, w, h, world, g, f, stream=torch.cuda.current_stream(dev).cuda_stream)
+            f = FrameGather(dist, w, h, dev, kind, unpack=unpack)
+            return None, f, f.local
+        return None, None, torch.zeros(w * h, dtype=torch.int32, device=dev)
 
-    def frame(i=None):
-        nonlocal xf
-        if masks:  # one input tick, then the frame at the new pose
-            obj.key_tick(masks[tick[0] % len(masks)])
-            tick[0] += 1
-            xf = obj.quat.xform()
-        if ng is not None:
-            # frame j renders into buffer set j % nbuf once the gather that
-            # last read it is done, then is gathered on the comm stream while
-            # frame j + 1 renders
-            k = seq[0] % nbuf
-            seq[0] += 1
-            stream.wait_event(sent[k])
-            if i in ev:
-                ev[i][0].record(stream)
-            cam.render_into(ng.local[k], xform=xf, mode=a.mode, flags=sflag, tile=tile, stream=sptr)
-            if i in ev:
-                ev[i][1].record(stream)
-            rendered[k].record(stream)
-            cstream.wait_event(rendered[k])
-            ng.gather(k, cam, xf, a.mode, cstream.cuda_stream)
-            sent[k].record(cstream)
-            return
-        with torch.cuda.stream(stream):
-            if i in ev:
-                ev[i][0].record(stream)
-            cam.render_into(out, xform=xf, mode=a.mode, flags=sflag, tile=tile if multi else None,
-                            stream=sptr)
-            if i in ev:
-                ev[i][1].record(stream)
-            if fg is not None:
-                fg.gather()
+    ng, fg, out = make_gather(collective)
+    cstream = torch.cuda.Stream(device=dev) if ng is not None else None
 
-    for _ in range(a.warmup):
-        frame()
+    def gathered_frame_ok(loop):
+        """Rank 0's last gathered frame against a full frame rendered here (untimed),
+        the verdict shared with every rank."""
+        ok = torch.ones(1, dtype=torch.int64, device=dev)
+        if rank == 0:
+            got = ng.frames[loop.last_set()] if ng is not None else fg.frame
+            full = torch.zeros(w * h, dtype=torch.int32, device=dev)
+            cam.render_into(full, xform=xf, mode=a.mode, flags=sflag, stream=sptr)
+            torch.cuda.synchronize(dev)
+            ok[0] = int(torch.equal(got, full))
+        dist.broadcast(ok, src=0)
+        return bool(ok[0])
+
+    class PyLoop:
+        """The frame loop in Python (torch collectives, --animate, --loop python)."""
+
+        def __init__(self):
+            self.seq = 0
+            self.tick = 0
+            self.nbuf = len(ng.local) if ng is not None else 1
+            if ng is not None:
+                self.rendered = [torch.cuda.Event() for _ in range(self.nbuf)]
+                self.sent = [torch.cuda.Event() for _ in range(self.nbuf)]
+                for k in range(self.nbuf):
+                    self.sent[k].record(cstream)
+
+        def last_set(self):
+            return (self.seq - 1) % self.nbuf
+
+        def frame(self, timed):
+            nonlocal xf
+            if masks:  # one input tick, then the frame at the new pose
+                obj.key_tick(masks[self.tick % len(masks)])
+                self.tick += 1
+                xf = obj.quat.xform()
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if timed else None
+            if ng is not None:
+                # frame j renders into buffer set j % nbuf once the gather that
+                # last read it is done, then is gathered on the comm stream
+                # while frame j + 1 renders
+                k = self.seq % self.nbuf
+                self.seq += 1
+                stream.wait_event(self.sent[k])
+                if ev:
+                    ev[0].record(stream)
+                cam.render_into(ng.local[k], xform=xf, mode=a.mode, flags=sflag, tile=tile, stream=sptr)
+                if ev:
+                    ev[1].record(stream)
+                self.rendered[k].record(stream)
+                cstream.wait_event(self.rendered[k])
+                ng.gather(k, cam, xf, a.mode, cstream.cuda_stream)
+                self.sent[k].record(cstream)
+                return ev
+            self.seq += 1
+            with torch.cuda.stream(stream):
+                if ev:
+                    ev[0].record(stream)
+                cam.render_into(out, xform=xf, mode=a.mode, flags=sflag, tile=tile if multi else None, stream=sptr)
+                if ev:
+                    ev[1].record(stream)
+                if fg is not None:
+                    fg.gather()
+            return ev
+
+        def run(self, n, time_frames):
+            evs = []
+            h0 = time.perf_counter()
+            for i in range(n):
+                e = self.frame(time_frames and i % a.event_every == 0)
+                if e:
+                    evs.append(e)
+            host_ms = 1e3 * (time.perf_counter() - h0)
+            torch.cuda.synchronize(dev)
+            ms = [s0.elapsed_time(s1) for s0, s1 in evs]
+            return (float(np.mean(ms)) if ms else 0.0), len(ms), host_ms
+
+    def make_loop():
+        if loop_kind == "native" and (not multi or ng is not None):
+            return R.FrameLoop(cam, ng.local if ng is not None else [out], xform=xf, mode=a.mode, flags=sflag,
+                               tile=tile if multi else None, render_stream=sptr, comm=ng,
+                               comm_stream=cstream.cuda_stream if ng is not None else None,
+                               event_every=a.event_every)
+        return PyLoop()
+
+    loop = make_loop()
+    loop.run(a.warmup, False) if isinstance(loop, PyLoop) else loop.run(a.warmup)
     torch.cuda.synchronize(dev)
+    if multi and ng is not None and not gathered_frame_ok(loop):
+        # the library's RCCL path has not been seen to work at N > 1 before
+        # (ADVICE r01): on a wrong warm-up frame every rank falls back to
+        # torch.distributed.gather and the line says so
+        gather_note = "rccl warm-up frame differed from the single-GPU frame; fell back to torch gather"
+        ng.close()
+        collective = "gather"
+        ng, fg, out = make_gather(collective)
+        cstream = None
+        loop = PyLoop()
+        loop.run(a.warmup, False)
+        torch.cuda.synchronize(dev)
     if multi:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for i in range(a.steps):
-        frame(i)
+    if isinstance(loop, PyLoop):
+        kern_ms, n_ev, host_ms = loop.run(a.steps, True)
+    else:
+        kern_ms, n_ev, host_ms = loop.run(a.steps)
     torch.cuda.synchronize(dev)
     if multi:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    host_us_per_frame = 1e3 * host_ms / max(1, a.steps)
     # the device error word of this rank's timed frames (stack / pool
     # overflow, a far-group proof that failed): reported, and fatal below
     dev_err = cam.device_error(reset=True)
@@ -537,15 +602,12 @@ def main():
     if not multi and rank == 0:
         frame_check = frame_check_n1(out.cpu().numpy().view(np.uint32), pts, nodes, cam_kw, a,
                                      xform=xf if masks else None)
-    if multi and rank == 0:
-        # the last gathered frame against a full frame rendered here (untimed)
-        got = ng.frames[(seq[0] - 1) % nbuf] if ng is not None else fg.frame
-        full = torch.zeros(w * h, dtype=torch.int32, device=dev)
-        cam.render_into(full, xform=xf, mode=a.mode, flags=sflag, stream=sptr)
-        torch.cuda.synchronize(dev)
-        frame_check = {"gathered_equals_single_gpu_frame": bool(torch.equal(got, full)),
-                       "collective": a.collective + (f", {nbuf} buffer sets" if ng is not None else "")}
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev.values()]))
+    if multi:
+        ok = gathered_frame_ok(loop)
+        if rank == 0:
+            frame_check = {"gathered_equals_single_gpu_frame": ok,
+                           "collective": collective + (f", {len(ng.local)} buffer sets" if ng is not None else ""),
+                           **({"note": gather_note} if gather_note else {})}
     full_walk = None
     if a.shadow and not masks:
         # shadow walks stop at their first occluder; the counting frame above
@@ -618,8 +680,8 @@ def main():
                 "resolution": [w, h],
                 "view": {"name": a.view, **cam_kw},
                 "coverage": round(hits_all / (w * h), 5),
-                "parallelism": f"screen bands x{world}" + ((" + RCCL send/recv to rank 0, pipelined" if a.collective == "rccl"
-                                                         else f" + torch {a.collective} to rank 0") if multi else ""),
+                "parallelism": f"screen bands x{world}" + ((" + RCCL send/recv to rank 0, pipelined" if collective == "rccl"
+                                                         else f" + torch {collective} to rank 0") if multi else ""),
             },
             "roofline": ({
                 "bound": "valu",
@@ -631,7 +693,7 @@ def main():
                 "kernel": "k_trace_flat",
                 "kernel_form": cam.get_option(_lib.RT_OPT_FLAT),
                 "kernel_ms_avg": round(kern_ms, 5),
-                "kernel_ms_frames": f"{len(ev)} of {a.steps} timed frames (every {max(1, a.event_every)})",
+                "kernel_ms_frames": f"{n_ev} of {a.steps} timed frames (every {max(1, a.event_every)})",
                 "kernel_ms_avg_max_rank": round(kern_ms_max, 5),
                 "tests_per_launch": tests,
                 "flops_per_launch": FLOPS_PER_TEST * tests,
@@ -662,7 +724,7 @@ def main():
                                        "shadow_push_order_mode": "timed" if a.shadow_order < 0 else "fixed"}
                                       if a.shadow else {})},
                 "kernel_ms_avg": round(kern_ms, 5),
-                "kernel_ms_frames": f"{len(ev)} of {a.steps} timed frames (every {max(1, a.event_every)})",
+                "kernel_ms_frames": f"{n_ev} of {a.steps} timed frames (every {max(1, a.event_every)})",
                 "kernel_ms_avg_max_rank": round(kern_ms_max, 5),
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "counts_per_launch": {"interior": int(cnt[0]), "leaf": int(cnt[1]), "accept": int(cnt[2]),
@@ -672,6 +734,9 @@ def main():
                 "bytes_model": "36*V_int + 40*V_leaf + 24*H + 4*P (SURVEY.md 8d)",
             }),
             "device_err": errs if multi else dev_err,
+            "host": {"us_per_frame": round(host_us_per_frame, 2), "loop": "native (rt_run_frames)"
+                     if not isinstance(loop, PyLoop) else "python",
+                     "what": "host time spent enqueueing the timed frames / steps (rank 0)"},
             "kd_build": build_times,
         }
         if frame_check is not None:

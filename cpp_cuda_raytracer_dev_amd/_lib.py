@@ -57,6 +57,16 @@ class RtTile(C.Structure):
     _fields_ = [("nranks", C.c_int32), ("rank", C.c_int32)]
 
 
+RT_LOOP_MAX_BUF = 4
+
+
+class RtFrameLoop(C.Structure):
+    _fields_ = [("xform", C.c_void_p), ("mode", C.c_uint32), ("flags", C.c_uint32), ("tile", RtTile),
+                ("nbuf", C.c_int32), ("d_local", C.c_void_p * RT_LOOP_MAX_BUF),
+                ("d_scratch", C.c_void_p * RT_LOOP_MAX_BUF), ("d_frame", C.c_void_p * RT_LOOP_MAX_BUF),
+                ("render_stream", C.c_void_p), ("comm_stream", C.c_void_p), ("event_every", C.c_int32)]
+
+
 class RtError(RuntimeError):
     def __init__(self, fn: str, code: int, msg: str):
         super().__init__(f"{fn} failed ({code}): {msg}")
@@ -99,6 +109,8 @@ SIGNATURES = {
     "rt_unpack_rect": (C.c_int, [C.c_int, C.c_int32, C.c_int32, C.c_int32, _P, _P, _P, _P, _P]),
     "rt_comm_info": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "rt_comm_destroy": (None, [_P]),
+    "rt_run_frames": (C.c_int, [_P, _P, C.POINTER(RtFrameLoop), C.c_int32, C.POINTER(C.c_int64),
+                                C.POINTER(C.c_double), C.POINTER(C.c_int32), C.POINTER(C.c_double)]),
     "rt_read_frame": (C.c_int, [_P, _P, _P]),
     "rt_camera_counters": (C.c_int, [_P, _P, C.c_int]),
     "rt_pinned_alloc": (C.c_int, [C.c_size_t, C.POINTER(_P)]),

@@ -9,6 +9,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <vector>
 
 #include "rt_internal.h"
@@ -97,6 +98,31 @@ struct rt_camera {
     int tune_frames = 0;             // frames since the last round's result
     bool tune_pending = false;
     hipEvent_t tune_ev[2 * 12] = {};
+    // Frame loops render the same (transform, tile, buffers) frame after
+    // frame: its launch geometry is kept and reused while nothing it depends
+    // on changed (options, object, tree: geom_gen / tree_version).
+    uint64_t geom_gen = 1;
+    struct ParamCache {
+        bool valid = false;
+        uint64_t gen = 0, tree = 0;
+        float xf[12];
+        uint32_t mode = 0;
+        int32_t nranks = 0, rank = 0;
+        uint32_t* argb = nullptr;
+        int64_t* hit = nullptr;
+        TraceParams p;
+    } pcache;
+    // rt_run_frames: events kept across calls (the timed call reuses the
+    // warm-up call's), pairs bracketing sampled frames' renders
+    std::vector<hipEvent_t> loop_ev;
+    struct RectCache {
+        bool valid = false;
+        uint64_t gen = 0, tree = 0;
+        float xf[12];
+        uint32_t mode = 0;
+        int32_t nranks = 0;
+        int32_t rect[4];
+    } rcache;
 };
 
 namespace {
@@ -935,6 +961,7 @@ extern "C" int rt_camera_add_object(rt_camera* c, rt_scene* s) {
     DeviceGuard g(c->device);
     c->obj = s;
     c->prepared_version = 0;
+    c->geom_gen++;
     return prepare_camera_object(c);
 }
 
@@ -1026,8 +1053,27 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
             return fail(RT_ERR_STATE, "rt_render: shadow rays run in the wave-cooperative kernel (3); kernel %d",
                         effective_kernel(c));
     }
+    static const float ident[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+    const float* xf = xform ? xform : ident;
+    const int32_t nr = tile ? tile->nranks : 1, rk = tile ? tile->rank : 0;
+    auto& pc = c->pcache;
     TraceParams p;
-    if ((rc = fill_params(c, xform, tile, argb, hit, mode, p))) return rc;
+    if (pc.valid && !(c->debug & 2) && pc.gen == c->geom_gen && pc.tree == c->obj->tree_version && pc.mode == mode &&
+        pc.nranks == nr && pc.rank == rk && pc.argb == argb && pc.hit == hit && !memcmp(pc.xf, xf, sizeof pc.xf)) {
+        p = pc.p;  // the same frame as the last one: its geometry stands
+    } else {
+        if ((rc = fill_params(c, xform, tile, argb, hit, mode, p))) return rc;
+        pc.valid = !(c->debug & 2);
+        pc.gen = c->geom_gen;
+        pc.tree = c->obj->tree_version;
+        memcpy(pc.xf, xf, sizeof pc.xf);
+        pc.mode = mode;
+        pc.nranks = nr;
+        pc.rank = rk;
+        pc.argb = argb;
+        pc.hit = hit;
+        pc.p = p;
+    }
     if (mode == RT_MODE_KD && effective_kernel(c) == 3) c->last_rays = p.rays;
     int trial;
     p.any_order = any_order_for(c, flags, stream, trial) | ((c->debug & 16) ? 4 : 0);
@@ -1068,12 +1114,35 @@ extern "C" int rt_unpack_bands(int device, int32_t w, int32_t h, int32_t nranks,
     return launch_unpack(w, h, nranks, d_gathered, d_frame, stream);
 }
 
+static int frame_rect_uncached(rt_camera* c, const float* xform, uint32_t mode, int32_t nranks, int32_t rect[4]);
+
 extern "C" int rt_frame_rect(rt_camera* c, const float* xform, uint32_t mode, int32_t nranks, int32_t rect[4]) {
     if (!c || !rect || nranks < 1) return fail(RT_ERR_INVALID, "rt_frame_rect: bad argument");
     if (mode != RT_MODE_KD && mode != RT_MODE_FLAT) return fail(RT_ERR_INVALID, "rt_frame_rect: mode %u", mode);
     DeviceGuard g(c->device);
     int rc;
     if ((rc = prepare_camera_object(c))) return rc;
+    static const float ident[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+    const float* xf = xform ? xform : ident;
+    auto& rcx = c->rcache;
+    if (rcx.valid && rcx.gen == c->geom_gen && rcx.tree == c->obj->tree_version && rcx.mode == mode &&
+        rcx.nranks == nranks && !memcmp(rcx.xf, xf, sizeof rcx.xf)) {
+        memcpy(rect, rcx.rect, sizeof rcx.rect);
+        return RT_OK;
+    }
+    rc = frame_rect_uncached(c, xform, mode, nranks, rect);
+    if (rc) return rc;
+    rcx.valid = true;
+    rcx.gen = c->geom_gen;
+    rcx.tree = c->obj->tree_version;
+    memcpy(rcx.xf, xf, sizeof rcx.xf);
+    rcx.mode = mode;
+    rcx.nranks = nranks;
+    memcpy(rcx.rect, rect, sizeof rcx.rect);
+    return RT_OK;
+}
+
+static int frame_rect_uncached(rt_camera* c, const float* xform, uint32_t mode, int32_t nranks, int32_t rect[4]) {
     const int32_t nbands = (c->h + kTileH - 1) / kTileH;
     rect[0] = 0; rect[1] = c->w; rect[2] = 0; rect[3] = nbands;  // no proof: the whole frame
     if (mode != RT_MODE_KD || !c->obj->d_nodes) return RT_OK;
@@ -1228,12 +1297,15 @@ extern "C" void rt_camera_destroy(rt_camera* c) {
     if (c->order_ev) (void)hipEventDestroy(c->order_ev);
     if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
     if (c->join_ev) (void)hipEventDestroy(c->join_ev);
+    for (hipEvent_t e : c->loop_ev)
+        if (e) (void)hipEventDestroy(e);
     if (c->side) (void)hipStreamDestroy(c->side);
     delete c;
 }
 
 extern "C" int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value) {
     if (!c) return fail(RT_ERR_INVALID, "rt_camera_set_option: null camera");
+    c->geom_gen++;  // cached launch geometry is stale
     switch (key) {
     case kOptKernel:
         if (value < 1 || value > 3) return fail(RT_ERR_INVALID, "kernel version %d", value);
@@ -1291,6 +1363,7 @@ extern "C" int rt_camera_get_option(const rt_camera* c, int32_t key, int32_t* va
     case kOptCoarse: *value = c->coarse; return RT_OK;
     case kOptFlat: *value = c->flat_variant; return RT_OK;
     case kOptRaysUsed: *value = c->last_rays; return RT_OK;
+    case kOptDebug: *value = c->debug; return RT_OK;
     case kOptShadowOrder: *value = c->shadow_order >= 0 ? c->shadow_order : c->any_best; return RT_OK;
     default: return fail(RT_ERR_INVALID, "rt_camera_get_option: unknown key %d", key);
     }
@@ -1315,4 +1388,86 @@ extern "C" int64_t rt_camera_debug_read(rt_camera* c, uint64_t* out, int64_t n) 
         hip_check(hipMemcpy(out, c->d_dbg, sizeof(uint64_t) * (size_t)m, hipMemcpyDeviceToHost), "D2H dbg"))
         return RT_ERR_HIP;
     return m;
+}
+
+// The frame loop in native code (bench.py, a headless viewer): per frame one
+// render into buffer set k = seq % nbuf and, with a communicator, its gather
+// on the comm stream while the next frame renders; a buffer set is reused
+// only after its gather has read it (events).  The host work per frame is the
+// cached launch (render_common) plus, with comm, the cached-rectangle gather:
+// a Python loop around the same calls costs tens of microseconds per frame.
+extern "C" int rt_run_frames(rt_camera* c, rt_comm* comm, const rt_frame_loop* a, int32_t nframes, int64_t* seq,
+                             double* kernel_ms_avg, int32_t* kernel_ms_frames, double* host_ms) {
+    if (!c || !a || !seq || nframes < 0 || a->nbuf < 1 || a->nbuf > RT_LOOP_MAX_BUF)
+        return fail(RT_ERR_INVALID, "rt_run_frames: bad argument");
+    for (int k = 0; k < a->nbuf; k++)
+        if (!a->d_local[k] || (comm && (!a->d_scratch[k] || !a->comm_stream)))
+            return fail(RT_ERR_INVALID, "rt_run_frames: missing buffer of set %d", k);
+    DeviceGuard g(c->device);
+    hipStream_t rs = (hipStream_t)a->render_stream, cs = (hipStream_t)a->comm_stream;
+    int rc;
+    hipEvent_t rendered[RT_LOOP_MAX_BUF] = {}, sent[RT_LOOP_MAX_BUF] = {};
+    auto cleanup = [&]() {
+        for (int k = 0; k < RT_LOOP_MAX_BUF; k++) {
+            if (rendered[k]) (void)hipEventDestroy(rendered[k]);
+            if (sent[k]) (void)hipEventDestroy(sent[k]);
+        }
+    };
+    for (int k = 0; k < a->nbuf && comm; k++) {
+        if ((rc = hip_check(hipEventCreateWithFlags(&rendered[k], hipEventDisableTiming), "loop event")) ||
+            (rc = hip_check(hipEventCreateWithFlags(&sent[k], hipEventDisableTiming), "loop event"))) {
+            cleanup();
+            return rc;
+        }
+    }
+    const int every = a->event_every;
+    const int64_t ntimed = every > 0 ? (nframes + every - 1) / every : 0;
+    while ((int64_t)c->loop_ev.size() < 2 * ntimed) {
+        hipEvent_t e = nullptr;
+        if ((rc = hip_check(hipEventCreate(&e), "loop timing event"))) {
+            cleanup();
+            return rc;
+        }
+        c->loop_ev.push_back(e);
+    }
+    const rt_tile* tile = a->tile.nranks > 0 ? &a->tile : nullptr;
+    const auto h0 = std::chrono::steady_clock::now();
+    for (int32_t j = 0; j < nframes; j++) {
+        const int k = (int)((*seq) % a->nbuf);
+        ++*seq;
+        const bool timed = every > 0 && j % every == 0;
+        const int64_t t = every > 0 ? j / every : 0;
+        rc = timed ? hip_check(hipEventRecord(c->loop_ev[(size_t)(2 * t)], rs), "loop timing") : RT_OK;
+        if (!rc) rc = render_common(c, a->xform, a->mode, a->flags, tile, a->d_local[k], nullptr, a->render_stream);
+        if (!rc && timed) rc = hip_check(hipEventRecord(c->loop_ev[(size_t)(2 * t + 1)], rs), "loop timing");
+        if (!rc && comm) {
+            // frame j renders into set k once the gather that last read it is done
+            if ((rc = hip_check(hipEventRecord(rendered[k], rs), "rendered")) ||
+                (rc = hip_check(hipStreamWaitEvent(cs, rendered[k], 0), "comm wait")) ||
+                (rc = rt_comm_gather_frame(comm, c, a->xform, a->mode, a->d_local[k], a->d_scratch[k], a->d_frame[k],
+                                           a->comm_stream)) ||
+                (rc = hip_check(hipEventRecord(sent[k], cs), "sent")))
+                break;
+            const int kn = (int)((*seq) % a->nbuf);
+            rc = hip_check(hipStreamWaitEvent(rs, sent[kn], 0), "render wait");
+        }
+        if (rc) break;
+    }
+    if (host_ms) *host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
+    if (!rc) rc = hip_check(hipStreamSynchronize(rs), "loop sync");
+    if (!rc && comm) rc = hip_check(hipStreamSynchronize(cs), "loop sync");
+    cleanup();
+    if (rc) return rc;
+    double sum = 0.0;
+    int32_t cnt = 0;
+    for (int64_t t = 0; t < ntimed; t++) {
+        float ms = 0.0f;
+        if (hipEventElapsedTime(&ms, c->loop_ev[(size_t)(2 * t)], c->loop_ev[(size_t)(2 * t + 1)]) == hipSuccess) {
+            sum += ms;
+            cnt++;
+        }
+    }
+    if (kernel_ms_avg) *kernel_ms_avg = cnt ? sum / cnt : 0.0;
+    if (kernel_ms_frames) *kernel_ms_frames = cnt;
+    return RT_OK;
 }

@@ -136,6 +136,23 @@ class NativeFrameGather:
         _lib.call("rt_comm_gather_frame", self._h, cam._h, _lib.ptr(xf), mode, _lib.ptr(self.local[k]),
                   _lib.ptr(self.scratch[k]), _lib.ptr(f) if f is not None else None, stream or None)
 
+    def verify(self, cam, xform, mode: int) -> tuple:
+        """Every rank must derive the same rectangle (rt_frame_rect) and render
+        with the same options, or rank 0's receive sizes would not match the
+        peers' sends (RCCL would hang or truncate instead of failing).  All
+        ranks exchange theirs (over `dist`) and raise if any differs.  Returns
+        the rectangle."""
+        from . import _lib
+        rect = self.frame_rect(cam, xform, mode)
+        opts = tuple(cam.get_option(k) for k in (_lib.RT_OPT_KERNEL, _lib.RT_OPT_RAYS, _lib.RT_OPT_COARSE,
+                                                 _lib.RT_OPT_DEBUG, _lib.RT_OPT_TILE_ORDER))
+        mine = (rect, opts, (self.w, self.h), int(mode))
+        every = [None] * self.world
+        self.dist.all_gather_object(every, mine)
+        if any(e != every[0] for e in every):
+            raise RuntimeError(f"NativeFrameGather: ranks disagree on the frame rectangle / camera options: {every}")
+        return rect
+
     def frame_rect(self, cam, xform, mode: int):
         """rt_frame_rect for this group's size: (x0, x1, b0, b1)."""
         import numpy as np

@@ -395,6 +395,51 @@ class Camera:
             pass
 
 
+class FrameLoop:
+    """rt_run_frames: the frame loop in native code.  `locals_` are the
+    render targets (one per buffer set); with `comm` (a NativeFrameGather),
+    each frame is gathered to rank 0 on `comm_stream` while the next renders.
+    ``run(n)`` renders n frames and returns (kernel ms mean, timed frames);
+    it synchronises the streams before returning."""
+
+    def __init__(self, cam: "Camera", locals_, xform=None, mode: int = RT_MODE_KD, flags: int = 0, tile=None,
+                 render_stream=None, comm=None, comm_stream=None, event_every: int = 0):
+        n = len(locals_)
+        if not 1 <= n <= _lib.RT_LOOP_MAX_BUF:
+            raise ValueError(f"FrameLoop: 1..{_lib.RT_LOOP_MAX_BUF} buffer sets")
+        self.cam = cam
+        self.comm = comm
+        self._xf = np.ascontiguousarray(xform if xform is not None else Quaternion().xform(), np.float32)
+        a = _lib.RtFrameLoop()
+        a.xform = self._xf.ctypes.data
+        a.mode, a.flags = mode, flags
+        a.tile = _lib.RtTile(*(tile if tile is not None else (0, 0)))
+        a.nbuf = n
+        for k in range(n):
+            a.d_local[k] = _lib.ptr(locals_[k]).value
+            if comm is not None:
+                a.d_scratch[k] = _lib.ptr(comm.scratch[k]).value
+                f = comm.frames[k]
+                a.d_frame[k] = _lib.ptr(f).value if f is not None else None
+        a.render_stream = render_stream
+        a.comm_stream = comm_stream
+        a.event_every = event_every
+        self._a = a
+        self._locals = list(locals_)
+        self.seq = C.c_int64(0)
+
+    def run(self, nframes: int):
+        """-> (kernel ms mean over the timed frames, timed frames, host ms spent enqueueing)."""
+        ms, cnt, host = C.c_double(), C.c_int32(), C.c_double()
+        _lib.call("rt_run_frames", self.cam._h, self.comm._h if self.comm is not None else None, C.byref(self._a),
+                  int(nframes), C.byref(self.seq), C.byref(ms), C.byref(cnt), C.byref(host))
+        return ms.value, cnt.value, host.value
+
+    def last_set(self) -> int:
+        """The buffer set the last frame used."""
+        return (self.seq.value - 1) % self._a.nbuf
+
+
 def packed_pixels(w: int, h: int, nranks: int) -> int:
     return int(_lib.lib().rt_tile_packed_pixels(w, h, nranks))
 

@@ -202,8 +202,12 @@ int rt_unpack_bands(int device, int32_t w, int32_t h, int32_t nranks,
  * into d_scratch (rt_tile_packed_pixels u32) and send it to rank 0; rank 0
  * receives the peers' parts into d_scratch ((N-1) * rt_tile_packed_pixels
  * u32) and assembles d_frame (w*h) from them, its own d_local and the
- * background.  Every rank must call it once per frame.  RCCL is loaded at
- * run time (librccl.so.1); rt_comm_available() says whether it was found. */
+ * background.  Every rank must call it once per frame, with a camera of the
+ * same resolution and options on every rank (message sizes are derived, not
+ * exchanged; distributed.NativeFrameGather.verify checks this once).  A rank
+ * with no part in the rectangle sends nothing, and rank 0 posts no receive
+ * for it.  RCCL is loaded at run time (librccl.so.1); rt_comm_available()
+ * says whether it was found. */
 #define RT_COMM_ID_BYTES 128
 typedef struct rt_comm rt_comm;
 int rt_comm_available(void);
@@ -230,6 +234,32 @@ int rt_unpack_rect(int device, int32_t w, int32_t h, int32_t nranks, const int32
                    const uint32_t* d_local0, const uint32_t* d_peers, uint32_t* d_frame, void* stream);
 int rt_comm_info(const rt_comm* c, int32_t* nranks, int32_t* rank);
 void rt_comm_destroy(rt_comm* c);
+
+/* A native frame loop (the headless replacement of WinMain's loop,
+ * TD/WinMain.cpp:174-239, without the window): nframes frames of `cam` into
+ * buffer set k = (*seq)++ % nbuf, each frame's render on render_stream and,
+ * when comm is non-NULL, its rt_comm_gather_frame on comm_stream while the
+ * next frame renders (a set is reused once its gather has read it).  With
+ * event_every > 0 every event_every-th frame's render is bracketed by HIP
+ * events on render_stream; *kernel_ms_avg / *kernel_ms_frames receive their
+ * mean and count; *host_ms (may be NULL) the host time spent enqueueing the
+ * frames.  Synchronises both streams before returning.  tile.nranks 0 (or
+ * 1) renders the whole frame. */
+#define RT_LOOP_MAX_BUF 4
+typedef struct rt_frame_loop {
+    const float* xform;
+    uint32_t mode, flags;
+    rt_tile tile;
+    int32_t nbuf;
+    uint32_t* d_local[RT_LOOP_MAX_BUF];
+    uint32_t* d_scratch[RT_LOOP_MAX_BUF];
+    uint32_t* d_frame[RT_LOOP_MAX_BUF];
+    void* render_stream;
+    void* comm_stream;
+    int32_t event_every;
+} rt_frame_loop;
+int rt_run_frames(rt_camera* cam, rt_comm* comm, const rt_frame_loop* loop, int32_t nframes, int64_t* seq,
+                  double* kernel_ms_avg, int32_t* kernel_ms_frames, double* host_ms);
 
 /* The D2H copy of color_camera_device (TD/Camera.cu:84) and d_rmi.index.
  * Synchronises the device.  argb: w*h u32 0x00RRGGBB; hit may be NULL. */

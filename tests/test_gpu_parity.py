@@ -7,6 +7,7 @@ reference's expressions in the same order and precision as the oracle.
 import numpy as np
 import pytest
 
+from cpp_cuda_raytracer_dev_amd import raytracer as R
 from tests import helpers as H
 
 pytestmark = pytest.mark.gpu
@@ -95,6 +96,26 @@ def test_rabbit_960x540_flat_band():
     # the flat and KD results agree on this scene (no boundary-pruned hits here)
     kargb, khit, _ = s.render(0)
     assert (khit[sl] == hit[sl]).all()
+
+
+def test_native_frame_loop_single_gpu():
+    """rt_run_frames without a communicator: the timed frames equal the
+    oracle's (committed hash), in one and in several buffer sets."""
+    import hashlib
+    import torch
+    ent = H.frame_hashes()["dragon_960x540_m0"]
+    s = H.GpuScene("dragon", 960, 540)
+    st = torch.cuda.Stream()
+    bufs = [torch.zeros(960 * 540, dtype=torch.int32, device="cuda:0") for _ in range(3)]
+    for n in (1, 3):
+        loop = R.FrameLoop(s.cam, bufs[:n], render_stream=st.cuda_stream, event_every=4)
+        ms, cnt, host = loop.run(10)
+        assert cnt == 3 and ms > 0
+        for b in bufs[:n]:
+            a = b.cpu().numpy().view(np.uint32)
+            if H.mesh_matches(ent):
+                assert hashlib.sha256(a.tobytes()).hexdigest() == ent["argb_sha"]
+    assert s.cam.device_error() == 0
 
 
 def test_auto_rays_choice():
@@ -787,8 +808,11 @@ def test_rect_gather_single_gpu(scene, w, h, nranks, moved):
 
 def test_native_comm_world1():
     """rt_comm_* end to end in a one-rank group: RCCL resolved at run time, the
-    id broadcast, the communicator, and rt_comm_gather_frame's in-place slot 0
-    + unpack on a side stream, pipelined over two buffer sets."""
+    id broadcast, the communicator, rt_comm_gather_frame's in-place slot 0 +
+    unpack on a side stream, pipelined over two buffer sets.  Each frame has
+    its own object transform and poisoned render target, and a set is reused
+    only once its gather has read it ('sent' events), so a frame gathered
+    from the wrong set or before its render shows."""
     import os
     import tempfile
     import torch
@@ -798,26 +822,43 @@ def test_native_comm_world1():
     assert _lib.lib().rt_comm_available() == 1
     w, h = 320, 180
     s = H.GpuScene("rabbit_70k", w, h)
-    full, _, _ = s.render(0)
+    poses = [_rot_y(0.0), _rot_y(7.0), _rot_y(-5.0, (0.004, 0.0, 0.0)), _rot_y(11.0), _rot_y(0.0, (0.0, 0.003, 0.0))]
+    fulls = [s.render(0, xform=xf)[0] for xf in poses]
     fd, path = tempfile.mkstemp()
     os.close(fd)
     dist.init_process_group("gloo", init_method=f"file://{path}", rank=0, world_size=1)
     try:
         dev = torch.device("cuda:0")
         ng = NativeFrameGather(dist, w, h, dev, nbuf=2)
-        cs = torch.cuda.Stream()
-        for j in range(4):
+        rs, cs = torch.cuda.Stream(), torch.cuda.Stream()
+        rendered = [torch.cuda.Event() for _ in range(2)]
+        sent = [torch.cuda.Event() for _ in range(2)]
+        got = []
+        for j, xf in enumerate(poses):
             k = j % 2
-            s.cam.render_into(ng.local[k], mode=0)
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream())
-            cs.wait_event(ev)
-            ng.gather(k, s.cam, None, 0, cs.cuda_stream)
+            rs.wait_event(sent[k])  # the gather that last read set k is done
+            with torch.cuda.stream(rs):
+                ng.local[k].fill_(0x7BADBEEF)
+            s.cam.render_into(ng.local[k], xform=xf, mode=0, stream=rs.cuda_stream)
+            rendered[k].record(rs)
+            cs.wait_event(rendered[k])
+            ng.gather(k, s.cam, xf, 0, cs.cuda_stream)
+            sent[k].record(cs)
+            if j >= 1:  # frame j-1's set: check it once its gather is done
+                sent[(j - 1) % 2].synchronize()
+                got.append(ng.frames[(j - 1) % 2].cpu().numpy().view(np.uint32).copy())
         torch.cuda.synchronize()
-        for k in range(2):
-            assert (ng.frames[k].cpu().numpy().view(np.uint32) == full).all()
-        x0, x1, b0, b1 = ng.frame_rect(s.cam, None, 0)
+        got.append(ng.frames[(len(poses) - 1) % 2].cpu().numpy().view(np.uint32).copy())
+        for j, (g, f) in enumerate(zip(got, fulls)):
+            assert (g == f).all(), f"frame {j}"
+        x0, x1, b0, b1 = ng.verify(s.cam, None, 0)
         assert (x1 - x0) * (b1 - b0) * 8 < w * h  # the fused render proves part of the frame background
+        # the native frame loop over the same communicator: identical frames
+        loop = R.FrameLoop(s.cam, ng.local, mode=0, render_stream=rs.cuda_stream, comm=ng,
+                           comm_stream=cs.cuda_stream, event_every=2)
+        ms, n, host = loop.run(9)
+        assert n == 5 and ms > 0 and host > 0
+        assert (ng.frames[loop.last_set()].cpu().numpy().view(np.uint32) == fulls[0]).all()
         ng.close()
     finally:
         dist.destroy_process_group()
