@@ -359,6 +359,11 @@ def key_masks(spec: str) -> list:
 
 def main():
     a = parse()
+    if os.environ.get("RT_BENCH_WATCHDOG"):
+        # diagnostics: dump every thread's Python stack and exit if the run
+        # takes longer than this many seconds
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["RT_BENCH_WATCHDOG"]), exit=True)
     if a.cpu_only:
         return cpu_only(a)
     import torch

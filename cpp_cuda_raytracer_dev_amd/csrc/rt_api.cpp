@@ -221,7 +221,13 @@ int ensure_order(rt_camera* c, const TraceParams& p) {
         order[(size_t)t] = (int32_t)t;
     }
     std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return dist2[(size_t)a] < dist2[(size_t)b]; });
+    // Earlier frames' kernels (on any stream) read d_order, and a cost-order
+    // upload may still be queued behind them: let them finish before the
+    // buffer is replaced or rewritten.  Runs only when the fine grid changes.
     int rc;
+    if ((rc = hip_check(hipDeviceSynchronize(), "order sync"))) return rc;
+    c->order_pending = false;
+    c->order_gen = ~0ull;
     if (c->order_cap < n) {
         dev_free(c->d_order);
         if ((rc = dev_alloc(&c->d_order, (size_t)n, "hipMalloc(order)"))) return rc;
@@ -244,6 +250,10 @@ constexpr int kTunePeriod = 2048;  // frames between timing rounds of the shadow
 int ensure_cost(rt_camera* c, int64_t n) {
     int rc;
     if (c->cost_cap < kCostSlots * n) {
+        // earlier frames' kernels write d_cost and a cost sample may be
+        // copying it: both done before the buffer goes
+        if ((rc = hip_check(hipDeviceSynchronize(), "cost sync"))) return rc;
+        c->cost_pending = false;
         dev_free(c->d_cost);
         if ((rc = dev_alloc(&c->d_cost, (size_t)(kCostSlots * n), "hipMalloc(cost)"))) return rc;
         // slots of waves a tile does not have stay zero
@@ -668,10 +678,12 @@ int check_tile(const rt_tile* tile) {
 }
 
 // The device error word: 1 = DFS stack overflow (kernels 1-2), 2 = item pool
-// overflow (kernel 3), 4 = a fused far group that was not far (kernel 3).
+// overflow (kernel 3), 4 = a fused far group that was not far (kernel 3),
+// 8 = a tile order entry outside the fine grid (kernel 3; the block skipped).
 int device_error(int32_t err) {
-    return fail(RT_ERR_OVERFLOW, "device reported %s%s%s", (err & 1) ? "[traversal stack overflow]" : "",
-                (err & 2) ? "[item pool overflow]" : "", (err & 4) ? "[far-group check failed]" : "");
+    return fail(RT_ERR_OVERFLOW, "device reported %s%s%s%s", (err & 1) ? "[traversal stack overflow]" : "",
+                (err & 2) ? "[item pool overflow]" : "", (err & 4) ? "[far-group check failed]" : "",
+                (err & 8) ? "[tile order out of range]" : "");
 }
 
 }  // namespace

@@ -1275,7 +1275,12 @@ __global__ RT_KD3_BOUNDS(64 * kd3_waves(kRays)) void k_trace_kd3(TraceParams P) 
         if (kCount) count_flush(P, C);
         return;
     }
-    uint32_t* cost = P.cost ? P.cost + kCostSlots * (size_t)tile_index(P, b) + wv : nullptr;
+    const int32_t ti = tile_index(P, b);
+    if ((uint32_t)ti >= (uint32_t)(P.tiles_x * P.block_rows)) {  // a stale order: never index past the grid
+        if (lane == 0) atomicOr(P.err, 8);
+        return;
+    }
+    uint32_t* cost = P.cost ? P.cost + kCostSlots * (size_t)ti + wv : nullptr;
     trace_unit<kRays, kCap, kRayVec, kTranslated, kWriteHit, kCount, kShadow>(P, s_lds[wv], unit_of(P, b, wv), lane,
                                                                              (size_t)b * kWaves + wv, cost, C);
     if (kCount) count_flush(P, C);

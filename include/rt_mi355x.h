@@ -284,7 +284,8 @@ int rt_camera_counters(rt_camera* c, uint64_t out[5], int reset);
 /* The camera's device error word, which every render ORs into: 1 = DFS
  * stack overflow (kernels 1-2), 2 = item pool overflow (kernel 3), 4 = a
  * fused far group that was not provably background (kernel 3; the gathered
- * frame's background then is not the rendered one).  The reference has no
+ * frame's background then is not the rendered one), 8 = a tile-order entry
+ * outside the fine grid (kernel 3; that block is skipped).  The reference has no
  * equivalent (its status is the last sync, TD/Trixel.cu:227-240).
  * Synchronises the device; *err receives the word; reset != 0 clears it.
  * Returns RT_OK even when *err is non-zero (the word is the report). */
