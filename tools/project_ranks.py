@@ -1,0 +1,75 @@
+#!/usr/bin/env python3
+"""Project the N-GPU frame on one GPU: render each rank's screen bands
+(rt_tile{N, r}) alone, timed with HIP events over many frames, for N = 1, 2,
+4, 8.  A rank's render time bounds its frame time at N GPUs (the gather
+overlaps the next frame's render), so max over r is the per-frame floor of the
+multi-GPU run and w*h / max the best N-GPU frame rate the render allows.  Also
+reports the bytes each peer sends to rank 0 (the rectangle gather).
+
+    python tools/project_ranks.py [--scene dragon] [--width 1920 --height 1080] [--frames 300] [--rays 0]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scene", default="dragon")
+    ap.add_argument("--view", default="default")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--frames", type=int, default=300)
+    ap.add_argument("--rays", type=int, default=0)
+    ap.add_argument("--ranks", default="1,2,4,8")
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    import torch
+    from cpp_cuda_raytracer_dev_amd import _lib, raytracer as R, scenes
+    import bench
+    pts, leafs, nodes, _ = bench.build_scene(a.scene)
+    w, h = a.width, a.height
+    t = R.Trixel(len(pts), pts)
+    t.set_kd_nodes(nodes)
+    kw = scenes.view(a.scene, a.view)
+    cam = R.Camera(w, h, R.film_w(w, h), np.float32(.024), np.float32(.055), *kw["pos"], *kw["look_at"],
+                   0.0, 1.0, 0.0)
+    obj = R.Object(t)
+    cam.add_object(obj)
+    cam.set_option(_lib.RT_OPT_RAYS, a.rays)
+    st = torch.cuda.Stream()
+    res = {"scene": a.scene, "view": a.view, "resolution": [w, h], "frames": a.frames, "per_n": {}}
+    for n in [int(x) for x in a.ranks.split(",")]:
+        npk = R.packed_pixels(w, h, n)
+        rect = np.zeros(4, np.int32)
+        _lib.call("rt_frame_rect", cam._h, None, 0, n, _lib.ptr(rect))
+        ranks = []
+        for r in range(n):
+            buf = torch.zeros(npk, dtype=torch.int32, device="cuda:0")
+            loop = R.FrameLoop(cam, [buf], tile=(n, r), render_stream=st.cuda_stream, event_every=1)
+            loop.run(20)
+            ms, cnt, host = loop.run(a.frames)
+            send = int(_lib.lib().rt_rect_pixels(w, h, n, r, _lib.ptr(rect))) * 4 if r else 0
+            ranks.append({"rank": r, "render_ms": round(ms, 5), "host_us_per_frame": round(1e3 * host / a.frames, 2),
+                          "rays_per_wave": cam.get_option(_lib.RT_OPT_RAYS_USED), "send_bytes": send})
+        worst = max(x["render_ms"] for x in ranks)
+        res["per_n"][str(n)] = {"ranks": ranks, "max_render_ms": worst,
+                                "render_bound_fps": round(1e3 / worst, 1) if worst else None,
+                                "rect": [int(v) for v in rect]}
+        print(f"N={n}: max render {worst:.4f} ms -> <= {1e3 / worst:.0f} FPS; per rank "
+              f"{[x['render_ms'] for x in ranks]}", flush=True)
+    if a.out:
+        with open(a.out, "w") as fp:
+            json.dump(res, fp, indent=1)
+    print(json.dumps(res))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
