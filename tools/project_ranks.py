@@ -19,6 +19,32 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def wave_stamps(cam, _lib, R, torch, st, n, r, npk):
+    """Per-wave (start, end, pool iterations, items popped) of one render of
+    rank r's tile (debug bit 2; s_memrealtime, 100 MHz): the longest waves."""
+    buf = torch.zeros(npk, dtype=torch.int32, device="cuda:0")
+    cam.set_option(_lib.RT_OPT_DEBUG, 2)
+    cam.render_into(buf, tile=(n, r), stream=st.cuda_stream)
+    st.synchronize()
+    raw = np.zeros(3 * 4 * 400000, np.uint64)
+    got = _lib.lib().rt_camera_debug_read(cam._h, _lib.ptr(raw), len(raw))
+    cam.set_option(_lib.RT_OPT_DEBUG, 0)
+    rec = raw[:got].reshape(-1, 3).astype(np.int64)
+    rec = rec[rec[:, 1] > 0]
+    t0 = rec[:, 0].min()
+    dur = (rec[:, 1] - rec[:, 0]) * 10e-3
+    end = (rec[:, 1] - t0) * 10e-3
+    it = rec[:, 2] & 0xFFFFFFFF
+    fine = it != 0xFFFFFFFF
+    top = np.argsort(-end)[:8]
+    return {"waves": int(fine.sum()), "kernel_span_us": float(end.max()),
+            "iters_p50_p99_max": [float(np.percentile(it[fine], q)) for q in (50, 99, 100)],
+            "dur_us_p50_p99_max": [float(np.percentile(dur[fine], q)) for q in (50, 99, 100)],
+            "us_per_iter_of_longest": [round(float(dur[i] / max(1, it[i])), 3) for i in np.argsort(-dur)[:8]],
+            "latest_finishers": [{"start_us": round(float((rec[i, 0] - t0) * 10e-3), 2), "dur_us": round(float(dur[i]), 2),
+                                  "iters": int(it[i]), "popped": int(rec[i, 2] >> 32)} for i in top]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scene", default="dragon")
@@ -29,6 +55,8 @@ def main():
     ap.add_argument("--rays", type=int, default=0)
     ap.add_argument("--ranks", default="1,2,4,8")
     ap.add_argument("--out", default="")
+    ap.add_argument("--stamps", action="store_true",
+                    help="also record per-wave clocks of the slowest rank at each N (pool iterations, duration)")
     a = ap.parse_args()
     import torch
     from cpp_cuda_raytracer_dev_amd import _lib, raytracer as R, scenes
@@ -59,6 +87,9 @@ def main():
             ranks.append({"rank": r, "render_ms": round(ms, 5), "host_us_per_frame": round(1e3 * host / a.frames, 2),
                           "rays_per_wave": cam.get_option(_lib.RT_OPT_RAYS_USED), "send_bytes": send})
         worst = max(x["render_ms"] for x in ranks)
+        if a.stamps:
+            r = max(range(n), key=lambda q: ranks[q]["render_ms"])
+            ranks[r]["waves"] = wave_stamps(cam, _lib, R, torch, st, n, r, npk)
         res["per_n"][str(n)] = {"ranks": ranks, "max_render_ms": worst,
                                 "render_bound_fps": round(1e3 / worst, 1) if worst else None,
                                 "rect": [int(v) for v in rect]}
