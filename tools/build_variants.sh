@@ -10,6 +10,6 @@ for v in "$@"; do
     name=${v%%:*}
     defs=${v#*:}
     [ "$defs" = "$v" ] && defs=""
-    python3 -m cpp_cuda_raytracer_dev_amd.build --variant "$name" --defs "$defs"
+    python3 -m cpp_cuda_raytracer_dev_amd.build --variant "$name" --defs="$defs"
 done
 ls -la "$ROOT"/tools/variants/*.so

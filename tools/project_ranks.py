@@ -55,11 +55,14 @@ def main():
     ap.add_argument("--rays", type=int, default=0)
     ap.add_argument("--ranks", default="1,2,4,8")
     ap.add_argument("--out", default="")
+    ap.add_argument("--lib", default="", help="an experiment build of librt_mi355x.so (tools/build_variants.sh)")
     ap.add_argument("--stamps", action="store_true",
                     help="also record per-wave clocks of the slowest rank at each N (pool iterations, duration)")
     a = ap.parse_args()
     import torch
     from cpp_cuda_raytracer_dev_amd import _lib, raytracer as R, scenes
+    if a.lib:
+        _lib.LIB_PATH = os.path.abspath(a.lib)
     import bench
     pts, leafs, nodes, _ = bench.build_scene(a.scene)
     w, h = a.width, a.height
@@ -72,7 +75,7 @@ def main():
     cam.add_object(obj)
     cam.set_option(_lib.RT_OPT_RAYS, a.rays)
     st = torch.cuda.Stream()
-    res = {"scene": a.scene, "view": a.view, "resolution": [w, h], "frames": a.frames, "per_n": {}}
+    res = {"lib": a.lib or "librt_mi355x.so", "scene": a.scene, "view": a.view, "resolution": [w, h], "frames": a.frames, "per_n": {}}
     for n in [int(x) for x in a.ranks.split(",")]:
         npk = R.packed_pixels(w, h, n)
         rect = np.zeros(4, np.int32)
