@@ -631,7 +631,7 @@ __device__ __forceinline__ uint32_t code_key(uint32_t marked) {
 #define RT_POOL_CAP_R16 352
 #endif
 #ifndef RT_POOL_CAP_R8
-#define RT_POOL_CAP_R8 256
+#define RT_POOL_CAP_R8 512
 #endif
 template <int kRays>
 constexpr int pool_cap_for() {

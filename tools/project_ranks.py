@@ -53,6 +53,7 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--frames", type=int, default=300)
     ap.add_argument("--rays", type=int, default=0)
+    ap.add_argument("--items", type=int, default=2)
     ap.add_argument("--ranks", default="1,2,4,8")
     ap.add_argument("--out", default="")
     ap.add_argument("--lib", default="", help="an experiment build of librt_mi355x.so (tools/build_variants.sh)")
@@ -74,8 +75,9 @@ def main():
     obj = R.Object(t)
     cam.add_object(obj)
     cam.set_option(_lib.RT_OPT_RAYS, a.rays)
+    cam.set_option(_lib.RT_OPT_ITEMS, a.items)
     st = torch.cuda.Stream()
-    res = {"lib": a.lib or "librt_mi355x.so", "scene": a.scene, "view": a.view, "resolution": [w, h], "frames": a.frames, "per_n": {}}
+    res = {"lib": a.lib or "librt_mi355x.so", "rays": a.rays, "items": a.items, "scene": a.scene, "view": a.view, "resolution": [w, h], "frames": a.frames, "per_n": {}}
     for n in [int(x) for x in a.ranks.split(",")]:
         npk = R.packed_pixels(w, h, n)
         rect = np.zeros(4, np.int32)
