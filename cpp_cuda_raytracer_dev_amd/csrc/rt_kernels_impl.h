@@ -385,10 +385,9 @@ struct Ray {
     bool sx, sy, sz;           // r > 0
 };
 
-// Slab test of one node, TD/Trixel.cu:76-95,146: entry/exit parameters and
-// whether the reference descends into the node.
-__device__ __forceinline__ bool slab(const Ray& R, float lx, float hx, float ly, float hy, float lz,
-                                     float hz, float& maxt0, float& mint1) {
+// Slab parameters of one node, TD/Trixel.cu:76-95: entry maxt0, exit mint1.
+__device__ __forceinline__ void slab_vals(const Ray& R, float lx, float hx, float ly, float hy, float lz,
+                                          float hz, float& maxt0, float& mint1) {
     const float t0x = R.sx ? lx * R.ix : hx * R.ix;
     const float t1x = R.sx ? hx * R.ix : lx * R.ix;
     const float t0y = R.sy ? ly * R.iy : hy * R.iy;
@@ -397,6 +396,13 @@ __device__ __forceinline__ bool slab(const Ray& R, float lx, float hx, float ly,
     const float t1z = R.sz ? hz * R.iz : lz * R.iz;
     maxt0 = fmaxf(t0z + R.oz, fmaxf(t0x + R.ox, t0y + R.oy));
     mint1 = fminf(t1z + R.oz, fminf(t1x + R.ox, t1y + R.oy));
+}
+
+// Slab test of one node, TD/Trixel.cu:76-95,146: entry/exit parameters and
+// whether the reference descends into the node.
+__device__ __forceinline__ bool slab(const Ray& R, float lx, float hx, float ly, float hy, float lz,
+                                     float hz, float& maxt0, float& mint1) {
+    slab_vals(R, lx, hx, ly, hy, lz, hz, maxt0, mint1);
     return pred::enter(maxt0, mint1);
 }
 
@@ -779,29 +785,44 @@ __device__ __forceinline__ void visit_interior(const float4* rd, uint4 it, float
     const uint32_t L = lw & ~(3u << kAxisShift), Rr = __float_as_uint(r3.w);
     const float dir = axis == 0 ? q2.y : axis == 1 ? q2.z : q2.w;
     const float mx = __uint_as_float(it.y) * dir, mn = __uint_as_float(it.z) * dir;
+    // children's slab parameters from the boxes in this record
+    float lt0, lt1, rt0, rt1;
+    slab_vals(Q, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, lt0, lt1);
+    slab_vals(Q, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w, rt0, rt1);
+    // The reference's double-promoted epsilon tests (TD/Trixel.cu:146-157):
+    // single float compares when every guard of the visit holds
+    // (rt_predicates.h, checked exhaustively on edge sets), the double forms
+    // otherwise.  Untranslated walks only.
     float s1, s2;
+    bool left_first, push_second, lpass, rpass;
     if (kTranslated) {
         const float ds = axis == 0 ? q3.w : axis == 1 ? q4.x : q4.y;
         s1 = (float)((double)r3.x + kEps + (double)ds);
         s2 = r3.y + ds;
     } else {
-        s1 = pred::add_eps(r3.x);
         s2 = r3.y;
     }
-    bool left_first, push_second;
-    if (pred::lt_eps(mx, s2)) {
-        left_first = true;
-        push_second = pred::gt_eps(mn, s2);
+#ifdef RT_NO_GUARDED_PRED
+    const bool guarded = false;  // experiments: always the double forms
+#else
+    const bool guarded = !kTranslated && pred::split_safe(r3.x) && pred::split_safe(s2) && mx != s2 && mn != s2 &&
+                         pred::entry_safe(lt0) && pred::entry_safe(rt0);
+#endif
+    if (guarded) {
+        s1 = r3.x;
+        left_first = pred::lt_eps_f(mx, s2);
+        push_second = left_first ? pred::gt_eps_f(mn, s2) : (mn < s1 || mx < s1);
+        lpass = pred::enter_f(lt0, lt1);
+        rpass = pred::enter_f(rt0, rt1);
     } else {
-        left_first = false;
-        push_second = (mn < s1 || mx < s1);
+        if (!kTranslated) s1 = pred::add_eps_ref(r3.x);
+        left_first = pred::lt_eps_ref(mx, s2);
+        push_second = left_first ? pred::gt_eps_ref(mn, s2) : (mn < s1 || mx < s1);
+        lpass = pred::enter_ref(lt0, lt1);
+        rpass = pred::enter_ref(rt0, rt1);
     }
     const uint32_t first = left_first ? L : Rr;
     const uint32_t second = left_first ? Rr : L;
-    // children's slab tests from the boxes in this record
-    float lt0, lt1, rt0, rt1;
-    const bool lpass = slab(Q, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, lt0, lt1);
-    const bool rpass = slab(Q, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w, rt0, rt1);
     const bool first_leaf = (first & kLeafBit) != 0, second_leaf = (second & kLeafBit) != 0;
     const bool keep_first = first_leaf || (left_first ? lpass : rpass);
     const bool keep_second = push_second && (second_leaf || (left_first ? rpass : lpass));

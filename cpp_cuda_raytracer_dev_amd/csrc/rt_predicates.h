@@ -78,5 +78,23 @@ RT_HD float add_eps(float s) {
     return fabsf(s) >= kSmall ? s : add_eps_ref(s);
 }
 
+// Guarded float forms: the double tests above reduced to one float compare,
+// exact whenever the guard holds (tests/predicates_check.cpp checks them on
+// edge sets and random sweeps).  The traversal evaluates the guards of a
+// whole node visit at once and takes these forms when every guard holds,
+// which is every visit of a camera more than ~1e-6 away from split planes
+// and box faces; otherwise it takes the double forms.
+//   split_safe(s): |s| >= 2^-20 or NaN  -> add_eps(s) == s and, for a != s,
+//                  lt_eps(a, s) == (a < s), gt_eps(a, s) == (a > s)
+//                  (at a == s the answer depends on whether 1e-16 exceeds
+//                  half a double ulp of s: the double form decides)
+//   entry_safe(m): m <= -eps_f() or m >= 2^-20 or NaN -> enter(m, t) == (m > -eps_f() && t >= m)
+//                  (t >= fl64(m - 1e-16) with fl64(m - 1e-16) in (pred(m), m])
+RT_HD bool split_safe(float s) { return !(fabsf(s) < kSmall); }
+RT_HD bool entry_safe(float m) { return !(m > -eps_f() && m < kSmall); }
+RT_HD bool lt_eps_f(float a, float s) { return a < s; }
+RT_HD bool gt_eps_f(float a, float s) { return a > s; }
+RT_HD bool enter_f(float maxt0, float mint1) { return maxt0 > -eps_f() && mint1 >= maxt0; }
+
 }  // namespace pred
 }  // namespace rt

@@ -27,7 +27,7 @@ int main(int argc, char** argv) {
             for (int d = -2; d <= 2; d++) edge.push_back(bits(u + d));
         }
     }
-    long bad = 0, checked = 0;
+    long bad = 0, checked = 0, guarded = 0;
     auto check = [&](float a, float b) {
         checked++;
         if (enter(a, b) != enter_ref(a, b)) { if (bad++ < 10) printf("enter %a %a\n", a, b); }
@@ -35,6 +35,16 @@ int main(int argc, char** argv) {
         if (gt_eps(a, b) != gt_eps_ref(a, b)) { if (bad++ < 10) printf("gt_eps %a %a\n", a, b); }
         const float x = add_eps(a), y = add_eps_ref(a);
         if (ubits(x) != ubits(y) && !(x != x && y != y)) { if (bad++ < 10) printf("add_eps %a\n", a); }
+        // the guarded float forms of the traversal (rt_predicates.h)
+        if (split_safe(b) && a != b) {
+            if (lt_eps_f(a, b) != lt_eps_ref(a, b)) { if (bad++ < 10) printf("lt_eps_f %a %a\n", a, b); }
+            if (gt_eps_f(a, b) != gt_eps_ref(a, b)) { if (bad++ < 10) printf("gt_eps_f %a %a\n", a, b); }
+            guarded++;
+        }
+        if (split_safe(a) && ubits(a) != ubits(add_eps_ref(a)) && !(a != a)) {
+            if (bad++ < 10) printf("add_eps_f %a\n", a);
+        }
+        if (entry_safe(a) && enter_f(a, b) != enter_ref(a, b)) { if (bad++ < 10) printf("enter_f %a %a\n", a, b); }
     };
     for (float a : edge)
         for (float b : edge) check(a, b);
@@ -52,6 +62,6 @@ int main(int argc, char** argv) {
         check(a, b);
         check(b, a);
     }
-    printf("checked %ld pairs, %ld mismatches\n", checked, bad);
+    printf("checked %ld pairs (%ld under split guards), %ld mismatches\n", checked, guarded, bad);
     return bad != 0;
 }
