@@ -789,10 +789,9 @@ __device__ __forceinline__ void visit_interior(const float4* rd, uint4 it, float
     float lt0, lt1, rt0, rt1;
     slab_vals(Q, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, lt0, lt1);
     slab_vals(Q, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w, rt0, rt1);
-    // The reference's double-promoted epsilon tests (TD/Trixel.cu:146-157):
-    // single float compares when every guard of the visit holds
-    // (rt_predicates.h, checked exhaustively on edge sets), the double forms
-    // otherwise.  Untranslated walks only.
+    // The reference's double-promoted epsilon tests (TD/Trixel.cu:146-157);
+    // with -DRT_GUARDED_PRED single float compares when every guard of the
+    // visit holds (rt_predicates.h, checked on edge sets), else these.
     float s1, s2;
     bool left_first, push_second, lpass, rpass;
     if (kTranslated) {
@@ -802,8 +801,11 @@ __device__ __forceinline__ void visit_interior(const float4* rd, uint4 it, float
     } else {
         s2 = r3.y;
     }
-#ifdef RT_NO_GUARDED_PRED
-    const bool guarded = false;  // experiments: always the double forms
+#ifndef RT_GUARDED_PRED
+    // The guarded float forms (-DRT_GUARDED_PRED) measured slower on gfx950:
+    // 94 vs 86.5 us per 1080p dragon frame, the guards and the branch cost
+    // more than the double arithmetic they skip.  The double forms stand.
+    const bool guarded = false;
 #else
     const bool guarded = !kTranslated && pred::split_safe(r3.x) && pred::split_safe(s2) && mx != s2 && mn != s2 &&
                          pred::entry_safe(lt0) && pred::entry_safe(rt0);
