@@ -45,6 +45,9 @@ if has bench; then
     step bench_fill_rabbit1080 300 python bench.py --steps 300 --warmup 30 --scene rabbit_70k --view fill \
         --no-cpu-baseline
     step bench_dragon_shadow 300 python bench.py --steps 500 --warmup 50 --shadow --no-cpu-baseline
+    step bench_big 300 python bench.py --steps 200 --warmup 20 --scene big --no-cpu-baseline
+    step bench_rehearse 300 python bench.py --steps 1000 --warmup 100 --rehearse-gather --no-cpu-baseline
+    step bench_animate 300 python bench.py --steps 500 --warmup 20 --animate R+W.Q.T.W --no-cpu-baseline
 fi
 if has prof; then
     step rocprof_c4 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c4" -o run -- \
