@@ -81,6 +81,13 @@ def parse():
     ap.add_argument("--loop", default="native", choices=["native", "python"],
                     help="frame loop: native = rt_run_frames (C++, the render + RCCL gather enqueued per frame "
                          "without Python), python = the same calls from Python (torch collectives, --animate)")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="native loop: frames in flight on the library's render lanes (rt_frame_loop.inflight; "
+                         "1 = one frame at a time).  The roofline's kernel time comes from a separate pass of "
+                         "solo frames (one in flight), since overlapped launches share the GPU")
+    ap.add_argument("--solo-frames", type=int, default=200,
+                    help="inflight > 1: solo frames (one in flight, every one bracketed by events) before the "
+                         "timed region, for the roofline's kernel time")
     ap.add_argument("--pipeline", type=int, default=2,
                     help="rccl: buffer sets in flight (frame i+1 renders while frame i is gathered)")
     ap.add_argument("--kernel", type=int, default=3,
@@ -101,8 +108,8 @@ def parse():
                     help="kernel 3: 8x8 groups per wave outside the root box's screen rectangle (0 = off)")
     ap.add_argument("--event-every", type=int, default=0,
                     help="bracket every Nth timed frame with HIP events for the kernel time (each pair costs "
-                         "queue time, so N > 1 keeps the frame rate closer to the uninstrumented one); 0 = every frame "
-                         "at one GPU, every 8th with more, where a frame is a few tens of microseconds")
+                         "~9 us of queue time, so N > 1 keeps the frame rate close to the uninstrumented one); "
+                         "0 = every 8th (every frame with --inflight 1 at one GPU)")
     ap.add_argument("--side-coarse", action="store_true",
                     help="kernel 3: run the coarse kernel beside the fine one on a side stream (default: before it)")
     ap.add_argument("--deliver", action="store_true",
@@ -463,16 +470,20 @@ def main():
     my_pix = int(np.count_nonzero(np.repeat(np.arange((h + 7) // 8) % world == rank, 8)[:h])) * w
     bytes_per_launch = B_INT * int(cnt[0]) + B_LEAF * int(cnt[1]) + B_HIT * int(cnt[2]) + B_PIX * my_pix
 
-    if a.event_every <= 0:
-        a.event_every = 8 if multi else 1
-    collective = a.collective
     loop_kind = a.loop if not masks else "python"  # a moving object ticks per frame in Python
+    inflight = max(1, a.inflight) if loop_kind == "native" else 1
+    if a.event_every <= 0:
+        a.event_every = 8 if (multi or inflight > 1) else 1
+    collective = a.collective
     gather_note = None
 
     def make_gather(kind):
         """(NativeFrameGather or None, FrameGather or None, render target)."""
         if multi and kind == "rccl":
-            g = NativeFrameGather(dist, w, h, dev, nbuf=max(1, min(a.pipeline, 4)))
+            # two sets per frame in flight: a set's next render then waits
+            # on a gather that finished long before (cross-queue waits that
+            # are still pending cost ~10-15 us each)
+            g = NativeFrameGather(dist, w, h, dev, nbuf=max(1, min(max(a.pipeline, 2 * inflight), 4)))
             # every rank must derive the same rectangle and options, or the
             # receive sizes would not match the sends (ADVICE r01)
             g.verify(cam, xf, a.mode)
@@ -482,9 +493,11 @@ def main():
                 R.unpack_bands(local, w, h, world, g, f, stream=torch.cuda.current_stream(dev).cuda_stream)
             f = FrameGather(dist, w, h, dev, kind, unpack=unpack)
             return None, f, f.local
-        return None, None, torch.zeros(w * h, dtype=torch.int32, device=dev)
+        return None, None, [torch.zeros(w * h, dtype=torch.int32, device=dev) for _ in range(inflight)]
 
     ng, fg, out = make_gather(collective)
+    outs = out if isinstance(out, list) else [out]  # N=1: one target per frame in flight
+    out = outs[0]
     cstream = torch.cuda.Stream(device=dev) if ng is not None else None
 
     def gathered_frame_ok(loop):
@@ -565,10 +578,10 @@ def main():
 
     def make_loop():
         if loop_kind == "native" and (not multi or ng is not None):
-            return R.FrameLoop(cam, ng.local if ng is not None else [out], xform=xf, mode=a.mode, flags=sflag,
+            return R.FrameLoop(cam, ng.local if ng is not None else outs, xform=xf, mode=a.mode, flags=sflag,
                                tile=tile if multi else None, render_stream=sptr, comm=ng,
                                comm_stream=cstream.cuda_stream if ng is not None else None,
-                               event_every=a.event_every)
+                               event_every=a.event_every, inflight=inflight)
         return PyLoop()
 
     loop = make_loop()
@@ -586,6 +599,14 @@ def main():
         loop = PyLoop()
         loop.run(a.warmup, False)
         torch.cuda.synchronize(dev)
+    solo = None
+    if not isinstance(loop, PyLoop) and inflight > 1 and a.solo_frames > 0:
+        # the roofline's kernel time: solo frames (one in flight, each
+        # bracketed), untimed; the timed frames overlap and share the GPU
+        sl = R.FrameLoop(cam, [ng.local[0] if ng is not None else outs[0]], xform=xf, mode=a.mode, flags=sflag,
+                         tile=tile if multi else None, render_stream=sptr, event_every=1, inflight=1)
+        solo = sl.run(a.solo_frames)[:2]
+        torch.cuda.synchronize(dev)
     if multi:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -600,12 +621,23 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     host_us_per_frame = 1e3 * host_ms / max(1, a.steps)
+    kern_ms_timed, n_ev_timed = kern_ms, n_ev
+    if solo is not None:
+        kern_ms, n_ev = solo
+    kern_label = (f"{n_ev} solo frames before the timed region (one in flight, each bracketed); the timed frames "
+                  f"keep {inflight} in flight" if solo is not None else
+                  f"{n_ev} of {a.steps} timed frames (every {max(1, a.event_every)})")
+    kern_extra = ({"kernel_ms_avg_timed": round(kern_ms_timed, 5),
+                   "kernel_ms_timed_frames": f"{n_ev_timed} of {a.steps} timed frames (every {a.event_every}), "
+                                             f"each sharing the GPU with the other frames in flight"}
+                  if solo is not None else {})
     # the device error word of this rank's timed frames (stack / pool
     # overflow, a far-group proof that failed): reported, and fatal below
     dev_err = cam.device_error(reset=True)
     frame_check = None
     if not multi and rank == 0:
-        frame_check = frame_check_n1(out.cpu().numpy().view(np.uint32), pts, nodes, cam_kw, a,
+        last = outs[loop.last_set()] if not isinstance(loop, PyLoop) else out
+        frame_check = frame_check_n1(last.cpu().numpy().view(np.uint32), pts, nodes, cam_kw, a,
                                      xform=xf if masks else None)
     if multi:
         ok = gathered_frame_ok(loop)
@@ -698,8 +730,9 @@ def main():
                 "kernel": "k_trace_flat",
                 "kernel_form": cam.get_option(_lib.RT_OPT_FLAT),
                 "kernel_ms_avg": round(kern_ms, 5),
-                "kernel_ms_frames": f"{n_ev} of {a.steps} timed frames (every {max(1, a.event_every)})",
+                "kernel_ms_frames": kern_label,
                 "kernel_ms_avg_max_rank": round(kern_ms_max, 5),
+                **kern_extra,
                 "tests_per_launch": tests,
                 "flops_per_launch": FLOPS_PER_TEST * tests,
                 "divides_per_launch": tests,
@@ -729,8 +762,9 @@ def main():
                                        "shadow_push_order_mode": "timed" if a.shadow_order < 0 else "fixed"}
                                       if a.shadow else {})},
                 "kernel_ms_avg": round(kern_ms, 5),
-                "kernel_ms_frames": f"{n_ev} of {a.steps} timed frames (every {max(1, a.event_every)})",
+                "kernel_ms_frames": kern_label,
                 "kernel_ms_avg_max_rank": round(kern_ms_max, 5),
+                **kern_extra,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "counts_per_launch": {"interior": int(cnt[0]), "leaf": int(cnt[1]), "accept": int(cnt[2]),
                                       "hit_pixels": int(cnt[3]), "pixels": my_pix},
@@ -741,6 +775,7 @@ def main():
             "device_err": errs if multi else dev_err,
             "host": {"us_per_frame": round(host_us_per_frame, 2), "loop": "native (rt_run_frames)"
                      if not isinstance(loop, PyLoop) else "python",
+                     "frames_in_flight": inflight if not isinstance(loop, PyLoop) else 1,
                      "what": "host time spent enqueueing the timed frames / steps (rank 0)"},
             "kd_build": build_times,
         }

@@ -58,13 +58,15 @@ class RtTile(C.Structure):
 
 
 RT_LOOP_MAX_BUF = 4
+RT_LOOP_MAX_LANES = 4
 
 
 class RtFrameLoop(C.Structure):
     _fields_ = [("xform", C.c_void_p), ("mode", C.c_uint32), ("flags", C.c_uint32), ("tile", RtTile),
                 ("nbuf", C.c_int32), ("d_local", C.c_void_p * RT_LOOP_MAX_BUF),
                 ("d_scratch", C.c_void_p * RT_LOOP_MAX_BUF), ("d_frame", C.c_void_p * RT_LOOP_MAX_BUF),
-                ("render_stream", C.c_void_p), ("comm_stream", C.c_void_p), ("event_every", C.c_int32)]
+                ("render_stream", C.c_void_p), ("comm_stream", C.c_void_p), ("event_every", C.c_int32),
+                ("inflight", C.c_int32)]
 
 
 class RtError(RuntimeError):

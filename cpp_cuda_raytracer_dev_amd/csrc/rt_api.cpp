@@ -108,10 +108,17 @@ struct rt_camera {
         float xf[12];
         uint32_t mode = 0;
         int32_t nranks = 0, rank = 0;
-        uint32_t* argb = nullptr;
-        int64_t* hit = nullptr;
-        TraceParams p;
+        TraceParams p;               // its argb / hit are set per call
     } pcache;
+    // rt_run_frames with frames in flight: the library's own render lanes
+    // (and, with a gather, its comm lane), each a stream created after the
+    // caller's, so on hardware queues of its own while queues are free.
+    // While a loop runs, `active` lists the lanes frames are issued to: a
+    // cost-order upload then waits for all of them and they wait for it.
+    hipStream_t lanes[RT_LOOP_MAX_LANES + 1] = {};
+    hipEvent_t lane_ev[RT_LOOP_MAX_LANES + 1] = {};
+    int nactive = 0;
+    hipStream_t active[RT_LOOP_MAX_LANES] = {};
     // rt_run_frames: events kept across calls (the timed call reuses the
     // warm-up call's), pairs bracketing sampled frames' renders
     std::vector<hipEvent_t> loop_ev;
@@ -388,10 +395,21 @@ int cost_feedback(rt_camera* c, const TraceParams& p, void* stream) {
         }
         if (same && c->order_gen == c->layout_gen) return RT_OK;  // d_order already holds it
         int rc;
+        // frames in flight on other lanes read d_order: the upload waits
+        // for them, and their later frames wait for the upload
+        for (int l = 0; l < c->nactive; l++) {
+            if (c->active[l] == st) continue;
+            if ((rc = hip_check(hipEventRecord(c->lane_ev[l], c->active[l]), "lane join")) ||
+                (rc = hip_check(hipStreamWaitEvent(st, c->lane_ev[l], 0), "lane join wait")))
+                return rc;
+        }
         if ((rc = hip_check(hipMemcpyAsync(c->d_order, c->h_order, sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice, st),
                             "H2D cost order")) ||
             (rc = hip_check(hipEventRecord(c->order_ev, st), "order event")))
             return rc;
+        for (int l = 0; l < c->nactive; l++)
+            if (c->active[l] != st && (rc = hip_check(hipStreamWaitEvent(c->active[l], c->order_ev, 0), "lane fork wait")))
+                return rc;
         c->order_pending = true;
         c->order_gen = c->layout_gen;
         return RT_OK;
@@ -1071,8 +1089,10 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
     auto& pc = c->pcache;
     TraceParams p;
     if (pc.valid && !(c->debug & 2) && pc.gen == c->geom_gen && pc.tree == c->obj->tree_version && pc.mode == mode &&
-        pc.nranks == nr && pc.rank == rk && pc.argb == argb && pc.hit == hit && !memcmp(pc.xf, xf, sizeof pc.xf)) {
+        pc.nranks == nr && pc.rank == rk && !memcmp(pc.xf, xf, sizeof pc.xf)) {
         p = pc.p;  // the same frame as the last one: its geometry stands
+        p.argb = argb;
+        p.hit = hit;
     } else {
         if ((rc = fill_params(c, xform, tile, argb, hit, mode, p))) return rc;
         pc.valid = !(c->debug & 2);
@@ -1082,19 +1102,30 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
         pc.mode = mode;
         pc.nranks = nr;
         pc.rank = rk;
-        pc.argb = argb;
-        pc.hit = hit;
         pc.p = p;
     }
     if (mode == RT_MODE_KD && effective_kernel(c) == 3) c->last_rays = p.rays;
     int trial;
     p.any_order = any_order_for(c, flags, stream, trial) | ((c->debug & 16) ? 4 : 0);
     hipStream_t st = (hipStream_t)stream;
+    // a trial frame is timed alone: with frames in flight on other lanes it
+    // starts after theirs and their later frames start after it
+    const bool solo = trial >= 0 && c->nactive > 1;
+    for (int l = 0; solo && l < c->nactive; l++) {
+        if (c->active[l] == st) continue;
+        if ((rc = hip_check(hipEventRecord(c->lane_ev[l], c->active[l]), "trial join")) ||
+            (rc = hip_check(hipStreamWaitEvent(st, c->lane_ev[l], 0), "trial join wait")))
+            return rc;
+    }
     if (trial >= 0 && (rc = hip_check(hipEventRecord(c->tune_ev[2 * trial], st), "order trial start"))) return rc;
     if ((rc = launch_split(c, p, mode, flags, stream))) return rc;
     if (trial >= 0) {
         if ((rc = hip_check(hipEventRecord(c->tune_ev[2 * trial + 1], st), "order trial stop"))) return rc;
         c->tune_pending = c->tune_next == kTuneTrials;
+        for (int l = 0; solo && l < c->nactive; l++)
+            if (c->active[l] != st &&
+                (rc = hip_check(hipStreamWaitEvent(c->active[l], c->tune_ev[2 * trial + 1], 0), "trial fork wait")))
+                return rc;
     }
     return p.cost ? cost_feedback(c, p, stream) : RT_OK;
 }
@@ -1312,6 +1343,10 @@ extern "C" void rt_camera_destroy(rt_camera* c) {
     for (hipEvent_t e : c->loop_ev)
         if (e) (void)hipEventDestroy(e);
     if (c->side) (void)hipStreamDestroy(c->side);
+    for (int k = 0; k <= RT_LOOP_MAX_LANES; k++) {
+        if (c->lanes[k]) (void)hipStreamDestroy(c->lanes[k]);
+        if (c->lane_ev[k]) (void)hipEventDestroy(c->lane_ev[k]);
+    }
     delete c;
 }
 
@@ -1408,18 +1443,44 @@ extern "C" int64_t rt_camera_debug_read(rt_camera* c, uint64_t* out, int64_t n) 
 // only after its gather has read it (events).  The host work per frame is the
 // cached launch (render_common) plus, with comm, the cached-rectangle gather:
 // a Python loop around the same calls costs tens of microseconds per frame.
+// The camera's lanes for a loop of L frames in flight: L render lanes and,
+// with a gather, one comm lane (index RT_LOOP_MAX_LANES), created on first
+// use, each with an event.
+static int ensure_lanes(rt_camera* c, int L, bool comm) {
+    int rc;
+    for (int k = 0; k <= RT_LOOP_MAX_LANES; k++) {
+        if (k >= L && !(comm && k == RT_LOOP_MAX_LANES)) continue;
+        if (!c->lanes[k] && (rc = hip_check(hipStreamCreateWithFlags(&c->lanes[k], hipStreamNonBlocking), "lane stream")))
+            return rc;
+        if (!c->lane_ev[k] && (rc = hip_check(hipEventCreateWithFlags(&c->lane_ev[k], hipEventDisableTiming), "lane event")))
+            return rc;
+    }
+    return RT_OK;
+}
+
 extern "C" int rt_run_frames(rt_camera* c, rt_comm* comm, const rt_frame_loop* a, int32_t nframes, int64_t* seq,
                              double* kernel_ms_avg, int32_t* kernel_ms_frames, double* host_ms) {
-    if (!c || !a || !seq || nframes < 0 || a->nbuf < 1 || a->nbuf > RT_LOOP_MAX_BUF)
+    if (!c || !a || !seq || nframes < 0 || a->nbuf < 1 || a->nbuf > RT_LOOP_MAX_BUF || a->inflight < 0 ||
+        a->inflight > RT_LOOP_MAX_LANES)
         return fail(RT_ERR_INVALID, "rt_run_frames: bad argument");
+    const int L = std::max(1, (int)a->inflight);
+    if (L > 1 && !comm && a->nbuf % L)
+        return fail(RT_ERR_INVALID, "rt_run_frames: %d buffer sets for %d frames in flight (need a multiple)", a->nbuf, L);
     for (int k = 0; k < a->nbuf; k++)
         if (!a->d_local[k] || (comm && (!a->d_scratch[k] || !a->comm_stream)))
             return fail(RT_ERR_INVALID, "rt_run_frames: missing buffer of set %d", k);
     DeviceGuard g(c->device);
     hipStream_t rs = (hipStream_t)a->render_stream, cs = (hipStream_t)a->comm_stream;
     int rc;
+    if (L > 1 && (rc = ensure_lanes(c, L, comm != nullptr))) return rc;
+    // the streams frames are issued to: the caller's, or the camera's lanes
+    hipStream_t lane[RT_LOOP_MAX_LANES];
+    for (int l = 0; l < L; l++) lane[l] = L > 1 ? c->lanes[l] : rs;
+    const hipStream_t gs = L > 1 && comm ? c->lanes[RT_LOOP_MAX_LANES] : cs;
     hipEvent_t rendered[RT_LOOP_MAX_BUF] = {}, sent[RT_LOOP_MAX_BUF] = {};
+    bool used[RT_LOOP_MAX_BUF] = {};
     auto cleanup = [&]() {
+        c->nactive = 0;
         for (int k = 0; k < RT_LOOP_MAX_BUF; k++) {
             if (rendered[k]) (void)hipEventDestroy(rendered[k]);
             if (sent[k]) (void)hipEventDestroy(sent[k]);
@@ -1442,32 +1503,57 @@ extern "C" int rt_run_frames(rt_camera* c, rt_comm* comm, const rt_frame_loop* a
         }
         c->loop_ev.push_back(e);
     }
+    // lanes start after the caller's queued work (fork) ...
+    if (L > 1) {
+        hipEvent_t fork = c->lane_ev[0];
+        rc = hip_check(hipEventRecord(fork, rs), "lane fork");
+        for (int l = 0; !rc && l < L; l++) rc = hip_check(hipStreamWaitEvent(lane[l], fork, 0), "lane fork wait");
+        if (!rc && comm && (rc = hip_check(hipEventRecord(fork, cs), "lane fork")) == RT_OK)
+            rc = hip_check(hipStreamWaitEvent(gs, fork, 0), "lane fork wait");
+        if (rc) {
+            cleanup();
+            return rc;
+        }
+        c->nactive = L;
+        for (int l = 0; l < L; l++) c->active[l] = lane[l];
+    }
     const rt_tile* tile = a->tile.nranks > 0 ? &a->tile : nullptr;
     const auto h0 = std::chrono::steady_clock::now();
-    for (int32_t j = 0; j < nframes; j++) {
+    for (int32_t j = 0; j < nframes && !rc; j++) {
         const int k = (int)((*seq) % a->nbuf);
         ++*seq;
+        hipStream_t ls = lane[j % L];
+        // set k is rendered again once the gather that last read it is done
+        if (comm && used[k] && (rc = hip_check(hipStreamWaitEvent(ls, sent[k], 0), "render wait"))) break;
+        used[k] = true;
         const bool timed = every > 0 && j % every == 0;
         const int64_t t = every > 0 ? j / every : 0;
-        rc = timed ? hip_check(hipEventRecord(c->loop_ev[(size_t)(2 * t)], rs), "loop timing") : RT_OK;
-        if (!rc) rc = render_common(c, a->xform, a->mode, a->flags, tile, a->d_local[k], nullptr, a->render_stream);
-        if (!rc && timed) rc = hip_check(hipEventRecord(c->loop_ev[(size_t)(2 * t + 1)], rs), "loop timing");
+        rc = timed ? hip_check(hipEventRecord(c->loop_ev[(size_t)(2 * t)], ls), "loop timing") : RT_OK;
+        if (!rc) rc = render_common(c, a->xform, a->mode, a->flags, tile, a->d_local[k], nullptr, ls);
+        if (!rc && timed) rc = hip_check(hipEventRecord(c->loop_ev[(size_t)(2 * t + 1)], ls), "loop timing");
         if (!rc && comm) {
-            // frame j renders into set k once the gather that last read it is done
-            if ((rc = hip_check(hipEventRecord(rendered[k], rs), "rendered")) ||
-                (rc = hip_check(hipStreamWaitEvent(cs, rendered[k], 0), "comm wait")) ||
-                (rc = rt_comm_gather_frame(comm, c, a->xform, a->mode, a->d_local[k], a->d_scratch[k], a->d_frame[k],
-                                           a->comm_stream)) ||
-                (rc = hip_check(hipEventRecord(sent[k], cs), "sent")))
-                break;
-            const int kn = (int)((*seq) % a->nbuf);
-            rc = hip_check(hipStreamWaitEvent(rs, sent[kn], 0), "render wait");
+            rc = hip_check(hipEventRecord(rendered[k], ls), "rendered");
+            if (!rc) rc = hip_check(hipStreamWaitEvent(gs, rendered[k], 0), "comm wait");
+            if (!rc) rc = rt_comm_gather_frame(comm, c, a->xform, a->mode, a->d_local[k], a->d_scratch[k], a->d_frame[k], gs);
+            if (!rc) rc = hip_check(hipEventRecord(sent[k], gs), "sent");
         }
-        if (rc) break;
     }
     if (host_ms) *host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
+    // ... and the caller's streams wait for the lanes (join)
+    if (!rc && L > 1) {
+        for (int l = 0; l < L && !rc; l++) {
+            rc = hip_check(hipEventRecord(c->lane_ev[l], lane[l]), "lane join");
+            if (!rc) rc = hip_check(hipStreamWaitEvent(rs, c->lane_ev[l], 0), "lane join wait");
+        }
+        if (!rc && comm) {
+            rc = hip_check(hipEventRecord(c->lane_ev[RT_LOOP_MAX_LANES], gs), "lane join");
+            if (!rc) rc = hip_check(hipStreamWaitEvent(cs, c->lane_ev[RT_LOOP_MAX_LANES], 0), "lane join wait");
+        }
+    }
+    c->nactive = 0;
     if (!rc) rc = hip_check(hipStreamSynchronize(rs), "loop sync");
     if (!rc && comm) rc = hip_check(hipStreamSynchronize(cs), "loop sync");
+    if (rc) (void)hipDeviceSynchronize();  // nothing of this loop may still use the events
     cleanup();
     if (rc) return rc;
     double sum = 0.0;

@@ -399,11 +399,13 @@ class FrameLoop:
     """rt_run_frames: the frame loop in native code.  `locals_` are the
     render targets (one per buffer set); with `comm` (a NativeFrameGather),
     each frame is gathered to rank 0 on `comm_stream` while the next renders.
+    `inflight` > 1 keeps that many frames in flight on the library's own
+    render lanes (without comm, len(locals_) must be a multiple of it).
     ``run(n)`` renders n frames and returns (kernel ms mean, timed frames);
     it synchronises the streams before returning."""
 
     def __init__(self, cam: "Camera", locals_, xform=None, mode: int = RT_MODE_KD, flags: int = 0, tile=None,
-                 render_stream=None, comm=None, comm_stream=None, event_every: int = 0):
+                 render_stream=None, comm=None, comm_stream=None, event_every: int = 0, inflight: int = 1):
         n = len(locals_)
         if not 1 <= n <= _lib.RT_LOOP_MAX_BUF:
             raise ValueError(f"FrameLoop: 1..{_lib.RT_LOOP_MAX_BUF} buffer sets")
@@ -424,6 +426,7 @@ class FrameLoop:
         a.render_stream = render_stream
         a.comm_stream = comm_stream
         a.event_every = event_every
+        a.inflight = inflight
         self._a = a
         self._locals = list(locals_)
         self.seq = C.c_int64(0)

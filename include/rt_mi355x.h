@@ -244,8 +244,20 @@ void rt_comm_destroy(rt_comm* c);
  * events on render_stream; *kernel_ms_avg / *kernel_ms_frames receive their
  * mean and count; *host_ms (may be NULL) the host time spent enqueueing the
  * frames.  Synchronises both streams before returning.  tile.nranks 0 (or
- * 1) renders the whole frame. */
+ * 1) renders the whole frame.
+ * inflight (0 or 1: off) > 1 keeps that many frames in flight: frame j
+ * renders on the library's render lane j % inflight (streams of the camera,
+ * created once, each on a hardware queue of its own while queues are free),
+ * the gather on the library's comm lane; the lanes start after the work
+ * already queued on render_stream / comm_stream, and those streams wait for
+ * the lanes before the call returns.  Frames that share a buffer set are
+ * ordered (a set is rendered again once its last frame, or its gather, is
+ * done), so without comm nbuf must be a multiple of inflight.  Frames are
+ * independent reads of the scene; a frame's tail overlaps the next frame's
+ * start, where one frame leaves most CUs idle.  Timing events then bracket
+ * renders that share the GPU with another frame. */
 #define RT_LOOP_MAX_BUF 4
+#define RT_LOOP_MAX_LANES 4
 typedef struct rt_frame_loop {
     const float* xform;
     uint32_t mode, flags;
@@ -257,6 +269,7 @@ typedef struct rt_frame_loop {
     void* render_stream;
     void* comm_stream;
     int32_t event_every;
+    int32_t inflight;
 } rt_frame_loop;
 int rt_run_frames(rt_camera* cam, rt_comm* comm, const rt_frame_loop* loop, int32_t nframes, int64_t* seq,
                   double* kernel_ms_avg, int32_t* kernel_ms_frames, double* host_ms);

@@ -118,6 +118,34 @@ def test_native_frame_loop_single_gpu():
     assert s.cam.device_error() == 0
 
 
+@pytest.mark.parametrize("inflight,nbuf", [(2, 2), (2, 4), (3, 3), (4, 4)])
+def test_native_frame_loop_inflight(inflight, nbuf):
+    """Frames in flight on the camera's render lanes: every buffer holds the
+    oracle's frame (committed hash) after enough frames for the tile-cost
+    samples and cost-order uploads to run while other lanes render."""
+    import hashlib
+    import torch
+    from cpp_cuda_raytracer_dev_amd import _lib
+    ent = H.frame_hashes()["dragon_960x540_m0"]
+    s = H.GpuScene("dragon", 960, 540)
+    st = torch.cuda.Stream()
+    bufs = [torch.full((960 * 540,), 0x7BADBEEF, dtype=torch.int32, device="cuda:0") for _ in range(nbuf)]
+    torch.cuda.synchronize()
+    loop = R.FrameLoop(s.cam, bufs, render_stream=st.cuda_stream, event_every=5, inflight=inflight)
+    ms, cnt, host = loop.run(80)
+    assert cnt == 16 and ms > 0
+    for b in bufs:
+        a = b.cpu().numpy().view(np.uint32)
+        if H.mesh_matches(ent):
+            assert hashlib.sha256(a.tobytes()).hexdigest() == ent["argb_sha"]
+        else:
+            assert (a == bufs[0].cpu().numpy().view(np.uint32)).all()
+    assert s.cam.device_error() == 0
+    if nbuf == 2 and inflight == 2:
+        with pytest.raises(_lib.RtError):  # sets must split evenly over the lanes
+            R.FrameLoop(s.cam, bufs[:1] * 3, render_stream=st.cuda_stream, inflight=2).run(1)
+
+
 def test_auto_rays_choice():
     """RT_OPT_RAYS 0 (default): 8 pixels per wave when the object's screen
     rectangle holds few 16-ray units (dragon 960x540), else 16 (1080p)."""
@@ -859,6 +887,17 @@ def test_native_comm_world1():
         ms, n, host = loop.run(9)
         assert n == 5 and ms > 0 and host > 0
         assert (ng.frames[loop.last_set()].cpu().numpy().view(np.uint32) == fulls[0]).all()
+        # two frames in flight on the library's lanes, gathers on its comm
+        # lane: every set's gathered frame is whole
+        for f in ng.frames:
+            f.fill_(0x7BADBEEF)
+        torch.cuda.synchronize()
+        loop = R.FrameLoop(s.cam, ng.local, mode=0, render_stream=rs.cuda_stream, comm=ng,
+                           comm_stream=cs.cuda_stream, event_every=3, inflight=2)
+        ms, n, host = loop.run(12)
+        assert n == 4 and ms > 0
+        for f in ng.frames:
+            assert (f.cpu().numpy().view(np.uint32) == fulls[0]).all()
         ng.close()
     finally:
         dist.destroy_process_group()

@@ -37,6 +37,30 @@ def test_cpp_facade_and_headless_driver_compile(tmp_path):
     assert out.exists()
 
 
+def test_ctypes_structs_match_header(tmp_path):
+    """The Python mirrors of the ABI's structs have the C layout (size and
+    every field's offset), compiled from include/rt_mi355x.h here."""
+    import ctypes as C
+    import subprocess
+    structs = {"rt_frame_loop": _lib.RtFrameLoop, "rt_tile": _lib.RtTile}
+    lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "rt_mi355x.h"', "int main(void) {"]
+    for name, py in structs.items():
+        lines.append(f'printf("{name} size %zu\\n", sizeof({name}));')
+        for f in py._fields_:
+            lines.append(f'printf("{name} {f[0]} %zu\\n", offsetof({name}, {f[0]}));')
+    lines += ["return 0;", "}"]
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines) + "\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.dirname(HEADER), "-o", str(exe), str(src)], check=True)
+    got = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    for line in filter(None, got):
+        name, field, val = line.split()
+        py = structs[name]
+        want = C.sizeof(py) if field == "size" else getattr(py, field).offset
+        assert int(val) == want, (name, field, int(val), want)
+
+
 def test_epsilon_threshold_is_exact():
     c = np.array([0x24E69595], np.uint32).view(np.float32)[0]
     assert np.float64(c) >= 1e-16
