@@ -144,6 +144,11 @@ extern "C" int rt_comm_create(int device, int32_t nranks, int32_t rank, const ui
 
 extern "C" int rt_comm_gather_frame(rt_comm* c, rt_camera* cam, const float* xform, uint32_t mode,
                                     const uint32_t* d_local, uint32_t* d_scratch, uint32_t* d_frame, void* stream) {
+    return rt::comm_gather_frame(c, cam, xform, mode, d_local, d_scratch, d_frame, stream, false, nullptr);
+}
+
+int rt::comm_gather_frame(rt_comm* c, rt_camera* cam, const float* xform, uint32_t mode, const uint32_t* d_local,
+                          uint32_t* d_scratch, uint32_t* d_frame, void* stream, bool rect_only, int32_t rect_out[4]) {
     if (!c || !cam || !d_local) return fail(RT_ERR_INVALID, "rt_comm_gather_frame: bad argument");
     if ((c->rank == 0 && !d_frame) || (c->nranks > 1 && !d_scratch))
         return fail(RT_ERR_INVALID, "rt_comm_gather_frame: missing scratch or frame buffer");
@@ -155,6 +160,7 @@ extern "C" int rt_comm_gather_frame(rt_comm* c, rt_camera* cam, const float* xfo
     // exchange
     int32_t rect[4];
     if ((rc = rt_frame_rect(cam, xform, mode, c->nranks, rect))) return rc;
+    if (rect_out) memcpy(rect_out, rect, sizeof rect);
     const Rccl* r = rccl();
     Guard g(c->device);
     if (!g.ok) return fail(RT_ERR_HIP, "rt_comm_gather_frame: hipSetDevice(%d) failed", c->device);
@@ -172,7 +178,7 @@ extern "C" int rt_comm_gather_frame(rt_comm* c, rt_camera* cam, const float* xfo
             if (rc) return rc;
             if ((rc = nccl_check(r, e, "ncclGroupEnd"))) return rc;
         }
-        return rt_unpack_rect(c->device, w, h, c->nranks, rect, d_local, d_scratch, d_frame, stream);
+        return launch_unpack_rect(w, h, c->nranks, rect, d_local, d_scratch, d_frame, stream, rect_only);
     }
     const int64_t n = rt_rect_pixels(w, h, c->nranks, c->rank, rect);
     if (n <= 0) return RT_OK;

@@ -592,8 +592,13 @@ bool set_fine_region(rt_camera* c, TraceParams& p, int per_wave, bool fused) {
 // units to fill the GPU -- then 8, which doubles the waves and halves the
 // heaviest unit's pool chain.  Measured on the dragon stand-in (one GPU):
 // 960x540 (3.4k 16-ray units) 67.7 -> 52.7 us with 8 rays, 1920x1080 (13.4k
-// units) 88 -> 130 us.
-constexpr int64_t kAutoRaysMinUnits = 8192;
+// units) 88 -> 130 us, one frame at a time.  With two frames in flight
+// (tools/project_ranks.py --inflight 2, frame period per rank, 16 vs 8
+// rays): 1920x1080 whole 74 vs 139 us, a rank of 2 (6.7k units) 43 vs 70,
+// of 4 (3.4k) 42 vs 36, of 8 (1.7k) 41 vs 24; 960x540 whole (3.4k) 35 vs 38,
+// a rank of 2 34 vs 22.  The 16-ray floor near 41 us is the heaviest unit's
+// chain; 8 rays scale with the work.
+constexpr int64_t kAutoRaysMinUnits = 4096;
 
 int auto_rays(const rt_camera* c, const TraceParams& p) {
     double r[4];
@@ -1479,6 +1484,10 @@ extern "C" int rt_run_frames(rt_camera* c, rt_comm* comm, const rt_frame_loop* a
     const hipStream_t gs = L > 1 && comm ? c->lanes[RT_LOOP_MAX_LANES] : cs;
     hipEvent_t rendered[RT_LOOP_MAX_BUF] = {}, sent[RT_LOOP_MAX_BUF] = {};
     bool used[RT_LOOP_MAX_BUF] = {};
+    // the rectangle each set's frame was last assembled with in this call:
+    // its background stands, so a frame with the same rectangle writes the
+    // rectangle alone (the frame buffers are the loop's during the call)
+    int32_t set_rect[RT_LOOP_MAX_BUF][4];
     auto cleanup = [&]() {
         c->nactive = 0;
         for (int k = 0; k < RT_LOOP_MAX_BUF; k++) {
@@ -1525,7 +1534,6 @@ extern "C" int rt_run_frames(rt_camera* c, rt_comm* comm, const rt_frame_loop* a
         hipStream_t ls = lane[j % L];
         // set k is rendered again once the gather that last read it is done
         if (comm && used[k] && (rc = hip_check(hipStreamWaitEvent(ls, sent[k], 0), "render wait"))) break;
-        used[k] = true;
         const bool timed = every > 0 && j % every == 0;
         const int64_t t = every > 0 ? j / every : 0;
         rc = timed ? hip_check(hipEventRecord(c->loop_ev[(size_t)(2 * t)], ls), "loop timing") : RT_OK;
@@ -1534,9 +1542,20 @@ extern "C" int rt_run_frames(rt_camera* c, rt_comm* comm, const rt_frame_loop* a
         if (!rc && comm) {
             rc = hip_check(hipEventRecord(rendered[k], ls), "rendered");
             if (!rc) rc = hip_check(hipStreamWaitEvent(gs, rendered[k], 0), "comm wait");
-            if (!rc) rc = rt_comm_gather_frame(comm, c, a->xform, a->mode, a->d_local[k], a->d_scratch[k], a->d_frame[k], gs);
+            int32_t rect[4] = {0, 0, 0, 0};
+            bool rect_only = false;
+            if (!rc && used[k]) {
+                int32_t nranks = 1;
+                rc = rt_comm_info(comm, &nranks, nullptr);
+                if (!rc) rc = rt_frame_rect(c, a->xform, a->mode, nranks, rect);
+                rect_only = !memcmp(rect, set_rect[k], sizeof rect);
+            }
+            if (!rc)
+                rc = comm_gather_frame(comm, c, a->xform, a->mode, a->d_local[k], a->d_scratch[k], a->d_frame[k], gs,
+                                       rect_only, set_rect[k]);
             if (!rc) rc = hip_check(hipEventRecord(sent[k], gs), "sent");
         }
+        used[k] = true;
     }
     if (host_ms) *host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
     // ... and the caller's streams wait for the lanes (join)

@@ -180,5 +180,11 @@ __host__ __device__ inline void rect_slots(int32_t b0, int32_t b1, int32_t nrank
 int launch_pack_rect(int32_t w, int32_t h, int32_t nranks, int32_t rank, const int32_t rect[4],
                      const uint32_t* local, uint32_t* out, void* stream);
 int launch_unpack_rect(int32_t w, int32_t h, int32_t nranks, const int32_t rect[4], const uint32_t* local0,
-                       const uint32_t* peers, uint32_t* frame, void* stream);
+                       const uint32_t* peers, uint32_t* frame, void* stream,
+                       bool rect_only = false);
+// rt_comm_gather_frame; rect_only: d_frame already holds this rectangle's
+// background (an earlier gather of the same rectangle into it), so rank 0
+// writes the rectangle alone.
+int comm_gather_frame(rt_comm* c, rt_camera* cam, const float* xform, uint32_t mode, const uint32_t* d_local,
+                      uint32_t* d_scratch, uint32_t* d_frame, void* stream, bool rect_only, int32_t rect_out[4]);
 }  // namespace rt

@@ -112,13 +112,21 @@ int launch_pack_rect(int32_t w, int32_t h, int32_t nranks, int32_t rank, const i
 }
 
 int launch_unpack_rect(int32_t w, int32_t h, int32_t nranks, const int32_t rect[4], const uint32_t* local0,
-                       const uint32_t* peers, uint32_t* frame, void* stream) {
+                       const uint32_t* peers, uint32_t* frame, void* stream, bool rect_only) {
     if ((int64_t)w * h == 0) return RT_OK;
     const int32_t vec = ((w & 3) == 0 && ((uintptr_t)frame & 15) == 0) ? 4 : 1;
-    const int32_t per_row = w / vec;
-    const dim3 grid((unsigned)((per_row + 255) / 256), (unsigned)h);
-    k_unpack_rect<<<grid, 256, 0, (hipStream_t)stream>>>(w, nranks, rect[0], rect[1], rect[2], rect[3], vec, local0,
-                                                         peers, frame);
+    int32_t y0 = 0, xa = 0, rows = h, cols = w;
+    if (rect_only) {
+        if (rect[0] >= rect[1] || rect[2] >= rect[3]) return RT_OK;
+        y0 = rect[2] * kTileH;
+        rows = std::min(rect[3] * kTileH, h) - y0;
+        xa = rect[0] - rect[0] % vec;
+        cols = rect[1] - xa;
+    }
+    const int32_t per_row = (cols + vec - 1) / vec;
+    const dim3 grid((unsigned)((per_row + 255) / 256), (unsigned)rows);
+    k_unpack_rect<<<grid, 256, 0, (hipStream_t)stream>>>(w, nranks, rect[0], rect[1], rect[2], rect[3], vec, y0, xa,
+                                                         local0, peers, frame);
     return check_launch<void>("k_unpack_rect");
 }
 

@@ -1699,15 +1699,17 @@ __global__ void k_pack_rect(int32_t w, int32_t x0, int32_t cw, int32_t s0, const
     out[(int64_t)row * cw + x] = local[((int64_t)s * kTileH + r) * w + x0 + x];
 }
 
-// Rank 0: frame row y (blockIdx.y) from rank 0's own packed buffer, a peer's
-// compact block (peers 1..N-1 back to back), or the background.
-// Each thread writes `vec` (4 or 1) consecutive pixels of the row; rows
-// outside the rectangle are pure background stores.
+// Rank 0: frame row y0 + blockIdx.y from rank 0's own packed buffer, a
+// peer's compact block (peers 1..N-1 back to back), or the background.
+// Each thread writes `vec` (4 or 1) consecutive pixels of the row from
+// column xa; rows outside the rectangle are pure background stores.  The
+// whole frame: y0 = xa = 0; the rectangle alone (its background already in
+// the frame): its rows, from column x0 rounded down to a multiple of vec.
 __global__ void k_unpack_rect(int32_t w, int32_t nranks, int32_t x0, int32_t x1, int32_t b0, int32_t b1, int32_t vec,
-                              const uint32_t* __restrict__ local0, const uint32_t* __restrict__ peers,
-                              uint32_t* __restrict__ frame) {
-    const int32_t y = blockIdx.y;
-    const int32_t xs = (blockIdx.x * blockDim.x + threadIdx.x) * vec;
+                              int32_t y0, int32_t xa, const uint32_t* __restrict__ local0,
+                              const uint32_t* __restrict__ peers, uint32_t* __restrict__ frame) {
+    const int32_t y = y0 + blockIdx.y;
+    const int32_t xs = xa + (blockIdx.x * blockDim.x + threadIdx.x) * vec;
     if (xs >= w) return;
     const int32_t band = y / kTileH, r = y - band * kTileH;
     const int32_t rank = band % nranks, slot = band / nranks;

@@ -12,6 +12,7 @@ import argparse
 import json
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -54,6 +55,9 @@ def main():
     ap.add_argument("--frames", type=int, default=300)
     ap.add_argument("--rays", type=int, default=0)
     ap.add_argument("--items", type=int, default=2)
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="frames in flight per rank (rt_frame_loop.inflight); the frame period then bounds the "
+                         "rank, not the kernel time")
     ap.add_argument("--ranks", default="1,2,4,8")
     ap.add_argument("--out", default="")
     ap.add_argument("--lib", default="", help="an experiment build of librt_mi355x.so (tools/build_variants.sh)")
@@ -77,19 +81,25 @@ def main():
     cam.set_option(_lib.RT_OPT_RAYS, a.rays)
     cam.set_option(_lib.RT_OPT_ITEMS, a.items)
     st = torch.cuda.Stream()
-    res = {"lib": a.lib or "librt_mi355x.so", "rays": a.rays, "items": a.items, "scene": a.scene, "view": a.view, "resolution": [w, h], "frames": a.frames, "per_n": {}}
+    res = {"lib": a.lib or "librt_mi355x.so", "inflight": a.inflight, "rays": a.rays, "items": a.items, "scene": a.scene, "view": a.view, "resolution": [w, h], "frames": a.frames, "per_n": {}}
     for n in [int(x) for x in a.ranks.split(",")]:
         npk = R.packed_pixels(w, h, n)
         rect = np.zeros(4, np.int32)
         _lib.call("rt_frame_rect", cam._h, None, 0, n, _lib.ptr(rect))
         ranks = []
         for r in range(n):
-            buf = torch.zeros(npk, dtype=torch.int32, device="cuda:0")
-            loop = R.FrameLoop(cam, [buf], tile=(n, r), render_stream=st.cuda_stream, event_every=1)
+            bufs = [torch.zeros(npk, dtype=torch.int32, device="cuda:0") for _ in range(max(1, a.inflight))]
+            loop = R.FrameLoop(cam, bufs, tile=(n, r), render_stream=st.cuda_stream,
+                               event_every=1 if a.inflight <= 1 else 8, inflight=a.inflight)
             loop.run(20)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
             ms, cnt, host = loop.run(a.frames)
+            period = 1e3 * (time.perf_counter() - t0) / a.frames
+            if a.inflight > 1:
+                ms = period  # the rank's frame period with frames overlapping
             send = int(_lib.lib().rt_rect_pixels(w, h, n, r, _lib.ptr(rect))) * 4 if r else 0
-            ranks.append({"rank": r, "render_ms": round(ms, 5), "host_us_per_frame": round(1e3 * host / a.frames, 2),
+            ranks.append({"rank": r, "render_ms": round(ms, 5), "period_ms": round(period, 5), "host_us_per_frame": round(1e3 * host / a.frames, 2),
                           "rays_per_wave": cam.get_option(_lib.RT_OPT_RAYS_USED), "send_bytes": send})
         worst = max(x["render_ms"] for x in ranks)
         if a.stamps:
