@@ -1533,7 +1533,10 @@ extern "C" int rt_run_frames(rt_camera* c, rt_comm* comm, const rt_frame_loop* a
         ++*seq;
         hipStream_t ls = lane[j % L];
         // set k is rendered again once the gather that last read it is done
-        if (comm && used[k] && (rc = hip_check(hipStreamWaitEvent(ls, sent[k], 0), "render wait"))) break;
+        // (no barrier packet when that gather has already finished)
+        if (comm && used[k] && hipEventQuery(sent[k]) != hipSuccess &&
+            (rc = hip_check(hipStreamWaitEvent(ls, sent[k], 0), "render wait")))
+            break;
         const bool timed = every > 0 && j % every == 0;
         const int64_t t = every > 0 ? j / every : 0;
         rc = timed ? hip_check(hipEventRecord(c->loop_ev[(size_t)(2 * t)], ls), "loop timing") : RT_OK;

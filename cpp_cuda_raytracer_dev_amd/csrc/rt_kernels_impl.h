@@ -1047,6 +1047,137 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
     }
 }
 
+// Measured slower for primary rays on gfx950 (dragon 1080p 13.7k -> 12.6k
+// FPS, 960x540 27.4k -> 24.5k, two frames in flight; leaf batches of 16-64
+// the same): slot 1 given to a few leaves caps the interior pops at 64 per
+// iteration, which costs more than the divergence it removes.  Off by
+// default; -DRT_SPLIT_LEAF=1 builds it (with RT_LEAF_BATCH 1, leaves tested
+// every iteration, it passed the GPU parity suite; dragon 1080p with shadow
+// rays was the one config it sped up, 4.8k -> 5.5k FPS).
+#ifndef RT_SPLIT_LEAF
+#define RT_SPLIT_LEAF 0
+#endif
+#ifndef RT_LEAF_BATCH
+#define RT_LEAF_BATCH 1
+#endif
+
+// Pushes an interior visit's children into the split pool: interior children
+// on the interior stack (items[0, ni), growing up; all first children, then
+// all second ones, or the any-hit order), leaf children on the leaf stack
+// (items[cap - nl, cap), growing down).
+template <bool kAny, int any_order>
+__device__ __forceinline__ void push_split(uint4* items, int cap, int& ni, int& nl, const Visit& v) {
+    const bool la = (v.ca.x & kLeafBit) != 0, lb = (v.cb.x & kLeafBit) != 0;
+    const bool ia = v.ka && !la, ib = v.kb && !lb;
+    const bool fa = v.ka && la, fb = v.kb && lb;
+    Visit w = v;
+    w.ka = ia;
+    w.kb = ib;
+    ni += push_children<kAny, any_order>(items, ni, w);
+    const unsigned long long m1 = __ballot(fa), m2 = __ballot(fb);
+    const int n1 = __builtin_popcountll(m1);
+    if (fa) items[cap - nl - 1 - (int)lanes_below(m1)] = v.ca;
+    if (fb) items[cap - nl - 1 - n1 - (int)lanes_below(m2)] = v.cb;
+    nl += n1 + __builtin_popcountll(m2);
+}
+
+// The pool walk with leaves apart (RT_SPLIT_LEAF, two items per lane): the
+// pool holds an interior stack and a leaf stack, and each iteration's two
+// slots are wave-uniform in kind -- slot 0 up to 64 interior items, slot 1
+// up to 64 leaf items when any are pooled, else up to 64 more interior
+// items.  A slot of mixed items runs both the interior and the leaf code
+// under divergence, so every iteration of the mixed pool paid both paths
+// twice; here it pays each at most once.  The nearest hit does not depend on
+// the visiting order (every intersected node is visited; the minimum of
+// (w, path code) is order-free), and a pooled leaf waits at most until the
+// next iteration.  Capacity: popping k interior and j leaf items pushes at
+// most 2k, so k <= cap - slack - (ni + nl - j) keeps the pool within
+// cap - slack; when that leaves no room a single interior pop runs (a DFS
+// step, growing the interior stack by at most the height over a run) while
+// slot 1 drains up to 64 leaves.
+template <int kCap, int kVec, bool kTranslated, bool kCount, bool kAny, int kOrder = 0>
+__device__ __forceinline__ void pool_walk_split(const TraceParams& P, uint4* items, const float4* s_ray,
+                                                unsigned long long* s_key, uint32_t* s_tri, int n, int lane,
+                                                uint32_t& iters, uint32_t& popped, uint32_t& n_int, uint32_t& n_leaf,
+                                                uint32_t& n_acc, uint32_t& n_desc) {
+    const int cap = min(P.pool_cap, kCap);
+    const int slack = P.tree_height + 1;
+    int ni = n, nl = 0;
+    if (P.root_ref & kLeafBit) {  // a leaf root: the seeded items are leaf items
+        const uint4 v = items[lane < n ? lane : 0];
+        __builtin_amdgcn_wave_barrier();
+        if (lane < n) items[cap - n + lane] = v;
+        __builtin_amdgcn_wave_barrier();
+        ni = 0;
+        nl = n;
+    }
+    while (ni + nl > 0) {
+        // slot 1 tests pooled leaves when slot 1 has no interior items to
+        // take anyway, or once RT_LEAF_BATCH leaves wait (wave-uniform)
+        // or when the pool has no room for a parallel pop: single interior
+        // pops then run with the leaves drained, so the pool cannot grow
+        // past the DFS bound
+        const bool leafslot = nl > 0 && (ni <= 64 || nl >= RT_LEAF_BATCH || cap - slack - (ni + nl) < 1);
+        const int j = leafslot ? min(nl, 64) : 0;
+        int k = min(min(ni, leafslot ? 64 : 128), cap - slack - (ni + nl - j));
+        if (k < 1) k = ni > 0 ? 1 : 0;
+        iters++;
+        popped += (uint32_t)(k + j);
+        const int bi = ni - k;
+        bool act0 = lane < k;
+        bool act1 = leafslot ? lane < j : lane + 64 < k;
+        // idle lanes re-read a live item (its record address is valid)
+        const int i0 = k > 0 ? bi + (act0 ? lane : 0) : cap - nl;
+        const int i1 = leafslot ? cap - nl + (act1 ? lane : 0) : bi + (act1 ? lane + 64 : 0);
+        const uint4 it0 = items[i0];
+        const uint4 it1 = items[i1];
+        __builtin_amdgcn_wave_barrier();
+        if (kAny && (!kCount || kOrder >= 4)) {
+            if (act0 && s_key[it0.w >> 26] == 0ull) act0 = false;
+            if (act1 && s_key[it1.w >> 26] == 0ull) act1 = false;
+        }
+        const float4* p0 = record_of(P, it0.x);
+        const float4* p1 = record_of(P, it1.x);
+        const float4 a0 = p0[0], a1 = p0[1], a2 = p0[2], a3 = p0[3];
+        const float4 b0 = p1[0], b1 = p1[1], b2 = p1[2], b3 = p1[3];
+        asm volatile("" ::"v"(a0.x), "v"(a0.y), "v"(a0.z), "v"(a0.w), "v"(a1.x), "v"(a1.y), "v"(a1.z), "v"(a1.w),
+                     "v"(a2.x), "v"(a2.y), "v"(a2.z), "v"(a2.w), "v"(a3.x), "v"(a3.y), "v"(a3.z), "v"(a3.w));
+        asm volatile("" ::"v"(b0.x), "v"(b0.y), "v"(b0.z), "v"(b0.w), "v"(b1.x), "v"(b1.y), "v"(b1.z), "v"(b1.w),
+                     "v"(b2.x), "v"(b2.y), "v"(b2.z), "v"(b2.w), "v"(b3.x), "v"(b3.y), "v"(b3.z), "v"(b3.w));
+        int ti = bi, tl = nl - j;
+        {
+            Visit v0;
+            v0.ka = v0.kb = false; v0.cand = false;
+            if (act0)
+                visit_interior<kTranslated, kCount>(s_ray + (size_t)(it0.w >> 26) * kVec, it0, a0, a1, a2, a3, v0,
+                                                    n_int, n_desc);
+            push_split<kAny, (kOrder & 3)>(items, cap, ti, tl, v0);
+        }
+        {
+            Visit v1;
+            v1.ka = v1.kb = false; v1.cand = false;
+            if (leafslot) {
+                if (act1)
+                    visit_leaf<kTranslated, kCount, kAny>(s_ray + (size_t)(it1.w >> 26) * kVec, it1, b0, b1, b2, v1,
+                                                          n_leaf, n_acc);
+                record_candidate<kAny>(s_key, s_tri, it1, v1);
+            } else {
+                if (act1)
+                    visit_interior<kTranslated, kCount>(s_ray + (size_t)(it1.w >> 26) * kVec, it1, b0, b1, b2, b3, v1,
+                                                        n_int, n_desc);
+                push_split<kAny, (kOrder & 3)>(items, cap, ti, tl, v1);
+            }
+        }
+        if (ti + tl > cap) {  // unreachable by the pop rule above; guard anyway
+            if (lane == 0) atomicOr(P.err, 2);
+            break;
+        }
+        ni = ti;
+        nl = tl;
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 // Per-wave LDS of the wave-cooperative kernel.
 template <int kRays, int kCap, int kRayVec>
 struct WaveLds {
@@ -1083,8 +1214,12 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
     }
 
     int n = seed_root<kCount>(P, items, R, live, lane, C.n_int, C.n_desc);
-    pool_walk<kCap, kRayVec, kTranslated, kCount, false>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters, popped, C.n_int,
-                                                        C.n_leaf, C.n_acc, C.n_desc);
+    if (RT_SPLIT_LEAF && P.items > 1)
+        pool_walk_split<kCap, kRayVec, kTranslated, kCount, false>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters,
+                                                                  popped, C.n_int, C.n_leaf, C.n_acc, C.n_desc);
+    else
+        pool_walk<kCap, kRayVec, kTranslated, kCount, false>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters, popped,
+                                                            C.n_int, C.n_leaf, C.n_acc, C.n_desc);
     unsigned long long kbest = ~0ull;
     uint32_t best = kMiss;
     if (lane < kRays) {
@@ -1115,8 +1250,13 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
         }
         __builtin_amdgcn_wave_barrier();
         n = seed_root<kCount>(P, items, Sh, sh_live, lane, C.n_int, C.n_desc);
-        pool_walk<kCap, kRayVec, true, kCount, true, kShadow - 1>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters, popped, C.n_int,
-                                                    C.n_leaf, C.n_acc, C.n_desc);
+        if (RT_SPLIT_LEAF && P.items > 1)
+            pool_walk_split<kCap, kRayVec, true, kCount, true, kShadow - 1>(P, items, S_.ray, S_.key, S_.tri, n, lane,
+                                                                           iters, popped, C.n_int, C.n_leaf, C.n_acc,
+                                                                           C.n_desc);
+        else
+            pool_walk<kCap, kRayVec, true, kCount, true, kShadow - 1>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters,
+                                                                     popped, C.n_int, C.n_leaf, C.n_acc, C.n_desc);
         if (lane < kRays) shadowed = S_.key[lane] == 0ull;
     }
     if (P.dbg && lane == 0 && dbg_slot != kNoDbg) {  // diagnostics: the unit's start/end clock (100 MHz) and pool iterations

@@ -18,7 +18,10 @@ fi
 while read -r name rest; do
   [ -z "$name" ] && continue
   case $name in \#*) continue ;; esac
-  timeout -k 10 300 python bench.py $rest > $OUT/bench_$name.log 2>&1
+  # "variant:<lib.so> args..." runs bench.py against that build
+  cmd="python bench.py"
+  case $rest in variant:*) lib=${rest%% *}; cmd="python tools/bench_variant.py ${lib#variant:}"; rest=${rest#* } ;; esac
+  timeout -k 10 300 $cmd $rest > $OUT/bench_$name.log 2>&1
   rc=$?
   case $rc in 0|3|4) ;; *) echo "bench $name exited $rc"; tail -5 $OUT/bench_$name.log; exit $rc ;; esac
 done < "$ARGS"
