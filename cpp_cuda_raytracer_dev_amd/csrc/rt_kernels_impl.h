@@ -636,8 +636,12 @@ __device__ __forceinline__ uint32_t code_key(uint32_t marked) {
 #ifndef RT_POOL_CAP_R16
 #define RT_POOL_CAP_R16 352
 #endif
+// 8 rays: 448 items (30.6 KB per 4-wave block, 5 blocks per CU).  Two
+// frames in flight (r02): 960x540 27.4k FPS at 512 (34.7 KB, 4 blocks),
+// 31.2k at 448, 33.1k at 384; a rank of 4 at 1080p 36.7 / 32.8 / 31.1 us, of
+// 8 24.1 / 24.2 / 25.9 us: 448 loses nowhere.
 #ifndef RT_POOL_CAP_R8
-#define RT_POOL_CAP_R8 512
+#define RT_POOL_CAP_R8 448
 #endif
 template <int kRays>
 constexpr int pool_cap_for() {
@@ -1409,7 +1413,16 @@ __device__ __forceinline__ unsigned long long coarse_root(const TraceParams& P, 
 // (2,2,2) to the hit, walked from the light with the reference's rules.
 // One fine tile per block (the tiles covering the root box's screen
 // rectangle, or the whole frame), one unit per wave.
-#ifdef RT_KD3_WAVES_PER_SIMD
+// Occupancy: a 16-ray block's LDS (26 KB) admits 6 blocks per CU, and 88
+// VGPRs would admit 5 waves per SIMD; asking for 6 makes the compiler fit 80
+// (4 VGPRs spill to scratch in the timed variant).  Measured with two frames
+// in flight: dragon 1080p 13.7k -> 14.7k FPS, the 93 % fill view 940 ->
+// 873 us per frame; one frame at a time unchanged (86.7 -> 88.8 us).  The
+// 8-ray blocks are LDS-bound at 4 and keep their registers.  0: no bound.
+#ifndef RT_KD3_WAVES_PER_SIMD
+#define RT_KD3_WAVES_PER_SIMD 6
+#endif
+#if RT_KD3_WAVES_PER_SIMD > 0
 #define RT_KD3_BOUNDS(threads) __launch_bounds__(threads, RT_KD3_WAVES_PER_SIMD)
 #else
 #define RT_KD3_BOUNDS(threads) __launch_bounds__(threads)
