@@ -601,12 +601,19 @@ def main():
         torch.cuda.synchronize(dev)
     solo = None
     if not isinstance(loop, PyLoop) and inflight > 1 and a.solo_frames > 0:
-        # the roofline's kernel time: solo frames (one in flight, each
-        # bracketed), untimed; the timed frames overlap and share the GPU
+        # the roofline's kernel time: solo frames (one in flight) back to
+        # back, untimed, one event pair around the batch (per-frame event
+        # pairs add ~5 us of queue time to each bracketed launch); the timed
+        # frames overlap and share the GPU
         sl = R.FrameLoop(cam, [ng.local[0] if ng is not None else outs[0]], xform=xf, mode=a.mode, flags=sflag,
-                         tile=tile if multi else None, render_stream=sptr, event_every=1, inflight=1)
-        solo = sl.run(a.solo_frames)[:2]
+                         tile=tile if multi else None, render_stream=sptr, event_every=0, inflight=1)
+        sl.run(20)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        sl.run(a.solo_frames)
+        e1.record(stream)
         torch.cuda.synchronize(dev)
+        solo = (e0.elapsed_time(e1) / a.solo_frames, a.solo_frames)
     if multi:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -624,8 +631,9 @@ def main():
     kern_ms_timed, n_ev_timed = kern_ms, n_ev
     if solo is not None:
         kern_ms, n_ev = solo
-    kern_label = (f"{n_ev} solo frames before the timed region (one in flight, each bracketed); the timed frames "
-                  f"keep {inflight} in flight" if solo is not None else
+    kern_label = (f"mean period of {n_ev} solo frames back to back before the timed region (one in flight; kernel "
+                  f"+ the launch gap, an upper bound of the kernel time); the timed frames keep {inflight} in flight"
+                  if solo is not None else
                   f"{n_ev} of {a.steps} timed frames (every {max(1, a.event_every)})")
     kern_extra = ({"kernel_ms_avg_timed": round(kern_ms_timed, 5),
                    "kernel_ms_timed_frames": f"{n_ev_timed} of {a.steps} timed frames (every {a.event_every}), "
@@ -766,6 +774,10 @@ def main():
                 "kernel_ms_avg_max_rank": round(kern_ms_max, 5),
                 **kern_extra,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
+                # with frames in flight, launches overlap: the bytes of one
+                # frame over the frame period (elapsed / steps) as well
+                "achieved_per_frame_period": round(bytes_per_launch / (elapsed / a.steps) / 1e9, 1),
+                "frac_per_frame_period": round(bytes_per_launch / (elapsed / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
                 "counts_per_launch": {"interior": int(cnt[0]), "leaf": int(cnt[1]), "accept": int(cnt[2]),
                                       "hit_pixels": int(cnt[3]), "pixels": my_pix},
                 **({"counts_full_shadow_walk": {"interior": int(full_walk[0]), "leaf": int(full_walk[1]),

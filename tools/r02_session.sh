@@ -52,6 +52,8 @@ fi
 if has prof; then
     step rocprof_c4 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c4" -o run -- \
         python3 bench.py --steps 1000 --warmup 100 --no-cpu-baseline
+    step rocprof_c4_solo 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c4_solo" -o run -- \
+        python3 bench.py --steps 1000 --warmup 100 --no-cpu-baseline --inflight 1
     step rocprof_c2 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c2" -o run -- \
         python3 bench.py --scene rabbit_70k --width 960 --height 540 --mode 1 --steps 20 --warmup 2 --no-cpu-baseline
 fi
