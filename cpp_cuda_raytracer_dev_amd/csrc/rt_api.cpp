@@ -59,9 +59,25 @@ struct rt_camera {
     int pool_cap = kPoolCapMax;      // kOptPoolCap
     unsigned long long* d_dbg = nullptr;
     int64_t dbg_cap = 0;             // in u64
-    int32_t* d_order = nullptr;      // centre-out tile permutation
-    int64_t order_cap = 0;
+    int32_t* d_order = nullptr;      // the current tile permutation (a slot's buffer)
     int64_t order_key[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+    // Tile permutations live in a ring of slots: a new fine grid (a moving
+    // object changes it every frame) writes the next slot behind the
+    // caller's stream instead of rewriting the buffer earlier frames still
+    // read.  A slot is retired with an event on every stream that used it,
+    // and written again kOrderSlots grids later, once those have fired.
+    struct OrderSlot {
+        int32_t* d = nullptr;        // device permutation
+        int32_t* h = nullptr;        // pinned source of its upload
+        int64_t cap = 0;
+        hipEvent_t ev[8] = {};
+        int nev = 0;
+        bool device_sync = false;    // used by more streams than ev holds
+    } oslot[8];
+    int ocur = -1;
+    hipStream_t oused[8] = {};       // streams that launched with the current slot
+    int noused = 0;
+    bool oused_overflow = false;
     int coarse = 8;                  // kOptCoarse: coarse groups per wave (0 = off)
     std::vector<int32_t> centre;     // centre-out permutation of the current fine grid (host copy)
     // 8x8 groups (x / 8, y / 8) holding a pixel whose primary ray has a zero
@@ -79,7 +95,7 @@ struct rt_camera {
     uint32_t* h_cost = nullptr;      // pinned D2H target
     int32_t* h_order = nullptr;      // pinned H2D source
     int64_t host_cap = 0;            // tiles h_cost / h_order hold
-    hipEvent_t cost_ev = nullptr, order_ev = nullptr;
+    hipEvent_t cost_ev = nullptr, order_ev = nullptr, order_up_ev = nullptr;
     bool cost_pending = false, order_pending = false;
     int frames_since = 0;
     uint64_t layout_gen = 0, cost_gen = 0;   // fine-grid generation, and the one h_cost was read for
@@ -211,37 +227,89 @@ int prepare_camera_object(rt_camera* c) {
 // Centre-out permutation of the launch's tiles: blocks are dispatched in
 // index order, so the expensive tiles (the object sits mid-frame) start
 // first and the cheap background tiles fill in behind them.
-int ensure_order(rt_camera* c, const TraceParams& p) {
+constexpr int kOrderSlots = 8;
+
+// The current slot was launched with on `st`.
+void note_order_stream(rt_camera* c, hipStream_t st) {
+    for (int i = 0; i < c->noused; i++)
+        if (c->oused[i] == st) return;
+    if (c->noused < 8) c->oused[c->noused++] = st;
+    else c->oused_overflow = true;
+}
+
+int ensure_order(rt_camera* c, const TraceParams& p, hipStream_t st) {
     const int64_t key[8] = {p.tile_w, p.tile_h, p.tiles_x, p.block_rows, p.nranks, p.rank, p.fine_tx0, p.fine_s0};
     if (std::equal(key, key + 8, c->order_key)) return RT_OK;
     const int64_t n = (int64_t)p.tiles_x * p.block_rows;
     const int64_t per_band = kTileH / p.tile_h;
-    std::vector<int32_t> order((size_t)n);
-    std::vector<double> dist2((size_t)n);
+    // centre-out: a counting sort of the tiles by their distance from the
+    // frame centre in 2-pixel rings, index order within a ring (O(n): a
+    // moving object changes the grid every frame, and a comparison sort of
+    // the 13k tiles of a 1080p frame took ~0.3 ms of host time per frame)
+    std::vector<int32_t> order((size_t)n), ring((size_t)n);
     const double cx = 0.5 * c->w, cy = 0.5 * c->h;
+    const int32_t nring = (int32_t)(0.5 * std::sqrt(cx * cx + cy * cy)) + 2;
+    std::vector<int32_t> start((size_t)nring + 1, 0);
     for (int64_t t = 0; t < n; t++) {
         const int64_t row = t / p.tiles_x, tx = t % p.tiles_x + p.fine_tx0;
         const int64_t slot = row / per_band + p.fine_s0, yin = (row % per_band) * p.tile_h;
         const double x = (tx + 0.5) * p.tile_w;
         const double y = (double)((p.rank + slot * (int64_t)p.nranks) * kTileH + yin) + 0.5 * p.tile_h;
-        dist2[(size_t)t] = (x - cx) * (x - cx) + (y - cy) * (y - cy);
-        order[(size_t)t] = (int32_t)t;
+        const int32_t k = std::min(nring - 1, (int32_t)(0.5 * std::sqrt((x - cx) * (x - cx) + (y - cy) * (y - cy))));
+        ring[(size_t)t] = k;
+        start[(size_t)k + 1]++;
     }
-    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return dist2[(size_t)a] < dist2[(size_t)b]; });
-    // Earlier frames' kernels (on any stream) read d_order, and a cost-order
-    // upload may still be queued behind them: let them finish before the
-    // buffer is replaced or rewritten.  Runs only when the fine grid changes.
+    for (int32_t k = 0; k < nring; k++) start[(size_t)k + 1] += start[(size_t)k];
+    for (int64_t t = 0; t < n; t++) order[(size_t)start[(size_t)ring[(size_t)t]]++] = (int32_t)t;
     int rc;
-    if ((rc = hip_check(hipDeviceSynchronize(), "order sync"))) return rc;
-    c->order_pending = false;
-    c->order_gen = ~0ull;
-    if (c->order_cap < n) {
-        dev_free(c->d_order);
-        if ((rc = dev_alloc(&c->d_order, (size_t)n, "hipMalloc(order)"))) return rc;
-        c->order_cap = n;
+    // retire the current slot: an event on each stream that launched with it
+    // (a pending cost-order upload into it was issued on one of them)
+    if (c->ocur >= 0) {
+        auto& o = c->oslot[c->ocur];
+        o.nev = 0;
+        o.device_sync = c->oused_overflow;
+        for (int i = 0; i < c->noused && !o.device_sync; i++) {
+            if (!o.ev[i] && (rc = hip_check(hipEventCreateWithFlags(&o.ev[i], hipEventDisableTiming), "order event")))
+                return rc;
+            if ((rc = hip_check(hipEventRecord(o.ev[i], c->oused[i]), "order retire"))) return rc;
+            o.nev++;
+        }
     }
-    if ((rc = hip_check(hipMemcpy(c->d_order, order.data(), sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice), "H2D order")))
+    c->noused = 0;
+    c->oused_overflow = false;
+    // the next slot, once every launch that read it (and its upload) is done
+    const int sl = (c->ocur + 1) % kOrderSlots;
+    auto& o = c->oslot[sl];
+    if (o.device_sync) rc = hip_check(hipDeviceSynchronize(), "order slot sync");
+    for (int i = 0; !rc && i < o.nev; i++) rc = hip_check(hipEventSynchronize(o.ev[i]), "order slot wait");
+    if (rc) return rc;
+    o.nev = 0;
+    o.device_sync = false;
+    if (o.cap < n) {
+        dev_free(o.d);
+        if (o.h) (void)hipHostFree(o.h);
+        o.h = nullptr;
+        o.cap = 0;
+        if ((rc = dev_alloc(&o.d, (size_t)n, "hipMalloc(order)")) ||
+            (rc = hip_check(hipHostMalloc((void**)&o.h, sizeof(int32_t) * (size_t)n, 0), "hipHostMalloc(order)")))
+            return rc;
+        o.cap = n;
+    }
+    std::copy(order.begin(), order.end(), o.h);
+    if ((rc = hip_check(hipMemcpyAsync(o.d, o.h, sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice, st), "H2D order")))
         return rc;
+    // frames in flight on other lanes launch with it only after the upload
+    if (c->nactive > 1) {
+        if (!c->order_up_ev && (rc = hip_check(hipEventCreateWithFlags(&c->order_up_ev, hipEventDisableTiming), "order event")))
+            return rc;
+        if ((rc = hip_check(hipEventRecord(c->order_up_ev, st), "order upload event"))) return rc;
+        for (int l = 0; l < c->nactive; l++)
+            if (c->active[l] != st && (rc = hip_check(hipStreamWaitEvent(c->active[l], c->order_up_ev, 0), "order upload wait")))
+                return rc;
+    }
+    c->ocur = sl;
+    c->d_order = o.d;
+    c->order_gen = ~0ull;  // no cost order for this grid yet
     std::copy(key, key + 8, c->order_key);
     c->centre.swap(order);
     c->layout_gen++;
@@ -295,17 +363,17 @@ int ensure_cost(rt_camera* c, int64_t n) {
 // of equal total cost, one per XCD (blocks b and b + 8 share an XCD), each
 // run heaviest first, interleaved so block b takes the next tile of run b % 8:
 // the XCDs finish together and each L2 serves one screen region's subtrees.
-std::vector<int32_t> cost_order(const rt_camera* c, const TraceParams& p, bool xcd_split) {
+std::vector<int32_t> cost_order(const rt_camera* c, const TraceParams& p, bool xcd_split, const uint32_t* cost) {
     const int64_t n = (int64_t)p.tiles_x * p.block_rows;
     uint32_t mx = 0;
     auto wave_max = [&](int64_t t) {
         uint32_t m = 0;
-        for (int k = 0; k < kCostSlots; k++) m = std::max(m, c->h_cost[kCostSlots * (size_t)t + k]);
+        for (int k = 0; k < kCostSlots; k++) m = std::max(m, cost[kCostSlots * (size_t)t + k]);
         return m;
     };
     auto wave_sum = [&](int64_t t) {
         double m = 0;
-        for (int k = 0; k < kCostSlots; k++) m += c->h_cost[kCostSlots * (size_t)t + k];
+        for (int k = 0; k < kCostSlots; k++) m += cost[kCostSlots * (size_t)t + k];
         return m;
     };
     for (int64_t t = 0; t < n; t++) mx = std::max(mx, wave_max(t));
@@ -387,7 +455,7 @@ int cost_feedback(rt_camera* c, const TraceParams& p, void* stream) {
         c->cost_pending = c->order_pending = false;
         c->frames_since = 0;
         if (c->cost_gen != c->layout_gen || (int64_t)c->centre.size() != n) return RT_OK;  // stale sample
-        const std::vector<int32_t> ord = cost_order(c, p, c->tile_order == 4);
+        const std::vector<int32_t> ord = cost_order(c, p, c->tile_order == 4, c->h_cost);
         bool same = true;
         for (int64_t k = 0; k < n; k++) {
             same = same && c->h_order[k] == ord[(size_t)k];
@@ -646,7 +714,7 @@ bool frame_geometry(rt_camera* c, const float* xform, const rt_tile* tile, uint3
 }
 
 int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t* argb, int64_t* hit,
-                uint32_t mode, TraceParams& p) {
+                uint32_t mode, TraceParams& p, hipStream_t st) {
     const rt_scene* s = c->obj;
     p.inode = c->d_inode;
     p.trec = c->d_trec;
@@ -683,7 +751,7 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
     }
     p.cost = nullptr;
     if (c->tile_order >= 2 && p.tiles_x * p.block_rows > 0) {
-        int rc = ensure_order(c, p);
+        int rc = ensure_order(c, p, st);
         if (rc) return rc;
         p.order = c->d_order;
         if (c->tile_order >= 3 && kernel == 3) {
@@ -1099,7 +1167,7 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
         p.argb = argb;
         p.hit = hit;
     } else {
-        if ((rc = fill_params(c, xform, tile, argb, hit, mode, p))) return rc;
+        if ((rc = fill_params(c, xform, tile, argb, hit, mode, p, (hipStream_t)stream))) return rc;
         pc.valid = !(c->debug & 2);
         pc.gen = c->geom_gen;
         pc.tree = c->obj->tree_version;
@@ -1124,6 +1192,10 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
     }
     if (trial >= 0 && (rc = hip_check(hipEventRecord(c->tune_ev[2 * trial], st), "order trial start"))) return rc;
     if ((rc = launch_split(c, p, mode, flags, stream))) return rc;
+    if (p.order) {  // the streams that read the current order slot
+        note_order_stream(c, st);
+        if ((c->debug & 8) && c->side) note_order_stream(c, c->side);
+    }
     if (trial >= 0) {
         if ((rc = hip_check(hipEventRecord(c->tune_ev[2 * trial + 1], st), "order trial stop"))) return rc;
         c->tune_pending = c->tune_next == kTuneTrials;
@@ -1334,7 +1406,14 @@ extern "C" void rt_camera_destroy(rt_camera* c) {
     dev_free(c->d_trec);
     dev_free(c->d_inode);
     dev_free(c->d_tpair);
-    dev_free(c->d_order);
+    for (auto& o : c->oslot) {
+        dev_free(o.d);
+        if (o.h) (void)hipHostFree(o.h);
+        for (hipEvent_t e : o.ev)
+            if (e) (void)hipEventDestroy(e);
+    }
+    c->d_order = nullptr;
+    if (c->order_up_ev) (void)hipEventDestroy(c->order_up_ev);
     dev_free(c->d_dbg);
     dev_free(c->d_cost);
     if (c->h_cost) (void)hipHostFree(c->h_cost);
