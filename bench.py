@@ -450,6 +450,15 @@ def main():
                 acc += cam.counters(reset=True)
         mo.close()
         cnt = acc / a.steps  # mean per frame
+        # the same poses for the native loop (rt_frame_loop.xforms): pose i
+        # is the object after tick i, frame i renders it
+        mo = R.ObjectMotion(cam.pos, cam.o_prop["n"], cam.o_prop["u"], cam.cam_speed)
+        poses = []
+        for i in range(a.warmup + a.steps):
+            mo.tick(masks[i % len(masks)])
+            poses.append(np.asarray(mo.xform(), np.float32).reshape(12))
+        mo.close()
+        anim_xfs = np.stack(poses)
     else:
         cam.render_into(scratch, mode=a.mode, flags=R.RT_FLAG_COUNT | sflag, tile=tile if multi else None,
                         stream=sptr)
@@ -470,7 +479,7 @@ def main():
     my_pix = int(np.count_nonzero(np.repeat(np.arange((h + 7) // 8) % world == rank, 8)[:h])) * w
     bytes_per_launch = B_INT * int(cnt[0]) + B_LEAF * int(cnt[1]) + B_HIT * int(cnt[2]) + B_PIX * my_pix
 
-    loop_kind = a.loop if not masks else "python"  # a moving object ticks per frame in Python
+    loop_kind = a.loop
     inflight = max(1, a.inflight) if loop_kind == "native" else 1
     if a.event_every <= 0:
         a.event_every = 8 if (multi or inflight > 1) else 1
@@ -581,7 +590,8 @@ def main():
             return R.FrameLoop(cam, ng.local if ng is not None else outs, xform=xf, mode=a.mode, flags=sflag,
                                tile=tile if multi else None, render_stream=sptr, comm=ng,
                                comm_stream=cstream.cuda_stream if ng is not None else None,
-                               event_every=a.event_every, inflight=inflight)
+                               event_every=a.event_every, inflight=inflight,
+                               xforms=anim_xfs if masks else None)
         return PyLoop()
 
     loop = make_loop()
@@ -605,15 +615,19 @@ def main():
         # back, untimed, one event pair around the batch (per-frame event
         # pairs add ~5 us of queue time to each bracketed launch); the timed
         # frames overlap and share the GPU
+        # (a moving object: the timed frames' own poses, all of them)
+        nsolo = a.steps if masks else a.solo_frames
         sl = R.FrameLoop(cam, [ng.local[0] if ng is not None else outs[0]], xform=xf, mode=a.mode, flags=sflag,
-                         tile=tile if multi else None, render_stream=sptr, event_every=0, inflight=1)
+                         tile=tile if multi else None, render_stream=sptr, event_every=0, inflight=1,
+                         xforms=anim_xfs[a.warmup:] if masks else None)
         sl.run(20)
+        sl.seq.value = 0
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
-        sl.run(a.solo_frames)
+        sl.run(nsolo)
         e1.record(stream)
         torch.cuda.synchronize(dev)
-        solo = (e0.elapsed_time(e1) / a.solo_frames, a.solo_frames)
+        solo = (e0.elapsed_time(e1) / nsolo, nsolo)
     if multi:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -628,6 +642,8 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     host_us_per_frame = 1e3 * host_ms / max(1, a.steps)
+    if masks and not isinstance(loop, PyLoop):
+        xf = anim_xfs[-1]  # the last timed frame's pose
     kern_ms_timed, n_ev_timed = kern_ms, n_ev
     if solo is not None:
         kern_ms, n_ev = solo

@@ -66,7 +66,7 @@ class RtFrameLoop(C.Structure):
                 ("nbuf", C.c_int32), ("d_local", C.c_void_p * RT_LOOP_MAX_BUF),
                 ("d_scratch", C.c_void_p * RT_LOOP_MAX_BUF), ("d_frame", C.c_void_p * RT_LOOP_MAX_BUF),
                 ("render_stream", C.c_void_p), ("comm_stream", C.c_void_p), ("event_every", C.c_int32),
-                ("inflight", C.c_int32)]
+                ("inflight", C.c_int32), ("xforms", C.c_void_p), ("nxforms", C.c_int32)]
 
 
 class RtError(RuntimeError):

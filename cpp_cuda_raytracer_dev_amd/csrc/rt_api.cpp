@@ -228,6 +228,7 @@ int prepare_camera_object(rt_camera* c) {
 // index order, so the expensive tiles (the object sits mid-frame) start
 // first and the cheap background tiles fill in behind them.
 constexpr int kOrderSlots = 8;
+constexpr int kCostPeriod = 16;  // frames between cost samples (tile order 3)
 
 // The current slot was launched with on `st`.
 void note_order_stream(rt_camera* c, hipStream_t st) {
@@ -313,11 +314,13 @@ int ensure_order(rt_camera* c, const TraceParams& p, hipStream_t st) {
     std::copy(key, key + 8, c->order_key);
     c->centre.swap(order);
     c->layout_gen++;
-    c->frames_since = 1 << 20;  // tile order 3: sample the new grid's costs at once
+    // tile order 3: sample the new grid's costs once it has held for two
+    // frames (a moving object changes it every frame; its samples would
+    // always be stale)
+    c->frames_since = kCostPeriod - 2;
     return RT_OK;
 }
 
-constexpr int kCostPeriod = 16;  // frames between cost samples (tile order 3)
 constexpr int kAnyOrders = 4, kTuneReps = 3, kTuneTrials = kAnyOrders * kTuneReps;
 constexpr int kTunePeriod = 2048;  // frames between timing rounds of the shadow push order
 
@@ -1547,6 +1550,8 @@ extern "C" int rt_run_frames(rt_camera* c, rt_comm* comm, const rt_frame_loop* a
     if (!c || !a || !seq || nframes < 0 || a->nbuf < 1 || a->nbuf > RT_LOOP_MAX_BUF || a->inflight < 0 ||
         a->inflight > RT_LOOP_MAX_LANES)
         return fail(RT_ERR_INVALID, "rt_run_frames: bad argument");
+    if (a->nxforms < 0 || (a->nxforms > 0 && !a->xforms))
+        return fail(RT_ERR_INVALID, "rt_run_frames: bad transform sequence");
     const int L = std::max(1, (int)a->inflight);
     if (L > 1 && !comm && a->nbuf % L)
         return fail(RT_ERR_INVALID, "rt_run_frames: %d buffer sets for %d frames in flight (need a multiple)", a->nbuf, L);
@@ -1609,6 +1614,7 @@ extern "C" int rt_run_frames(rt_camera* c, rt_comm* comm, const rt_frame_loop* a
     const auto h0 = std::chrono::steady_clock::now();
     for (int32_t j = 0; j < nframes && !rc; j++) {
         const int k = (int)((*seq) % a->nbuf);
+        const float* xf = a->nxforms > 0 ? a->xforms + 12 * (size_t)((*seq) % a->nxforms) : a->xform;
         ++*seq;
         hipStream_t ls = lane[j % L];
         // set k is rendered again once the gather that last read it is done
@@ -1619,7 +1625,7 @@ extern "C" int rt_run_frames(rt_camera* c, rt_comm* comm, const rt_frame_loop* a
         const bool timed = every > 0 && j % every == 0;
         const int64_t t = every > 0 ? j / every : 0;
         rc = timed ? hip_check(hipEventRecord(c->loop_ev[(size_t)(2 * t)], ls), "loop timing") : RT_OK;
-        if (!rc) rc = render_common(c, a->xform, a->mode, a->flags, tile, a->d_local[k], nullptr, ls);
+        if (!rc) rc = render_common(c, xf, a->mode, a->flags, tile, a->d_local[k], nullptr, ls);
         if (!rc && timed) rc = hip_check(hipEventRecord(c->loop_ev[(size_t)(2 * t + 1)], ls), "loop timing");
         if (!rc && comm) {
             rc = hip_check(hipEventRecord(rendered[k], ls), "rendered");
@@ -1629,11 +1635,11 @@ extern "C" int rt_run_frames(rt_camera* c, rt_comm* comm, const rt_frame_loop* a
             if (!rc && used[k]) {
                 int32_t nranks = 1;
                 rc = rt_comm_info(comm, &nranks, nullptr);
-                if (!rc) rc = rt_frame_rect(c, a->xform, a->mode, nranks, rect);
+                if (!rc) rc = rt_frame_rect(c, xf, a->mode, nranks, rect);
                 rect_only = !memcmp(rect, set_rect[k], sizeof rect);
             }
             if (!rc)
-                rc = comm_gather_frame(comm, c, a->xform, a->mode, a->d_local[k], a->d_scratch[k], a->d_frame[k], gs,
+                rc = comm_gather_frame(comm, c, xf, a->mode, a->d_local[k], a->d_scratch[k], a->d_frame[k], gs,
                                        rect_only, set_rect[k]);
             if (!rc) rc = hip_check(hipEventRecord(sent[k], gs), "sent");
         }

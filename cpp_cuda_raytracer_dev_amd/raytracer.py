@@ -401,11 +401,13 @@ class FrameLoop:
     each frame is gathered to rank 0 on `comm_stream` while the next renders.
     `inflight` > 1 keeps that many frames in flight on the library's own
     render lanes (without comm, len(locals_) must be a multiple of it).
+    `xforms` (n x 12): frame k of the loop renders with pose k mod n.
     ``run(n)`` renders n frames and returns (kernel ms mean, timed frames);
     it synchronises the streams before returning."""
 
     def __init__(self, cam: "Camera", locals_, xform=None, mode: int = RT_MODE_KD, flags: int = 0, tile=None,
-                 render_stream=None, comm=None, comm_stream=None, event_every: int = 0, inflight: int = 1):
+                 render_stream=None, comm=None, comm_stream=None, event_every: int = 0, inflight: int = 1,
+                 xforms=None):
         n = len(locals_)
         if not 1 <= n <= _lib.RT_LOOP_MAX_BUF:
             raise ValueError(f"FrameLoop: 1..{_lib.RT_LOOP_MAX_BUF} buffer sets")
@@ -427,6 +429,10 @@ class FrameLoop:
         a.comm_stream = comm_stream
         a.event_every = event_every
         a.inflight = inflight
+        if xforms is not None:  # one pose per frame, cycled (rt_frame_loop.xforms)
+            self._xfs = np.ascontiguousarray(np.asarray(xforms, np.float32).reshape(-1, 12))
+            a.xforms = self._xfs.ctypes.data
+            a.nxforms = len(self._xfs)
         self._a = a
         self._locals = list(locals_)
         self.seq = C.c_int64(0)

@@ -270,6 +270,11 @@ typedef struct rt_frame_loop {
     void* comm_stream;
     int32_t event_every;
     int32_t inflight;
+    /* nxforms > 0: frame k = (*seq) of the loop renders with the object
+     * transform xforms + 12 * (k % nxforms) (a moving object's poses, one per
+     * frame, e.g. Object::transform after each input tick), instead of xform */
+    const float* xforms;
+    int32_t nxforms;
 } rt_frame_loop;
 int rt_run_frames(rt_camera* cam, rt_comm* comm, const rt_frame_loop* loop, int32_t nframes, int64_t* seq,
                   double* kernel_ms_avg, int32_t* kernel_ms_frames, double* host_ms);

@@ -146,6 +146,26 @@ def test_native_frame_loop_inflight(inflight, nbuf):
             R.FrameLoop(s.cam, bufs[:1] * 3, render_stream=st.cuda_stream, inflight=2).run(1)
 
 
+@pytest.mark.parametrize("inflight", [1, 2])
+def test_native_frame_loop_poses(inflight):
+    """rt_frame_loop.xforms: frame k renders pose k mod n (a moving object's
+    per-frame transforms), with one or two frames in flight; each buffer set
+    holds the frame of its pose, equal to a single render at that pose."""
+    import torch
+    w, h = 320, 180
+    s = H.GpuScene("rabbit_70k", w, h)
+    poses = [_rot_y(0.0), _rot_y(7.0), _rot_y(-5.0, (0.004, 0.0, 0.0)), _rot_y(11.0, (0.0, 0.003, 0.0))]
+    fulls = [s.render(0, xform=xf)[0] for xf in poses]
+    st = torch.cuda.Stream()
+    bufs = [torch.full((w * h,), 0x7BADBEEF, dtype=torch.int32, device="cuda:0") for _ in poses]
+    torch.cuda.synchronize()
+    loop = R.FrameLoop(s.cam, bufs, render_stream=st.cuda_stream, event_every=3, inflight=inflight, xforms=poses)
+    loop.run(10)
+    for k, (b, f) in enumerate(zip(bufs, fulls)):
+        assert (b.cpu().numpy().view(np.uint32) == f).all(), f"pose {k}"
+    assert s.cam.device_error() == 0
+
+
 def test_auto_rays_choice():
     """RT_OPT_RAYS 0 (default): 8 pixels per wave when the object's screen
     rectangle holds few 16-ray units (dragon 960x540), else 16 (1080p)."""
