@@ -492,7 +492,7 @@ def main():
             # two sets per frame in flight: a set's next render then waits
             # on a gather that finished long before (cross-queue waits that
             # are still pending cost ~10-15 us each)
-            g = NativeFrameGather(dist, w, h, dev, nbuf=max(1, min(max(a.pipeline, 2 * inflight), 4)))
+            g = NativeFrameGather(dist, w, h, dev, nbuf=max(1, min(max(a.pipeline, 2 * inflight), 8)))
             # every rank must derive the same rectangle and options, or the
             # receive sizes would not match the sends
             g.verify(cam, xf, a.mode)

@@ -57,7 +57,7 @@ class RtTile(C.Structure):
     _fields_ = [("nranks", C.c_int32), ("rank", C.c_int32)]
 
 
-RT_LOOP_MAX_BUF = 4
+RT_LOOP_MAX_BUF = 8
 RT_LOOP_MAX_LANES = 4
 
 

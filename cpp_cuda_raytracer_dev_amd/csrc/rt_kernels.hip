@@ -124,9 +124,12 @@ int launch_unpack_rect(int32_t w, int32_t h, int32_t nranks, const int32_t rect[
         cols = rect[1] - xa;
     }
     const int32_t per_row = (cols + vec - 1) / vec;
-    const dim3 grid((unsigned)((per_row + 255) / 256), (unsigned)rows);
+    // the rectangle alone runs beside the next frames' renders: 8 rows per
+    // block keeps its dispatch short (one block per row took 18 us there)
+    const int32_t rpb = rect_only ? 8 : 1;
+    const dim3 grid((unsigned)((per_row + 255) / 256), (unsigned)((rows + rpb - 1) / rpb));
     k_unpack_rect<<<grid, 256, 0, (hipStream_t)stream>>>(w, nranks, rect[0], rect[1], rect[2], rect[3], vec, y0, xa,
-                                                         local0, peers, frame);
+                                                         rows, rpb, local0, peers, frame);
     return check_launch<void>("k_unpack_rect");
 }
 

@@ -1852,52 +1852,55 @@ __global__ void k_pack_rect(int32_t w, int32_t x0, int32_t cw, int32_t s0, const
     out[(int64_t)row * cw + x] = local[((int64_t)s * kTileH + r) * w + x0 + x];
 }
 
-// Rank 0: frame row y0 + blockIdx.y from rank 0's own packed buffer, a
-// peer's compact block (peers 1..N-1 back to back), or the background.
+// Rank 0: frame rows y0 + blockIdx.y * rpb ... (rpb of them, within rows)
+// from rank 0's own packed buffer, a peer's compact block (peers 1..N-1 back
+// to back), or the background.
 // Each thread writes `vec` (4 or 1) consecutive pixels of the row from
 // column xa; rows outside the rectangle are pure background stores.  The
 // whole frame: y0 = xa = 0; the rectangle alone (its background already in
 // the frame): its rows, from column x0 rounded down to a multiple of vec.
 __global__ void k_unpack_rect(int32_t w, int32_t nranks, int32_t x0, int32_t x1, int32_t b0, int32_t b1, int32_t vec,
-                              int32_t y0, int32_t xa, const uint32_t* __restrict__ local0,
+                              int32_t y0, int32_t xa, int32_t rows, int32_t rpb, const uint32_t* __restrict__ local0,
                               const uint32_t* __restrict__ peers, uint32_t* __restrict__ frame) {
-    const int32_t y = y0 + blockIdx.y;
     const int32_t xs = xa + (blockIdx.x * blockDim.x + threadIdx.x) * vec;
     if (xs >= w) return;
-    const int32_t band = y / kTileH, r = y - band * kTileH;
-    const int32_t rank = band % nranks, slot = band / nranks;
-    uint32_t v0 = kBackground, v1 = kBackground, v2 = kBackground, v3 = kBackground;
-    if (band >= b0 && band < b1 && xs + vec > x0 && xs < x1) {
-        const uint32_t* src;
-        int32_t sx;  // source index of column x: src[x - sx]
-        if (rank == 0) {
-            src = local0 + ((int64_t)slot * kTileH + r) * w;
-            sx = 0;
-        } else {
-            const int32_t cw = x1 - x0;
-            int64_t off = 0;
-            int32_t s0, s1;
-            for (int32_t q = 1; q < rank; q++) {
-                rect_slots(b0, b1, nranks, q, s0, s1);
-                off += (int64_t)(s1 - s0) * kTileH * cw;
+    const int32_t ye = y0 + min(rows, (int32_t)(blockIdx.y + 1) * rpb);
+    for (int32_t y = y0 + (int32_t)blockIdx.y * rpb; y < ye; y++) {
+        const int32_t band = y / kTileH, r = y - band * kTileH;
+        const int32_t rank = band % nranks, slot = band / nranks;
+        uint32_t v0 = kBackground, v1 = kBackground, v2 = kBackground, v3 = kBackground;
+        if (band >= b0 && band < b1 && xs + vec > x0 && xs < x1) {
+            const uint32_t* src;
+            int32_t sx;  // source index of column x: src[x - sx]
+            if (rank == 0) {
+                src = local0 + ((int64_t)slot * kTileH + r) * w;
+                sx = 0;
+            } else {
+                const int32_t cw = x1 - x0;
+                int64_t off = 0;
+                int32_t s0, s1;
+                for (int32_t q = 1; q < rank; q++) {
+                    rect_slots(b0, b1, nranks, q, s0, s1);
+                    off += (int64_t)(s1 - s0) * kTileH * cw;
+                }
+                rect_slots(b0, b1, nranks, rank, s0, s1);
+                src = peers + off + ((int64_t)(slot - s0) * kTileH + r) * cw;
+                sx = x0;
             }
-            rect_slots(b0, b1, nranks, rank, s0, s1);
-            src = peers + off + ((int64_t)(slot - s0) * kTileH + r) * cw;
-            sx = x0;
+            // straight-line per pixel (an indexed array would live in scratch)
+            if (xs >= x0 && xs < x1) v0 = src[xs - sx];
+            if (vec == 4) {
+                if (xs + 1 >= x0 && xs + 1 < x1) v1 = src[xs + 1 - sx];
+                if (xs + 2 >= x0 && xs + 2 < x1) v2 = src[xs + 2 - sx];
+                if (xs + 3 >= x0 && xs + 3 < x1) v3 = src[xs + 3 - sx];
+            }
         }
-        // straight-line per pixel (an indexed array would live in scratch)
-        if (xs >= x0 && xs < x1) v0 = src[xs - sx];
+        uint32_t* dst = frame + (int64_t)y * w + xs;
         if (vec == 4) {
-            if (xs + 1 >= x0 && xs + 1 < x1) v1 = src[xs + 1 - sx];
-            if (xs + 2 >= x0 && xs + 2 < x1) v2 = src[xs + 2 - sx];
-            if (xs + 3 >= x0 && xs + 3 < x1) v3 = src[xs + 3 - sx];
+            *reinterpret_cast<uint4*>(dst) = make_uint4(v0, v1, v2, v3);
+        } else {
+            dst[0] = v0;
         }
-    }
-    uint32_t* dst = frame + (int64_t)y * w + xs;
-    if (vec == 4) {
-        *reinterpret_cast<uint4*>(dst) = make_uint4(v0, v1, v2, v3);
-    } else {
-        dst[0] = v0;
     }
 }
 

@@ -256,7 +256,7 @@ void rt_comm_destroy(rt_comm* c);
  * independent reads of the scene; a frame's tail overlaps the next frame's
  * start, where one frame leaves most CUs idle.  Timing events then bracket
  * renders that share the GPU with another frame. */
-#define RT_LOOP_MAX_BUF 4
+#define RT_LOOP_MAX_BUF 8
 #define RT_LOOP_MAX_LANES 4
 typedef struct rt_frame_loop {
     const float* xform;
