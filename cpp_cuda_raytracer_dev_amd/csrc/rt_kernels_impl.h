@@ -616,6 +616,29 @@ constexpr int kPoolCap = kPoolCapMax;
 constexpr int kCodeBits = kMaxDepth;       // left-aligned code width in the key
 constexpr uint32_t kCodeMarkMask = (1u << 26) - 1;
 
+// Both records of an iteration are issued before either is consumed.  1
+// (default): a scheduling barrier after the loads, so item 0 waits only for
+// its own record (vmcnt counts loads in order) while item 1's is still in
+// flight; 0 (rounds 1-2): an empty asm reading all 32 registers, which also
+// made the wave wait for both records before visiting item 0.  Measured, two
+// frames in flight: dragon 1080p 14.6k -> 15.3k FPS (solo 86.7 -> 82.2 us),
+// 960x540 30.4k -> 32.7k, the 1080p fill view 868 -> 829 us, happy 4K with
+// shadow rays 464 -> 436 us.
+#ifndef RT_FENCE_MODE
+#define RT_FENCE_MODE 1
+#endif
+#if RT_FENCE_MODE == 0
+#define RT_RECORD_FENCE(a0, a1, a2, a3, b0, b1, b2, b3)                                                              \
+    do {                                                                                                            \
+        asm volatile("" ::"v"(a0.x), "v"(a0.y), "v"(a0.z), "v"(a0.w), "v"(a1.x), "v"(a1.y), "v"(a1.z), "v"(a1.w),  \
+                     "v"(a2.x), "v"(a2.y), "v"(a2.z), "v"(a2.w), "v"(a3.x), "v"(a3.y), "v"(a3.z), "v"(a3.w));      \
+        asm volatile("" ::"v"(b0.x), "v"(b0.y), "v"(b0.z), "v"(b0.w), "v"(b1.x), "v"(b1.y), "v"(b1.z), "v"(b1.w),  \
+                     "v"(b2.x), "v"(b2.y), "v"(b2.z), "v"(b2.w), "v"(b3.x), "v"(b3.y), "v"(b3.z), "v"(b3.w));      \
+    } while (0)
+#else
+#define RT_RECORD_FENCE(a0, a1, a2, a3, b0, b1, b2, b3) __builtin_amdgcn_sched_barrier(0)
+#endif
+
 struct Item {
     uint32_t ref;      // node ref (kLeafBit | tri, or interior index)
     float t0, t1;      // the node's (maxt0, mint1) for interior refs
@@ -991,10 +1014,7 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
         const float4 a0 = p0[0], a1 = p0[1], a2 = p0[2], a3 = p0[3];
         const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         const float4 b0 = kTwo ? p1[0] : z, b1 = kTwo ? p1[1] : z, b2 = kTwo ? p1[2] : z, b3 = kTwo ? p1[3] : z;
-        asm volatile("" ::"v"(a0.x), "v"(a0.y), "v"(a0.z), "v"(a0.w), "v"(a1.x), "v"(a1.y), "v"(a1.z), "v"(a1.w),
-                     "v"(a2.x), "v"(a2.y), "v"(a2.z), "v"(a2.w), "v"(a3.x), "v"(a3.y), "v"(a3.z), "v"(a3.w));
-        asm volatile("" ::"v"(b0.x), "v"(b0.y), "v"(b0.z), "v"(b0.w), "v"(b1.x), "v"(b1.y), "v"(b1.z), "v"(b1.w),
-                     "v"(b2.x), "v"(b2.y), "v"(b2.z), "v"(b2.w), "v"(b3.x), "v"(b3.y), "v"(b3.z), "v"(b3.w));
+        RT_RECORD_FENCE(a0, a1, a2, a3, b0, b1, b2, b3);
 #if RT_SEQ_PUSH
         // item 0 is visited, recorded and pushed before item 1 is visited, so
         // its results die before item 1's are made (fewer live VGPRs)
@@ -1144,10 +1164,7 @@ __device__ __forceinline__ void pool_walk_split(const TraceParams& P, uint4* ite
         const float4* p1 = record_of(P, it1.x);
         const float4 a0 = p0[0], a1 = p0[1], a2 = p0[2], a3 = p0[3];
         const float4 b0 = p1[0], b1 = p1[1], b2 = p1[2], b3 = p1[3];
-        asm volatile("" ::"v"(a0.x), "v"(a0.y), "v"(a0.z), "v"(a0.w), "v"(a1.x), "v"(a1.y), "v"(a1.z), "v"(a1.w),
-                     "v"(a2.x), "v"(a2.y), "v"(a2.z), "v"(a2.w), "v"(a3.x), "v"(a3.y), "v"(a3.z), "v"(a3.w));
-        asm volatile("" ::"v"(b0.x), "v"(b0.y), "v"(b0.z), "v"(b0.w), "v"(b1.x), "v"(b1.y), "v"(b1.z), "v"(b1.w),
-                     "v"(b2.x), "v"(b2.y), "v"(b2.z), "v"(b2.w), "v"(b3.x), "v"(b3.y), "v"(b3.z), "v"(b3.w));
+        RT_RECORD_FENCE(a0, a1, a2, a3, b0, b1, b2, b3);
         int ti = bi, tl = nl - j;
         {
             Visit v0;
