@@ -1242,23 +1242,37 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
     const unsigned long long t_start = P.dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
     uint32_t iters = 0, popped = 0;
 
-    float cam[3];
-    Ray R;
-    camera_ray(P, px, live, cam, R);
-    const float* X = P.xf;
-    if (lane < kRays) {
-        store_ray(&S_.ray[lane * kRayVec], R, kTranslated, 0.0f, 0u);
-        S_.key[lane] = ~0ull;
-        S_.tri[lane] = kMiss;
+    int n;
+    {
+        // the ray goes to LDS for the walk; shading recomputes it afterwards
+        // (the same float expressions), so it is not live across the walk
+        float cam0[3];
+        Ray R0;
+        camera_ray(P, px, live, cam0, R0);
+        if (lane < kRays) {
+            store_ray(&S_.ray[lane * kRayVec], R0, kTranslated, 0.0f, 0u);
+            S_.key[lane] = ~0ull;
+            S_.tri[lane] = kMiss;
+        }
+        n = seed_root<kCount>(P, items, R0, live, lane, C.n_int, C.n_desc);
     }
-
-    int n = seed_root<kCount>(P, items, R, live, lane, C.n_int, C.n_desc);
     if (RT_SPLIT_LEAF && P.items > 1)
         pool_walk_split<kCap, kRayVec, kTranslated, kCount, false>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters,
                                                                   popped, C.n_int, C.n_leaf, C.n_acc, C.n_desc);
     else
         pool_walk<kCap, kRayVec, kTranslated, kCount, false>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters, popped,
                                                             C.n_int, C.n_leaf, C.n_acc, C.n_desc);
+    float cam[3];
+    Ray R;
+    {
+        // the pixel coordinates pass an empty asm, so the compiler recomputes
+        // the ray rather than keeping the first computation's partial
+        // products live (and spilled) across the walk
+        Pixel pr = px;
+        asm volatile("" : "+v"(pr.x), "+v"(pr.y));
+        camera_ray(P, pr, live, cam, R);
+    }
+    const float* X = P.xf;
     unsigned long long kbest = ~0ull;
     uint32_t best = kMiss;
     if (lane < kRays) {

@@ -11,7 +11,7 @@ shift 3
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-BENCH="bench.py --steps 30 --warmup 5 --no-cpu-baseline $*"
+BENCH="bench.py --steps 30 --warmup 5 --no-cpu-baseline --inflight 1 $*"
 i=0
 for ctr in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" \
            "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU" \
