@@ -21,6 +21,7 @@ RT_MODE_FLAT = 1
 RT_FLAG_WRITE_HIT = 1
 RT_FLAG_COUNT = 2
 RT_FLAG_SHADOW = 4
+RT_FLAG_FRAME_OUT = 8
 RT_OPT_KERNEL = 1
 RT_OPT_TILE_ORDER = 2
 RT_OPT_RAYS = 3

@@ -178,7 +178,12 @@ int rt::comm_gather_frame(rt_comm* c, rt_camera* cam, const float* xform, uint32
             if (rc) return rc;
             if ((rc = nccl_check(r, e, "ncclGroupEnd"))) return rc;
         }
-        return launch_unpack_rect(w, h, c->nranks, rect, d_local, d_scratch, d_frame, stream, rect_only);
+        // d_local == d_frame: rank 0 rendered its bands into the frame itself
+        // (RT_FLAG_FRAME_OUT), so the assembly leaves them alone
+        const bool own_in_frame = d_local == d_frame;
+        if (own_in_frame && c->nranks == 1) return RT_OK;
+        return launch_unpack_rect(w, h, c->nranks, rect, own_in_frame ? nullptr : d_local, d_scratch, d_frame, stream,
+                                  rect_only);
     }
     const int64_t n = rt_rect_pixels(w, h, c->nranks, c->rank, rect);
     if (n <= 0) return RT_OK;

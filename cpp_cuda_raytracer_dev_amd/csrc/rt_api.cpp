@@ -103,7 +103,7 @@ struct rt_camera {
     int rays = 0;                    // kOptRays: pixels per wave of kernel 3 (0: auto_rays)
     int last_rays = 0;               // the pixels per wave the last kernel-3 render used
     int items = 2;                   // kOptItems: items per lane per pool iteration
-    int flat_variant = 2;            // kOptFlat: flat-list kernel form
+    int flat_variant = 5;            // kOptFlat: flat-list kernel form
     // shadow renders: the any-hit push order, fixed (kOptShadowOrder 0..3)
     // or timed (-1): a round of trial frames runs each order kTuneReps times,
     // interleaved, bracketed by events; the fastest is kept for kTunePeriod
@@ -1151,7 +1151,7 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
     if (mode == RT_MODE_KD && !c->obj->d_nodes)
         return fail(RT_ERR_STATE, "rt_render: KD mode needs rt_scene_set_kd (Trixel::create_kd) first");
     if (c->obj->ntri == 0) return fail(RT_ERR_STATE, "rt_render: empty scene");
-    if (flags & ~(RT_FLAG_WRITE_HIT | RT_FLAG_COUNT | RT_FLAG_SHADOW))
+    if (flags & ~(RT_FLAG_WRITE_HIT | RT_FLAG_COUNT | RT_FLAG_SHADOW | RT_FLAG_FRAME_OUT))
         return fail(RT_ERR_INVALID, "rt_render: unknown flags 0x%x", flags);
     if (flags & RT_FLAG_SHADOW) {
         if (mode != RT_MODE_KD) return fail(RT_ERR_INVALID, "rt_render: RT_FLAG_SHADOW needs RT_MODE_KD");
@@ -1180,6 +1180,7 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
         pc.rank = rk;
         pc.p = p;
     }
+    p.frame_out = (flags & RT_FLAG_FRAME_OUT) ? 1 : 0;
     if (mode == RT_MODE_KD && effective_kernel(c) == 3) c->last_rays = p.rays;
     int trial;
     p.any_order = any_order_for(c, flags, stream, trial) | ((c->debug & 16) ? 4 : 0);
@@ -1318,7 +1319,8 @@ extern "C" int rt_unpack_rect(int device, int32_t w, int32_t h, int32_t nranks, 
     if ((rc = check_rect(w, h, nranks, rect, "rt_unpack_rect"))) return rc;
     if (!d_local0 || !d_frame || (nranks > 1 && !d_peers)) return fail(RT_ERR_INVALID, "rt_unpack_rect: bad argument");
     DeviceGuard g(device);
-    return launch_unpack_rect(w, h, nranks, rect, d_local0, d_peers, d_frame, stream);
+    // d_local0 == d_frame: rank 0's bands were rendered into the frame (RT_FLAG_FRAME_OUT)
+    return launch_unpack_rect(w, h, nranks, rect, d_local0 == d_frame ? nullptr : d_local0, d_peers, d_frame, stream);
 }
 
 extern "C" int rt_read_frame(rt_camera* c, uint32_t* argb, int64_t* hit) {
@@ -1475,7 +1477,7 @@ extern "C" int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value) {
         c->tune_pending = false;
         return RT_OK;
     case kOptFlat:
-        if (value < 0 || value > 3) return fail(RT_ERR_INVALID, "flat kernel form %d (0..3)", value);
+        if (value < 0 || value > 6) return fail(RT_ERR_INVALID, "flat kernel form %d (0..6)", value);
         c->flat_variant = value;
         return RT_OK;
     case kOptTileOrder:
@@ -1611,6 +1613,25 @@ extern "C" int rt_run_frames(rt_camera* c, rt_comm* comm, const rt_frame_loop* a
         for (int l = 0; l < L; l++) c->active[l] = lane[l];
     }
     const rt_tile* tile = a->tile.nranks > 0 ? &a->tile : nullptr;
+    // rank 0 renders its bands straight into the frame it assembles (its
+    // part of the frame is never copied); the gather places the peers' parts
+    int32_t crank = -1;
+    if (comm && (rc = rt_comm_info(comm, nullptr, &crank))) {
+        cleanup();
+        return rc;
+    }
+    const bool direct = comm && crank == 0 && tile;
+    // a peer's gather packs what its render wrote (render -> gather), and its
+    // next render into the set waits for that pack (gather -> render); rank
+    // 0's gather writes the peers' rows beside the rows its render writes,
+    // so its lanes need no cross-queue events (each lane keeps frame order,
+    // and the loop's end joins them)
+    const bool linked = comm && !direct;
+    for (int k = 0; direct && k < a->nbuf; k++)
+        if (!a->d_frame[k]) {
+            cleanup();
+            return fail(RT_ERR_INVALID, "rt_run_frames: rank 0 has no frame buffer in set %d", k);
+        }
     const auto h0 = std::chrono::steady_clock::now();
     for (int32_t j = 0; j < nframes && !rc; j++) {
         const int k = (int)((*seq) % a->nbuf);
@@ -1619,17 +1640,20 @@ extern "C" int rt_run_frames(rt_camera* c, rt_comm* comm, const rt_frame_loop* a
         hipStream_t ls = lane[j % L];
         // set k is rendered again once the gather that last read it is done
         // (no barrier packet when that gather has already finished)
-        if (comm && used[k] && hipEventQuery(sent[k]) != hipSuccess &&
+        if (linked && used[k] && hipEventQuery(sent[k]) != hipSuccess &&
             (rc = hip_check(hipStreamWaitEvent(ls, sent[k], 0), "render wait")))
             break;
         const bool timed = every > 0 && j % every == 0;
         const int64_t t = every > 0 ? j / every : 0;
         rc = timed ? hip_check(hipEventRecord(c->loop_ev[(size_t)(2 * t)], ls), "loop timing") : RT_OK;
-        if (!rc) rc = render_common(c, xf, a->mode, a->flags, tile, a->d_local[k], nullptr, ls);
+        uint32_t* target = direct ? a->d_frame[k] : a->d_local[k];
+        if (!rc) rc = render_common(c, xf, a->mode, a->flags | (direct ? RT_FLAG_FRAME_OUT : 0u), tile, target, nullptr, ls);
         if (!rc && timed) rc = hip_check(hipEventRecord(c->loop_ev[(size_t)(2 * t + 1)], ls), "loop timing");
         if (!rc && comm) {
-            rc = hip_check(hipEventRecord(rendered[k], ls), "rendered");
-            if (!rc) rc = hip_check(hipStreamWaitEvent(gs, rendered[k], 0), "comm wait");
+            if (linked) {
+                rc = hip_check(hipEventRecord(rendered[k], ls), "rendered");
+                if (!rc) rc = hip_check(hipStreamWaitEvent(gs, rendered[k], 0), "comm wait");
+            }
             int32_t rect[4] = {0, 0, 0, 0};
             bool rect_only = false;
             if (!rc && used[k]) {
@@ -1639,9 +1663,9 @@ extern "C" int rt_run_frames(rt_camera* c, rt_comm* comm, const rt_frame_loop* a
                 rect_only = !memcmp(rect, set_rect[k], sizeof rect);
             }
             if (!rc)
-                rc = comm_gather_frame(comm, c, xf, a->mode, a->d_local[k], a->d_scratch[k], a->d_frame[k], gs,
+                rc = comm_gather_frame(comm, c, xf, a->mode, target, a->d_scratch[k], a->d_frame[k], gs,
                                        rect_only, set_rect[k]);
-            if (!rc) rc = hip_check(hipEventRecord(sent[k], gs), "sent");
+            if (!rc && linked) rc = hip_check(hipEventRecord(sent[k], gs), "sent");
         }
         used[k] = true;
     }

@@ -98,6 +98,7 @@ struct TraceParams {
     float xf[12];
     int32_t w, h;
     int32_t nranks, rank;
+    int32_t frame_out;             // RT_FLAG_FRAME_OUT: tile pixels at their frame rows
     int32_t tiles_x, block_rows;   // fine grid = tiles_x * block_rows blocks
     // Fine region (kernel 3): the tiles covering the root box's screen
     // rectangle start at tile column fine_tx0 and band slot fine_s0; every

@@ -146,7 +146,7 @@ __device__ __forceinline__ bool unit_pixel(const TraceParams& P, const Unit& u, 
     const int32_t ly = u.yin + (lane >> 3);
     px.x = u.x0 + (lane & 7);
     px.y = band * kTileH + ly;
-    px.out = (int64_t)(u.slot * kTileH + ly) * P.w + px.x;
+    px.out = (int64_t)((P.frame_out ? band : u.slot) * kTileH + ly) * P.w + px.x;
     return lane < rows * 8 && px.x < P.w && px.y < P.h;
 }
 
@@ -1628,6 +1628,30 @@ struct FlatPair {
             if (c1) flat_accept(f.y, U.y, V.y, dw.y, t + 1, d, best, n_acc);
         }
     }
+    // Form 4: the same products over the signed layout (k_pair_tri: d_w >= 0,
+    // so a ray can pass only where f > 0, u >= 0 and v >= 0 in the primed
+    // values), screened by one min3 per triangle: a pair is skipped unless
+    // max(min3(U, V, f) of each half) is > 0 (or NaN).  min3 ignores NaN, so
+    // a NaN U or V never rejects by itself; a triangle whose min3 is NaN has
+    // f NaN, which the full test rejects.
+    __device__ __forceinline__ void products(const f2v X, const f2v Y, const f2v Z, f2v& f, f2v& U, f2v& V) const {
+        const f2v qx = Y * e2z - Z * e2y;
+        const f2v qy = Z * e2x - X * e2z;
+        const f2v qz = X * e2y - Y * e2x;
+        f = (qx * e1x + qy * e1y) + qz * e1z;
+        U = (qx * tx + qy * ty) + qz * tz;
+        V = (X * dqx + Y * dqy) + Z * dqz;
+    }
+    __device__ __forceinline__ void test_signed(const f2v X, const f2v Y, const f2v Z, uint32_t t, float& d,
+                                                uint32_t& best, uint32_t& n_acc) const {
+        f2v f, U, V;
+        products(X, Y, Z, f, U, V);
+        const float m0 = fminf(fminf(U.x, V.x), f.x), m1 = fminf(fminf(U.y, V.y), f.y);
+        if (!(fmaxf(m0, m1) <= 0.0f)) {
+            if (!(m0 <= 0.0f)) flat_accept(f.x, U.x, V.x, dw.x, t, d, best, n_acc);
+            if (!(m1 <= 0.0f)) flat_accept(f.y, U.y, V.y, dw.y, t + 1, d, best, n_acc);
+        }
+    }
 };
 
 // kVariant 0: one triangle per iteration, the 64-B camera-relative record
@@ -1709,6 +1733,53 @@ __global__ __launch_bounds__(kTileWFlat * kTileH) void k_trace_flat(TraceParams 
                 c.load(Q + 16 * (size_t)p);
                 c.test(X, Y, Z, 2 * p, d, best, n_acc);
             }
+        } else if (kVariant == 4) {
+            for (uint32_t p = 0; p < npair; p++) {
+                FlatPair c;
+                c.load(Q + 16 * (size_t)p);
+                c.test_signed(X, Y, Z, 2 * p, d, best, n_acc);
+            }
+        } else if (kVariant == 6) {
+            // form 4, two pairs per iteration behind one screen branch (the
+            // four triangles' accepts in index order inside it)
+            uint32_t p = 0;
+            for (; p + 1 < npair; p += 2) {
+                FlatPair a, b;
+                a.load(Q + 16 * (size_t)p);
+                b.load(Q + 16 * (size_t)p + 16);
+                f2v fa, Ua, Va, fb, Ub, Vb;
+                a.products(X, Y, Z, fa, Ua, Va);
+                b.products(X, Y, Z, fb, Ub, Vb);
+                const float m0 = fminf(fminf(Ua.x, Va.x), fa.x), m1 = fminf(fminf(Ua.y, Va.y), fa.y);
+                const float m2 = fminf(fminf(Ub.x, Vb.x), fb.x), m3 = fminf(fminf(Ub.y, Vb.y), fb.y);
+                if (!(fmaxf(fmaxf(m0, m1), fmaxf(m2, m3)) <= 0.0f)) {
+                    const uint32_t t = 2 * p;
+                    if (!(m0 <= 0.0f)) flat_accept(fa.x, Ua.x, Va.x, a.dw.x, t, d, best, n_acc);
+                    if (!(m1 <= 0.0f)) flat_accept(fa.y, Ua.y, Va.y, a.dw.y, t + 1, d, best, n_acc);
+                    if (!(m2 <= 0.0f)) flat_accept(fb.x, Ub.x, Vb.x, b.dw.x, t + 2, d, best, n_acc);
+                    if (!(m3 <= 0.0f)) flat_accept(fb.y, Ub.y, Vb.y, b.dw.y, t + 3, d, best, n_acc);
+                }
+            }
+            if (p < npair) {
+                FlatPair a;
+                a.load(Q + 16 * (size_t)p);
+                a.test_signed(X, Y, Z, 2 * p, d, best, n_acc);
+            }
+        } else if (kVariant == 5) {
+            // form 4, two pairs per iteration
+            uint32_t p = 0;
+            for (; p + 1 < npair; p += 2) {
+                FlatPair a, b;
+                a.load(Q + 16 * (size_t)p);
+                b.load(Q + 16 * (size_t)p + 16);
+                a.test_signed(X, Y, Z, 2 * p, d, best, n_acc);
+                b.test_signed(X, Y, Z, 2 * p + 2, d, best, n_acc);
+            }
+            if (p < npair) {
+                FlatPair a;
+                a.load(Q + 16 * (size_t)p);
+                a.test_signed(X, Y, Z, 2 * p, d, best, n_acc);
+            }
         } else {
             // software pipelined: pair p + 1's scalar loads are issued once
             // pair p's have arrived (scalar loads return out of order, so a
@@ -1747,6 +1818,14 @@ __global__ __launch_bounds__(kTileWFlat * kTileH) void k_trace_flat(TraceParams 
 // The flat kernel's pair layout: pair p <- camera-relative records 2p, 2p+1,
 // each field as (value of 2p, value of 2p+1); a missing twin is dead (all
 // zero: d_w = 0 fails the screen, and its full test gives w = 0 < eps).
+//
+// Signed: a triangle with d_w < 0 is stored with e1, d_t and d_q negated and
+// d_w = |d_w|.  Negation is exact and commutes with every rounded product and
+// sum, so the kernel's f, U, V come out exactly negated and u = U/f, v, w =
+// d_w/f are unchanged bit for bit; only signs move, so that a triangle can be
+// accepted only where f > 0 (w = d_w/f >= eps needs sign f = sign d_w).  A
+// triangle with d_w = +-0 or NaN can never be accepted (w = 0 < eps, or
+// w < d false): its e1 is stored as zero, so f = 0 and every form rejects it.
 __global__ void k_pair_tri(const float4* __restrict__ trec, uint32_t ntri, float4* __restrict__ tpair) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t npair = (ntri + 1) >> 1;
@@ -1763,6 +1842,17 @@ __global__ void k_pair_tri(const float4* __restrict__ trec, uint32_t ntri, float
         const float4 A1 = r1[0], B1 = r1[1], C1 = r1[2], D1 = r1[3];
         b[0] = A1.x; b[1] = A1.y; b[2] = A1.z; b[3] = A1.w; b[4] = B1.x; b[5] = B1.y; b[6] = B1.z; b[7] = B1.w;
         b[8] = C1.x; b[9] = C1.y; b[10] = C1.z; b[11] = C1.w; b[12] = D1.x;
+    }
+    for (int j = 0; j < 2; j++) {
+        float* r = j ? b : a;
+        const float dw = r[12];
+        if (!(dw > 0.0f)) {
+            // e1: 0-2, e2: 3-5 (kept), d_t: 6-8, d_q: 9-11 (k_cam_tri's order)
+            const bool dead = !(dw < 0.0f);
+            for (int k = 0; k < 12; k++)
+                if (k < 3 || k >= 6) r[k] = (dead && k < 3) ? 0.0f : -r[k];
+            r[12] = dead ? 0.0f : -dw;
+        }
     }
     // field order of the kernel: e1 (3), e2 (3), d_t (3), d_q (3), d_w
     float4* o = tpair + 8 * (size_t)p;
@@ -1908,6 +1998,7 @@ __global__ void k_pack_rect(int32_t w, int32_t x0, int32_t cw, int32_t s0, const
 // column xa; rows outside the rectangle are pure background stores.  The
 // whole frame: y0 = xa = 0; the rectangle alone (its background already in
 // the frame): its rows, from column x0 rounded down to a multiple of vec.
+// local0 = null: rank 0's rows are in the frame already (RT_FLAG_FRAME_OUT).
 __global__ void k_unpack_rect(int32_t w, int32_t nranks, int32_t x0, int32_t x1, int32_t b0, int32_t b1, int32_t vec,
                               int32_t y0, int32_t xa, int32_t rows, int32_t rpb, const uint32_t* __restrict__ local0,
                               const uint32_t* __restrict__ peers, uint32_t* __restrict__ frame) {
@@ -1917,6 +2008,7 @@ __global__ void k_unpack_rect(int32_t w, int32_t nranks, int32_t x0, int32_t x1,
     for (int32_t y = y0 + (int32_t)blockIdx.y * rpb; y < ye; y++) {
         const int32_t band = y / kTileH, r = y - band * kTileH;
         const int32_t rank = band % nranks, slot = band / nranks;
+        if (rank == 0 && !local0) continue;  // rank 0 rendered these rows into the frame
         uint32_t v0 = kBackground, v1 = kBackground, v2 = kBackground, v3 = kBackground;
         if (band >= b0 && band < b1 && xs + vec > x0 && xs < x1) {
             const uint32_t* src;

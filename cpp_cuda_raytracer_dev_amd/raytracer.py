@@ -24,7 +24,8 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from ._lib import KD_NODE_DTYPE, LEAF_AABB_DTYPE, RT_FLAG_COUNT, RT_FLAG_SHADOW, RT_FLAG_WRITE_HIT, RT_MODE_FLAT, RT_MODE_KD
+from ._lib import (KD_NODE_DTYPE, LEAF_AABB_DTYPE, RT_FLAG_COUNT, RT_FLAG_FRAME_OUT, RT_FLAG_SHADOW, RT_FLAG_WRITE_HIT,
+                   RT_MODE_FLAT, RT_MODE_KD)
 
 SET_COLOR_TAG = 1      # TD/Camera.h:13
 PHONG_COLOR_TAG = 2    # TD/Camera.h:14
@@ -495,4 +496,4 @@ class PinnedFrames:
 
 __all__ = ["read_ply", "assemble_mesh", "kd_build", "film_w", "camera_basis", "Quaternion", "Trixel", "Object",
            "Camera", "PinnedFrames", "packed_pixels", "unpack_bands", "SET_COLOR_TAG", "PHONG_COLOR_TAG", "RT_MODE_KD",
-           "RT_MODE_FLAT", "RT_FLAG_WRITE_HIT", "RT_FLAG_COUNT", "RT_FLAG_SHADOW", "BACKGROUND_ARGB", "DEFAULT_RAD"]
+           "RT_MODE_FLAT", "RT_FLAG_WRITE_HIT", "RT_FLAG_COUNT", "RT_FLAG_SHADOW", "RT_FLAG_FRAME_OUT", "BACKGROUND_ARGB", "DEFAULT_RAD"]

@@ -49,6 +49,11 @@ typedef enum rt_status {
  * the wave-cooperative kernel only; the shadow rays'
  * visits are added to the same counters. */
 #define RT_FLAG_SHADOW 4u
+/* With a tile: write the tile's pixels at their frame positions in a w*h
+ * buffer (argb and hit) instead of the packed band buffer; pixels of other
+ * ranks' bands are not touched.  Rank 0 of a gather renders straight into
+ * the frame it assembles (rt_comm_gather_frame with d_local == d_frame). */
+#define RT_FLAG_FRAME_OUT 8u
 
 /* Per-triangle AABB = kd_leaf (TD/Trixel.h:31-37); `tri` = tri_list_index. */
 typedef struct rt_leaf_aabb {
@@ -202,7 +207,9 @@ int rt_unpack_bands(int device, int32_t w, int32_t h, int32_t nranks,
  * into d_scratch (rt_tile_packed_pixels u32) and send it to rank 0; rank 0
  * receives the peers' parts into d_scratch ((N-1) * rt_tile_packed_pixels
  * u32) and assembles d_frame (w*h) from them, its own d_local and the
- * background.  Every rank must call it once per frame, with a camera of the
+ * background.  On rank 0 d_local may be d_frame itself: its bands were
+ * rendered into the frame (RT_FLAG_FRAME_OUT, what rt_run_frames does) and
+ * are left as they are.  Every rank must call it once per frame, with a camera of the
  * same resolution and options on every rank (message sizes are derived, not
  * exchanged; distributed.NativeFrameGather.verify checks this once).  A rank
  * with no part in the rectangle sends nothing, and rank 0 posts no receive
@@ -229,7 +236,8 @@ int64_t rt_rect_pixels(int32_t w, int32_t h, int32_t nranks, int32_t rank, const
 int rt_pack_rect(int device, int32_t w, int32_t h, int32_t nranks, int32_t rank, const int32_t rect[4],
                  const uint32_t* d_local, uint32_t* d_out, void* stream);
 /* Rank 0: the frame from its own packed buffer, the peers' parts (ranks
- * 1..N-1 back to back) and the background. */
+ * 1..N-1 back to back) and the background.  d_local0 == d_frame: rank 0's
+ * bands are in the frame already (RT_FLAG_FRAME_OUT) and are not written. */
 int rt_unpack_rect(int device, int32_t w, int32_t h, int32_t nranks, const int32_t rect[4],
                    const uint32_t* d_local0, const uint32_t* d_peers, uint32_t* d_frame, void* stream);
 int rt_comm_info(const rt_comm* c, int32_t* nranks, int32_t* rank);
@@ -331,8 +339,10 @@ int rt_camera_info(const rt_camera* c, int32_t* w, int32_t* h, int32_t* max_dept
  * stream capture).  Get returns the order in use. */
 #define RT_OPT_SHADOW_ORDER 6
 /* Flat-list kernel form (same frame): 0 one triangle per iteration, 1 two
- * per iteration, 2 two per iteration as packed float2 arithmetic (default),
- * 3 = 2 software pipelined. */
+ * per iteration, 2 two per iteration as packed float2 arithmetic,
+ * 3 = 2 software pipelined, 4 = 2 over the signed pair layout with one min3
+ * screen per triangle, 5 = 4 unrolled to two pairs (default), 6 = 5 behind
+ * one screen branch per two pairs. */
 #define RT_OPT_FLAT 7
 #define RT_OPT_RAYS_USED 8 /* get only: the pixels per wave the last kernel-3 render used */
 int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value);

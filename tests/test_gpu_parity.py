@@ -225,7 +225,7 @@ def test_interior_record_orders(order, height, kernel, shadow):
     _counters_match(cnt, ocnt, kernel)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("name,w,h", [("dump_test", 64, 36), ("tester", 80, 45), ("dump", 48, 27),
                                       ("tester", 33, 9)])
 def test_flat_kernel_variants(variant, name, w, h):
@@ -241,7 +241,7 @@ def test_flat_kernel_variants(variant, name, w, h):
     assert [int(cnt[i]) for i in (1, 2, 3)] == [int(ocnt[i]) for i in (1, 2, 3)]
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
 def test_flat_kernel_variants_rabbit_hash(variant):
     import hashlib
     from cpp_cuda_raytracer_dev_amd import _lib
@@ -252,6 +252,46 @@ def test_flat_kernel_variants_rabbit_hash(variant):
     assert hashlib.sha256(argb.tobytes()).hexdigest() == ent["argb_sha"]
     assert hashlib.sha256(hit.tobytes()).hexdigest() == ent["hit_sha"]
     assert [int(cnt[i]) for i in (1, 2, 3)] == [ent["counters"][i] for i in (1, 2, 3)]
+
+
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("ntri", [1, 2, 3, 257])
+def test_flat_signed_layout_edge_triangles(variant, ntri):
+    """The signed pair layout (forms 2-5) on triangles of both windings, facing
+    and behind the camera, zero-area ones and ones whose plane holds the camera
+    (d_w = 0): every form renders the oracle's flat frame and counters."""
+    import numpy as np
+    from cpp_cuda_raytracer_dev_amd import _lib
+    from oracle import _oracle as O
+    rng = np.random.default_rng(1000 + ntri)
+    v = rng.uniform(-0.4, 0.4, size=(3 * ntri, 3)).astype(np.float32)
+    v[:, 1] += 0.1
+    f = np.arange(3 * ntri, dtype=np.int32).reshape(ntri, 3)
+    if ntri > 3:
+        f[1::2] = f[1::2, ::-1]                        # both windings
+        v[3 * 5 + 2] = v[3 * 5]                        # zero-area triangle (e2 = 0)
+        v[3 * 7:3 * 7 + 3, 0] = 0.0                    # plane x = 0 holds the camera: d_w = 0
+        v[3 * 9:3 * 9 + 3, 2] -= 1.5                   # behind the camera
+    pts, _, leafs = R.assemble_mesh(v, f)
+    opts, _ = O.assemble(v, np.full(ntri, 3, np.int32), f.reshape(-1))
+    assert pts.tobytes() == opts.tobytes()
+    w, h = 40, 24
+    trixel = R.Trixel(len(pts), pts)
+    cam = R.Camera.default(w, h)
+    cam.set_option(_lib.RT_OPT_FLAT, variant)
+    obj = R.Object(trixel)
+    cam.add_object(obj)
+    obj.render(cam, mode=1, flags=R.RT_FLAG_WRITE_HIT | R.RT_FLAG_COUNT)
+    cam.color_pixels(R.PHONG_COLOR_TAG)
+    cnt = cam.counters()
+    ocam = O.camera(w, h)
+    osc = O.Scene(pts, O.default_rad(len(pts)), None, ocam)
+    try:
+        oargb, ohit, ocnt = osc.render(1, nthreads=4)
+    finally:
+        osc.close()
+    _assert_same((cam.h_color.copy(), cam.h_rmi.copy()), (oargb, ohit), f"signed flat v{variant} n{ntri}")
+    assert [int(cnt[i]) for i in (1, 2, 3)] == [int(ocnt[i]) for i in (1, 2, 3)]
 
 
 # Full frames against the oracle's committed SHA-256 (tests/golden/frame_hashes.json,
@@ -809,13 +849,17 @@ def test_unpack_bands_shapes(w, h, nranks):
     assert (frame2[1:].cpu().numpy().view(np.uint32) == D.unpack_bands_numpy(g, w, h, nranks)).all()
 
 
+@pytest.mark.parametrize("direct", [False, True])
 @pytest.mark.parametrize("scene,w,h,nranks,moved", [("dragon", 1920, 1080, 2, False), ("dragon", 1920, 1080, 8, False),
-                                                     ("rabbit_70k", 81, 45, 3, False), ("dragon", 960, 540, 4, True)])
-def test_rect_gather_single_gpu(scene, w, h, nranks, moved):
+                                                     ("rabbit_70k", 81, 45, 3, False), ("dragon", 960, 540, 4, True),
+                                                     ("dragon", 960, 540, 1, False)])
+def test_rect_gather_single_gpu(scene, w, h, nranks, moved, direct):
     """The rectangle gather of rt_comm_gather_frame, every rank simulated on
     one GPU: each rank's tile render -> rt_pack_rect -> (the peers' parts back
     to back) -> rt_unpack_rect with rank 0's own buffer equals the full frame.
-    A moved object has no background proof: the rectangle is the whole frame."""
+    A moved object has no background proof: the rectangle is the whole frame.
+    direct: rank 0 renders its bands into the (poisoned) frame itself
+    (RT_FLAG_FRAME_OUT, what rt_run_frames does) and the assembly leaves them."""
     import ctypes as C
     import torch
     from cpp_cuda_raytracer_dev_amd import _lib, raytracer as R
@@ -847,11 +891,38 @@ def test_rect_gather_single_gpu(scene, w, h, nranks, moved):
                       C.c_void_p(peers.data_ptr() + 4 * off), None)
         off += counts[r]
     frame = torch.full((w * h,), -1, dtype=torch.int32, device=dev)
-    _lib.call("rt_unpack_rect", 0, w, h, nranks, _lib.ptr(rect), _lib.ptr(locs[0]), _lib.ptr(peers),
-              _lib.ptr(frame), None)
+    if direct:
+        s.cam.render_into(frame, xform=xf, mode=0, flags=R.RT_FLAG_FRAME_OUT, tile=(nranks, 0))
+    _lib.call("rt_unpack_rect", 0, w, h, nranks, _lib.ptr(rect), _lib.ptr(frame if direct else locs[0]),
+              _lib.ptr(peers), _lib.ptr(frame), None)
     torch.cuda.synchronize()
     got = frame.cpu().numpy().view(np.uint32)
     assert (got == full).all(), int((got != full).sum())
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("nranks", [1, 2, 3, 8])
+def test_frame_out_tile_rows(nranks, mode):
+    """RT_FLAG_FRAME_OUT: a rank's bands land on their frame rows of a w*h
+    buffer (colour and hit), every other row untouched; all ranks together
+    give the full frame."""
+    import torch
+    s = H.GpuScene("rabbit_70k", 81, 45)
+    full, fhit, _ = s.render(mode)
+    dev = torch.device("cuda:0")
+    w, h = 81, 45
+    frame = torch.full((w * h,), -1, dtype=torch.int32, device=dev)
+    hit = torch.full((w * h,), -7, dtype=torch.int64, device=dev)
+    rows = np.arange(h) // 8 % nranks
+    for r in range(nranks):
+        s.cam.render_into(frame, hit, mode=mode, flags=R.RT_FLAG_FRAME_OUT | R.RT_FLAG_WRITE_HIT, tile=(nranks, r))
+        torch.cuda.synchronize()
+        got = frame.cpu().numpy().view(np.uint32).reshape(h, w)
+        gh = hit.cpu().numpy().reshape(h, w)
+        done = rows <= r
+        assert (got[done] == full.reshape(h, w)[done]).all()
+        assert (gh[done] == fhit.reshape(h, w)[done]).all()
+        assert (got[~done] == 0xFFFFFFFF).all() and (gh[~done] == -7).all()
 
 
 def test_native_comm_world1():
