@@ -62,8 +62,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--scene", default="dragon", choices=["dragon", "happy", "rabbit_70k", "tester", "big"],
-                    help="dragon / happy: seeded stand-ins for the missing meshes (big: a 3.1M-triangle one); rabbit_70k / tester: the "
+    ap.add_argument("--scene", default="dragon", choices=["dragon", "happy", "rabbit_70k", "tester", "big", "knot"],
+                    help="dragon / happy: seeded stand-ins for the missing meshes (big: a 3.1M-triangle one; knot: "
+                         "the dragon's count and box as a torus-knot tube, ~2x the traversal work); rabbit_70k / tester: the "
                          "reference's own meshes")
     ap.add_argument("--view", default="default", choices=["default", "fill"],
                     help="default: WinMain's camera; fill: the object over >= 90%% of the pixels (README.md:19)")

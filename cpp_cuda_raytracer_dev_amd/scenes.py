@@ -29,6 +29,12 @@ STANDINS = {
     # not a reference mesh: > 2^21 triangles, so its median tree is 22 levels
     # tall (kernel 3's former path-code limit was 21); dragon-sized box
     "big": (3_146_328, (-0.112, 0.052, -0.067), (0.093, 0.199, 0.054), (1536, 1025), (60, 6)),
+    # not a reference mesh: the dragon's triangle count and box as a
+    # noise-displaced (5, 12) torus-knot tube (SURVEY.md §8d's suggestion):
+    # strands in front of strands, so a covered ray crosses ~1.9x the boxes
+    # of the convex-ish blob (183 vs 98 interior visits per hit pixel at
+    # 480x270).  (U, V) = curve samples x tube samples, then the small blob
+    "knot": (871_414, (-0.112, 0.052, -0.067), (0.093, 0.199, 0.054), (3000, 145), (101, 8)),
 }
 STANDIN_SEED = 20221015
 
@@ -84,7 +90,8 @@ def _uv_sphere(U: int, V: int):
     return verts, np.concatenate(faces).astype(np.int32)
 
 
-def _displace(v: np.ndarray, rng: np.random.Generator, octaves: int, amp: float) -> np.ndarray:
+def _noise(v: np.ndarray, rng: np.random.Generator, octaves: int, amp: float) -> np.ndarray:
+    """1 + a sum of seeded plane waves at the points v (a radial factor)."""
     r = np.ones(len(v))
     for o in range(octaves):
         k = 3.0 * (1.9 ** o)
@@ -93,17 +100,63 @@ def _displace(v: np.ndarray, rng: np.random.Generator, octaves: int, amp: float)
             d /= np.linalg.norm(d)
             ph = rng.uniform(0, 2 * np.pi)
             r += (amp / (1.7 ** o)) * np.sin(k * (v @ d) + ph)
-    return v * r[:, None]
+    return r
+
+
+def _displace(v: np.ndarray, rng: np.random.Generator, octaves: int, amp: float) -> np.ndarray:
+    return v * _noise(v, rng, octaves, amp)[:, None]
+
+
+def _knot_tube(U: int, V: int, rng: np.random.Generator, p: int = 5, q: int = 12, tube: float = 0.28):
+    """A closed tube around the (p, q) torus knot: U rings of V vertices
+    (2*U*V triangles, torus topology), parallel-transported frames with the
+    closing twist spread along the curve, and a noise-displaced radius."""
+    t = 2 * np.pi * np.arange(U, dtype=np.float64) / U
+    r = 2.0 + np.cos(q * t)
+    curve = np.stack([r * np.cos(p * t), r * np.sin(p * t), 1.1 * np.sin(q * t)], -1)
+    tan = np.roll(curve, -1, 0) - np.roll(curve, 1, 0)
+    tan /= np.linalg.norm(tan, axis=1, keepdims=True)
+    nrm = np.zeros_like(curve)
+    n = np.cross(tan[0], [0.0, 0.0, 1.0])
+    n /= np.linalg.norm(n)
+    for i in range(U):  # parallel transport: remove the tangential part
+        n = n - tan[i] * (n @ tan[i])
+        n /= np.linalg.norm(n)
+        nrm[i] = n
+    bin_ = np.cross(tan, nrm)
+    # the transported frame comes back rotated by `twist`: spread it out
+    n_end = nrm[-1] - tan[0] * (nrm[-1] @ tan[0])
+    twist = np.arctan2(n_end @ bin_[0], n_end @ nrm[0])
+    a = -twist * np.arange(U) / U
+    nrm, bin_ = (np.cos(a)[:, None] * nrm + np.sin(a)[:, None] * bin_,
+                 -np.sin(a)[:, None] * nrm + np.cos(a)[:, None] * bin_)
+    th = 2 * np.pi * np.arange(V, dtype=np.float64) / V
+    ring = np.cos(th)[None, :, None] * nrm[:, None, :] + np.sin(th)[None, :, None] * bin_[:, None, :]
+    base = curve[:, None, :] + tube * ring
+    rad = _noise(base.reshape(-1, 3) / 3.0, rng, octaves=6, amp=0.05).reshape(U, V, 1)
+    verts = curve[:, None, :] + tube * ring * rad
+    i = np.arange(U)[:, None]
+    j = np.arange(V)[None, :]
+    a0 = i * V + j
+    b0 = i * V + (j + 1) % V
+    c0 = ((i + 1) % U) * V + j
+    d0 = ((i + 1) % U) * V + (j + 1) % V
+    faces = np.concatenate([np.stack([a0, b0, d0], -1).reshape(-1, 3), np.stack([a0, d0, c0], -1).reshape(-1, 3)])
+    return verts.reshape(-1, 3), faces.astype(np.int32)
 
 
 def standin(name: str):
     """Synthetic stand-in mesh: (verts [nv,3] f32, faces [nf,3] i32)."""
     ntri, lo, hi, (U, V), (u2, v2) = STANDINS[name]
-    rng = np.random.default_rng(STANDIN_SEED + {"dragon": 0, "happy": 1, "big": 2}[name])
+    rng = np.random.default_rng(STANDIN_SEED + {"dragon": 0, "happy": 1, "big": 2, "knot": 3}[name])
     lo, hi = np.asarray(lo), np.asarray(hi)
     c, half = (lo + hi) / 2, (hi - lo) / 2
-    v, f = _uv_sphere(U, V)
-    v = _displace(v, rng, octaves=6, amp=0.06)
+    if name == "knot":
+        v, f = _knot_tube(U, V, rng)
+        v = v - (v.max(axis=0) + v.min(axis=0)) / 2
+    else:
+        v, f = _uv_sphere(U, V)
+        v = _displace(v, rng, octaves=6, amp=0.06)
     v = v / np.abs(v).max(axis=0)  # fill the box
     body = c + half * v
     # a small closed blob near the +x end (head/eye), fully inside the box

@@ -44,6 +44,9 @@ FRAMES = [
     ("happy", 3840, 2160, 0, True, "default"),      # C5
     ("big", 1920, 1080, 0, False, "default"),       # 3.1M triangles: a 22-level tree in kernel 3
     ("big", 1920, 1080, 0, True, "default"),
+    ("knot", 960, 540, 0, False, "default"),       # the harder dragon-sized stand-in
+    ("knot", 1920, 1080, 0, False, "default"),
+    ("knot", 1920, 1080, 0, True, "default"),
 ]
 
 

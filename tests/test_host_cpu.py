@@ -394,3 +394,19 @@ def test_band_pack_unpack_roundtrip():
             g = np.concatenate([D.pack_bands_numpy(frame, w, h, n, r) for r in range(n)])
             assert D.packed_pixels(w, h, n) == R.packed_pixels(w, h, n)
             assert (D.unpack_bands_numpy(g, w, h, n) == frame).all()
+
+
+def test_knot_standin_is_closed_manifold():
+    """The torus-knot stand-in (scenes.STANDINS["knot"]): the dragon's
+    triangle count inside the dragon's box, every edge shared by exactly two
+    triangles (a closed 2-manifold, like the blob stand-ins), deterministic."""
+    v, f = scenes.standin("knot")
+    assert len(f) == 871_414 and np.isfinite(v).all()
+    lo, hi = np.array(scenes.STANDINS["knot"][1]), np.array(scenes.STANDINS["knot"][2])
+    assert np.allclose(v.min(0), lo, atol=1e-6) and np.allclose(v.max(0), hi, atol=1e-6)
+    e = np.sort(np.concatenate([f[:, [0, 1]], f[:, [1, 2]], f[:, [2, 0]]]), axis=1).astype(np.int64)
+    _, cnt = np.unique(e[:, 0] * len(v) + e[:, 1], return_counts=True)
+    assert (cnt == 2).all()
+    v2, f2 = scenes.standin("knot")
+    assert v.tobytes() == v2.tobytes() and f.tobytes() == f2.tobytes()
+    assert scenes.mesh_sha("knot") == H.frame_hashes()["knot_1920x1080_m0"]["mesh_sha"]

@@ -46,6 +46,10 @@ if has bench; then
         --no-cpu-baseline
     step bench_dragon_shadow 300 python bench.py --steps 500 --warmup 50 --shadow --no-cpu-baseline
     step bench_big 300 python bench.py --steps 200 --warmup 20 --scene big --no-cpu-baseline
+    step bench_knot1080 300 python bench.py --steps 1000 --warmup 100 --scene knot --no-cpu-baseline
+    step bench_knot960 300 python bench.py --steps 1000 --warmup 100 --scene knot --width 960 --height 540 \
+        --no-cpu-baseline
+    step bench_knot1080_shadow 300 python bench.py --steps 500 --warmup 50 --scene knot --shadow --no-cpu-baseline
     step bench_rehearse 300 python bench.py --steps 1000 --warmup 100 --rehearse-gather --no-cpu-baseline
     step bench_animate 300 python bench.py --steps 500 --warmup 20 --animate R+W.Q.T.W --no-cpu-baseline
 fi
