@@ -252,7 +252,9 @@ void rt_comm_destroy(rt_comm* c);
  * events on render_stream; *kernel_ms_avg / *kernel_ms_frames receive their
  * mean and count; *host_ms (may be NULL) the host time spent enqueueing the
  * frames.  Synchronises both streams before returning.  tile.nranks 0 (or
- * 1) renders the whole frame.
+ * 1) renders the whole frame.  On rank 0 of comm (with a tile) frame j renders
+ * straight into d_frame[k] (RT_FLAG_FRAME_OUT; d_local is unused there) and
+ * the gather adds the peers' rows: the two lanes then share no events.
  * inflight (0 or 1: off) > 1 keeps that many frames in flight: frame j
  * renders on the library's render lane j % inflight (streams of the camera,
  * created once, each on a hardware queue of its own while queues are free),
