@@ -103,7 +103,7 @@ struct rt_camera {
     int rays = 0;                    // kOptRays: pixels per wave of kernel 3 (0: auto_rays)
     int last_rays = 0;               // the pixels per wave the last kernel-3 render used
     int items = 2;                   // kOptItems: items per lane per pool iteration
-    int flat_variant = 5;            // kOptFlat: flat-list kernel form
+    int flat_variant = 9;            // kOptFlat: flat-list kernel form
     // shadow renders: the any-hit push order, fixed (kOptShadowOrder 0..3)
     // or timed (-1): a round of trial frames runs each order kTuneReps times,
     // interleaved, bracketed by events; the fastest is kept for kTunePeriod
@@ -1477,7 +1477,7 @@ extern "C" int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value) {
         c->tune_pending = false;
         return RT_OK;
     case kOptFlat:
-        if (value < 0 || value > 6) return fail(RT_ERR_INVALID, "flat kernel form %d (0..6)", value);
+        if (value < 0 || value > 9) return fail(RT_ERR_INVALID, "flat kernel form %d (0..9)", value);
         c->flat_variant = value;
         return RT_OK;
     case kOptTileOrder:

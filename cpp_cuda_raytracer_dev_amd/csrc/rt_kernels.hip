@@ -47,7 +47,10 @@ TraceFn flat_kernel(bool wh, bool cnt, int variant) {
     if (variant == 3) return flat_kernel_v<3>(wh, cnt);
     if (variant == 4) return flat_kernel_v<4>(wh, cnt);
     if (variant == 5) return flat_kernel_v<5>(wh, cnt);
-    return flat_kernel_v<6>(wh, cnt);
+    if (variant == 6) return flat_kernel_v<6>(wh, cnt);
+    if (variant == 7) return flat_kernel_v<7>(wh, cnt);
+    if (variant == 8) return flat_kernel_v<8>(wh, cnt);
+    return flat_kernel_v<9>(wh, cnt);
 }
 
 int launch_pair_tri(const float4* trec, uint32_t ntri, float4* tpair, void* stream) {

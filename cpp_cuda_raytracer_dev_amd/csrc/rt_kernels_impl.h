@@ -1642,6 +1642,29 @@ struct FlatPair {
         U = (qx * tx + qy * ty) + qz * tz;
         V = (X * dqx + Y * dqy) + Z * dqz;
     }
+    // Form 7: V first.  v's numerator V = r . d_q depends on the ray only
+    // through one dot product, and the signed layout needs V > 0 (or NaN)
+    // for an accept; V <= 0 in every lane of the wave for both triangles --
+    // an 8x8 pixel tile wholly on the outer side of the two edge planes,
+    // about half the (tile, pair) combinations -- skips the cross product,
+    // f and U (19 of the pair's 24 packed operations).  The lanes that go on
+    // compute exactly form 4's values.
+    __device__ __forceinline__ void test_signed_v(const f2v X, const f2v Y, const f2v Z, uint32_t t, float& d,
+                                                  uint32_t& best, uint32_t& n_acc) const {
+        const f2v V = (X * dqx + Y * dqy) + Z * dqz;
+        if (!(V.x <= 0.0f) || !(V.y <= 0.0f)) {
+            const f2v qx = Y * e2z - Z * e2y;
+            const f2v qy = Z * e2x - X * e2z;
+            const f2v qz = X * e2y - Y * e2x;
+            const f2v f = (qx * e1x + qy * e1y) + qz * e1z;
+            const f2v U = (qx * tx + qy * ty) + qz * tz;
+            const float m0 = fminf(fminf(U.x, V.x), f.x), m1 = fminf(fminf(U.y, V.y), f.y);
+            if (!(fmaxf(m0, m1) <= 0.0f)) {
+                if (!(m0 <= 0.0f)) flat_accept(f.x, U.x, V.x, dw.x, t, d, best, n_acc);
+                if (!(m1 <= 0.0f)) flat_accept(f.y, U.y, V.y, dw.y, t + 1, d, best, n_acc);
+            }
+        }
+    }
     __device__ __forceinline__ void test_signed(const f2v X, const f2v Y, const f2v Z, uint32_t t, float& d,
                                                 uint32_t& best, uint32_t& n_acc) const {
         f2v f, U, V;
@@ -1764,6 +1787,37 @@ __global__ __launch_bounds__(kTileWFlat * kTileH) void k_trace_flat(TraceParams 
                 FlatPair a;
                 a.load(Q + 16 * (size_t)p);
                 a.test_signed(X, Y, Z, 2 * p, d, best, n_acc);
+            }
+        } else if (kVariant == 9) {
+            // form 7 software pipelined as form 3: pair p + 1's scalar loads
+            // issued once pair p's have arrived, in flight during its tests
+            const uint32_t zero = ntri >> 31;  // 0: scenes hold < 2^29 triangles
+            FlatPair a, b;
+            a.load(Q);
+            uint32_t p = 0;
+            for (; p + 1 < npair; p += 2) {
+                b.load_after(Q, p + 1, a, zero);
+                a.test_signed_v(X, Y, Z, 2 * p, d, best, n_acc);
+                a.load_after(Q, min(p + 2, npair - 1), b, zero);
+                b.test_signed_v(X, Y, Z, 2 * p + 2, d, best, n_acc);
+            }
+            if (p < npair) a.test_signed_v(X, Y, Z, 2 * p, d, best, n_acc);
+        } else if (kVariant == 7 || kVariant == 8) {
+            // form 7: form 5 with V first (test_signed_v); 8: one pair per iteration
+            uint32_t p = 0;
+            if (kVariant == 7) {
+                for (; p + 1 < npair; p += 2) {
+                    FlatPair a, b;
+                    a.load(Q + 16 * (size_t)p);
+                    b.load(Q + 16 * (size_t)p + 16);
+                    a.test_signed_v(X, Y, Z, 2 * p, d, best, n_acc);
+                    b.test_signed_v(X, Y, Z, 2 * p + 2, d, best, n_acc);
+                }
+            }
+            for (; p < npair; p++) {
+                FlatPair a;
+                a.load(Q + 16 * (size_t)p);
+                a.test_signed_v(X, Y, Z, 2 * p, d, best, n_acc);
             }
         } else if (kVariant == 5) {
             // form 4, two pairs per iteration

@@ -343,8 +343,10 @@ int rt_camera_info(const rt_camera* c, int32_t* w, int32_t* h, int32_t* max_dept
 /* Flat-list kernel form (same frame): 0 one triangle per iteration, 1 two
  * per iteration, 2 two per iteration as packed float2 arithmetic,
  * 3 = 2 software pipelined, 4 = 2 over the signed pair layout with one min3
- * screen per triangle, 5 = 4 unrolled to two pairs (default), 6 = 5 behind
- * one screen branch per two pairs. */
+ * screen per triangle, 5 = 4 unrolled to two pairs, 6 = 5 behind one screen
+ * branch per two pairs, 7 = 5 with v's numerator first (a wave whose rays
+ * all have V <= 0 skips the rest of the pair), 8 = 7 one pair per
+ * iteration, 9 = 7 software pipelined as 3 (default). */
 #define RT_OPT_FLAT 7
 #define RT_OPT_RAYS_USED 8 /* get only: the pixels per wave the last kernel-3 render used */
 int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value);

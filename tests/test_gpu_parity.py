@@ -225,7 +225,7 @@ def test_interior_record_orders(order, height, kernel, shadow):
     _counters_match(cnt, ocnt, kernel)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("name,w,h", [("dump_test", 64, 36), ("tester", 80, 45), ("dump", 48, 27),
                                       ("tester", 33, 9)])
 def test_flat_kernel_variants(variant, name, w, h):
@@ -241,7 +241,7 @@ def test_flat_kernel_variants(variant, name, w, h):
     assert [int(cnt[i]) for i in (1, 2, 3)] == [int(ocnt[i]) for i in (1, 2, 3)]
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 def test_flat_kernel_variants_rabbit_hash(variant):
     import hashlib
     from cpp_cuda_raytracer_dev_amd import _lib
@@ -254,7 +254,7 @@ def test_flat_kernel_variants_rabbit_hash(variant):
     assert [int(cnt[i]) for i in (1, 2, 3)] == [ent["counters"][i] for i in (1, 2, 3)]
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("ntri", [1, 2, 3, 257])
 def test_flat_signed_layout_edge_triangles(variant, ntri):
     """The signed pair layout (forms 2-5) on triangles of both windings, facing
