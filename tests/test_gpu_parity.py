@@ -239,6 +239,8 @@ def test_flat_kernel_variants(variant, name, w, h):
     oargb, ohit, ocnt = H.oracle_render(name, w, h, 1)
     _assert_same((argb, hit), (oargb, ohit), f"{name} flat v{variant}")
     assert [int(cnt[i]) for i in (1, 2, 3)] == [int(ocnt[i]) for i in (1, 2, 3)]
+    argb, hit, _ = s.render(1)
+    _assert_same((argb, hit), (oargb, ohit), f"{name} flat v{variant} timed")
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
@@ -252,6 +254,10 @@ def test_flat_kernel_variants_rabbit_hash(variant):
     assert hashlib.sha256(argb.tobytes()).hexdigest() == ent["argb_sha"]
     assert hashlib.sha256(hit.tobytes()).hexdigest() == ent["hit_sha"]
     assert [int(cnt[i]) for i in (1, 2, 3)] == [ent["counters"][i] for i in (1, 2, 3)]
+    # the timed (non-counting) instance as well
+    argb, hit, _ = s.render(1)
+    assert hashlib.sha256(argb.tobytes()).hexdigest() == ent["argb_sha"]
+    assert hashlib.sha256(hit.tobytes()).hexdigest() == ent["hit_sha"]
 
 
 @pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9])
@@ -292,6 +298,9 @@ def test_flat_signed_layout_edge_triangles(variant, ntri):
         osc.close()
     _assert_same((cam.h_color.copy(), cam.h_rmi.copy()), (oargb, ohit), f"signed flat v{variant} n{ntri}")
     assert [int(cnt[i]) for i in (1, 2, 3)] == [int(ocnt[i]) for i in (1, 2, 3)]
+    obj.render(cam, mode=1, flags=R.RT_FLAG_WRITE_HIT)  # the timed (non-counting) instance
+    cam.color_pixels(R.PHONG_COLOR_TAG)
+    _assert_same((cam.h_color.copy(), cam.h_rmi.copy()), (oargb, ohit), f"signed flat v{variant} n{ntri} timed")
 
 
 # Full frames against the oracle's committed SHA-256 (tests/golden/frame_hashes.json,
