@@ -434,6 +434,32 @@ __device__ __forceinline__ bool leaf_test_rec(const Ray& R, const float4 A, cons
     return false;
 }
 
+// leaf_test_rec for a ray from the camera (no object translation): t = d_t,
+// so cross(t, e1) is the record's d_q and dot(e2, cross(t, e1)) its d_w,
+// both computed by k_cam_tri with the same float operations (products
+// commute exactly): 14 fewer VALU operations per leaf visit, the same bits.
+__device__ __forceinline__ bool leaf_test_cam(const Ray& R, const float4 A, const float4 B, const float4 Cq,
+                                              const float4 Dq, uint32_t t, float& d, uint32_t& best) {
+    const float e1x = A.x, e1y = A.y, e1z = A.z;
+    const float e2x = A.w, e2y = B.x, e2z = B.y;
+    const float tx = B.z, ty = B.w, tz = Cq.x;
+    float qpx, qpy, qpz;
+    cross3(qpx, qpy, qpz, R.rx, R.ry, R.rz, e2x, e2y, e2z);
+    const float f = dot3(qpx, qpy, qpz, e1x, e1y, e1z);
+    if (!(f < kEpsF && f > -kEpsF)) {
+        const float pe1 = 1.0f / f;   // == (float)(1.0 / (double)f)
+        const float u = pe1 * dot3(qpx, qpy, qpz, tx, ty, tz);
+        const float v = pe1 * dot3(R.rx, R.ry, R.rz, Cq.y, Cq.z, Cq.w);
+        const float w = pe1 * Dq.x;
+        if ((w < d) && !((u < kEpsF) || (v < kEpsF) || ((u + v) > 1.0f) || (w < kEpsF))) {
+            d = w;
+            best = t;
+            return true;
+        }
+    }
+    return false;
+}
+
 __device__ __forceinline__ bool leaf_test(const Ray& R, const float4* __restrict__ trec, uint32_t t,
                                           float& d, uint32_t& best) {
     return leaf_test_rec(R, trec[4 * (size_t)t], trec[4 * (size_t)t + 1], trec[4 * (size_t)t + 2], t, d, best);
@@ -781,15 +807,17 @@ __device__ __forceinline__ void ray_of(const float4* rd, Ray& Q, float4& q2, flo
 // TD/Trixel.cu:98-145.  kAny: shadow walk (Lmax and the hit triangle come
 // from rd[4]).
 template <bool kTranslated, bool kCount, bool kAny>
-__device__ __forceinline__ void visit_leaf(const float4* rd, uint4 it, float4 r0, float4 r1, float4 r2, Visit& o,
-                                           uint32_t& n_leaf, uint32_t& n_acc) {
+__device__ __forceinline__ void visit_leaf(const float4* rd, uint4 it, float4 r0, float4 r1, float4 r2, float4 r3,
+                                           Visit& o, uint32_t& n_leaf, uint32_t& n_acc) {
     Ray Q;
     float4 q2, q3, q4;
     ray_of<kTranslated>(rd, Q, q2, q3, q4);
     if (kCount) n_leaf++;
     float d = kAny ? q4.z : kDrawDistance;
     uint32_t best = kMiss;
-    if (leaf_test_rec(Q, r0, r1, r2, it.x & ~kLeafBit, d, best) && (!kAny || best != __float_as_uint(q4.w))) {
+    const bool acc = kTranslated ? leaf_test_rec(Q, r0, r1, r2, it.x & ~kLeafBit, d, best)
+                                 : leaf_test_cam(Q, r0, r1, r2, r3, it.x & ~kLeafBit, d, best);
+    if (acc && (!kAny || best != __float_as_uint(q4.w))) {
         o.cand = true;
         o.ctri = best;
         o.key = kAny ? 0ull : ((unsigned long long)__float_as_uint(d) << 32) | code_key(it.w & kCodeMarkMask);
@@ -877,7 +905,7 @@ template <int kVec, bool kTranslated, bool kCount, bool kAny>
 __device__ __forceinline__ void visit_item(const float4* rd, uint4 it, float4 r0, float4 r1, float4 r2, float4 r3,
                                            Visit& o, uint32_t& n_int, uint32_t& n_leaf, uint32_t& n_acc,
                                            uint32_t& n_desc) {
-    if (it.x & kLeafBit) visit_leaf<kTranslated, kCount, kAny>(rd, it, r0, r1, r2, o, n_leaf, n_acc);
+    if (it.x & kLeafBit) visit_leaf<kTranslated, kCount, kAny>(rd, it, r0, r1, r2, r3, o, n_leaf, n_acc);
     else visit_interior<kTranslated, kCount>(rd, it, r0, r1, r2, r3, o, n_int, n_desc);
 }
 
@@ -1197,7 +1225,7 @@ __device__ __forceinline__ void pool_walk_split(const TraceParams& P, uint4* ite
             v1.ka = v1.kb = false; v1.cand = false;
             if (leafslot) {
                 if (act1)
-                    visit_leaf<kTranslated, kCount, kAny>(s_ray + (size_t)(it1.w >> 26) * kVec, it1, b0, b1, b2, v1,
+                    visit_leaf<kTranslated, kCount, kAny>(s_ray + (size_t)(it1.w >> 26) * kVec, it1, b0, b1, b2, b3, v1,
                                                           n_leaf, n_acc);
                 record_candidate<kAny>(s_key, s_tri, it1, v1);
             } else {
