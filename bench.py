@@ -105,7 +105,8 @@ def parse():
     ap.add_argument("--flat", type=int, default=-1,
                     help="flat-list kernel form: 0 one triangle per iteration, 1 pairs, 2 packed float2 pairs, "
                          "3 pipelined 2, 4 signed pairs + min3 screen, 5 4 unrolled x2, 6 5 behind one branch, "
-                         "7 5 with V first, 8 7 one pair per iteration, 9 7 pipelined (-1: the library default, 9)")
+                         "7 5 with V first, 8 7 one pair per iteration, 9 7 pipelined, 10-13 9 over 8/4/16/32 chunks "
+                         "(-1: the library default, 12)")
     ap.add_argument("--coarse", type=int, default=8,
                     help="kernel 3: 8x8 groups per wave outside the root box's screen rectangle (0 = off)")
     ap.add_argument("--event-every", type=int, default=0,

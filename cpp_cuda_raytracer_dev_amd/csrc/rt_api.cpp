@@ -103,7 +103,15 @@ struct rt_camera {
     int rays = 0;                    // kOptRays: pixels per wave of kernel 3 (0: auto_rays)
     int last_rays = 0;               // the pixels per wave the last kernel-3 render used
     int items = 2;                   // kOptItems: items per lane per pool iteration
-    int flat_variant = 9;            // kOptFlat: flat-list kernel form
+    int flat_variant = 12;           // kOptFlat: flat-list kernel form
+    // chunked flat forms: one per-pixel key buffer per stream that renders
+    // (frames in flight use several), all ones between frames
+    struct FlatKeys {
+        hipStream_t stream = nullptr;
+        unsigned long long* d = nullptr;
+        int64_t cap = 0;
+    };
+    FlatKeys flat_keys[8];
     // shadow renders: the any-hit push order, fixed (kOptShadowOrder 0..3)
     // or timed (-1): a round of trial frames runs each order kTuneReps times,
     // interleaved, bracketed by events; the fastest is kept for kTunePeriod
@@ -1139,6 +1147,45 @@ static int launch_split(rt_camera* c, const TraceParams& p, uint32_t mode, uint3
     return RT_OK;
 }
 
+// The key buffer of the chunked flat forms for renders on `stream` (at least
+// `npix` keys): allocated all ones once, reset by every frame's shading.
+static int flat_keys_for(rt_camera* c, hipStream_t stream, int64_t npix, unsigned long long** out) {
+    rt_camera::FlatKeys* slot = nullptr;
+    for (auto& k : c->flat_keys)
+        if (k.d && k.stream == stream) slot = &k;
+    if (!slot)
+        for (auto& k : c->flat_keys)
+            if (!k.d) {
+                slot = &k;
+                break;
+            }
+    if (!slot) {  // more streams than slots: start over once nothing uses them
+        int rc = hip_check(hipDeviceSynchronize(), "flat keys sync");
+        if (rc) return rc;
+        for (auto& k : c->flat_keys) {
+            dev_free(k.d);
+            k = rt_camera::FlatKeys{};
+        }
+        slot = &c->flat_keys[0];
+    }
+    if (slot->cap < npix) {
+        if (slot->d) {  // the stream's earlier frames may still use it
+            int rc = hip_check(hipStreamSynchronize(stream), "flat keys sync");
+            if (rc) return rc;
+        }
+        dev_free(slot->d);
+        slot->d = nullptr;
+        int rc = dev_alloc(&slot->d, (size_t)npix, "hipMalloc(flat keys)");
+        if (!rc) rc = hip_check(hipMemsetAsync(slot->d, 0xFF, sizeof(unsigned long long) * (size_t)npix, stream),
+                                "flat keys init");
+        if (rc) return rc;
+        slot->cap = npix;
+    }
+    slot->stream = stream;
+    *out = slot->d;
+    return RT_OK;
+}
+
 static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32_t flags, const rt_tile* tile,
                          uint32_t* argb, int64_t* hit, void* stream) {
     if (!c) return fail(RT_ERR_INVALID, "rt_render: null camera");
@@ -1181,6 +1228,15 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
         pc.p = p;
     }
     p.frame_out = (flags & RT_FLAG_FRAME_OUT) ? 1 : 0;
+    p.flat_key = nullptr;
+    p.flat_chunks = 0;
+    if (mode == RT_MODE_FLAT && c->flat_variant >= 10 && !(flags & RT_FLAG_COUNT)) {
+        const int64_t npix = std::max<int64_t>((int64_t)c->w * c->h, rt_tile_packed_pixels(c->w, c->h, nr));
+        if ((rc = flat_keys_for(c, (hipStream_t)stream, npix, &p.flat_key))) return rc;
+        p.flat_chunks = c->flat_variant == 10 ? 8 : c->flat_variant == 11 ? 4 : c->flat_variant == 12 ? 16 : 32;
+        const int64_t npair = (c->obj->ntri + 1) / 2;
+        if (p.flat_chunks > npair) p.flat_chunks = (int32_t)npair;
+    }
     if (mode == RT_MODE_KD && effective_kernel(c) == 3) c->last_rays = p.rays;
     int trial;
     p.any_order = any_order_for(c, flags, stream, trial) | ((c->debug & 16) ? 4 : 0);
@@ -1420,6 +1476,7 @@ extern "C" void rt_camera_destroy(rt_camera* c) {
     c->d_order = nullptr;
     if (c->order_up_ev) (void)hipEventDestroy(c->order_up_ev);
     dev_free(c->d_dbg);
+    for (auto& k : c->flat_keys) dev_free(k.d);
     dev_free(c->d_cost);
     if (c->h_cost) (void)hipHostFree(c->h_cost);
     if (c->h_order) (void)hipHostFree(c->h_order);
@@ -1477,7 +1534,7 @@ extern "C" int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value) {
         c->tune_pending = false;
         return RT_OK;
     case kOptFlat:
-        if (value < 0 || value > 9) return fail(RT_ERR_INVALID, "flat kernel form %d (0..9)", value);
+        if (value < 0 || value > 13) return fail(RT_ERR_INVALID, "flat kernel form %d (0..13)", value);
         c->flat_variant = value;
         return RT_OK;
     case kOptTileOrder:

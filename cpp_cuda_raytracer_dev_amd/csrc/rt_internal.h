@@ -130,7 +130,11 @@ struct TraceParams {
     uint32_t ntri;
     int32_t max_depth;
     int32_t tree_height;           // the scene tree's height (kernel 3's pool slack is height + 1)
-    int32_t flat_variant;          // Option kOptFlat: flat-list kernel form (0, 1, 2)
+    int32_t flat_variant;          // Option kOptFlat: flat-list kernel form (0..12)
+    // chunked flat forms (10-12, non-counting renders): per-pixel (w bits, triangle)
+    // minima of the chunks, all ones between frames; and the chunk count
+    unsigned long long* flat_key;
+    int32_t flat_chunks;
 };
 
 }  // namespace rt

@@ -68,7 +68,16 @@ int launch_trace(const TraceParams& p, uint32_t mode, uint32_t flags, int kernel
     const unsigned threads = (unsigned)((p.tile_w / 8) * (p.tile_h / (p.rays / 8)) * 64);
     if (mode == RT_MODE_FLAT) {
         if (fine == 0) return RT_OK;
-        TraceFn fn = flat_kernel(wh, cnt, p.flat_variant);
+        if (p.flat_key && !cnt) {  // chunked forms: the chunks, then the shading
+            k_flat_chunk<<<fine * (unsigned)p.flat_chunks, threads, 0, s>>>(p);
+            int rc = check_launch<void>("k_flat_chunk");
+            if (rc) return rc;
+            (wh ? k_flat_shade<true> : k_flat_shade<false>)<<<fine, threads, 0, s>>>(p);
+            return check_launch<void>("k_flat_shade");
+        }
+        // counting renders of the chunked forms take form 9 (the accept
+        // counter counts updates of the running minimum in index order)
+        TraceFn fn = flat_kernel(wh, cnt, p.flat_variant >= 10 ? 9 : p.flat_variant);
         fn<<<fine, threads, 0, s>>>(p);
         return check_launch<void>("k_trace_flat");
     }

@@ -1705,6 +1705,24 @@ struct FlatPair {
     }
 };
 
+// Phong of a flat-list pixel (TD/Camera.cu:19-69) from its nearest hit
+// (w = d, triangle best), or the background; writes the pixel (and hit).
+template <bool kWriteHit>
+__device__ __forceinline__ void flat_shade_out(const TraceParams& P, const Pixel& px, const float rmd[3], float d,
+                                               uint32_t best) {
+    uint32_t argb = kBackground;
+    if (best != kMiss) {
+        const float4 N = P.shade[2 * (size_t)best];
+        const float4 M = P.shade[2 * (size_t)best + 1];
+        const float pnt[3] = {d * rmd[0], d * rmd[1], d * rmd[2]};
+        const float nrm[3] = {N.x, N.y, N.z};
+        const float rad[3] = {M.x, M.y, M.z};
+        argb = phong(pnt, nrm, rmd, rad);
+    }
+    P.argb[px.out] = argb;
+    if (kWriteHit) P.hit[px.out] = best == kMiss ? (int64_t)-1 : (int64_t)best;
+}
+
 // kVariant 0: one triangle per iteration, the 64-B camera-relative record
 // (the first form).  1: two triangles per iteration, both records loaded
 // before either is tested, branch-free screen.  2: the same pair as packed
@@ -1879,22 +1897,64 @@ __global__ __launch_bounds__(kTileWFlat * kTileH) void k_trace_flat(TraceParams 
             if (p < npair) a.test(X, Y, Z, 2 * p, d, best, n_acc);
         }
     }
-    uint32_t argb = kBackground;
-    if (best != kMiss) {
-        const float4 N = P.shade[2 * (size_t)best];
-        const float4 M = P.shade[2 * (size_t)best + 1];
-        const float pnt[3] = {d * rx, d * ry, d * rz};
-        const float nrm[3] = {N.x, N.y, N.z};
-        const float rad[3] = {M.x, M.y, M.z};
-        argb = phong(pnt, nrm, rmd, rad);
-    }
-    P.argb[px.out] = argb;
-    if (kWriteHit) P.hit[px.out] = best == kMiss ? (int64_t)-1 : (int64_t)best;
+    flat_shade_out<kWriteHit>(P, px, rmd, d, best);
     if (kCount) {
         wave_count_add(&P.counters[1], ntri);
         wave_count_add(&P.counters[2], n_acc);
         wave_count_add(&P.counters[3], best != kMiss ? 1u : 0u);
     }
+}
+
+// Chunked flat list (forms 10-12, renders without counters): block b of a
+// grid of fine blocks x P.flat_chunks tests its tile's rays against chunk
+// b / fine of the pair list (form 9's loop: V first, pipelined loads) and
+// folds each ray's nearest hit into P.flat_key[pixel] as the 64-bit minimum
+// of (w bits, triangle); k_flat_shade then shades every pixel from its key
+// and resets it.  w >= eps > 0, so the float bits order as the values, and
+// the minimum over chunks of each chunk's first nearest triangle is the
+// reference's first nearest triangle: the lowest index among equal w.  A
+// chunk is an eighth (a quarter, a sixteenth) of a wave's work, so the grid
+// runs in several rounds of short waves instead of one round of long ones.
+__global__ __launch_bounds__(kTileWFlat * kTileH) void k_flat_chunk(TraceParams P) {
+    const int32_t fine = P.tiles_x * P.block_rows;
+    const int32_t chunk = (int32_t)blockIdx.x / fine, tb = (int32_t)blockIdx.x - chunk * fine;
+    Pixel px;
+    if (!pixel_of(P, tb, wave_id(), px)) return;
+    float rmd[3];
+    primary_ray(P, px.x, px.y, rmd);
+    const f2v X = {rmd[0], rmd[0]}, Y = {rmd[1], rmd[1]}, Z = {rmd[2], rmd[2]};
+    const f2v* __restrict__ Q = reinterpret_cast<const f2v*>(P.tpair);
+    const uint32_t npair = (P.ntri + 1) >> 1;
+    const uint32_t p0 = (uint32_t)(((uint64_t)chunk * npair) / (uint32_t)P.flat_chunks);
+    const uint32_t p1 = (uint32_t)(((uint64_t)(chunk + 1) * npair) / (uint32_t)P.flat_chunks);
+    if (p0 >= p1) return;
+    float d = kDrawDistance;
+    uint32_t best = kMiss, n_acc = 0;
+    const uint32_t zero = P.ntri >> 31;  // 0: scenes hold < 2^29 triangles
+    FlatPair a, b;
+    a.load(Q + 16 * (size_t)p0);
+    uint32_t p = p0;
+    for (; p + 1 < p1; p += 2) {
+        b.load_after(Q, p + 1, a, zero);
+        a.test_signed_v(X, Y, Z, 2 * p, d, best, n_acc);
+        a.load_after(Q, min(p + 2, p1 - 1), b, zero);
+        b.test_signed_v(X, Y, Z, 2 * p + 2, d, best, n_acc);
+    }
+    if (p < p1) a.test_signed_v(X, Y, Z, 2 * p, d, best, n_acc);
+    if (best != kMiss) atomicMin(&P.flat_key[px.out], ((unsigned long long)__float_as_uint(d) << 32) | best);
+}
+
+template <bool kWriteHit>
+__global__ __launch_bounds__(kTileWFlat * kTileH) void k_flat_shade(TraceParams P) {
+    Pixel px;
+    if (!pixel_of_thread(P, px)) return;
+    const unsigned long long key = P.flat_key[px.out];
+    P.flat_key[px.out] = ~0ull;  // ready for the next frame on this stream
+    float rmd[3];
+    primary_ray(P, px.x, px.y, rmd);
+    const bool hit = key != ~0ull;
+    flat_shade_out<kWriteHit>(P, px, rmd, hit ? __uint_as_float((uint32_t)(key >> 32)) : kDrawDistance,
+                              hit ? (uint32_t)key : kMiss);
 }
 
 // The flat kernel's pair layout: pair p <- camera-relative records 2p, 2p+1,

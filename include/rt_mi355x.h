@@ -346,7 +346,10 @@ int rt_camera_info(const rt_camera* c, int32_t* w, int32_t* h, int32_t* max_dept
  * screen per triangle, 5 = 4 unrolled to two pairs, 6 = 5 behind one screen
  * branch per two pairs, 7 = 5 with v's numerator first (a wave whose rays
  * all have V <= 0 skips the rest of the pair), 8 = 7 one pair per
- * iteration, 9 = 7 software pipelined as 3 (default). */
+ * iteration, 9 = 7 software pipelined as 3; 10, 11, 12 (default), 13 = 9
+ * over 8, 4, 16, 32 chunks of the list (a grid of short waves; the chunks'
+ * nearest hits meet in a per-pixel 64-bit minimum, then a shading pass;
+ * counting renders take 9). */
 #define RT_OPT_FLAT 7
 #define RT_OPT_RAYS_USED 8 /* get only: the pixels per wave the last kernel-3 render used */
 int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value);

@@ -225,7 +225,7 @@ def test_interior_record_orders(order, height, kernel, shadow):
     _counters_match(cnt, ocnt, kernel)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13])
 @pytest.mark.parametrize("name,w,h", [("dump_test", 64, 36), ("tester", 80, 45), ("dump", 48, 27),
                                       ("tester", 33, 9)])
 def test_flat_kernel_variants(variant, name, w, h):
@@ -243,7 +243,7 @@ def test_flat_kernel_variants(variant, name, w, h):
     _assert_same((argb, hit), (oargb, ohit), f"{name} flat v{variant} timed")
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13])
 def test_flat_kernel_variants_rabbit_hash(variant):
     import hashlib
     from cpp_cuda_raytracer_dev_amd import _lib
@@ -260,7 +260,7 @@ def test_flat_kernel_variants_rabbit_hash(variant):
     assert hashlib.sha256(hit.tobytes()).hexdigest() == ent["hit_sha"]
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13])
 @pytest.mark.parametrize("ntri", [1, 2, 3, 257])
 def test_flat_signed_layout_edge_triangles(variant, ntri):
     """The signed pair layout (forms 2-5) on triangles of both windings, facing
@@ -998,6 +998,20 @@ def test_native_comm_world1():
         assert n == 4 and ms > 0
         for f in ng.frames:
             assert (f.cpu().numpy().view(np.uint32) == fulls[0]).all()
+        # with a tile, rank 0 renders straight into each set's frame
+        # (RT_FLAG_FRAME_OUT) and its lanes share no events: one pose per
+        # frame, poisoned frames, 1 and 2 frames in flight
+        xfs = np.stack([np.asarray(xf, np.float32).reshape(12) for xf in poses])
+        for inflight in (1, 2):
+            for f in ng.frames:
+                f.fill_(0x7BADBEEF)
+            torch.cuda.synchronize()
+            loop = R.FrameLoop(s.cam, ng.local, mode=0, tile=(1, 0), render_stream=rs.cuda_stream, comm=ng,
+                               comm_stream=cs.cuda_stream, inflight=inflight, xforms=xfs)
+            loop.run(len(poses) + 2)  # frames 0..6 at poses j % 5: the sets end with frames 5 and 6
+            for j in (len(poses), len(poses) + 1):
+                got = ng.frames[j % 2].cpu().numpy().view(np.uint32)
+                assert (got == fulls[j % len(poses)]).all(), (inflight, j)
         ng.close()
     finally:
         dist.destroy_process_group()
