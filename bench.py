@@ -507,7 +507,26 @@ def main():
             return None, f, f.local
         return None, None, [torch.zeros(w * h, dtype=torch.int32, device=dev) for _ in range(inflight)]
 
-    ng, fg, out = make_gather(collective)
+    try:
+        ng, fg, out = make_gather(collective)
+        failed = None
+    except Exception as e:  # the library's communicator could not be set up on this rank
+        ng, failed = None, e
+    if multi and collective == "rccl":
+        # every rank must take the same path: fall back to torch.distributed
+        # gather everywhere when any rank failed
+        bad = torch.tensor([1 if failed is not None else 0], dtype=torch.int64, device=dev)
+        dist.all_reduce(bad)
+        if int(bad[0]):
+            if ng is not None:
+                ng.close()
+            gather_note = (f"native RCCL communicator failed on {int(bad[0])} rank(s)"
+                           + (f" ({type(failed).__name__}: {failed})" if failed is not None else "")
+                           + "; fell back to torch gather")
+            collective = "gather"
+            ng, fg, out = make_gather(collective)
+    elif failed is not None:
+        raise failed
     outs = out if isinstance(out, list) else [out]  # N=1: one target per frame in flight
     out = outs[0]
     cstream = torch.cuda.Stream(device=dev) if ng is not None else None
