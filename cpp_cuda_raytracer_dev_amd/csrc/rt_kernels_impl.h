@@ -1386,8 +1386,8 @@ __device__ __forceinline__ void count_flush(const TraceParams& P, const Counts& 
 // pixels are exactly what fine units would produce; only the packing of work
 // into waves differs.
 //
-// With the identity object transform (P.plain_xf) a group first tries a
-// cheap test: the ray normalised by the hardware rsqrt / rcp instead of the
+// A group first tries a cheap test (below: identity transform, then any
+// transform): the ray normalised by the hardware rsqrt / rcp instead of the
 // 21-step Newton loop and correctly rounded divisions.  Its slab parameters
 // are within ~1e-6 (relative) of the exact ones, so a pixel whose test fails
 // by a 1e-3 relative margin (or whose entry lies behind the eye by more than
@@ -1412,6 +1412,51 @@ __device__ __forceinline__ bool root_certain_miss(const TraceParams& P, int32_t 
     if (!(fabsf(maxt0) < 1e30f && fabsf(mint1) < 1e30f)) return false;  // NaN or huge: exact test
     const float tol = 1e-3f * (fabsf(maxt0) + fabsf(mint1));
     return mint1 < maxt0 - tol || (maxt0 < -tol && maxt0 < -1e-12f);
+}
+
+// The same under an object transform (rotation rows X, offset od; the
+// reference's ray R = X3 * cam, slab parameters t = (b + od) / R per axis,
+// TD/Trixel.cu:60-95).  Bounds, per axis i, with S_i = sum_j |X_ij cam_j|:
+//   * cam from the hardware rsq differs from the exact (21-step) ray by a
+//     common factor within ~1.2e-6, and each path's dot product rounds by at
+//     most 3 ulps of S_i, so |R_i(approx) - R_i(exact)| <= E_i = 4e-6 S_i;
+//   * with |R_i| > 4e-3 S_i (rho_i = E_i / |R_i| < 1e-3, so both rays share
+//     the sign and no component is near zero), b / R_i and od_i / R_i move by
+//     at most 1.01 rho_i of their size, and the float roundings of either
+//     path's t0 / t1 (rcp, products, sum) stay below 2e-6 of
+//     M_i = (max |b| + |od_i|) / |R_i|;
+//   * max / min move by at most the largest per-axis bound e.
+// So exact maxt0, mint1 lie within e of these, and a miss by a margin of
+// 2e + 1e-3 (|maxt0| + |mint1|) + 1e-12 is a miss of the exact double test
+// (mint1 >= maxt0 - 1e-16 && maxt0 > -1e-16).  Any doubt: the exact test.
+__device__ __forceinline__ bool root_certain_miss_xf(const TraceParams& P, int32_t ix, int32_t iy) {
+    const float fx = (float)(uint32_t)ix, fy = (float)(uint32_t)iy;
+    const float x = P.n_mod[0] + P.u_mod[0] * fx + P.v_mod[0] * fy;
+    const float y = P.n_mod[1] + P.u_mod[1] * fx + P.v_mod[1] * fy;
+    const float z = P.n_mod[2] + P.u_mod[2] * fx + P.v_mod[2] * fy;
+    const float r = __builtin_amdgcn_rsqf((x * x) + (y * y) + (z * z));
+    const float c0 = x * r, c1 = y * r, c2 = z * r;
+    const float* X = P.xf;
+    const float* b = P.root_box;
+    float maxt0 = -INFINITY, mint1 = INFINITY, e = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        const float a0 = X[4 * i], a1 = X[4 * i + 1], a2 = X[4 * i + 2], od = X[4 * i + 3];
+        const float ri = -1 * (a0 * -c0 + a1 * -c1 + a2 * -c2);
+        const float si = fabsf(a0 * c0) + fabsf(a1 * c1) + fabsf(a2 * c2);
+        if (!(fabsf(ri) > 4e-3f * si && si < 1e30f)) return false;
+        const float inv = __builtin_amdgcn_rcpf(ri), o = od * inv;
+        const float lo = b[2 * i], hi = b[2 * i + 1];
+        const float t0 = (ri > 0 ? lo : hi) * inv + o, t1 = (ri > 0 ? hi : lo) * inv + o;
+        const float rho = 4.01e-6f * si * fabsf(inv);  // rcp within an ulp of 1 / ri: no divide
+        const float m = (fmaxf(fabsf(lo), fabsf(hi)) + fabsf(od)) * fabsf(inv);
+        maxt0 = fmaxf(maxt0, t0);
+        mint1 = fminf(mint1, t1);
+        e = fmaxf(e, m * (1.01f * rho + 2e-6f));
+    }
+    if (!(fabsf(maxt0) < 1e30f && fabsf(mint1) < 1e30f && e < 1e30f)) return false;  // NaN or huge: exact test
+    const float tol = 2.0f * e + 1e-3f * (fabsf(maxt0) + fabsf(mint1)) + 1e-12f;
+    return mint1 < maxt0 - tol || maxt0 < -tol;
 }
 
 //
@@ -1456,8 +1501,8 @@ template <int kRays, bool kWriteHit, bool kCount>
 __device__ __forceinline__ unsigned long long coarse_root(const TraceParams& P, const Unit& G, int lane, Counts& C) {
     Pixel px;
     const bool live = unit_pixel(P, G, 8, lane, px);
-    if (P.plain_xf && !(P.root_ref & kLeafBit) && !(P.debug & 1)) {
-        const bool sure = !live || root_certain_miss(P, px.x, px.y);
+    if (!(P.root_ref & kLeafBit) && !(P.debug & 1)) {
+        const bool sure = !live || (P.plain_xf ? root_certain_miss(P, px.x, px.y) : root_certain_miss_xf(P, px.x, px.y));
         if (__ballot(!sure) == 0ull) {
             if (live) {
                 P.argb[px.out] = kBackground;

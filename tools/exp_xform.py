@@ -21,6 +21,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=300)
     ap.add_argument("--scene", default="dragon")
+    ap.add_argument("--tile-orders", default="3", help="comma list of RT_OPT_TILE_ORDER values")
+    ap.add_argument("--debug", default="0", help="comma list of RT_OPT_DEBUG values (32: no device cost reorder)")
+    ap.add_argument("--only", default="", help="comma list of pose names to run (default: all)")
+    ap.add_argument("--spin", type=float, default=0.01, help="rad per frame of the moving pose sequence")
     a = ap.parse_args()
     import torch
     from cpp_cuda_raytracer_dev_amd import _lib, raytracer as R, scenes
@@ -38,13 +42,29 @@ def main():
         "translate": [1, 0, 0, 0.01, 0, 1, 0, -0.005, 0, 0, 1, 0.02],
         "rotate+translate": [c, 0, s, 0.01, 0, 1, 0, -0.005, -s, 0, c, 0.02],
     }
+    # a moving object: rotate about y by `spin` per frame and drift, one pose per frame
+    seq = []
+    for k in range(64):
+        ck, sk = np.cos(a.spin * k), np.sin(a.spin * k)
+        seq.append([ck, 0, sk, 0.0002 * k, 0, 1, 0, 0, -sk, 0, ck, 0.0003 * k])
+    poses["moving"] = seq
+    if a.only:
+        poses = {k: v for k, v in poses.items() if k in a.only.split(",")}
     dev = torch.device("cuda:0")
     st = torch.cuda.Stream(dev)
     out = {}
-    for name, xf in poses.items():
+    cases = [(o, d) for o in a.tile_orders.split(",") for d in a.debug.split(",")]
+    for order, dbg in [(int(o), int(d)) for o, d in cases]:
+      cam.set_option(_lib.RT_OPT_TILE_ORDER, order)
+      cam.set_option(_lib.RT_OPT_DEBUG, dbg)
+      for name0, xf in poses.items():
+        name = f"{name0}/order{order}/debug{dbg}"
         xf = np.asarray(xf, np.float32)
         bufs = [torch.zeros(1920 * 1080, dtype=torch.int32, device=dev)]
-        loop = R.FrameLoop(cam, bufs, xform=xf, render_stream=st.cuda_stream, event_every=0, inflight=1)
+        if xf.ndim == 2:
+            loop = R.FrameLoop(cam, bufs, xforms=xf, render_stream=st.cuda_stream, event_every=0, inflight=1)
+        else:
+            loop = R.FrameLoop(cam, bufs, xform=xf, render_stream=st.cuda_stream, event_every=0, inflight=1)
         loop.run(50)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)
