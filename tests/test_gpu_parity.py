@@ -559,9 +559,9 @@ def test_shadow_rejected_outside_kernel3_kd(kernel, mode):
 # one or many groups per wave, and the diagnostic "every group coarse" (debug
 # bit 4), which sends the whole object through the coarse kernel's tracing;
 # debug bit 8 runs the coarse kernel on a side stream beside the fine one.
-# With the identity transform the coarse kernel first tries its certain-miss
-# test (hardware rsqrt/rcp with a 1e-3 margin); the transform cases take the
-# exact test only.
+# The coarse kernel first tries its certain-miss test (hardware rsqrt/rcp
+# with a 1e-3 margin; under a transform, root_certain_miss_xf with explicit
+# error bounds); any doubt takes the exact test.
 COARSE = [(0, None), (1, None), (8, None), (32, None), (8, 4), (1, 4), (32, 4), (8, 8), (2, 12)]  # (groups per wave, debug)
 
 
@@ -586,6 +586,39 @@ def test_coarse_poses_and_transforms(pose, debug):
         argb, hit, _ = s.render(0, xform=xf)
         oargb, ohit, _ = H.oracle_render("rabbit_70k", 200, 120, 0, cam_kw=pose, xform=xf)
         _assert_same((argb, hit), (oargb, ohit), f"pose {pose} xf {xf is not None} debug {debug}")
+
+
+def _quat_xform(axis, deg, t):
+    """rot_m rows of a rotation by `deg` about `axis` (float32) and offset t."""
+    a = np.asarray(axis, np.float64)
+    a = a / np.linalg.norm(a)
+    h = np.deg2rad(deg) / 2
+    w, x, y, z = np.cos(h), *(np.sin(h) * a)
+    m = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                  [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+                  [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
+    return np.hstack([m, np.asarray(t, np.float64).reshape(3, 1)]).astype(np.float32).reshape(12)
+
+
+# general rotations (random axes, up to 120 degrees), offsets, and a signed
+# permutation (exact zeros in rot_m, so rotated components vanish with the
+# camera's own) exercise root_certain_miss_xf's bounds against the oracle
+_XF_RNG = np.random.default_rng(20261017)
+_GENERAL_XFS = [_quat_xform(_XF_RNG.normal(size=3), _XF_RNG.uniform(-120, 120), _XF_RNG.uniform(-0.03, 0.03, 3))
+                for _ in range(5)] + [np.array([0, 0, 1, 0.01, 0, 1, 0, 0, -1, 0, 0, 0], np.float32)]
+
+
+@pytest.mark.parametrize("debug", [None, 4])
+@pytest.mark.parametrize("k", range(len(_GENERAL_XFS)))
+def test_coarse_general_transforms(k, debug):
+    xf = _GENERAL_XFS[k]
+    s = H.GpuScene("rabbit_70k", 240, 136, kernel=3, debug=debug)
+    argb, hit, cnt = s.render(0, xform=xf, count=True)
+    oargb, ohit, ocnt = H.oracle_render("rabbit_70k", 240, 136, 0, xform=xf)
+    _assert_same((argb, hit), (oargb, ohit), f"xf {k} debug {debug}")
+    _counters_match(cnt, ocnt, 3)
+    argb2, hit2, _ = s.render(0, xform=xf)
+    _assert_same((argb2, hit2), (oargb, ohit), f"xf {k} debug {debug} (no counters)")
 
 
 @pytest.mark.parametrize("debug", [None, 4])
