@@ -1427,7 +1427,7 @@ __device__ __forceinline__ bool root_certain_miss(const TraceParams& P, int32_t 
 //     M_i = (max |b| + |od_i|) / |R_i|;
 //   * max / min move by at most the largest per-axis bound e.
 // So exact maxt0, mint1 lie within e of these, and a miss by a margin of
-// 2e + 1e-3 (|maxt0| + |mint1|) + 1e-12 is a miss of the exact double test
+// 2e + 1e-5 (|maxt0| + |mint1|) + 1e-12 is a miss of the exact double test
 // (mint1 >= maxt0 - 1e-16 && maxt0 > -1e-16).  Any doubt: the exact test.
 __device__ __forceinline__ bool root_certain_miss_xf(const TraceParams& P, int32_t ix, int32_t iy) {
     const float fx = (float)(uint32_t)ix, fy = (float)(uint32_t)iy;
@@ -1455,7 +1455,10 @@ __device__ __forceinline__ bool root_certain_miss_xf(const TraceParams& P, int32
         e = fmaxf(e, m * (1.01f * rho + 2e-6f));
     }
     if (!(fabsf(maxt0) < 1e30f && fabsf(mint1) < 1e30f && e < 1e30f)) return false;  // NaN or huge: exact test
-    const float tol = 2.0f * e + 1e-3f * (fabsf(maxt0) + fabsf(mint1)) + 1e-12f;
+    // 2e is the bound; the relative 1e-5 is a safety factor over its 2e-6
+    // rounding allowance (1e-3, the identity test's margin, left the ring of
+    // groups next to the fine tiles to the exact test: 18.7 us per kernel)
+    const float tol = 2.0f * e + 1e-5f * (fabsf(maxt0) + fabsf(mint1)) + 1e-12f;
     return mint1 < maxt0 - tol || maxt0 < -tol;
 }
 
@@ -1497,21 +1500,27 @@ __device__ __forceinline__ bool fill_far(const TraceParams& P, const Unit& G, in
     return true;
 }
 
+// A coarse group every pixel of which is a certain miss (above) is
+// background: writes it and returns true; otherwise writes nothing.
+template <bool kWriteHit, bool kCount>
+__device__ __forceinline__ bool coarse_sure(const TraceParams& P, const Unit& G, int lane, Counts& C) {
+    Pixel px;
+    const bool live = unit_pixel(P, G, 8, lane, px);
+    const bool sure = !live || (P.plain_xf ? root_certain_miss(P, px.x, px.y) : root_certain_miss_xf(P, px.x, px.y));
+    if (__ballot(!sure) != 0ull) return false;
+    if (live) {
+        P.argb[px.out] = kBackground;
+        if (kWriteHit) P.hit[px.out] = (int64_t)-1;
+        if (kCount) C.n_int += 1u;  // the root visit, which fails
+    }
+    return true;
+}
+
+// The exact root test of a coarse group (after coarse_sure, when it applies).
 template <int kRays, bool kWriteHit, bool kCount>
 __device__ __forceinline__ unsigned long long coarse_root(const TraceParams& P, const Unit& G, int lane, Counts& C) {
     Pixel px;
     const bool live = unit_pixel(P, G, 8, lane, px);
-    if (!(P.root_ref & kLeafBit) && !(P.debug & 1)) {
-        const bool sure = !live || (P.plain_xf ? root_certain_miss(P, px.x, px.y) : root_certain_miss_xf(P, px.x, px.y));
-        if (__ballot(!sure) == 0ull) {
-            if (live) {
-                P.argb[px.out] = kBackground;
-                if (kWriteHit) P.hit[px.out] = (int64_t)-1;
-                if (kCount) C.n_int += 1u;  // the root visit, which fails
-            }
-            return 0ull;
-        }
-    }
     float cam[3], t0, t1;
     Ray R;
     camera_ray(P, px, live, cam, R);
@@ -1608,6 +1617,15 @@ __global__ __launch_bounds__(128) void k_coarse_kd3(TraceParams P) {
     for (int g = 0; g < kCoarseMax; g++) {
         const int32_t j = j0 + g;
         if (j < j1 && !(far_ok && fill_far<kWriteHit, kCount>(P, coarse_unit(P, j), lane, C))) pending |= 1u << g;
+    }
+    // then the certain-miss test of the rest, unrolled the same way (one
+    // group after another, its rsq / rcp chains cost ~1 us each); the groups
+    // left take the exact root test
+    if (!(P.root_ref & kLeafBit) && !(P.debug & 1)) {
+#pragma unroll 8
+        for (int g = 0; g < kCoarseMax; g++)
+            if (((pending >> g) & 1u) && coarse_sure<kWriteHit, kCount>(P, coarse_unit(P, j0 + g), lane, C))
+                pending &= ~(1u << g);
     }
     while (pending) {
         const int32_t j = j0 + __builtin_ctz(pending);
