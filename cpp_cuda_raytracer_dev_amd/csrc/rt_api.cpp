@@ -55,7 +55,10 @@ struct rt_camera {
     int prepared_layout = 0;         // interior record layout of d_inode (1 or 2)
     int kernel_version = 3;          // kOptKernel
     int tile_order = 3;              // kOptTileOrder
-    int debug = 0;                   // kOptDebug (diagnostics)
+    // kOptDebug (diagnostics): 1 skip traversal, 2 per-wave stamps, 4 every
+    // group coarse, 8 coarse kernel on a side stream, 16 counted shadow walks
+    // stop at occluders, 32 centre-out order until a grid's cost order arrives
+    int debug = 0;
     int pool_cap = kPoolCapMax;      // kOptPoolCap
     unsigned long long* d_dbg = nullptr;
     int64_t dbg_cap = 0;             // in u64
@@ -1226,6 +1229,18 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
         pc.nranks = nr;
         pc.rank = rk;
         pc.p = p;
+    }
+    // Tile order 3 before this grid's first cost order has been uploaded
+    // (a new grid: a moving object makes one every frame): the XCD-contiguous
+    // mapping of order 0, not the centre-out permutation.  Measured, dragon
+    // 1080p, one frame in flight (tools/exp_xform.py): a moving pose sequence
+    // 104.4 -> 98.5 us per frame (order 0 vs centre-out), a held pose before
+    // its costs arrive 119 -> 111 (identity), 144 -> 131 (translated).  Costs
+    // are kept per tile index under any mapping, so the samples stand.
+    // Debug bit 32 keeps the centre-out permutation.
+    if (p.cost && p.tile_order == 3 && c->order_gen != c->layout_gen && !(c->debug & 32)) {
+        p.tile_order = 0;
+        p.order = nullptr;
     }
     p.frame_out = (flags & RT_FLAG_FRAME_OUT) ? 1 : 0;
     p.flat_key = nullptr;
