@@ -113,6 +113,8 @@ def parse():
                     help="bracket every Nth timed frame with HIP events for the kernel time (each pair costs "
                          "~9 us of queue time, so N > 1 keeps the frame rate close to the uninstrumented one); "
                          "0 = every 8th (every frame with --inflight 1 at one GPU)")
+    ap.add_argument("--debug-bits", type=int, default=0,
+                    help="diagnostics: extra RT_OPT_DEBUG bits for the timed camera (A/B builds of host policies)")
     ap.add_argument("--side-coarse", action="store_true",
                     help="kernel 3: run the coarse kernel beside the fine one on a side stream (default: before it)")
     ap.add_argument("--deliver", action="store_true",
@@ -474,8 +476,9 @@ def main():
     cam.set_option(_lib.RT_OPT_SHADOW_ORDER, a.shadow_order)
     if a.flat >= 0:
         cam.set_option(_lib.RT_OPT_FLAT, a.flat)
-    if a.side_coarse:
-        cam.set_option(_lib.RT_OPT_DEBUG, 8)
+    dbg_bits = (8 if a.side_coarse else 0) | a.debug_bits
+    if dbg_bits:
+        cam.set_option(_lib.RT_OPT_DEBUG, dbg_bits)
     cam.render_into(scratch, mode=a.mode, flags=sflag, tile=tile if multi else None,
                     stream=sptr)  # re-prepares layout
     torch.cuda.synchronize(dev)
@@ -697,7 +700,7 @@ def main():
         # walked them in full (the oracle's counters).  Count the timed walk
         # (same push order) for the algorithmic bytes, untimed.
         full_walk = cnt
-        cam.set_option(_lib.RT_OPT_DEBUG, 16 | (8 if a.side_coarse else 0))
+        cam.set_option(_lib.RT_OPT_DEBUG, 16 | dbg_bits)
         cam.render_into(scratch, xform=xf, mode=a.mode, flags=R.RT_FLAG_COUNT | sflag,
                         tile=tile if multi else None, stream=sptr)
         torch.cuda.synchronize(dev)

@@ -57,7 +57,7 @@ struct rt_camera {
     int tile_order = 3;              // kOptTileOrder
     // kOptDebug (diagnostics): 1 skip traversal, 2 per-wave stamps, 4 every
     // group coarse, 8 coarse kernel on a side stream, 16 counted shadow walks
-    // stop at occluders, 32 centre-out order until a grid's cost order arrives
+    // stop at occluders, 64 order / cost buffers sized for the current grid only
     int debug = 0;
     int pool_cap = kPoolCapMax;      // kOptPoolCap
     unsigned long long* d_dbg = nullptr;
@@ -249,6 +249,16 @@ void note_order_stream(rt_camera* c, hipStream_t st) {
     else c->oused_overflow = true;
 }
 
+// Tiles of this rank's whole frame in p's tiling: the most any fine grid of
+// this camera and tiling holds.  Order slots and cost buffers are sized for
+// it, so a moving object's growing grid never reallocates them (each
+// reallocation freed device memory, a device-wide synchronisation, and
+// re-pinned host memory).
+int64_t all_tiles(const rt_camera* c, const TraceParams& p) {
+    if (c->debug & 64) return 0;  // A/B: sized for the current grid only
+    return (int64_t)((c->w + p.tile_w - 1) / p.tile_w) * p.nslots * (kTileH / p.tile_h);
+}
+
 int ensure_order(rt_camera* c, const TraceParams& p, hipStream_t st) {
     const int64_t key[8] = {p.tile_w, p.tile_h, p.tiles_x, p.block_rows, p.nranks, p.rank, p.fine_tx0, p.fine_s0};
     if (std::equal(key, key + 8, c->order_key)) return RT_OK;
@@ -298,14 +308,15 @@ int ensure_order(rt_camera* c, const TraceParams& p, hipStream_t st) {
     o.nev = 0;
     o.device_sync = false;
     if (o.cap < n) {
+        const int64_t want = std::max(n, all_tiles(c, p));
         dev_free(o.d);
         if (o.h) (void)hipHostFree(o.h);
         o.h = nullptr;
         o.cap = 0;
-        if ((rc = dev_alloc(&o.d, (size_t)n, "hipMalloc(order)")) ||
-            (rc = hip_check(hipHostMalloc((void**)&o.h, sizeof(int32_t) * (size_t)n, 0), "hipHostMalloc(order)")))
+        if ((rc = dev_alloc(&o.d, (size_t)want, "hipMalloc(order)")) ||
+            (rc = hip_check(hipHostMalloc((void**)&o.h, sizeof(int32_t) * (size_t)want, 0), "hipHostMalloc(order)")))
             return rc;
-        o.cap = n;
+        o.cap = want;
     }
     std::copy(order.begin(), order.end(), o.h);
     if ((rc = hip_check(hipMemcpyAsync(o.d, o.h, sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice, st), "H2D order")))
@@ -769,7 +780,7 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
         if (rc) return rc;
         p.order = c->d_order;
         if (c->tile_order >= 3 && kernel == 3) {
-            if ((rc = ensure_cost(c, (int64_t)p.tiles_x * p.block_rows))) return rc;
+            if ((rc = ensure_cost(c, std::max<int64_t>(all_tiles(c, p), (int64_t)p.tiles_x * p.block_rows)))) return rc;
             p.cost = c->d_cost;
         }
     }
@@ -1229,18 +1240,6 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
         pc.nranks = nr;
         pc.rank = rk;
         pc.p = p;
-    }
-    // Tile order 3 before this grid's first cost order has been uploaded
-    // (a new grid: a moving object makes one every frame): the XCD-contiguous
-    // mapping of order 0, not the centre-out permutation.  Measured, dragon
-    // 1080p, one frame in flight (tools/exp_xform.py): a moving pose sequence
-    // 104.4 -> 98.5 us per frame (order 0 vs centre-out), a held pose before
-    // its costs arrive 119 -> 111 (identity), 144 -> 131 (translated).  Costs
-    // are kept per tile index under any mapping, so the samples stand.
-    // Debug bit 32 keeps the centre-out permutation.
-    if (p.cost && p.tile_order == 3 && c->order_gen != c->layout_gen && !(c->debug & 32)) {
-        p.tile_order = 0;
-        p.order = nullptr;
     }
     p.frame_out = (flags & RT_FLAG_FRAME_OUT) ? 1 : 0;
     p.flat_key = nullptr;

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--tile-orders", default="3", help="comma list of RT_OPT_TILE_ORDER values")
     ap.add_argument("--debug", default="0", help="comma list of RT_OPT_DEBUG values (32: no device cost reorder)")
     ap.add_argument("--only", default="", help="comma list of pose names to run (default: all)")
+    ap.add_argument("--holds", default="1", help="comma list: frames each pose of the moving sequence is held")
     ap.add_argument("--spin", type=float, default=0.01, help="rad per frame of the moving pose sequence")
     a = ap.parse_args()
     import torch
@@ -47,7 +48,8 @@ def main():
     for k in range(64):
         ck, sk = np.cos(a.spin * k), np.sin(a.spin * k)
         seq.append([ck, 0, sk, 0.0002 * k, 0, 1, 0, 0, -sk, 0, ck, 0.0003 * k])
-    poses["moving"] = seq
+    for hold in [int(x) for x in a.holds.split(",")]:
+        poses["moving" if hold == 1 else f"moving_hold{hold}"] = [x for x in seq for _ in range(hold)]
     if a.only:
         poses = {k: v for k, v in poses.items() if k in a.only.split(",")}
     dev = torch.device("cuda:0")
