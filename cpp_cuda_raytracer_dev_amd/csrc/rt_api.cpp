@@ -76,6 +76,11 @@ struct rt_camera {
         hipEvent_t ev[8] = {};
         int nev = 0;
         bool device_sync = false;    // used by more streams than ev holds
+        // frames in flight: the upload's event and stream; a frame on
+        // another lane waits for it only when it renders with this slot
+        hipEvent_t up_ev = nullptr;
+        hipStream_t up_stream = nullptr;
+        bool up_valid = false;
     } oslot[8];
     int ocur = -1;
     hipStream_t oused[8] = {};       // streams that launched with the current slot
@@ -98,7 +103,7 @@ struct rt_camera {
     uint32_t* h_cost = nullptr;      // pinned D2H target
     int32_t* h_order = nullptr;      // pinned H2D source
     int64_t host_cap = 0;            // tiles h_cost / h_order hold
-    hipEvent_t cost_ev = nullptr, order_ev = nullptr, order_up_ev = nullptr;
+    hipEvent_t cost_ev = nullptr, order_ev = nullptr;
     bool cost_pending = false, order_pending = false;
     int frames_since = 0;
     uint64_t layout_gen = 0, cost_gen = 0;   // fine-grid generation, and the one h_cost was read for
@@ -272,14 +277,23 @@ int ensure_order(rt_camera* c, const TraceParams& p, hipStream_t st) {
     const double cx = 0.5 * c->w, cy = 0.5 * c->h;
     const int32_t nring = (int32_t)(0.5 * std::sqrt(cx * cx + cy * cy)) + 2;
     std::vector<int32_t> start((size_t)nring + 1, 0);
-    for (int64_t t = 0; t < n; t++) {
-        const int64_t row = t / p.tiles_x, tx = t % p.tiles_x + p.fine_tx0;
+    // row by row, the column terms once (a moving object recomputes this
+    // every frame: four 64-bit divisions per tile cost ~100 us of host time
+    // per 1080p frame)
+    std::vector<double> dx2((size_t)p.tiles_x);
+    for (int64_t c0 = 0; c0 < p.tiles_x; c0++) {
+        const double x = ((c0 + p.fine_tx0) + 0.5) * p.tile_w;
+        dx2[(size_t)c0] = (x - cx) * (x - cx);
+    }
+    for (int64_t row = 0, t = 0; row < p.block_rows; row++) {
         const int64_t slot = row / per_band + p.fine_s0, yin = (row % per_band) * p.tile_h;
-        const double x = (tx + 0.5) * p.tile_w;
         const double y = (double)((p.rank + slot * (int64_t)p.nranks) * kTileH + yin) + 0.5 * p.tile_h;
-        const int32_t k = std::min(nring - 1, (int32_t)(0.5 * std::sqrt((x - cx) * (x - cx) + (y - cy) * (y - cy))));
-        ring[(size_t)t] = k;
-        start[(size_t)k + 1]++;
+        const double dy2 = (y - cy) * (y - cy);
+        for (int64_t c0 = 0; c0 < p.tiles_x; c0++, t++) {
+            const int32_t k = std::min(nring - 1, (int32_t)(0.5 * std::sqrt(dx2[(size_t)c0] + dy2)));
+            ring[(size_t)t] = k;
+            start[(size_t)k + 1]++;
+        }
     }
     for (int32_t k = 0; k < nring; k++) start[(size_t)k + 1] += start[(size_t)k];
     for (int64_t t = 0; t < n; t++) order[(size_t)start[(size_t)ring[(size_t)t]]++] = (int32_t)t;
@@ -321,14 +335,17 @@ int ensure_order(rt_camera* c, const TraceParams& p, hipStream_t st) {
     std::copy(order.begin(), order.end(), o.h);
     if ((rc = hip_check(hipMemcpyAsync(o.d, o.h, sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice, st), "H2D order")))
         return rc;
-    // frames in flight on other lanes launch with it only after the upload
+    // frames in flight on other lanes that render with this slot wait for
+    // the upload (order_wait); a moving object's next grid, on the other
+    // lane, has a slot of its own and does not (a wait on every lane here
+    // tied each lane's next frame to the other's previous one)
+    o.up_valid = false;
     if (c->nactive > 1) {
-        if (!c->order_up_ev && (rc = hip_check(hipEventCreateWithFlags(&c->order_up_ev, hipEventDisableTiming), "order event")))
+        if (!o.up_ev && (rc = hip_check(hipEventCreateWithFlags(&o.up_ev, hipEventDisableTiming), "order event")))
             return rc;
-        if ((rc = hip_check(hipEventRecord(c->order_up_ev, st), "order upload event"))) return rc;
-        for (int l = 0; l < c->nactive; l++)
-            if (c->active[l] != st && (rc = hip_check(hipStreamWaitEvent(c->active[l], c->order_up_ev, 0), "order upload wait")))
-                return rc;
+        if ((rc = hip_check(hipEventRecord(o.up_ev, st), "order upload event"))) return rc;
+        o.up_stream = st;
+        o.up_valid = true;
     }
     c->ocur = sl;
     c->d_order = o.d;
@@ -1265,6 +1282,13 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
             return rc;
     }
     if (trial >= 0 && (rc = hip_check(hipEventRecord(c->tune_ev[2 * trial], st), "order trial start"))) return rc;
+    // a slot uploaded on another lane: this frame's launch waits for it
+    for (int k = 0; p.order && c->nactive > 1 && k < kOrderSlots; k++) {
+        const auto& o = c->oslot[k];
+        if (o.d == p.order && o.up_valid && o.up_stream != st &&
+            (rc = hip_check(hipStreamWaitEvent(st, o.up_ev, 0), "order upload wait")))
+            return rc;
+    }
     if ((rc = launch_split(c, p, mode, flags, stream))) return rc;
     if (p.order) {  // the streams that read the current order slot
         note_order_stream(c, st);
@@ -1486,9 +1510,9 @@ extern "C" void rt_camera_destroy(rt_camera* c) {
         if (o.h) (void)hipHostFree(o.h);
         for (hipEvent_t e : o.ev)
             if (e) (void)hipEventDestroy(e);
+        if (o.up_ev) (void)hipEventDestroy(o.up_ev);
     }
     c->d_order = nullptr;
-    if (c->order_up_ev) (void)hipEventDestroy(c->order_up_ev);
     dev_free(c->d_dbg);
     for (auto& k : c->flat_keys) dev_free(k.d);
     dev_free(c->d_cost);
