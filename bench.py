@@ -2,6 +2,12 @@
 """Benchmark: frames/s and Mray/s at 1920x1080 on the dragon (stand-in),
 KD traversal, 1..N MI355X GPUs (BASELINE.json metric; configs C3/C4).
 
+The default workload is the torus-knot stand-in (`--scene knot`): the
+dragon's 871,414 triangles in the dragon's box as a noise-displaced (5, 12)
+torus-knot tube, strands in front of strands, ~1.9x the interior visits per
+covered ray of the displaced-sphere blob (`--scene dragon`), which stays as a
+secondary line.  SURVEY.md §8d suggests the knot as the dragon stand-in.
+
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
         --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
@@ -11,7 +17,7 @@ Trumbore -> Phong into the u32 frame (one fused kernel), plus, for N > 1,
 the RCCL gather to rank 0 of every rank's screen bands (the part of them
 not provably background) and the frame assembly kernel there, pipelined
 with the next frame's render.  Frames are fixed-size (1920x1080), so N > 1 is strong
-scaling.  The scene is the seeded synthetic stand-in for
+scaling.  The scene is a seeded synthetic stand-in for
 dragon_vrip_mod.ply (missing from the reference; 871,414 triangles).
 Rank 0 prints one JSON line.
 
@@ -62,10 +68,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--scene", default="dragon", choices=["dragon", "happy", "rabbit_70k", "tester", "big", "knot"],
-                    help="dragon / happy: seeded stand-ins for the missing meshes (big: a 3.1M-triangle one; knot: "
-                         "the dragon's count and box as a torus-knot tube, ~2x the traversal work); rabbit_70k / tester: the "
-                         "reference's own meshes")
+    ap.add_argument("--scene", default="knot", choices=["dragon", "happy", "rabbit_70k", "tester", "big", "knot"],
+                    help="knot (default) / dragon / happy: seeded stand-ins for the missing meshes (knot: the dragon's "
+                         "count and box as a torus-knot tube, ~2x the blob's traversal work; dragon: a displaced-sphere "
+                         "blob; big: a 3.1M-triangle one); rabbit_70k / tester: the reference's own meshes")
     ap.add_argument("--view", default="default", choices=["default", "fill"],
                     help="default: WinMain's camera; fill: the object over >= 90%% of the pixels (README.md:19)")
     ap.add_argument("--cpu-only", action="store_true",
@@ -150,13 +156,33 @@ def build_scene(name):
     return pts, leafs, nodes, {"kd_build_s": round(t1 - t0, 4), "kd_build_s_1thread": round(t2 - t1, 4)}
 
 
+def cpu_quota():
+    """CPUs' worth of time the cgroup grants this process (cgroup v2 cpu.max or
+    v1 cfs_quota/period), or None when unlimited / unknown."""
+    import math
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fp:
+            q, per = fp.read().split()[:2]
+            return None if q == "max" else max(1, math.ceil(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else max(1, math.ceil(q / per))
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_threads(requested: int) -> int:
+    """Threads of the CPU baseline: every CPU this process may use -- its
+    affinity mask, capped by its cgroup CPU quota (threads beyond the quota
+    only time-slice).  OMP_NUM_THREADS is not consulted."""
     if requested > 0:
         return requested
-    env = os.environ.get("OMP_NUM_THREADS", "")
-    if env.isdigit() and int(env) > 0:
-        return int(env)
-    return len(os.sched_getaffinity(0))
+    n = len(os.sched_getaffinity(0))
+    q = cpu_quota()
+    return min(n, q) if q else n
 
 
 def cpu_model() -> str:
@@ -249,12 +275,23 @@ def cpu_baseline(pts, nodes, w, h, seconds, threads, mode, shadow=False, rays_pe
     fps, frames, dt = _oracle_fps(s, mode, rows, h, seconds, threads, shadow)
     rows1 = rows if mode == 1 else (h // 2 - h // 16, h // 2 + h // 16)  # one thread: the middle eighth
     fps1, frames1, dt1 = _oracle_fps(s, mode, rows1, h, seconds, 1, shadow)
+    extra = {}
+    allowed = len(os.sched_getaffinity(0))
+    if threads < allowed:
+        # the whole affinity mask too (beyond the quota it only time-slices)
+        fa, _, _ = _oracle_fps(s, mode, rows, h, seconds / 2, allowed, shadow)
+        extra = {"value_cpus_allowed_threads": round(fa, 3), "cpus_allowed_threads": allowed}
+    if threads != 16 and allowed >= 16:
+        f16, _, _ = _oracle_fps(s, mode, rows, h, seconds / 2, 16, shadow)
+        extra["value_16threads"] = round(f16, 3)
     s.close()
     rpf = rays_per_frame or w * h
     out = {"value": round(fps, 3), "unit": "frames/s", "cores": threads, "kind": "port",
            "mray_per_s": round(fps * rpf / 1e6, 3),
-           "value_1thread": round(fps1, 3), "mray_per_s_1thread": round(fps1 * rpf / 1e6, 3),
-           "nproc": os.cpu_count(), "cpus_allowed": len(os.sched_getaffinity(0)), "cpu_model": cpu_model(),
+           "value_1thread": round(fps1, 3), "mray_per_s_1thread": round(fps1 * rpf / 1e6, 3), **extra,
+           "nproc": os.cpu_count(), "cpus_allowed": allowed, "cpu_quota_cpus": cpu_quota(),
+           "threads_rule": "every CPU of the affinity mask, capped by the cgroup CPU quota",
+           "cpu_model": cpu_model(),
            "sample": f"{frames} x rows {rows[0]}-{rows[1]} of the same {w}x{h} frame with {threads} threads "
                      f"({dt:.1f} s), {frames1} x rows {rows1[0]}-{rows1[1]} with 1 thread ({dt1:.1f} s); "
                      "oracle/oracle.c (gcc -O3 -ffp-contract=off, OpenMP over rows)"}
@@ -498,7 +535,10 @@ def main():
             # two sets per frame in flight: a set's next render then waits
             # on a gather that finished long before (cross-queue waits that
             # are still pending cost ~10-15 us each)
-            g = NativeFrameGather(dist, w, h, dev, nbuf=max(1, min(max(a.pipeline, 2 * inflight), 8)))
+            # (a multiple of the frames in flight: a set is always rendered
+            # by the same lane, rt_run_frames requires it)
+            nb = -(-max(a.pipeline, 2 * inflight) // inflight) * inflight
+            g = NativeFrameGather(dist, w, h, dev, nbuf=max(inflight, min(nb, 8 // inflight * inflight)))
             # every rank must derive the same rectangle and options, or the
             # receive sizes would not match the sends
             g.verify(cam, xf, a.mode)

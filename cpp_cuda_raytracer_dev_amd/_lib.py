@@ -54,6 +54,12 @@ class RtCameraBasis(C.Structure):
                 ("pix_w", C.c_float), ("pix_h", C.c_float)]
 
 
+class RtFrameGeometry(C.Structure):
+    _fields_ = [("w", C.c_int32), ("h", C.c_int32), ("n_mod", C.c_float * 3), ("u_mod", C.c_float * 3),
+                ("v_mod", C.c_float * 3), ("root_box", C.c_float * 6), ("root_is_leaf", C.c_int32),
+                ("kernel", C.c_int32), ("rays", C.c_int32), ("coarse", C.c_int32), ("debug", C.c_int32)]
+
+
 class RtTile(C.Structure):
     _fields_ = [("nranks", C.c_int32), ("rank", C.c_int32)]
 
@@ -100,6 +106,7 @@ SIGNATURES = {
     "rt_camera_add_object": (C.c_int, [_P, _P]),
     "rt_render": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, C.POINTER(RtTile), _P]),
     "rt_render_into": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, C.POINTER(RtTile), _P, _P, _P]),
+    "rt_render_display": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, C.POINTER(RtTile), _P, _P, _P, _P]),
     "rt_tile_packed_pixels": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),
     "rt_unpack_bands": (C.c_int, [C.c_int, C.c_int32, C.c_int32, C.c_int32, _P, _P, _P]),
     "rt_comm_available": (C.c_int, []),
@@ -110,6 +117,10 @@ SIGNATURES = {
     "rt_rect_pixels": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P]),
     "rt_pack_rect": (C.c_int, [C.c_int, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, _P, _P, _P]),
     "rt_unpack_rect": (C.c_int, [C.c_int, C.c_int32, C.c_int32, C.c_int32, _P, _P, _P, _P, _P]),
+    "rt_camera_frame_geometry": (C.c_int, [_P, C.POINTER(RtFrameGeometry)]),
+    "rt_frame_rect_host": (C.c_int, [C.POINTER(RtFrameGeometry), _P, C.c_uint32, C.c_int32, _P]),
+    "rt_pack_rect_host": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, _P, _P]),
+    "rt_unpack_rect_host": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, _P, _P, _P, _P]),
     "rt_comm_info": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "rt_comm_destroy": (None, [_P]),
     "rt_run_frames": (C.c_int, [_P, _P, C.POINTER(RtFrameLoop), C.c_int32, C.POINTER(C.c_int64),

@@ -98,8 +98,17 @@ struct rt_camera {
     hipEvent_t fork_ev = nullptr, join_ev = nullptr;
     // tile order 3: each frame's per-unit pool iterations feed the next
     // frames' dispatch order, read back asynchronously (never a sync).
-    uint32_t* d_cost = nullptr;      // [tile][2] iterations, written by every frame
-    int64_t cost_cap = 0;            // in u32
+    // one buffer per stream that renders (cost_set): a sample copies the
+    // buffer of the stream that queues it, which only that stream's frames
+    // write, so frames in flight on other lanes (under motion, with another
+    // fine grid) never tear it
+    uint32_t* d_cost = nullptr;      // [cost set][tile][kCostSlots] iterations
+    int64_t cost_cap = 0;            // u32 per cost set
+    hipStream_t cost_stream[RT_LOOP_MAX_LANES] = {};   // the stream that owns each cost set
+    int cost_next = 0;                                 // the set reclaimed next when all are owned
+    hipEvent_t slot_join_ev[8] = {};  // cost-order upload: joins the streams that read the slot
+    hipStream_t cost_up_stream = nullptr;   // the last cost-order upload's stream ...
+    bool cost_up_valid = false;             // ... while it may be pending
     uint32_t* h_cost = nullptr;      // pinned D2H target
     int32_t* h_order = nullptr;      // pinned H2D source
     int64_t host_cap = 0;            // tiles h_cost / h_order hold
@@ -339,14 +348,15 @@ int ensure_order(rt_camera* c, const TraceParams& p, hipStream_t st) {
     // the upload (order_wait); a moving object's next grid, on the other
     // lane, has a slot of its own and does not (a wait on every lane here
     // tied each lane's next frame to the other's previous one)
+    // (always recorded: a caller that renders on several streams of its own
+    // needs the wait as much as the library's lanes do)
     o.up_valid = false;
-    if (c->nactive > 1) {
-        if (!o.up_ev && (rc = hip_check(hipEventCreateWithFlags(&o.up_ev, hipEventDisableTiming), "order event")))
-            return rc;
-        if ((rc = hip_check(hipEventRecord(o.up_ev, st), "order upload event"))) return rc;
-        o.up_stream = st;
-        o.up_valid = true;
-    }
+    if (!o.up_ev && (rc = hip_check(hipEventCreateWithFlags(&o.up_ev, hipEventDisableTiming), "order event")))
+        return rc;
+    if ((rc = hip_check(hipEventRecord(o.up_ev, st), "order upload event"))) return rc;
+    o.up_stream = st;
+    o.up_valid = true;
+    c->cost_up_valid = false;  // a cost order of the previous slot
     c->ocur = sl;
     c->d_order = o.d;
     c->order_gen = ~0ull;  // no cost order for this grid yet
@@ -372,9 +382,10 @@ int ensure_cost(rt_camera* c, int64_t n) {
         if ((rc = hip_check(hipDeviceSynchronize(), "cost sync"))) return rc;
         c->cost_pending = false;
         dev_free(c->d_cost);
-        if ((rc = dev_alloc(&c->d_cost, (size_t)(kCostSlots * n), "hipMalloc(cost)"))) return rc;
+        const size_t all = (size_t)(kCostSlots * n) * RT_LOOP_MAX_LANES;
+        if ((rc = dev_alloc(&c->d_cost, all, "hipMalloc(cost)"))) return rc;
         // slots of waves a tile does not have stay zero
-        if ((rc = hip_check(hipMemset(c->d_cost, 0, sizeof(uint32_t) * kCostSlots * (size_t)n), "memset cost"))) return rc;
+        if ((rc = hip_check(hipMemset(c->d_cost, 0, sizeof(uint32_t) * all), "memset cost"))) return rc;
         c->cost_cap = kCostSlots * n;
     }
     if (c->host_cap < n) {
@@ -486,7 +497,23 @@ std::vector<int32_t> cost_order(const rt_camera* c, const TraceParams& p, bool x
 // the order behind this frame; otherwise, every kCostPeriod frames, queue a
 // sample of this frame's costs.  Stream-ordered and non-blocking (events are
 // only queried); skipped while the stream is being captured into a graph.
-int cost_feedback(rt_camera* c, const TraceParams& p, void* stream) {
+// The cost set a stream's frames write: its own, claimed on first use (when
+// every set is owned, one is reclaimed round robin: a stale sample costs at
+// worst a dispatch order, never a frame).
+int cost_set(rt_camera* c, hipStream_t st) {
+    for (int l = 0; l < RT_LOOP_MAX_LANES; l++)
+        if (c->cost_stream[l] == st) return l;
+    for (int l = 0; l < RT_LOOP_MAX_LANES; l++)
+        if (!c->cost_stream[l]) {
+            c->cost_stream[l] = st;
+            return l;
+        }
+    const int l = c->cost_next++ % RT_LOOP_MAX_LANES;
+    c->cost_stream[l] = st;
+    return l;
+}
+
+int cost_feedback(rt_camera* c, const TraceParams& p, void* stream, int set) {
     hipStream_t st = (hipStream_t)stream;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return RT_OK;
@@ -505,28 +532,34 @@ int cost_feedback(rt_camera* c, const TraceParams& p, void* stream) {
         }
         if (same && c->order_gen == c->layout_gen) return RT_OK;  // d_order already holds it
         int rc;
-        // frames in flight on other lanes read d_order: the upload waits
-        // for them, and their later frames wait for the upload
-        for (int l = 0; l < c->nactive; l++) {
-            if (c->active[l] == st) continue;
-            if ((rc = hip_check(hipEventRecord(c->lane_ev[l], c->active[l]), "lane join")) ||
-                (rc = hip_check(hipStreamWaitEvent(st, c->lane_ev[l], 0), "lane join wait")))
+        // frames on other streams (frames in flight on the library's lanes,
+        // or a caller's own streams) read d_order: the upload waits for every
+        // stream that launched with this slot, and a later frame on another
+        // stream waits for the upload (render_common)
+        if (c->oused_overflow && (rc = hip_check(hipDeviceSynchronize(), "cost order sync"))) return rc;
+        for (int i = 0; i < c->noused && !c->oused_overflow; i++) {
+            if (c->oused[i] == st) continue;
+            if (!c->slot_join_ev[i] &&
+                (rc = hip_check(hipEventCreateWithFlags(&c->slot_join_ev[i], hipEventDisableTiming), "join event")))
+                return rc;
+            if ((rc = hip_check(hipEventRecord(c->slot_join_ev[i], c->oused[i]), "slot join")) ||
+                (rc = hip_check(hipStreamWaitEvent(st, c->slot_join_ev[i], 0), "slot join wait")))
                 return rc;
         }
         if ((rc = hip_check(hipMemcpyAsync(c->d_order, c->h_order, sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice, st),
                             "H2D cost order")) ||
             (rc = hip_check(hipEventRecord(c->order_ev, st), "order event")))
             return rc;
-        for (int l = 0; l < c->nactive; l++)
-            if (c->active[l] != st && (rc = hip_check(hipStreamWaitEvent(c->active[l], c->order_ev, 0), "lane fork wait")))
-                return rc;
+        c->cost_up_stream = st;
+        c->cost_up_valid = true;
         c->order_pending = true;
         c->order_gen = c->layout_gen;
         return RT_OK;
     }
     if (++c->frames_since < kCostPeriod) return RT_OK;
     int rc;
-    if ((rc = hip_check(hipMemcpyAsync(c->h_cost, c->d_cost, sizeof(uint32_t) * kCostSlots * (size_t)n, hipMemcpyDeviceToHost, st),
+    if ((rc = hip_check(hipMemcpyAsync(c->h_cost, c->d_cost + (size_t)set * c->cost_cap,
+                                       sizeof(uint32_t) * kCostSlots * (size_t)n, hipMemcpyDeviceToHost, st),
                         "D2H cost")) ||
         (rc = hip_check(hipEventRecord(c->cost_ev, st), "cost event")))
         return rc;
@@ -544,9 +577,25 @@ int cost_feedback(rt_camera* c, const TraceParams& p, void* stream) {
 // at or behind the eye plane, a singular A): the whole frame is then fine.
 // The rectangle is a work-packing hint only -- pixels outside it still run the
 // exact root test (coarse groups), so it need not be conservative.
-bool root_rect(const rt_camera* c, const TraceParams& p, double r[4]) {
+// Everything the launch geometry (tiling, fine region, frame rectangle)
+// depends on: a device camera's fields (camera_geom) or the host-only inputs
+// of rt_frame_rect_host, so both derive the same rectangle by one code path.
+struct FrameGeom {
+    int32_t w = 0, h = 0;
+    const float* n_mod = nullptr;
+    const float* u_mod = nullptr;
+    const float* v_mod = nullptr;
+    float root_box[6] = {0, 0, 0, 0, 0, 0};  // camera-relative root box
+    bool root_leaf = false;
+    int kernel = 3, rays = 0, coarse = 8, debug = 0;
+    // groups holding a pixel with a tiny ray component (find_tiny_groups):
+    // the camera's cached list, or computed by the caller
+    const std::vector<std::pair<int32_t, int32_t>>* tiny = nullptr;
+};
+
+bool root_rect(const FrameGeom& g, const TraceParams& p, double r[4]) {
     const float* X = p.xf;
-    const float* cols[3] = {c->basis.u_mod, c->basis.v_mod, c->basis.n_mod};
+    const float* cols[3] = {g.u_mod, g.v_mod, g.n_mod};
     double A[3][3];
     for (int i = 0; i < 3; i++)
         for (int j = 0; j < 3; j++)
@@ -592,26 +641,29 @@ bool root_rect(const rt_camera* c, const TraceParams& p, double r[4]) {
 // Groups with a pixel whose unnormalised primary ray q = n + u*x + v*y (the
 // kernels' float expression) has a component of magnitude <= 1e-30: their
 // slab tests may see 0/0 = NaN, so they never take the far-group shortcut.
-void find_tiny_groups(rt_camera* c) {
-    if (c->tiny_done) return;
-    const float* n = c->basis.n_mod;
-    const float* u = c->basis.u_mod;
-    const float* v = c->basis.v_mod;
-    for (int32_t y = 0; y < c->h; y++) {
+void tiny_groups_of(int32_t w, int32_t h, const float* n, const float* u, const float* v,
+                    std::vector<std::pair<int32_t, int32_t>>& out) {
+    out.clear();
+    for (int32_t y = 0; y < h; y++) {
         const float fy = (float)(uint32_t)y;
-        for (int32_t x = 0; x < c->w; x++) {
+        for (int32_t x = 0; x < w; x++) {
             const float fx = (float)(uint32_t)x;
             const float qx = n[0] + u[0] * fx + v[0] * fy;
             const float qy = n[1] + u[1] * fx + v[1] * fy;
             const float qz = n[2] + u[2] * fx + v[2] * fy;
             if (!(fabsf(qx) > 1e-30f && fabsf(qy) > 1e-30f && fabsf(qz) > 1e-30f)) {
                 const std::pair<int32_t, int32_t> g{x / 8, y / kTileH};
-                if (c->tiny_groups.empty() || c->tiny_groups.back() != g) c->tiny_groups.push_back(g);
+                if (out.empty() || out.back() != g) out.push_back(g);
             }
         }
     }
-    std::sort(c->tiny_groups.begin(), c->tiny_groups.end());
-    c->tiny_groups.erase(std::unique(c->tiny_groups.begin(), c->tiny_groups.end()), c->tiny_groups.end());
+    std::sort(out.begin(), out.end());
+    out.erase(std::unique(out.begin(), out.end()), out.end());
+}
+
+void find_tiny_groups(rt_camera* c) {
+    if (c->tiny_done) return;
+    tiny_groups_of(c->w, c->h, c->basis.n_mod, c->basis.u_mod, c->basis.v_mod, c->tiny_groups);
     c->tiny_done = true;
 }
 
@@ -619,10 +671,10 @@ void find_tiny_groups(rt_camera* c) {
 // blocks; the fine region then covers every group that is not far, and
 // fusion is refused (returns false, region set as unfused) when a tiny-ray
 // group would fall outside it.
-bool set_fine_region(rt_camera* c, TraceParams& p, int per_wave, bool fused) {
-    const int32_t nbands = (c->h + kTileH - 1) / kTileH;
+bool set_fine_region(const FrameGeom& c, TraceParams& p, int per_wave, bool fused) {
+    const int32_t nbands = (c.h + kTileH - 1) / kTileH;
     const int32_t per_band = kTileH / p.tile_h;
-    p.groups_x = (c->w + 7) / 8;
+    p.groups_x = (c.w + 7) / 8;
     p.nslots = (nbands + p.nranks - 1) / p.nranks;
     p.fine_tx0 = p.fine_s0 = 0;
     p.cg_x0 = 0; p.cg_x1 = p.groups_x;
@@ -644,9 +696,9 @@ bool set_fine_region(rt_camera* c, TraceParams& p, int per_wave, bool fused) {
     if (fused) {  // fine tiles over everything within the far rectangle
         r[0] -= 2; r[1] += 2; r[2] -= 2; r[3] += 2;
     }
-    if (c->debug & 4) r[0] = r[1] = r[2] = r[3] = -8.0;  // tests: every group coarse
-    const double x0 = std::max(r[0], 0.0), x1 = std::min(r[1], (double)c->w - 1);
-    const double y0 = std::max(r[2], 0.0), y1 = std::min(r[3], (double)c->h - 1);
+    if (c.debug & 4) r[0] = r[1] = r[2] = r[3] = -8.0;  // tests: every group coarse
+    const double x0 = std::max(r[0], 0.0), x1 = std::min(r[1], (double)c.w - 1);
+    const double y0 = std::max(r[2], 0.0), y1 = std::min(r[3], (double)c.h - 1);
     int32_t tx0 = 0, tx1 = -1, s0 = 0, s1 = -1;
     if (x0 <= x1 && y0 <= y1) {
         tx0 = (int32_t)x0 / p.tile_w;
@@ -678,8 +730,7 @@ bool set_fine_region(rt_camera* c, TraceParams& p, int per_wave, bool fused) {
     const int64_t waves = (p.coarse_groups + per_wave - 1) / per_wave;
     p.coarse_blocks = (int32_t)((waves + 1) / 2);  // kernel 3 runs two waves per block
     if (fused) {
-        find_tiny_groups(c);
-        for (const auto& g : c->tiny_groups) {
+        for (const auto& g : *c.tiny) {
             const int32_t band = g.second;
             if ((band - p.rank) % p.nranks != 0 || band < p.rank) continue;  // not this rank's band
             const int32_t slot = (band - p.rank) / p.nranks;
@@ -710,33 +761,32 @@ bool set_fine_region(rt_camera* c, TraceParams& p, int per_wave, bool fused) {
 // chain; 8 rays scale with the work.
 constexpr int64_t kAutoRaysMinUnits = 4096;
 
-int auto_rays(const rt_camera* c, const TraceParams& p) {
+int auto_rays(const FrameGeom& c, const TraceParams& p) {
     double r[4];
     if (!root_rect(c, p, r)) return 16;  // no bounded rectangle: the whole frame is fine
-    const double x0 = std::max(r[0] - 2, 0.0), x1 = std::min(r[1] + 2, (double)c->w - 1);
-    const double y0 = std::max(r[2] - 2, 0.0), y1 = std::min(r[3] + 2, (double)c->h - 1);
+    const double x0 = std::max(r[0] - 2, 0.0), x1 = std::min(r[1] + 2, (double)c.w - 1);
+    const double y0 = std::max(r[2] - 2, 0.0), y1 = std::min(r[3] + 2, (double)c.h - 1);
     if (x1 < x0 || y1 < y0) return 16;
     const double px = (x1 - x0 + 1) * (y1 - y0 + 1) / p.nranks;
     return px / 16 < (double)kAutoRaysMinUnits ? 8 : 16;
 }
 
-bool frame_geometry(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t mode, TraceParams& p) {
+bool frame_geometry(const FrameGeom& g, const float* xform, const rt_tile* tile, uint32_t mode, TraceParams& p) {
     static const float ident[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
-    const rt_scene* s = c->obj;
     for (int k = 0; k < 3; k++) {
-        p.n_mod[k] = c->basis.n_mod[k];
-        p.u_mod[k] = c->basis.u_mod[k];
-        p.v_mod[k] = c->basis.v_mod[k];
+        p.n_mod[k] = g.n_mod[k];
+        p.u_mod[k] = g.u_mod[k];
+        p.v_mod[k] = g.v_mod[k];
     }
     memcpy(p.xf, xform ? xform : ident, sizeof p.xf);
-    p.w = c->w;
-    p.h = c->h;
+    p.w = g.w;
+    p.h = g.h;
     p.nranks = tile ? tile->nranks : 1;
     p.rank = tile ? tile->rank : 0;
-    camera_relative_box(s->root, c->pos, p.root_box);
-    const int32_t nbands = (c->h + kTileH - 1) / kTileH;
-    const int kernel = mode == RT_MODE_KD ? effective_kernel(c) : 0;
-    p.rays = kernel == 3 ? (c->rays > 0 ? c->rays : auto_rays(c, p)) : 64;
+    memcpy(p.root_box, g.root_box, sizeof p.root_box);
+    const int32_t nbands = (g.h + kTileH - 1) / kTileH;
+    const int kernel = mode == RT_MODE_KD ? g.kernel : 0;
+    p.rays = kernel == 3 ? (g.rays > 0 ? g.rays : auto_rays(g, p)) : 64;
     if (kernel == 0 || kernel == 1) {        // flat / v1: 32x8 tiles, four 8x8 waves
         p.tile_w = kTileWFlat; p.tile_h = kTileH;
     } else if (p.rays == 64) {               // v2 / v3: 16x8 tiles, two 8x8 waves
@@ -744,15 +794,38 @@ bool frame_geometry(rt_camera* c, const float* xform, const rt_tile* tile, uint3
     } else {                                 // v3, two stacked 8 x (rays/8) waves
         p.tile_w = 8; p.tile_h = kd3_waves(p.rays) * (p.rays / 8);
     }
-    p.tiles_x = (c->w + p.tile_w - 1) / p.tile_w;
+    p.tiles_x = (g.w + p.tile_w - 1) / p.tile_w;
     p.block_rows = ((nbands + p.nranks - 1) / p.nranks) * (kTileH / p.tile_h);
     p.plain_xf = 1;
     for (int k = 0; k < 12; k++) p.plain_xf &= (p.xf[k] == ident[k]) ? 1 : 0;
     // Far groups go to the fine kernel's extra blocks when every coarse group
     // can be far (identity transform, interior root, no diagnostics);
     // otherwise to k_coarse_kd3.
-    const bool fuse = kernel == 3 && p.plain_xf && !(s->root_ref & kLeafBit) && !(c->debug & (1 | 4 | 8));
-    return set_fine_region(c, p, kernel == 3 ? c->coarse : 0, fuse);
+    const bool fuse = kernel == 3 && p.plain_xf && !g.root_leaf && !(g.debug & (1 | 4 | 8));
+    return set_fine_region(g, p, kernel == 3 ? g.coarse : 0, fuse);
+}
+
+// The geometry inputs of a device camera (its object prepared).
+FrameGeom camera_geom(rt_camera* c) {
+    FrameGeom g;
+    g.w = c->w;
+    g.h = c->h;
+    g.n_mod = c->basis.n_mod;
+    g.u_mod = c->basis.u_mod;
+    g.v_mod = c->basis.v_mod;
+    camera_relative_box(c->obj->root, c->pos, g.root_box);
+    g.root_leaf = (c->obj->root_ref & kLeafBit) != 0;
+    g.kernel = effective_kernel(c);
+    g.rays = c->rays;
+    g.coarse = c->coarse;
+    g.debug = c->debug;
+    find_tiny_groups(c);
+    g.tiny = &c->tiny_groups;
+    return g;
+}
+
+bool frame_geometry(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t mode, TraceParams& p) {
+    return frame_geometry(camera_geom(c), xform, tile, mode, p);
 }
 
 int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t* argb, int64_t* hit,
@@ -1218,7 +1291,7 @@ static int flat_keys_for(rt_camera* c, hipStream_t stream, int64_t npix, unsigne
 }
 
 static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32_t flags, const rt_tile* tile,
-                         uint32_t* argb, int64_t* hit, void* stream) {
+                         uint32_t* argb, int64_t* hit, void* stream, uint32_t* display = nullptr) {
     if (!c) return fail(RT_ERR_INVALID, "rt_render: null camera");
     if (mode != RT_MODE_KD && mode != RT_MODE_FLAT) return fail(RT_ERR_INVALID, "rt_render: mode %u", mode);
     int rc = check_tile(tile);
@@ -1259,6 +1332,7 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
         pc.p = p;
     }
     p.frame_out = (flags & RT_FLAG_FRAME_OUT) ? 1 : 0;
+    p.display = display;
     p.flat_key = nullptr;
     p.flat_chunks = 0;
     if (mode == RT_MODE_FLAT && c->flat_variant >= 10 && !(flags & RT_FLAG_COUNT)) {
@@ -1282,12 +1356,22 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
             return rc;
     }
     if (trial >= 0 && (rc = hip_check(hipEventRecord(c->tune_ev[2 * trial], st), "order trial start"))) return rc;
-    // a slot uploaded on another lane: this frame's launch waits for it
-    for (int k = 0; p.order && c->nactive > 1 && k < kOrderSlots; k++) {
-        const auto& o = c->oslot[k];
-        if (o.d == p.order && o.up_valid && o.up_stream != st &&
-            (rc = hip_check(hipStreamWaitEvent(st, o.up_ev, 0), "order upload wait")))
-            return rc;
+    // a slot (or its cost order) uploaded on another stream: this frame's
+    // launch waits for it (no barrier packet once the upload has landed)
+    for (int k = 0; p.order && k < kOrderSlots; k++) {
+        auto& o = c->oslot[k];
+        if (o.d != p.order || !o.up_valid || o.up_stream == st) continue;
+        if (hipEventQuery(o.up_ev) == hipSuccess) o.up_valid = false;
+        else if ((rc = hip_check(hipStreamWaitEvent(st, o.up_ev, 0), "order upload wait"))) return rc;
+    }
+    if (p.order && p.order == c->d_order && c->cost_up_valid && c->cost_up_stream != st) {
+        if (hipEventQuery(c->order_ev) == hipSuccess) c->cost_up_valid = false;
+        else if ((rc = hip_check(hipStreamWaitEvent(st, c->order_ev, 0), "cost order wait"))) return rc;
+    }
+    int cset = 0;
+    if (p.cost) {  // this stream's own cost set
+        cset = cost_set(c, st);
+        p.cost = c->d_cost + (size_t)cset * c->cost_cap;
     }
     if ((rc = launch_split(c, p, mode, flags, stream))) return rc;
     if (p.order) {  // the streams that read the current order slot
@@ -1302,7 +1386,7 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
                 (rc = hip_check(hipStreamWaitEvent(c->active[l], c->tune_ev[2 * trial + 1], 0), "trial fork wait")))
                 return rc;
     }
-    return p.cost ? cost_feedback(c, p, stream) : RT_OK;
+    return p.cost ? cost_feedback(c, p, stream, cset) : RT_OK;
 }
 
 extern "C" int rt_render(rt_camera* c, const float* xform, uint32_t mode, uint32_t flags, const rt_tile* tile,
@@ -1311,6 +1395,13 @@ extern "C" int rt_render(rt_camera* c, const float* xform, uint32_t mode, uint32
     if (tile && tile->nranks != 1)
         return fail(RT_ERR_INVALID, "rt_render: the camera's own buffer holds a full frame; use rt_render_into for tiles");
     return render_common(c, xform, mode, flags, tile, c->d_argb, c->d_hit, stream);
+}
+
+extern "C" int rt_render_display(rt_camera* c, const float* xform, uint32_t mode, uint32_t flags, const rt_tile* tile,
+                                 uint32_t* d_clean, uint32_t* d_display, int64_t* d_hit, void* stream) {
+    if (!d_clean || !d_display || d_clean == d_display)
+        return fail(RT_ERR_INVALID, "rt_render_display: needs distinct clean and display buffers");
+    return render_common(c, xform, mode, flags, tile, d_clean, d_hit, stream, d_display);
 }
 
 extern "C" int rt_render_into(rt_camera* c, const float* xform, uint32_t mode, uint32_t flags, const rt_tile* tile,
@@ -1360,18 +1451,22 @@ extern "C" int rt_frame_rect(rt_camera* c, const float* xform, uint32_t mode, in
     return RT_OK;
 }
 
-static int frame_rect_uncached(rt_camera* c, const float* xform, uint32_t mode, int32_t nranks, int32_t rect[4]) {
-    const int32_t nbands = (c->h + kTileH - 1) / kTileH;
-    rect[0] = 0; rect[1] = c->w; rect[2] = 0; rect[3] = nbands;  // no proof: the whole frame
-    if (mode != RT_MODE_KD || !c->obj->d_nodes) return RT_OK;
+// The rectangle from the geometry inputs alone (the device camera's, or the
+// host-only ones of rt_frame_rect_host): every rank's tiling, as its render
+// would derive it.
+static void frame_rect_geom(const FrameGeom& g, bool kd_tree, const float* xform, uint32_t mode, int32_t nranks,
+                            int32_t rect[4]) {
+    const int32_t nbands = (g.h + kTileH - 1) / kTileH;
+    rect[0] = 0; rect[1] = g.w; rect[2] = 0; rect[3] = nbands;  // no proof: the whole frame
+    if (mode != RT_MODE_KD || !kd_tree) return;
     int32_t x0 = INT32_MAX, x1 = INT32_MIN, b0 = INT32_MAX, b1 = INT32_MIN;
     for (int32_t r = 0; r < nranks; r++) {
         TraceParams p{};
         const rt_tile t{nranks, r};
-        if (!frame_geometry(c, xform, &t, mode, p)) return RT_OK;  // a rank renders unfused
+        if (!frame_geometry(g, xform, &t, mode, p)) return;  // a rank renders unfused
         if (p.cs1 <= p.cs0 || p.cg_x1 <= p.cg_x0) continue;     // nothing fine on this rank
         x0 = std::min(x0, p.cg_x0 * 8);
-        x1 = std::max(x1, std::min(p.cg_x1 * 8, c->w));
+        x1 = std::max(x1, std::min(p.cg_x1 * 8, g.w));
         b0 = std::min(b0, r + p.cs0 * nranks);
         b1 = std::max(b1, r + (p.cs1 - 1) * nranks + 1);
     }
@@ -1380,6 +1475,58 @@ static int frame_rect_uncached(rt_camera* c, const float* xform, uint32_t mode, 
     } else {
         rect[0] = x0; rect[1] = x1; rect[2] = b0; rect[3] = std::min(b1, nbands);
     }
+}
+
+static int frame_rect_uncached(rt_camera* c, const float* xform, uint32_t mode, int32_t nranks, int32_t rect[4]) {
+    frame_rect_geom(camera_geom(c), c->obj->d_nodes != nullptr, xform, mode, nranks, rect);
+    return RT_OK;
+}
+
+extern "C" int rt_camera_frame_geometry(rt_camera* c, rt_frame_geometry* out) {
+    if (!c || !out) return fail(RT_ERR_INVALID, "rt_camera_frame_geometry: bad argument");
+    DeviceGuard g(c->device);
+    int rc;
+    if ((rc = prepare_camera_object(c))) return rc;
+    const FrameGeom f = camera_geom(c);
+    out->w = f.w;
+    out->h = f.h;
+    for (int k = 0; k < 3; k++) {
+        out->n_mod[k] = f.n_mod[k];
+        out->u_mod[k] = f.u_mod[k];
+        out->v_mod[k] = f.v_mod[k];
+    }
+    memcpy(out->root_box, f.root_box, sizeof out->root_box);
+    out->root_is_leaf = f.root_leaf ? 1 : 0;
+    out->kernel = f.kernel;
+    out->rays = f.rays;
+    out->coarse = f.coarse;
+    out->debug = f.debug;
+    return RT_OK;
+}
+
+extern "C" int rt_frame_rect_host(const rt_frame_geometry* in, const float* xform, uint32_t mode, int32_t nranks,
+                                  int32_t rect[4]) {
+    if (!in || !rect || nranks < 1 || in->w <= 0 || in->h <= 0) return fail(RT_ERR_INVALID, "rt_frame_rect_host: bad argument");
+    if (mode != RT_MODE_KD && mode != RT_MODE_FLAT) return fail(RT_ERR_INVALID, "rt_frame_rect_host: mode %u", mode);
+    if (in->kernel < 1 || in->kernel > 3 || (in->rays != 0 && in->rays != 8 && in->rays != 16 && in->rays != 32 &&
+                                              in->rays != 64) || in->coarse < 0 || in->coarse > 32)
+        return fail(RT_ERR_INVALID, "rt_frame_rect_host: bad kernel options");
+    FrameGeom g;
+    g.w = in->w;
+    g.h = in->h;
+    g.n_mod = in->n_mod;
+    g.u_mod = in->u_mod;
+    g.v_mod = in->v_mod;
+    memcpy(g.root_box, in->root_box, sizeof g.root_box);
+    g.root_leaf = in->root_is_leaf != 0;
+    g.kernel = in->kernel;
+    g.rays = in->rays;
+    g.coarse = in->coarse;
+    g.debug = in->debug;
+    std::vector<std::pair<int32_t, int32_t>> tiny;
+    tiny_groups_of(g.w, g.h, g.n_mod, g.u_mod, g.v_mod, tiny);
+    g.tiny = &tiny;
+    frame_rect_geom(g, true, xform, mode, nranks, rect);
     return RT_OK;
 }
 
@@ -1405,6 +1552,55 @@ extern "C" int rt_pack_rect(int device, int32_t w, int32_t h, int32_t nranks, in
     if (rank < 0 || rank >= nranks || !d_local || !d_out) return fail(RT_ERR_INVALID, "rt_pack_rect: bad argument");
     DeviceGuard g(device);
     return launch_pack_rect(w, h, nranks, rank, rect, d_local, d_out, stream);
+}
+
+// Host-memory forms of the rectangle gather's pack and assembly (the same
+// index maps as k_pack_rect / k_unpack_rect), for a gather over host buffers
+// (distributed.HostRectGather: the protocol over gloo, tests on CPU).
+extern "C" int rt_pack_rect_host(int32_t w, int32_t h, int32_t nranks, int32_t rank, const int32_t rect[4],
+                                 const uint32_t* local, uint32_t* out) {
+    int rc;
+    if ((rc = check_rect(w, h, nranks, rect, "rt_pack_rect_host"))) return rc;
+    if (rank < 0 || rank >= nranks || !local || !out) return fail(RT_ERR_INVALID, "rt_pack_rect_host: bad argument");
+    int32_t s0, s1;
+    rect_slots(rect[2], rect[3], nranks, rank, s0, s1);
+    const int32_t cw = rect[1] - rect[0];
+    for (int32_t row = 0; row < (s1 - s0) * kTileH; row++) {
+        const int32_t s = s0 + row / kTileH, r = row % kTileH;
+        memcpy(out + (int64_t)row * cw, local + ((int64_t)s * kTileH + r) * w + rect[0], sizeof(uint32_t) * (size_t)cw);
+    }
+    return RT_OK;
+}
+
+extern "C" int rt_unpack_rect_host(int32_t w, int32_t h, int32_t nranks, const int32_t rect[4], const uint32_t* local0,
+                                   const uint32_t* peers, uint32_t* frame) {
+    int rc;
+    if ((rc = check_rect(w, h, nranks, rect, "rt_unpack_rect_host"))) return rc;
+    if (!local0 || !frame || (nranks > 1 && !peers)) return fail(RT_ERR_INVALID, "rt_unpack_rect_host: bad argument");
+    const int32_t x0 = rect[0], x1 = rect[1], b0 = rect[2], b1 = rect[3], cw = x1 - x0;
+    std::vector<int64_t> off((size_t)nranks + 1, 0);  // each peer's part, back to back
+    for (int32_t q = 1; q < nranks; q++) {
+        int32_t s0, s1;
+        rect_slots(b0, b1, nranks, q, s0, s1);
+        off[(size_t)q + 1] = off[(size_t)q] + (int64_t)(s1 - s0) * kTileH * cw;
+    }
+    for (int32_t y = 0; y < h; y++) {
+        const int32_t band = y / kTileH, r = y - band * kTileH;
+        const int32_t rank = band % nranks, slot = band / nranks;
+        uint32_t* dst = frame + (int64_t)y * w;
+        for (int32_t x = 0; x < w; x++) dst[x] = 0x00F08200u;  // the background, TD/Camera.cpp:72
+        if (band < b0 || band >= b1 || cw <= 0) continue;
+        const uint32_t* src;
+        if (rank == 0) {
+            src = local0 + ((int64_t)slot * kTileH + r) * w + x0;
+        } else {
+            int32_t s0, s1;
+            rect_slots(b0, b1, nranks, rank, s0, s1);
+            src = peers + off[(size_t)rank] + ((int64_t)(slot - s0) * kTileH + r) * cw;
+        }
+        memcpy(dst + x0, src, sizeof(uint32_t) * (size_t)cw);
+    }
+    return RT_OK;
 }
 
 extern "C" int rt_unpack_rect(int device, int32_t w, int32_t h, int32_t nranks, const int32_t rect[4],
@@ -1516,6 +1712,8 @@ extern "C" void rt_camera_destroy(rt_camera* c) {
     dev_free(c->d_dbg);
     for (auto& k : c->flat_keys) dev_free(k.d);
     dev_free(c->d_cost);
+    for (hipEvent_t e : c->slot_join_ev)
+        if (e) (void)hipEventDestroy(e);
     if (c->h_cost) (void)hipHostFree(c->h_cost);
     if (c->h_order) (void)hipHostFree(c->h_order);
     if (c->cost_ev) (void)hipEventDestroy(c->cost_ev);
@@ -1650,7 +1848,11 @@ extern "C" int rt_run_frames(rt_camera* c, rt_comm* comm, const rt_frame_loop* a
     if (a->nxforms < 0 || (a->nxforms > 0 && !a->xforms))
         return fail(RT_ERR_INVALID, "rt_run_frames: bad transform sequence");
     const int L = std::max(1, (int)a->inflight);
-    if (L > 1 && !comm && a->nbuf % L)
+    // a set is rendered by one lane only: frames j and j + nbuf share a set,
+    // and with nbuf a multiple of L they also share a lane, so they are
+    // ordered (without a gather, and on rank 0's direct path, no event orders
+    // two lanes' renders of one set: ADVICE r02)
+    if (L > 1 && a->nbuf % L)
         return fail(RT_ERR_INVALID, "rt_run_frames: %d buffer sets for %d frames in flight (need a multiple)", a->nbuf, L);
     for (int k = 0; k < a->nbuf; k++)
         if (!a->d_local[k] || (comm && (!a->d_scratch[k] || !a->comm_stream)))

@@ -92,6 +92,11 @@ struct TraceParams {
     const float4* shade;
     uint32_t* argb;
     int64_t* hit;
+    // rt_render_display: the frame the reference's window shows
+    // (TD/WinMain.cpp:212-237), or null: argb holds the previous frame's
+    // clean buffer on entry; a hit pixel shows this frame's Phong, a miss
+    // keeps the previous clean value (color_cam_cuda writes rmi >= 0 only)
+    uint32_t* display;
     unsigned long long* counters;  // 5 x u64 or null
     int32_t* err;                  // device error word
     float n_mod[3], u_mod[3], v_mod[3];

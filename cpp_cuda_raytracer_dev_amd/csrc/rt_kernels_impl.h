@@ -105,6 +105,17 @@ __device__ __forceinline__ uint32_t phong(const float pnt[3], const float nrm[3]
 // order 3: the host's permutation by the tiles' measured cost in an earlier
 // frame, heaviest first (centre-out until costs arrive); order 4: the same
 // per XCD over 8 screen regions of equal cost.
+// A pixel's frame write.  With P.display (rt_render_display) it also writes
+// the reference's displayed frame: the clean buffer argb still holds the
+// previous frame, which a miss keeps on screen (ghosting under motion: the
+// window's buffer is overwritten by color_cam_cuda only where rmi >= 0,
+// TD/Camera.cu:27-61, and reset to background + Phong by the SET pass after
+// the blit, TD/WinMain.cpp:212-237, TD/Camera.cu:77-84).
+__device__ __forceinline__ void put_pixel(const TraceParams& P, int64_t out, uint32_t argb, bool hit) {
+    if (P.display) P.display[out] = hit ? argb : P.argb[out];
+    P.argb[out] = argb;
+}
+
 __device__ __forceinline__ int32_t tile_index(const TraceParams& P, int32_t b) {
     const int32_t nblocks = P.tiles_x * P.block_rows;
     if (P.tile_order == 0) {
@@ -352,7 +363,7 @@ __global__ __launch_bounds__(kTileWFlat * kTileH) void k_trace_kd(TraceParams P)
         const float rad[3] = {M.x, M.y, M.z};
         argb = phong(pnt, nrm, cam, rad);
     }
-    P.argb[px.out] = argb;
+    put_pixel(P, px.out, argb, best != kMiss);
     if (kWriteHit) P.hit[px.out] = best == kMiss ? (int64_t)-1 : (int64_t)best;
     if (kCount) {
         wave_count_add(&P.counters[0], n_int);
@@ -601,7 +612,7 @@ __global__ __launch_bounds__(kTileWKd * kTileH) void k_trace_kd2(TraceParams P) 
         const float rad[3] = {M.x, M.y, M.z};
         argb = phong(pnt, nrm, cam, rad);
     }
-    P.argb[px.out] = argb;
+    put_pixel(P, px.out, argb, best != kMiss);
     if (kWriteHit) P.hit[px.out] = best == kMiss ? (int64_t)-1 : (int64_t)best;
     if (kCount) {
         wave_count_add(&P.counters[0], n_int);
@@ -701,20 +712,52 @@ constexpr int pool_cap_for() {
 // rd[1] = (1/ry, 1/rz, odx/rx, ody/ry), rd[2] = (odz/rz, dir per cut axis),
 // translated walks add rd[3] = (od, ds of axis 0), rd[4] = (ds of axes 1-2,
 // shadow walks: Lmax, hit triangle).
-__device__ __forceinline__ void store_ray(float4* rd, const Ray& R, bool translated, float lmax, uint32_t self) {
+// Per-ray data of the pool walk in a wave's LDS: six float2 fields per ray
+// (ten for translated and shadow walks), field-major -- field k of ray r at
+// ray[k * kRays + r] -- so that every read of a field by the lanes of a wave
+// (items of up to kRays distinct rays) hits distinct banks, whatever width
+// the compiler reads it with: for kRays <= 16 a ds_read_b64 (64 banks) and a
+// ds_read_b32 / ds_read2_b32 (32 banks) of one component both spread the
+// rays over distinct banks.  Round 2's ray-major float4 records (48 B per
+// ray) put rays r and r + 8 on the same banks: 1.36 conflict cycles per LDS
+// instruction in the 16-ray instance at C4 (the 8-ray one 0.05); float4
+// fields (r03a) still conflicted through the ds_read2_b32 halves the compiler
+// split them into (0.71).
+//   f0 (rx, ry)  f1 (rz, 1/rx)  f2 (1/ry, 1/rz)  f3 (odx/rx, ody/ry)
+//   f4 (odz/rz, dir axis 0)  f5 (dir axis 1, dir axis 2)
+//   translated / shadow walks add f6 (odx, ody)  f7 (odz, ds axis 0)
+//   f8 (ds axis 1, ds axis 2)  f9 (Lmax, hit triangle)
+// RT_RAY_HOIST 1: an item's ray fields are read once before the leaf /
+// interior branch (no faster on gfx950, and it spilled 3 VGPRs of the 16-ray
+// instance); 0 (default): each path reads its own.
+#ifndef RT_RAY_HOIST
+#define RT_RAY_HOIST 0
+#endif
+template <int kRays>
+struct RayLayout {
+    static constexpr int kStride = kRays;  // float2s between the fields of one ray
+};
+
+__device__ __forceinline__ void store_ray(float2* rd, int stride, const Ray& R, bool translated, float lmax,
+                                          uint32_t self) {
     // dir and ds for each one-hot cut axis (TD/Trixel.cu:88-90)
     const float d0 = (R.rx * 1.0f) + (R.ry * 0.0f) + (R.rz * 0.0f);
     const float d1 = (R.rx * 0.0f) + (R.ry * 1.0f) + (R.rz * 0.0f);
     const float d2 = (R.rx * 0.0f) + (R.ry * 0.0f) + (R.rz * 1.0f);
-    rd[0] = make_float4(R.rx, R.ry, R.rz, R.ix);
-    rd[1] = make_float4(R.iy, R.iz, R.ox, R.oy);
-    rd[2] = make_float4(R.oz, d0, d1, d2);
+    rd[0] = make_float2(R.rx, R.ry);
+    rd[stride] = make_float2(R.rz, R.ix);
+    rd[2 * stride] = make_float2(R.iy, R.iz);
+    rd[3 * stride] = make_float2(R.ox, R.oy);
+    rd[4 * stride] = make_float2(R.oz, d0);
+    rd[5 * stride] = make_float2(d1, d2);
     if (translated) {
         const float e0 = (R.odx * 1.0f) + (R.ody * 0.0f) + (R.odz * 0.0f);
         const float e1 = (R.odx * 0.0f) + (R.ody * 1.0f) + (R.odz * 0.0f);
         const float e2 = (R.odx * 0.0f) + (R.ody * 0.0f) + (R.odz * 1.0f);
-        rd[3] = make_float4(R.odx, R.ody, R.odz, e0);
-        rd[4] = make_float4(e1, e2, lmax, __uint_as_float(self));
+        rd[6 * stride] = make_float2(R.odx, R.ody);
+        rd[7 * stride] = make_float2(R.odz, e0);
+        rd[8 * stride] = make_float2(e1, e2);
+        rd[9 * stride] = make_float2(lmax, __uint_as_float(self));
     }
 }
 
@@ -788,16 +831,22 @@ __device__ __forceinline__ const float4* record_of(const TraceParams& P, uint32_
     return (ref & kLeafBit) ? P.trec + 4 * (size_t)(ref & ~kLeafBit) : P.inode + 4 * (size_t)ref;
 }
 
-// The per-ray data of an item's ray from LDS (see store_ray).
-template <bool kTranslated>
-__device__ __forceinline__ void ray_of(const float4* rd, Ray& Q, float4& q2, float4& q3, float4& q4) {
-    const float4 q0 = rd[0], q1 = rd[1];
-    q2 = rd[2];
-    q3 = kTranslated ? rd[3] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    q4 = kTranslated ? rd[4] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    Q.rx = q0.x; Q.ry = q0.y; Q.rz = q0.z; Q.ix = q0.w;
-    Q.iy = q1.x; Q.iz = q1.y; Q.ox = q1.z; Q.oy = q1.w;
-    Q.oz = q2.x;
+// The per-ray data of an item's ray from LDS (see store_ray), as the float4s
+// (q2 = (odz/rz, dir per axis), q3 = (od, ds axis 0), q4 = (ds axes 1-2,
+// Lmax, hit triangle)) the visits read.
+template <bool kTranslated, int kStride>
+__device__ __forceinline__ void ray_of(const float2* rd, Ray& Q, float4& q2, float4& q3, float4& q4) {
+    const float2 f0 = rd[0], f1 = rd[kStride], f2 = rd[2 * kStride], f3 = rd[3 * kStride], f4 = rd[4 * kStride],
+                 f5 = rd[5 * kStride];
+    const float2 z = make_float2(0.0f, 0.0f);
+    const float2 f6 = kTranslated ? rd[6 * kStride] : z, f7 = kTranslated ? rd[7 * kStride] : z,
+                 f8 = kTranslated ? rd[8 * kStride] : z, f9 = kTranslated ? rd[9 * kStride] : z;
+    q2 = make_float4(f4.x, f4.y, f5.x, f5.y);
+    q3 = make_float4(f6.x, f6.y, f7.x, f7.y);
+    q4 = make_float4(f8.x, f8.y, f9.x, f9.y);
+    Q.rx = f0.x; Q.ry = f0.y; Q.rz = f1.x; Q.ix = f1.y;
+    Q.iy = f2.x; Q.iz = f2.y; Q.ox = f3.x; Q.oy = f3.y;
+    Q.oz = f4.x;
     // object translation (exact zeros when untranslated, as X[3], X[7], X[11] are)
     Q.odx = kTranslated ? q3.x : 0.0f; Q.ody = kTranslated ? q3.y : 0.0f; Q.odz = kTranslated ? q3.z : 0.0f;
     Q.sx = Q.rx > 0; Q.sy = Q.ry > 0; Q.sz = Q.rz > 0;
@@ -807,11 +856,8 @@ __device__ __forceinline__ void ray_of(const float4* rd, Ray& Q, float4& q2, flo
 // TD/Trixel.cu:98-145.  kAny: shadow walk (Lmax and the hit triangle come
 // from rd[4]).
 template <bool kTranslated, bool kCount, bool kAny>
-__device__ __forceinline__ void visit_leaf(const float4* rd, uint4 it, float4 r0, float4 r1, float4 r2, float4 r3,
-                                           Visit& o, uint32_t& n_leaf, uint32_t& n_acc) {
-    Ray Q;
-    float4 q2, q3, q4;
-    ray_of<kTranslated>(rd, Q, q2, q3, q4);
+__device__ __forceinline__ void visit_leaf(const Ray& Q, float4 q4, uint4 it, float4 r0, float4 r1, float4 r2,
+                                           float4 r3, Visit& o, uint32_t& n_leaf, uint32_t& n_acc) {
     if (kCount) n_leaf++;
     float d = kAny ? q4.z : kDrawDistance;
     uint32_t best = kMiss;
@@ -828,11 +874,9 @@ __device__ __forceinline__ void visit_leaf(const float4* rd, uint4 it, float4 r0
 // An interior item whose child-box record (r0..r3) has arrived: the node's
 // child ordering (TD/Trixel.cu:146-170) and the children's slab tests.
 template <bool kTranslated, bool kCount>
-__device__ __forceinline__ void visit_interior(const float4* rd, uint4 it, float4 r0, float4 r1, float4 r2,
-                                               float4 r3, Visit& o, uint32_t& n_int, uint32_t& n_desc) {
-    Ray Q;
-    float4 q2, q3, q4;
-    ray_of<kTranslated>(rd, Q, q2, q3, q4);
+__device__ __forceinline__ void visit_interior(const Ray& Q, float4 q2, float4 q3, float4 q4, uint4 it, float4 r0,
+                                               float4 r1, float4 r2, float4 r3, Visit& o, uint32_t& n_int,
+                                               uint32_t& n_desc) {
     const uint32_t ray = it.w >> 26;
     const uint32_t marked = it.w & kCodeMarkMask;
     const uint32_t lw = __float_as_uint(r3.z);
@@ -901,12 +945,23 @@ __device__ __forceinline__ void visit_interior(const float4* rd, uint4 it, float
 
 // Visits one item whose record has arrived: a leaf's MT test or an interior
 // node's child ordering and slab tests.
-template <int kVec, bool kTranslated, bool kCount, bool kAny>
-__device__ __forceinline__ void visit_item(const float4* rd, uint4 it, float4 r0, float4 r1, float4 r2, float4 r3,
+template <int kStride, bool kTranslated, bool kCount, bool kAny>
+__device__ __forceinline__ void visit_item(const float2* rd, uint4 it, float4 r0, float4 r1, float4 r2, float4 r3,
                                            Visit& o, uint32_t& n_int, uint32_t& n_leaf, uint32_t& n_acc,
                                            uint32_t& n_desc) {
-    if (it.x & kLeafBit) visit_leaf<kTranslated, kCount, kAny>(rd, it, r0, r1, r2, r3, o, n_leaf, n_acc);
-    else visit_interior<kTranslated, kCount>(rd, it, r0, r1, r2, r3, o, n_int, n_desc);
+    Ray Q;
+    float4 q2, q3, q4;
+    if (RT_RAY_HOIST) {
+        ray_of<kTranslated, kStride>(rd, Q, q2, q3, q4);
+        if (it.x & kLeafBit) visit_leaf<kTranslated, kCount, kAny>(Q, q4, it, r0, r1, r2, r3, o, n_leaf, n_acc);
+        else visit_interior<kTranslated, kCount>(Q, q2, q3, q4, it, r0, r1, r2, r3, o, n_int, n_desc);
+    } else if (it.x & kLeafBit) {
+        ray_of<kTranslated, kStride>(rd, Q, q2, q3, q4);
+        visit_leaf<kTranslated, kCount, kAny>(Q, q4, it, r0, r1, r2, r3, o, n_leaf, n_acc);
+    } else {
+        ray_of<kTranslated, kStride>(rd, Q, q2, q3, q4);
+        visit_interior<kTranslated, kCount>(Q, q2, q3, q4, it, r0, r1, r2, r3, o, n_int, n_desc);
+    }
 }
 
 __device__ __forceinline__ uint32_t lanes_below(unsigned long long b) {
@@ -1017,8 +1072,8 @@ __device__ __forceinline__ int push_children(uint4* items, int at, const Visit& 
 // key[ray] = 0; without counters the items of such rays are dropped.
 // Each lane pops up to P.items (1 or 2) items per iteration and fetches their
 // records together, so a lane keeps two memory round trips in flight.
-template <int kCap, int kVec, bool kTranslated, bool kCount, bool kAny, int kOrder = 0>
-__device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, const float4* s_ray,
+template <int kCap, int kStride, bool kTranslated, bool kCount, bool kAny, int kOrder = 0>
+__device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, const float2* s_ray,
                                           unsigned long long* s_key, uint32_t* s_tri, int n, int lane,
                                           uint32_t& iters, uint32_t& popped, uint32_t& n_int, uint32_t& n_leaf,
                                           uint32_t& n_acc,
@@ -1069,7 +1124,7 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
             Visit v0;
             v0.ka = v0.kb = false; v0.cand = false;
             if (act0)
-                visit_item<kVec, kTranslated, kCount, kAny>(s_ray + (size_t)(it0.w >> 26) * kVec, it0, a0, a1, a2, a3,
+                visit_item<kStride, kTranslated, kCount, kAny>(s_ray + (size_t)(it0.w >> 26), it0, a0, a1, a2, a3,
                                                             v0, n_int, n_leaf, n_acc, n_desc);
             record_candidate<kAny>(s_key, s_tri, it0, v0);
             total += push_children<kAny, (kOrder & 3)>(items, base + total, v0);
@@ -1078,7 +1133,7 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
             Visit v1;
             v1.ka = v1.kb = false; v1.cand = false;
             if (act1)
-                visit_item<kVec, kTranslated, kCount, kAny>(s_ray + (size_t)(it1.w >> 26) * kVec, it1, b0, b1, b2, b3,
+                visit_item<kStride, kTranslated, kCount, kAny>(s_ray + (size_t)(it1.w >> 26), it1, b0, b1, b2, b3,
                                                             v1, n_int, n_leaf, n_acc, n_desc);
             record_candidate<kAny>(s_key, s_tri, it1, v1);
             total += push_children<kAny, (kOrder & 3)>(items, base + total, v1);
@@ -1092,10 +1147,10 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
         v0.ka = v0.kb = false; v0.cand = false;
         v1.ka = v1.kb = false; v1.cand = false;
         if (act0)
-            visit_item<kVec, kTranslated, kCount, kAny>(s_ray + (size_t)(it0.w >> 26) * kVec, it0, a0, a1, a2, a3, v0,
+            visit_item<kStride, kTranslated, kCount, kAny>(s_ray + (size_t)(it0.w >> 26), it0, a0, a1, a2, a3, v0,
                                                         n_int, n_leaf, n_acc, n_desc);
         if (act1)
-            visit_item<kVec, kTranslated, kCount, kAny>(s_ray + (size_t)(it1.w >> 26) * kVec, it1, b0, b1, b2, b3, v1,
+            visit_item<kStride, kTranslated, kCount, kAny>(s_ray + (size_t)(it1.w >> 26), it1, b0, b1, b2, b3, v1,
                                                         n_int, n_leaf, n_acc, n_desc);
         record_candidates<kAny>(s_key, s_tri, it0, it1, v0, v1);
         // push the children (all first children of item 0, all second ones, then item 1's): ballot compaction
@@ -1165,8 +1220,8 @@ __device__ __forceinline__ void push_split(uint4* items, int cap, int& ni, int& 
 // cap - slack; when that leaves no room a single interior pop runs (a DFS
 // step, growing the interior stack by at most the height over a run) while
 // slot 1 drains up to 64 leaves.
-template <int kCap, int kVec, bool kTranslated, bool kCount, bool kAny, int kOrder = 0>
-__device__ __forceinline__ void pool_walk_split(const TraceParams& P, uint4* items, const float4* s_ray,
+template <int kCap, int kStride, bool kTranslated, bool kCount, bool kAny, int kOrder = 0>
+__device__ __forceinline__ void pool_walk_split(const TraceParams& P, uint4* items, const float2* s_ray,
                                                 unsigned long long* s_key, uint32_t* s_tri, int n, int lane,
                                                 uint32_t& iters, uint32_t& popped, uint32_t& n_int, uint32_t& n_leaf,
                                                 uint32_t& n_acc, uint32_t& n_desc) {
@@ -1216,8 +1271,8 @@ __device__ __forceinline__ void pool_walk_split(const TraceParams& P, uint4* ite
             Visit v0;
             v0.ka = v0.kb = false; v0.cand = false;
             if (act0)
-                visit_interior<kTranslated, kCount>(s_ray + (size_t)(it0.w >> 26) * kVec, it0, a0, a1, a2, a3, v0,
-                                                    n_int, n_desc);
+                visit_item<kStride, kTranslated, kCount, kAny>(s_ray + (size_t)(it0.w >> 26), it0, a0, a1, a2,
+                                                               a3, v0, n_int, n_leaf, n_acc, n_desc);
             push_split<kAny, (kOrder & 3)>(items, cap, ti, tl, v0);
         }
         {
@@ -1225,13 +1280,13 @@ __device__ __forceinline__ void pool_walk_split(const TraceParams& P, uint4* ite
             v1.ka = v1.kb = false; v1.cand = false;
             if (leafslot) {
                 if (act1)
-                    visit_leaf<kTranslated, kCount, kAny>(s_ray + (size_t)(it1.w >> 26) * kVec, it1, b0, b1, b2, b3, v1,
-                                                          n_leaf, n_acc);
+                    visit_item<kStride, kTranslated, kCount, kAny>(s_ray + (size_t)(it1.w >> 26), it1, b0, b1,
+                                                                   b2, b3, v1, n_int, n_leaf, n_acc, n_desc);
                 record_candidate<kAny>(s_key, s_tri, it1, v1);
             } else {
                 if (act1)
-                    visit_interior<kTranslated, kCount>(s_ray + (size_t)(it1.w >> 26) * kVec, it1, b0, b1, b2, b3, v1,
-                                                        n_int, n_desc);
+                    visit_item<kStride, kTranslated, kCount, kAny>(s_ray + (size_t)(it1.w >> 26), it1, b0, b1,
+                                                                   b2, b3, v1, n_int, n_leaf, n_acc, n_desc);
                 push_split<kAny, (kOrder & 3)>(items, cap, ti, tl, v1);
             }
         }
@@ -1249,7 +1304,7 @@ __device__ __forceinline__ void pool_walk_split(const TraceParams& P, uint4* ite
 template <int kRays, int kCap, int kRayVec>
 struct WaveLds {
     uint4 items[kCap];
-    float4 ray[kRays * kRayVec];
+    float2 ray[kRays * kRayVec * 2];
     unsigned long long key[kRays];
     uint32_t tri[kRays];
 };
@@ -1264,6 +1319,7 @@ constexpr int kCoarseMax = 32;  // coarse groups per wave (RT_OPT_COARSE <= 32)
 template <int kRays, int kCap, int kRayVec, bool kTranslated, bool kWriteHit, bool kCount, int kShadow>
 __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, kCap, kRayVec>& S_, const Unit& U,
                                            int lane, size_t dbg_slot, uint32_t* cost, Counts& C) {
+    using RL = RayLayout<kRays>;
     uint4* items = S_.items;
     Pixel px;
     const bool live = unit_pixel(P, U, kRays / 8, lane, px);  // every lane stays for the ballots
@@ -1278,17 +1334,17 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
         Ray R0;
         camera_ray(P, px, live, cam0, R0);
         if (lane < kRays) {
-            store_ray(&S_.ray[lane * kRayVec], R0, kTranslated, 0.0f, 0u);
+            store_ray(&S_.ray[lane], RL::kStride, R0, kTranslated, 0.0f, 0u);
             S_.key[lane] = ~0ull;
             S_.tri[lane] = kMiss;
         }
         n = seed_root<kCount>(P, items, R0, live, lane, C.n_int, C.n_desc);
     }
     if (RT_SPLIT_LEAF && P.items > 1)
-        pool_walk_split<kCap, kRayVec, kTranslated, kCount, false>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters,
+        pool_walk_split<kCap, RL::kStride, kTranslated, kCount, false>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters,
                                                                   popped, C.n_int, C.n_leaf, C.n_acc, C.n_desc);
     else
-        pool_walk<kCap, kRayVec, kTranslated, kCount, false>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters, popped,
+        pool_walk<kCap, RL::kStride, kTranslated, kCount, false>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters, popped,
                                                             C.n_int, C.n_leaf, C.n_acc, C.n_desc);
     float cam[3];
     Ray R;
@@ -1326,17 +1382,17 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
         }
         finish_ray(Sh);
         if (lane < kRays) {
-            store_ray(&S_.ray[lane * kRayVec], Sh, true, lmax, best);
+            store_ray(&S_.ray[lane], RL::kStride, Sh, true, lmax, best);
             S_.key[lane] = ~0ull;
         }
         __builtin_amdgcn_wave_barrier();
         n = seed_root<kCount>(P, items, Sh, sh_live, lane, C.n_int, C.n_desc);
         if (RT_SPLIT_LEAF && P.items > 1)
-            pool_walk_split<kCap, kRayVec, true, kCount, true, kShadow - 1>(P, items, S_.ray, S_.key, S_.tri, n, lane,
+            pool_walk_split<kCap, RL::kStride, true, kCount, true, kShadow - 1>(P, items, S_.ray, S_.key, S_.tri, n, lane,
                                                                            iters, popped, C.n_int, C.n_leaf, C.n_acc,
                                                                            C.n_desc);
         else
-            pool_walk<kCap, kRayVec, true, kCount, true, kShadow - 1>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters,
+            pool_walk<kCap, RL::kStride, true, kCount, true, kShadow - 1>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters,
                                                                      popped, C.n_int, C.n_leaf, C.n_acc, C.n_desc);
         if (lane < kRays) shadowed = S_.key[lane] == 0ull;
     }
@@ -1364,7 +1420,7 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
         const float rad[3] = {M.x, M.y, M.z};
         argb = phong(pnt, nrm, cam, rad);
     }
-    P.argb[px.out] = argb;
+    put_pixel(P, px.out, argb, best != kMiss);
     if (kWriteHit) P.hit[px.out] = best == kMiss ? (int64_t)-1 : (int64_t)best;
     if (kCount && best != kMiss) C.n_hit++;
 }
@@ -1493,7 +1549,7 @@ __device__ __forceinline__ bool fill_far(const TraceParams& P, const Unit& G, in
     const bool live = unit_pixel(P, G, 8, lane, px);
     if (__ballot(live && ray_has_tiny_component(P, px.x, px.y)) != 0ull) return false;
     if (live) {
-        P.argb[px.out] = kBackground;
+        put_pixel(P, px.out, kBackground, false);
         if (kWriteHit) P.hit[px.out] = (int64_t)-1;
         if (kCount) C.n_int += 1u;  // the root visit, which fails
     }
@@ -1509,7 +1565,7 @@ __device__ __forceinline__ bool coarse_sure(const TraceParams& P, const Unit& G,
     const bool sure = !live || (P.plain_xf ? root_certain_miss(P, px.x, px.y) : root_certain_miss_xf(P, px.x, px.y));
     if (__ballot(!sure) != 0ull) return false;
     if (live) {
-        P.argb[px.out] = kBackground;
+        put_pixel(P, px.out, kBackground, false);
         if (kWriteHit) P.hit[px.out] = (int64_t)-1;
         if (kCount) C.n_int += 1u;  // the root visit, which fails
     }
@@ -1530,7 +1586,7 @@ __device__ __forceinline__ unsigned long long coarse_root(const TraceParams& P, 
     constexpr unsigned long long kSub = kRays == 64 ? ~0ull : ((1ull << (kRays & 63)) - 1);
     const bool traced = ((b >> ((lane / kRays) * kRays)) & kSub) != 0;
     if (live && !traced) {
-        P.argb[px.out] = kBackground;
+        put_pixel(P, px.out, kBackground, false);
         if (kWriteHit) P.hit[px.out] = (int64_t)-1;
         if (kCount) C.n_int += ni;  // the root visit; no root test passed in this sub-tile
     }
@@ -1782,7 +1838,7 @@ __device__ __forceinline__ void flat_shade_out(const TraceParams& P, const Pixel
         const float rad[3] = {M.x, M.y, M.z};
         argb = phong(pnt, nrm, rmd, rad);
     }
-    P.argb[px.out] = argb;
+    put_pixel(P, px.out, argb, best != kMiss);
     if (kWriteHit) P.hit[px.out] = best == kMiss ? (int64_t)-1 : (int64_t)best;
 }
 

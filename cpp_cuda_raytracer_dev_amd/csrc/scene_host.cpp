@@ -4,8 +4,9 @@
 // These are the producers of the hot path's inputs (SURVEY.md §8a rows a1,
 // a11).  They reproduce the reference's results exactly (tests compare them
 // with the oracle) but are organised for speed: the six merge sorts become
-// comparison sorts with the merge sort's tie order, and the per-level
-// partitions run in parallel because sibling ranges are disjoint.
+// stable radix sorts with the merge sort's tie order, and every level's
+// partitions run as chunked count / scan / scatter passes on a thread pool
+// (sibling ranges are disjoint; a big node's range is cut into chunks).
 #include <math.h>
 #include <sched.h>
 #include <stdarg.h>
@@ -16,6 +17,9 @@
 #include <algorithm>
 #include <atomic>
 #include <charconv>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <numeric>
 #include <string>
 #include <thread>
@@ -504,29 +508,136 @@ int validate_leafs(const rt_leaf_aabb* leafs, uint32_t n, const char* what) {
 }
 }  // namespace rt
 
+namespace {
+
+// A fixed pool of worker threads for the builder's many short parallel
+// phases (about 100 per build): run(n, body) runs body(i) for i in [0, n)
+// on the workers and the caller, and returns when all are done.  Spawning
+// threads per phase (round 2) cost more than the phases on a many-core box.
+class Pool {
+public:
+    explicit Pool(int threads) {
+        for (int k = 1; k < threads; k++) workers_.emplace_back([this] { loop(); });
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+            gen_++;
+        }
+        cv_.notify_all();
+        for (auto& t : workers_) t.join();
+    }
+    template <class F>
+    void run(int64_t n, F&& body) {
+        if (n <= 0) return;
+        if (workers_.empty() || n == 1) {
+            for (int64_t i = 0; i < n; i++) body(i);
+            return;
+        }
+        std::function<void(int64_t)> f(body);
+        {
+            std::lock_guard<std::mutex> g(m_);
+            fn_ = &f;
+            n_ = n;
+            next_.store(0);
+            busy_ = (int)workers_.size();
+            gen_++;
+        }
+        cv_.notify_all();
+        drain();
+        std::unique_lock<std::mutex> g(m_);
+        done_.wait(g, [&] { return busy_ == 0; });
+        fn_ = nullptr;
+    }
+    int size() const { return (int)workers_.size() + 1; }
+
+private:
+    void drain() {
+        for (int64_t i; (i = next_.fetch_add(1)) < n_;) (*fn_)(i);
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> g(m_);
+                cv_.wait(g, [&] { return gen_ != seen; });
+                seen = gen_;
+                if (stop_) return;
+            }
+            drain();
+            std::lock_guard<std::mutex> g(m_);
+            if (--busy_ == 0) done_.notify_one();
+        }
+    }
+    std::vector<std::thread> workers_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    std::function<void(int64_t)>* fn_ = nullptr;
+    int64_t n_ = 0;
+    std::atomic<int64_t> next_{0};
+    int busy_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+// Order-preserving unsigned image of a (non-NaN) float key, with -0.0 as
+// +0.0: merge_sort compares with `<`, under which they are equal.
+inline uint32_t key_bits(float f) {
+    if (f == 0.0f) f = 0.0f;
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+constexpr int64_t kChunk = 1 << 15;  // elements per partition task
+
+}  // namespace
+
 extern "C" int rt_kd_build(const rt_leaf_aabb* leafs, uint32_t n, rt_kd_node* nodes, int nthreads) {
     if (!nodes) return fail(RT_ERR_INVALID, "rt_kd_build: null nodes");
     int vrc = validate_leafs(leafs, n, "rt_kd_build");
     if (vrc) return vrc;
-    const int T = resolve_threads(nthreads);
+    Pool pool(resolve_threads(nthreads));
     // Six sorted position lists.  merge_sort (TD/sort.h:25-60) takes the right
-    // run on ties, so equal keys end up in descending input position: sort by
-    // (key ascending, position descending).
-    std::vector<uint32_t> list[6];
-    parallel_for(6, T, [&](int64_t k) {
-        auto& L = list[k];
-        L.resize(n);
-        std::iota(L.begin(), L.end(), 0u);
-        std::sort(L.begin(), L.end(), [&](uint32_t a, uint32_t b) {
-            float ka = list_key(leafs[a], (int)k), kb = list_key(leafs[b], (int)k);
-            return ka < kb || (!(kb < ka) && a > b);
-        });
+    // run on ties, so equal keys end up in descending input position: a
+    // stable LSD radix sort (11 + 11 + 10 bits) of the order-preserving key
+    // images, fed in descending position order, one list per task.
+    std::vector<uint32_t> list[6], other[6];
+    pool.run(6, [&](int64_t k) {
+        std::vector<uint32_t> ka(n), kb(n), pb(n);
+        auto& pa = list[k];
+        pa.resize(n);
+        other[k].resize(n);
+        for (uint32_t i = 0; i < n; i++) {
+            const uint32_t pos = n - 1 - i;
+            ka[i] = key_bits(list_key(leafs[pos], (int)k));
+            pa[i] = pos;
+        }
+        uint32_t *K = ka.data(), *P = pa.data(), *K2 = kb.data(), *P2 = pb.data();
+        static const int shift[3] = {0, 11, 22};
+        for (int pass = 0; pass < 3; pass++) {
+            uint32_t cnt[2049] = {0};
+            const int sh = shift[pass];
+            for (uint32_t i = 0; i < n; i++) cnt[((K[i] >> sh) & 2047u) + 1]++;
+            for (int d = 0; d < 2048; d++) cnt[d + 1] += cnt[d];
+            for (uint32_t i = 0; i < n; i++) {
+                const uint32_t o = cnt[(K[i] >> sh) & 2047u]++;
+                K2[o] = K[i];
+                P2[o] = P[i];
+            }
+            std::swap(K, K2);
+            std::swap(P, P2);
+        }
+        if (P != pa.data()) memcpy(pa.data(), P, sizeof(uint32_t) * n);  // odd pass count: result in pb
     });
     const int64_t nnode = 2 * (int64_t)n - 1;
     std::vector<Range> rng((size_t)nnode);
     std::vector<uint8_t> in_left(n, 0);
-    std::vector<uint32_t> scratch(n);
-    memset(nodes, 0, sizeof(rt_kd_node) * (size_t)nnode);
+    pool.run((nnode + 65535) / 65536, [&](int64_t b) {  // (first touch of the caller's pages, in parallel)
+        const int64_t a = b * 65536, e = std::min(nnode, a + 65536);
+        memset(nodes + a, 0, sizeof(rt_kd_node) * (size_t)(e - a));
+    });
 
     auto key_at = [&](int k, int64_t pos) { return list_key(leafs[list[k][(size_t)pos]], k); };
 
@@ -539,107 +650,154 @@ extern "C" int rt_kd_build(const rt_leaf_aabb* leafs, uint32_t n, rt_kd_node* no
     root.x0 = key_at(3, 0);     root.x1 = key_at(0, n - 1);
     rng[0] = {0, (int64_t)(n - 1) / 2, (int64_t)n - 1};
 
-    // BFS one level at a time: nodes [lv0, lv1) are siblings-at-depth with
-    // disjoint ranges, so their partitions are independent.
+    // BFS one level at a time (TD/Trixel.h:135-385): nodes [lv0, lv1) are the
+    // level's nodes, their ranges disjoint.  Each level: pick every node's
+    // cut (strict `>`, H11) and finish its leaves; mark which elements go
+    // left; stable-partition the five other lists of every interior node
+    // (TD/Trixel.h:214-327) in chunks -- count each chunk's left elements,
+    // scan within the node, scatter -- into the second buffer of each list
+    // (the cut list is copied: its [l, m] is already the left child's); swap
+    // the buffers; write the children (:329-376).
+    struct Task { int64_t node, p0, p1; };
+    std::vector<Task> tasks;
+    std::vector<int64_t> child_base, task0, blocks;
+    std::vector<uint32_t> lefts;  // [task][6]
     int64_t lv0 = 0, lv1 = 1, wr = 1;
-    std::vector<int64_t> child_base;
     while (lv0 < lv1) {
         const int64_t cnt = lv1 - lv0;
-        // child slots in BFS order (create_kd appends two per interior node)
         child_base.assign((size_t)cnt, -1);
         for (int64_t i = 0; i < cnt; i++) {
             const Range& R = rng[(size_t)(lv0 + i)];
             if (R.r != R.l) { child_base[(size_t)i] = wr; wr += 2; }
         }
         if (wr > nnode) return fail(RT_ERR_INVALID, "rt_kd_build: node overflow");
-        auto process = [&](int64_t i, int inner_threads) {
-            const int64_t id = lv0 + i;
-            rt_kd_node& nd = nodes[id];
-            const Range R = rng[(size_t)id];
-            // axis/key selection with strict `>` in the order x1,x0,y1,y0,z1,z0 (H11)
-            float best = key_at(0, R.r) - key_at(0, R.l);
-            int cut = 0;
-            static const int order[5] = {3, 1, 4, 2, 5};
-            for (int q = 0; q < 5; q++) {
-                const int k = order[q];
-                float span = key_at(k, R.r) - key_at(k, R.l);
-                if (span > best) { best = span; cut = k; }
-            }
-            if (R.r == R.l) {  // leaf: TD/Trixel.h:194-205
-                nd.cut_flag = nodes[nd.parent].cut_flag;
-                nd.is_leaf = 1;
-                nd.left = -1; nd.right = -1;
-                nd.tri_index = leafs[list[0][(size_t)R.l]].tri;
-                return;
-            }
-            nd.cut_flag = cut;
-            nd.is_leaf = 0;
-            nd.tri_index = -1;
-            const auto& C = list[cut];
-            for (int64_t p = R.l; p <= R.m; p++) in_left[C[(size_t)p]] = 1;
-            for (int64_t p = R.m + 1; p <= R.r; p++) in_left[C[(size_t)p]] = 0;
-            // stable partition of the other five lists (TD/Trixel.h:214-327)
-            int others[5], no = 0;
-            for (int k = 0; k < 6; k++) if (k != cut) others[no++] = k;
-            auto part = [&](int64_t j) {
-                auto& L = list[others[j]];
-                int64_t a = R.l, b = R.m + 1;
-                for (int64_t p = R.l; p <= R.r; p++) {
-                    uint32_t e = L[(size_t)p];
-                    scratch[(size_t)(in_left[e] ? a++ : b++)] = e;
+        // cut selection and leaves
+        pool.run((cnt + 4095) / 4096, [&](int64_t blk) {
+            for (int64_t i = blk * 4096; i < std::min(cnt, (blk + 1) * 4096); i++) {
+                const int64_t id = lv0 + i;
+                rt_kd_node& nd = nodes[id];
+                const Range R = rng[(size_t)id];
+                float best = key_at(0, R.r) - key_at(0, R.l);
+                int cut = 0;
+                static const int order[5] = {3, 1, 4, 2, 5};
+                for (int q = 0; q < 5; q++) {
+                    const int k = order[q];
+                    float span = key_at(k, R.r) - key_at(k, R.l);
+                    if (span > best) { best = span; cut = k; }
                 }
-                // scratch is shared, but each list uses it in turn below
-                memcpy(&L[(size_t)R.l], &scratch[(size_t)R.l], sizeof(uint32_t) * (size_t)(R.r - R.l + 1));
-            };
-            if (inner_threads > 1) {
-                // big node: give every list its own scratch to partition concurrently
-                std::vector<uint32_t> own[5];
-                parallel_for(5, inner_threads, [&](int64_t j) {
-                    auto& L = list[others[j]];
-                    auto& S = own[j];
-                    S.resize((size_t)(R.r - R.l + 1));
-                    int64_t a = 0, b = R.m + 1 - R.l;
-                    for (int64_t p = R.l; p <= R.r; p++) {
-                        uint32_t e = L[(size_t)p];
-                        S[(size_t)(in_left[e] ? a++ : b++)] = e;
-                    }
-                    memcpy(&L[(size_t)R.l], S.data(), sizeof(uint32_t) * S.size());
-                });
-            } else {
-                for (int j = 0; j < 5; j++) part(j);
+                if (R.r == R.l) {  // leaf: TD/Trixel.h:194-205
+                    nd.cut_flag = nodes[nd.parent].cut_flag;
+                    nd.is_leaf = 1;
+                    nd.left = -1; nd.right = -1;
+                    nd.tri_index = leafs[list[0][(size_t)R.l]].tri;
+                } else {
+                    nd.cut_flag = cut;
+                    nd.is_leaf = 0;
+                    nd.tri_index = -1;
+                }
             }
-            // children (TD/Trixel.h:329-352)
-            const int64_t cb = child_base[(size_t)i];
-            nd.left = cb; nd.right = cb + 1;
-            for (int br = 0; br < 2; br++) {
-                rt_kd_node& c = nodes[cb + br];
-                c.parent = id;
-                c.is_leaf = 0;
-                c.tri_index = -1;
-                int64_t nl = br == 0 ? R.l : R.m + 1, nr = br == 0 ? R.m : R.r;
-                rng[(size_t)(cb + br)] = {nl, ((nr - nl) / 2) + nl, nr};
-                c.x1 = key_at(0, nr); c.x0 = key_at(3, nl);
-                c.y1 = key_at(1, nr); c.y0 = key_at(4, nl);
-                c.z1 = key_at(2, nr); c.z0 = key_at(5, nl);
-            }
-            // s1 = left child's max, s2 = right child's min on the cut axis (:353-376)
-            const rt_kd_node& Lc = nodes[cb];
-            const rt_kd_node& Rc = nodes[cb + 1];
-            switch (cut) {
-            case 0: case 3: nd.s2 = Rc.x0; nd.s1 = Lc.x1; break;
-            case 1: case 4: nd.s2 = Rc.y0; nd.s1 = Lc.y1; break;
-            default:        nd.s2 = Rc.z0; nd.s1 = Lc.z1; break;
-            }
-        };
-        if (cnt < T) {
-            for (int64_t i = 0; i < cnt; i++) {
-                const Range& R = rng[(size_t)(lv0 + i)];
-                process(i, (R.r - R.l) > 65536 ? std::min(T, 5) : 1);
-            }
-        } else {
-            // scratch is indexed by position; sibling ranges are disjoint
-            parallel_for(cnt, T, [&](int64_t i) { process(i, 1); });
+        });
+        // the level's interior nodes in chunks of <= kChunk elements
+        tasks.clear();
+        task0.assign((size_t)cnt + 1, 0);
+        for (int64_t i = 0; i < cnt; i++) {
+            task0[(size_t)i] = (int64_t)tasks.size();
+            const Range& R = rng[(size_t)(lv0 + i)];
+            if (R.r == R.l) continue;
+            for (int64_t p = R.l; p <= R.r; p += kChunk) tasks.push_back({i, p, std::min(R.r + 1, p + kChunk)});
         }
+        task0[(size_t)cnt] = (int64_t)tasks.size();
+        const int64_t nt = (int64_t)tasks.size();
+        if (nt == 0) break;
+        // runs of consecutive tasks of ~kChunk elements, one pool item each
+        // (deep levels have a task per node: an item per task would make the
+        // pool's work counter the bottleneck)
+        blocks.clear();
+        for (int64_t t = 0, acc = 0; t < nt; t++) {
+            if (acc == 0) blocks.push_back(t);
+            acc += tasks[(size_t)t].p1 - tasks[(size_t)t].p0;
+            if (acc >= kChunk) acc = 0;
+        }
+        blocks.push_back(nt);
+        const int64_t nb = (int64_t)blocks.size() - 1;
+        // which elements go left: positions l..m of the node's cut list
+        pool.run(nb, [&](int64_t j) {
+            for (int64_t t = blocks[(size_t)j]; t < blocks[(size_t)j + 1]; t++) {
+                const Task T = tasks[(size_t)t];
+                const Range& R = rng[(size_t)(lv0 + T.node)];
+                const auto& C = list[nodes[lv0 + T.node].cut_flag];
+                for (int64_t p = T.p0; p < T.p1; p++) in_left[C[(size_t)p]] = p <= R.m ? 1 : 0;
+            }
+        });
+        // left elements per chunk of the big nodes (a node of one chunk needs none)
+        lefts.assign((size_t)nt * 6, 0);
+        pool.run(nb * 6, [&](int64_t q) {
+            const int k = (int)(q % 6);
+            const uint32_t* L = list[k].data();
+            for (int64_t t = blocks[(size_t)(q / 6)]; t < blocks[(size_t)(q / 6) + 1]; t++) {
+                const Task T = tasks[(size_t)t];
+                if (task0[(size_t)T.node + 1] - task0[(size_t)T.node] < 2 || k == (int)nodes[lv0 + T.node].cut_flag)
+                    continue;
+                uint32_t c = 0;
+                for (int64_t p = T.p0; p < T.p1; p++) c += in_left[L[p]];
+                lefts[(size_t)t * 6 + k] = c;
+            }
+        });
+        // scatter: left elements from l + (lefts of earlier chunks), right
+        // ones from m + 1 + (rights of earlier chunks)
+        pool.run(nb * 6, [&](int64_t q) {
+            const int k = (int)(q % 6);
+            const uint32_t* L = list[k].data();
+            uint32_t* O = other[k].data();
+            for (int64_t t = blocks[(size_t)(q / 6)]; t < blocks[(size_t)(q / 6) + 1]; t++) {
+                const Task T = tasks[(size_t)t];
+                const Range& R = rng[(size_t)(lv0 + T.node)];
+                if (k == (int)nodes[lv0 + T.node].cut_flag) {
+                    memcpy(O + T.p0, L + T.p0, sizeof(uint32_t) * (size_t)(T.p1 - T.p0));
+                    continue;
+                }
+                int64_t a = R.l, b = R.m + 1;
+                for (int64_t u = task0[(size_t)T.node]; u < t; u++) {
+                    const uint32_t c = lefts[(size_t)u * 6 + k];
+                    a += c;
+                    b += (tasks[(size_t)u].p1 - tasks[(size_t)u].p0) - c;
+                }
+                for (int64_t p = T.p0; p < T.p1; p++) {
+                    const uint32_t e = L[p];
+                    O[in_left[e] ? a++ : b++] = e;
+                }
+            }
+        });
+        for (int k = 0; k < 6; k++) list[k].swap(other[k]);
+        // children (TD/Trixel.h:329-352), s1 / s2 (:353-376)
+        pool.run((cnt + 4095) / 4096, [&](int64_t blk) {
+            for (int64_t i = blk * 4096; i < std::min(cnt, (blk + 1) * 4096); i++) {
+                const int64_t id = lv0 + i;
+                const Range R = rng[(size_t)id];
+                if (R.r == R.l) continue;
+                rt_kd_node& nd = nodes[id];
+                const int64_t cb = child_base[(size_t)i];
+                nd.left = cb; nd.right = cb + 1;
+                for (int br = 0; br < 2; br++) {
+                    rt_kd_node& c = nodes[cb + br];
+                    c.parent = id;
+                    c.is_leaf = 0;
+                    c.tri_index = -1;
+                    int64_t nl = br == 0 ? R.l : R.m + 1, nr = br == 0 ? R.m : R.r;
+                    rng[(size_t)(cb + br)] = {nl, ((nr - nl) / 2) + nl, nr};
+                    c.x1 = key_at(0, nr); c.x0 = key_at(3, nl);
+                    c.y1 = key_at(1, nr); c.y0 = key_at(4, nl);
+                    c.z1 = key_at(2, nr); c.z0 = key_at(5, nl);
+                }
+                const rt_kd_node& Lc = nodes[cb];
+                const rt_kd_node& Rc = nodes[cb + 1];
+                switch (nd.cut_flag) {
+                case 0: case 3: nd.s2 = Rc.x0; nd.s1 = Lc.x1; break;
+                case 1: case 4: nd.s2 = Rc.y0; nd.s1 = Lc.y1; break;
+                default:        nd.s2 = Rc.z0; nd.s1 = Lc.z1; break;
+                }
+            }
+        });
         lv0 = lv1;
         lv1 = wr;
     }

@@ -146,12 +146,7 @@ class NativeFrameGather:
         rect = self.frame_rect(cam, xform, mode)
         opts = tuple(cam.get_option(k) for k in (_lib.RT_OPT_KERNEL, _lib.RT_OPT_RAYS, _lib.RT_OPT_COARSE,
                                                  _lib.RT_OPT_DEBUG, _lib.RT_OPT_TILE_ORDER))
-        mine = (rect, opts, (self.w, self.h), int(mode))
-        every = [None] * self.world
-        self.dist.all_gather_object(every, mine)
-        if any(e != every[0] for e in every):
-            raise RuntimeError(f"NativeFrameGather: ranks disagree on the frame rectangle / camera options: {every}")
-        return rect
+        return verify_agreement(self.dist, self.world, "NativeFrameGather", rect, opts, (self.w, self.h), mode)
 
     def frame_rect(self, cam, xform, mode: int):
         """rt_frame_rect for this group's size: (x0, x1, b0, b1)."""
@@ -167,3 +162,108 @@ class NativeFrameGather:
         if self._h:
             _lib.lib().rt_comm_destroy(self._h)
             self._h = None
+
+
+def verify_agreement(dist, world: int, who: str, rect, opts, size, mode: int) -> tuple:
+    """All ranks exchange (rect, options, size, mode) over `dist` and raise
+    RuntimeError on every rank if any differs: message sizes are derived on
+    each rank, never exchanged, so a disagreement would otherwise hang or
+    truncate the point-to-point transfers."""
+    mine = (tuple(int(v) for v in rect), tuple(int(v) for v in opts), tuple(size), int(mode))
+    every = [None] * world
+    dist.all_gather_object(every, mine)
+    if any(e != every[0] for e in every):
+        raise RuntimeError(f"{who}: ranks disagree on the frame rectangle / camera options: {every}")
+    return mine[0]
+
+
+def frame_geometry(w: int, h: int, basis, root_box, root_is_leaf: bool = False, kernel: int = 3, rays: int = 0,
+                   coarse: int = 8, debug: int = 0):
+    """rt_frame_geometry from host-side inputs: `basis` the camera basis
+    (raytracer.camera_basis's dict, or an RtCameraBasis), `root_box` the root node's box minus the camera
+    position (x0, x1, y0, y1, z0, z1; float32 subtractions)."""
+    from . import _lib
+    get = (lambda k: basis[k]) if isinstance(basis, dict) else (lambda k: getattr(basis, k))  # noqa: E731
+    g = _lib.RtFrameGeometry()
+    g.w, g.h = w, h
+    for k in range(3):
+        g.n_mod[k], g.u_mod[k], g.v_mod[k] = get("n_mod")[k], get("u_mod")[k], get("v_mod")[k]
+    for k in range(6):
+        g.root_box[k] = float(root_box[k])
+    g.root_is_leaf = int(bool(root_is_leaf))
+    g.kernel, g.rays, g.coarse, g.debug = kernel, rays, coarse, debug
+    return g
+
+
+def frame_rect_host(geom, xform, mode: int, nranks: int) -> tuple:
+    """rt_frame_rect_host: (x0, x1, b0, b1), as rt_frame_rect derives it for a
+    camera with this geometry."""
+    import ctypes as C
+    from . import _lib
+    xf = None if xform is None else np.ascontiguousarray(xform, np.float32)
+    rect = np.zeros(4, np.int32)
+    _lib.call("rt_frame_rect_host", C.byref(geom), _lib.ptr(xf), mode, nranks, _lib.ptr(rect))
+    return tuple(int(v) for v in rect)
+
+
+class HostRectGather:
+    """The rectangle gather of rt_comm_gather_frame (csrc/comm.cpp) over host
+    buffers and any torch.distributed backend (gloo on CPU): every rank
+    derives the rectangle from the same geometry (rt_frame_rect_host, no
+    exchange); a peer packs its slots' rows inside it (rt_pack_rect_host) and
+    sends exactly rt_rect_pixels(w, h, N, rank, rect) u32 to rank 0; rank 0
+    receives the peers' parts in rank order 1..N-1, back to back, and
+    assembles the frame from its own packed buffer, those parts and the
+    background (rt_unpack_rect_host).  The same protocol as the RCCL path,
+    point to point, sizes derived rather than exchanged."""
+
+    def __init__(self, dist, w: int, h: int, geom, xform, mode: int, opts=()):
+        self.dist = dist
+        self.w, self.h = w, h
+        self.rank = dist.get_rank()
+        self.world = dist.get_world_size()
+        self.rect = frame_rect_host(geom, xform, mode, self.world)
+        self.opts = tuple(opts) or (geom.kernel, geom.rays, geom.coarse, geom.debug)
+        self.mode = mode
+
+    def verify(self) -> tuple:
+        return verify_agreement(self.dist, self.world, "HostRectGather", self.rect, self.opts, (self.w, self.h),
+                                self.mode)
+
+    def part_pixels(self, rank: int) -> int:
+        from . import _lib
+        r = np.ascontiguousarray(self.rect, np.int32)
+        n = int(_lib.lib().rt_rect_pixels(self.w, self.h, self.world, rank, _lib.ptr(r)))
+        if n < 0:
+            raise RuntimeError(f"rt_rect_pixels failed for rank {rank}")
+        return n
+
+    def gather(self, local: np.ndarray):
+        """local: this rank's packed band buffer (u32).  Returns the frame on
+        rank 0 (w*h u32), None elsewhere."""
+        import torch
+        from . import _lib
+        local = np.ascontiguousarray(local, np.uint32)
+        rect = np.ascontiguousarray(self.rect, np.int32)
+        if self.rank != 0:
+            n = self.part_pixels(self.rank)
+            if n == 0:
+                return None
+            out = np.zeros(n, np.uint32)
+            _lib.call("rt_pack_rect_host", self.w, self.h, self.world, self.rank, _lib.ptr(rect), _lib.ptr(local),
+                      _lib.ptr(out))
+            self.dist.send(torch.from_numpy(out.view(np.int32)), dst=0)
+            return None
+        sizes = [self.part_pixels(p) for p in range(1, self.world)]
+        peers = np.zeros(max(1, sum(sizes)), np.uint32)
+        off = 0
+        for p, n in zip(range(1, self.world), sizes):
+            if n > 0:
+                buf = torch.zeros(n, dtype=torch.int32)
+                self.dist.recv(buf, src=p)
+                peers[off:off + n] = buf.numpy().view(np.uint32)
+            off += n
+        frame = np.zeros(self.w * self.h, np.uint32)
+        _lib.call("rt_unpack_rect_host", self.w, self.h, self.world, _lib.ptr(rect), _lib.ptr(local),
+                  _lib.ptr(peers), _lib.ptr(frame))
+        return frame

@@ -349,6 +349,19 @@ class Camera:
         _lib.call("rt_render_into", self._h, _lib.ptr(xf), mode, flags, t, a, h, s)
         return 0
 
+    def render_display(self, clean, display, hit=None, xform=None, mode=RT_MODE_KD, flags=0, tile=None,
+                       stream=None) -> int:
+        """rt_render_display: the frame the reference's window shows
+        (TD/WinMain.cpp:212-237, ghosting under motion).  `clean` (device,
+        zeros before the first frame) holds the previous clean frame and
+        receives this one; `display` receives the displayed frame."""
+        xf = np.ascontiguousarray(xform if xform is not None else Quaternion().xform(), np.float32)
+        t = None if tile is None else C.byref(_lib.RtTile(tile[0], tile[1]))
+        s = C.c_void_p(stream) if isinstance(stream, int) else C.c_void_p(None)
+        _lib.call("rt_render_display", self._h, _lib.ptr(xf), mode, flags, t, _lib.ptr(clean), _lib.ptr(display),
+                  _lib.ptr(hit), s)
+        return 0
+
     def color_pixels(self, color_tag_select: int = PHONG_COLOR_TAG) -> int:
         """Camera::color_pixels (TD/Camera.cpp:229): the frame D2H into h_color.
 

@@ -188,6 +188,21 @@ int rt_render(rt_camera* c, const float* xform, uint32_t mode, uint32_t flags,
 int rt_render_into(rt_camera* c, const float* xform, uint32_t mode, uint32_t flags,
                    const rt_tile* tile, uint32_t* d_argb, int64_t* d_hit, void* stream);
 
+/* The frame the reference's window shows (TD/WinMain.cpp:212-237), ghosting
+ * included.  The window's buffer persists: color_pixels(PHONG) overwrites
+ * only the pixels whose ray hit (color_cam_cuda tests rmi >= 0,
+ * TD/Camera.cu:27-61) before the blit, and color_pixels(SET) resets it to the
+ * background and, through the missing `break`, this frame's Phong again
+ * (TD/Camera.cu:77-84).  So the displayed frame k is the clean frame k-1
+ * (background + Phong) overwritten by frame k's Phong on frame k's hits, and
+ * frame 0 shows 0x00000000 where it misses (init_cam_mem_cuda zeroes the
+ * buffer, TD/Camera.cu:98).  d_clean holds the previous clean frame on entry
+ * (all zeros before the first frame) and this frame's on exit (what
+ * rt_render_into writes); d_display receives the displayed frame.  One
+ * traversal per frame; the two buffers must be distinct. */
+int rt_render_display(rt_camera* c, const float* xform, uint32_t mode, uint32_t flags, const rt_tile* tile,
+                      uint32_t* d_clean, uint32_t* d_display, int64_t* d_hit, void* stream);
+
 /* Pixels in one rank's packed buffer (uniform across ranks). */
 int64_t rt_tile_packed_pixels(int32_t w, int32_t h, int32_t nranks);
 
@@ -240,6 +255,30 @@ int rt_pack_rect(int device, int32_t w, int32_t h, int32_t nranks, int32_t rank,
  * bands are in the frame already (RT_FLAG_FRAME_OUT) and are not written. */
 int rt_unpack_rect(int device, int32_t w, int32_t h, int32_t nranks, const int32_t rect[4],
                    const uint32_t* d_local0, const uint32_t* d_peers, uint32_t* d_frame, void* stream);
+/* The frame rectangle without a device camera (no reference counterpart: the
+ * reference is single-GPU).  rt_frame_geometry holds everything
+ * rt_frame_rect derives it from: the camera basis (rt_camera_basis), the
+ * root node's box minus the camera position (float subtraction, as
+ * init_cam_voxel_mem_cuda does, TD/Camera.cu:142-147), whether the root is a
+ * leaf, and the kernel-3 options that shape the tiling (RT_OPT_KERNEL,
+ * RT_OPT_RAYS, RT_OPT_COARSE, RT_OPT_DEBUG).  rt_frame_rect_host(g, ...)
+ * equals rt_frame_rect(cam, ...) whenever rt_camera_frame_geometry(cam, g)
+ * filled g, so every rank (any process, no GPU needed) derives the same
+ * message sizes.  rt_pack_rect_host / rt_unpack_rect_host: rt_pack_rect /
+ * rt_unpack_rect on host buffers (local0 distinct from frame). */
+typedef struct rt_frame_geometry {
+    int32_t w, h;
+    float n_mod[3], u_mod[3], v_mod[3];
+    float root_box[6];      /* x0, x1, y0, y1, z0, z1 relative to the camera */
+    int32_t root_is_leaf;
+    int32_t kernel, rays, coarse, debug;
+} rt_frame_geometry;
+int rt_camera_frame_geometry(rt_camera* cam, rt_frame_geometry* out);
+int rt_frame_rect_host(const rt_frame_geometry* g, const float* xform, uint32_t mode, int32_t nranks, int32_t rect[4]);
+int rt_pack_rect_host(int32_t w, int32_t h, int32_t nranks, int32_t rank, const int32_t rect[4],
+                      const uint32_t* local, uint32_t* out);
+int rt_unpack_rect_host(int32_t w, int32_t h, int32_t nranks, const int32_t rect[4], const uint32_t* local0,
+                        const uint32_t* peers, uint32_t* frame);
 int rt_comm_info(const rt_comm* c, int32_t* nranks, int32_t* rank);
 void rt_comm_destroy(rt_comm* c);
 

@@ -75,6 +75,7 @@ def lib():
         L.orc_primary_ray.argtypes = [C.POINTER(OrcCamera), C.c_int32, C.c_int32, P]
         L.orc_phong.argtypes = [P, P, P, P]
         L.orc_phong.restype = C.c_uint32
+        L.orc_window_frame.argtypes = [P, P, P, C.c_int64, P]
         _lib = L
     return _lib
 
@@ -177,6 +178,22 @@ class Scene:
             self.close()
         except Exception:
             pass
+
+
+class Window:
+    """The reference's persistent window buffer (orc_window_frame): zero at
+    first (TD/Camera.cu:98); frame() returns what the window shows for one
+    frame's steady-state render (clean argb, hit)."""
+
+    def __init__(self, npix: int):
+        self.buf = np.zeros(npix, np.uint32)
+
+    def frame(self, clean: np.ndarray, hit: np.ndarray) -> np.ndarray:
+        clean = np.ascontiguousarray(clean, np.uint32)
+        hit = np.ascontiguousarray(hit, np.int64)
+        out = np.zeros_like(self.buf)
+        lib().orc_window_frame(_ptr(self.buf), _ptr(clean), _ptr(hit), len(self.buf), _ptr(out))
+        return out
 
 
 def default_rad(ntri: int) -> np.ndarray:

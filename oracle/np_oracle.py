@@ -349,3 +349,20 @@ def render(points9, nodes, cam, mode=0, xform=None, shadow=False):
                     if shadow and trace_shadow(S, rmi, d, ray):
                         argb[i] = 0
     return argb, hit
+
+
+def window_frames(frames, hits):
+    """The reference's window across frames (TD/WinMain.cpp:212-237), restated
+    independently of oracle.c's orc_window_frame: the buffer starts zeroed
+    (TD/Camera.cu:98); color_cam_cuda writes only rmi >= 0 pixels before the
+    blit (TD/Camera.cu:27-61); the SET pass leaves background + Phong
+    (TD/Camera.cu:77-84).  Returns the displayed frames."""
+    buf = np.zeros_like(np.asarray(frames[0], np.uint32))
+    out = []
+    for argb, hit in zip(frames, hits):
+        argb = np.asarray(argb, np.uint32)
+        hitm = np.asarray(hit) >= 0
+        buf = np.where(hitm, argb, buf)
+        out.append(buf.copy())
+        buf = np.where(hitm, argb, np.uint32(BG))
+    return out

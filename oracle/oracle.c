@@ -908,6 +908,26 @@ int orc_render_ex(const orc_scene* s, const float xform[12], int mode, int flags
     return status;
 }
 
+/* The reference's window buffer across frames (TD/WinMain.cpp:174-239).  The
+ * u32 buffer persists from frame to frame; init_cam_mem_cuda zeroes it
+ * (TD/Camera.cu:98).  Each frame after intersect:
+ *   color_pixels(PHONG_COLOR_TAG) -> color_cam_cuda writes only the pixels
+ *     whose rmi >= 0 (TD/Camera.cu:27-61, :81), D2H (:84), blit
+ *     (TD/WinMain.cpp:213-217): that is the displayed frame;
+ *   color_pixels(SET_COLOR_TAG) -> set_cam_cuda fills the background and,
+ *     the `break` missing, color_cam_cuda runs again (TD/Camera.cu:77-82):
+ *     the buffer is this frame's clean frame (background + Phong).
+ * `window` (npix, zero before the first frame) is that buffer; `clean` and
+ * `hit` are the frame's steady-state render (orc_render); `displayed`
+ * receives what the window shows. */
+void orc_window_frame(uint32_t* window, const uint32_t* clean, const int64_t* hit, int64_t npix,
+                      uint32_t* displayed) {
+    for (int64_t i = 0; i < npix; i++)
+        if (hit[i] >= 0) window[i] = clean[i];
+    memcpy(displayed, window, sizeof(uint32_t) * (size_t)npix);
+    for (int64_t i = 0; i < npix; i++) window[i] = hit[i] >= 0 ? clean[i] : ORC_BG;
+}
+
 /* Per-pixel pop counts (interior + leaf) of the KD traversal: a workload
  * profile for the kernels' load balance (not part of the reference). */
 int orc_pixel_visits(const orc_scene* s, const float xform[12], uint32_t* visits, int nthreads) {

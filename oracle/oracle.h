@@ -127,6 +127,12 @@ int orc_render_ex(const orc_scene* s, const float xform[12], int mode, int flags
 /* One primary ray (init_cam_mem_cuda, TD/Camera.cu:103-104). */
 void orc_primary_ray(const orc_camera* cam, int32_t ix, int32_t iy, float out[3]);
 
+/* The reference's persistent window buffer for one frame (oracle.c): the
+ * displayed frame (ghosting under motion) from `window` (zero before the
+ * first frame) and the frame's clean render; `window` becomes the clean frame. */
+void orc_window_frame(uint32_t* window, const uint32_t* clean, const int64_t* hit, int64_t npix,
+                      uint32_t* displayed);
+
 /* Per-pixel visit counts (interior + leaf pops) of the KD traversal. */
 int orc_pixel_visits(const orc_scene* s, const float xform[12], uint32_t* visits, int nthreads);
 

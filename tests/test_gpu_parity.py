@@ -776,6 +776,38 @@ def test_animated_key_sequence(kernel):
     assert max(hits) > 100
 
 
+@pytest.mark.parametrize("kernel", [2, 3])
+def test_animated_key_sequence_display(kernel):
+    """rt_render_display over a moving key sequence: the displayed frames
+    (the reference's window, ghosting included: TD/WinMain.cpp:212-237,
+    TD/Camera.cu:27-61,77-84,98) equal oracle.c's orc_window_frame
+    composition bit for bit, and the clean buffer is the oracle's frame."""
+    import torch
+    from oracle import _oracle as O
+    from tests.test_motion import GHOST_KEYS, ghost_sequence
+    w, h = 160, 90
+    frames, hits, poses = ghost_sequence(w=w, h=h)
+    s = H.GpuScene("rabbit_70k", w, h, kernel=kernel)
+    dev = torch.device("cuda:0")
+    clean = torch.zeros(w * h, dtype=torch.int32, device=dev)  # init_cam_mem_cuda's zeroed buffer
+    shown = torch.full((w * h,), -1, dtype=torch.int32, device=dev)
+    win = O.Window(w * h)
+    ghosts = 0
+    for k, keys in enumerate(GHOST_KEYS):
+        s.obj.key_tick(keys)
+        xf = s.obj.quat.xform()
+        assert (xf.view(np.uint32) == np.asarray(poses[k], np.float32).view(np.uint32)).all()
+        s.cam.render_display(clean, shown, xform=xf)
+        torch.cuda.synchronize()
+        want = win.frame(frames[k], hits[k])
+        got = shown.cpu().numpy().view(np.uint32)
+        assert (got == want).all(), (k, int((got != want).sum()))
+        assert (clean.cpu().numpy().view(np.uint32) == frames[k]).all(), k
+        if k:
+            ghosts += int(((hits[k - 1] >= 0) & (hits[k] < 0)).sum())
+    assert ghosts > 20
+
+
 def test_animated_shadow_frame():
     from cpp_cuda_raytracer_dev_amd import raytracer as R
     from oracle import motion as M
@@ -940,6 +972,66 @@ def test_rect_gather_single_gpu(scene, w, h, nranks, moved, direct):
     torch.cuda.synchronize()
     got = frame.cpu().numpy().view(np.uint32)
     assert (got == full).all(), int((got != full).sum())
+
+
+@pytest.mark.parametrize("scene,w,h,moved,rays,coarse", [("dragon", 1920, 1080, False, 0, 8),
+                                                         ("knot", 1920, 1080, False, 0, 8),
+                                                         ("rabbit_70k", 960, 540, False, 8, 4),
+                                                         ("dragon", 960, 540, True, 0, 8),
+                                                         ("rabbit_70k", 81, 45, False, 0, 8)])
+def test_frame_rect_host_equals_camera(scene, w, h, moved, rays, coarse):
+    """rt_frame_rect_host from the host-side inputs (the basis of
+    rt_camera_basis, the root box minus the camera position, the options: what
+    tests/test_distributed_gloo.py's ranks derive without a GPU) equals the
+    device camera's rt_frame_rect for every rank count; rt_camera_frame_geometry
+    reports the same inputs; the host pack / assembly equal the device ones."""
+    import ctypes as C
+    import torch
+    from cpp_cuda_raytracer_dev_amd import _lib, raytracer as R
+    from cpp_cuda_raytracer_dev_amd.distributed import frame_geometry, frame_rect_host
+    s = H.GpuScene(scene, w, h, rays=rays, coarse=coarse)
+    xf = np.array([1, 0, 0, 0.01, 0, 1, 0, 0, 0, 0, 1, 0.02], np.float32) if moved else None
+    g = _lib.RtFrameGeometry()
+    _lib.call("rt_camera_frame_geometry", s.cam._h, C.byref(g))
+    pos, la, up = (0.0, 0.1, -1.0), (0.0, 0.1, 0.0), (0.0, 1.0, 0.0)
+    basis = R.camera_basis(w, h, R.film_w(w, h), np.float32(.024), np.float32(.055), pos, la, up)
+    root = H.product_tree(scene)[0]
+    p = np.float32(pos)
+    box = [np.float32(root[k]) - p[i // 2] for i, k in enumerate(("x0", "x1", "y0", "y1", "z0", "z1"))]
+    hg = frame_geometry(w, h, basis, box, bool(root["is_leaf"]), kernel=3, rays=rays, coarse=coarse)
+    assert bytes(hg) == bytes(g)
+    for nranks in (1, 2, 3, 4, 8):
+        rect = np.zeros(4, np.int32)
+        _lib.call("rt_frame_rect", s.cam._h, _lib.ptr(xf), 0, nranks, _lib.ptr(rect))
+        assert frame_rect_host(hg, xf, 0, nranks) == tuple(int(v) for v in rect), nranks
+    # host and device pack / assembly of the same packed buffers
+    nranks = 4
+    rect = np.array(frame_rect_host(hg, xf, 0, nranks), np.int32)
+    npk = R.packed_pixels(w, h, nranks)
+    dev = torch.device("cuda:0")
+    locs = [torch.zeros(npk, dtype=torch.int32, device=dev) for _ in range(nranks)]
+    for r in range(nranks):
+        s.cam.render_into(locs[r], xform=xf, mode=0, tile=(nranks, r))
+    torch.cuda.synchronize()
+    counts = [int(_lib.lib().rt_rect_pixels(w, h, nranks, r, _lib.ptr(rect))) for r in range(nranks)]
+    hpeers = np.zeros(max(1, sum(counts[1:])), np.uint32)
+    off = 0
+    for r in range(1, nranks):
+        part = np.zeros(max(1, counts[r]), np.uint32)
+        loc = locs[r].cpu().numpy().view(np.uint32).copy()
+        _lib.call("rt_pack_rect_host", w, h, nranks, r, _lib.ptr(rect), _lib.ptr(loc), _lib.ptr(part))
+        dpart = torch.zeros(max(1, counts[r]), dtype=torch.int32, device=dev)
+        if counts[r]:
+            _lib.call("rt_pack_rect", 0, w, h, nranks, r, _lib.ptr(rect), _lib.ptr(locs[r]), _lib.ptr(dpart), None)
+        torch.cuda.synchronize()
+        assert (dpart.cpu().numpy().view(np.uint32)[:counts[r]] == part[:counts[r]]).all()
+        hpeers[off:off + counts[r]] = part[:counts[r]]
+        off += counts[r]
+    frame = np.zeros(w * h, np.uint32)
+    loc0 = locs[0].cpu().numpy().view(np.uint32).copy()
+    _lib.call("rt_unpack_rect_host", w, h, nranks, _lib.ptr(rect), _lib.ptr(loc0), _lib.ptr(hpeers), _lib.ptr(frame))
+    full, _, _ = s.render(0, xform=xf)
+    assert (frame == full).all(), int((frame != full).sum())
 
 
 @pytest.mark.parametrize("mode", [0, 1])

@@ -114,3 +114,54 @@ def test_errors_and_object_api():
     obj.motion = None
     with pytest.raises(_lib.RtError):
         obj.key_tick(R.KEY_W)
+
+
+# The reference's displayed frame under motion (ghosting): its window buffer
+# persists, color_cam_cuda overwrites only hit pixels before the blit and the
+# SET pass resets it to background + Phong afterwards (TD/WinMain.cpp:212-237,
+# TD/Camera.cu:27-61,77-84,98).  oracle.c's orc_window_frame and
+# np_oracle.window_frames restate it independently.
+
+GHOST_KEYS = [R.KEY_W | R.KEY_R, R.KEY_R, R.KEY_R | R.KEY_Q, R.KEY_T, R.KEY_R | R.KEY_W, R.KEY_E, R.KEY_S | R.KEY_T,
+              R.KEY_R]
+
+
+def ghost_sequence(name="rabbit_70k", w=160, h=90, keys=GHOST_KEYS):
+    """Clean frames, hits and poses of a key sequence (the oracle, one tick
+    before each frame, as TD/WinMain.cpp:186-213 orders them)."""
+    from oracle import np_oracle as N
+    from tests import helpers as H
+    cam = N.camera(w, h)
+    mo = M.Motion(cam["pos"], cam["n"], cam["u"])
+    frames, hits, poses = [], [], []
+    for k in keys:
+        mo.tick(k)
+        xf = mo.xform()
+        argb, hit, _ = H.oracle_render(name, w, h, 0, xform=xf)
+        frames.append(argb)
+        hits.append(hit)
+        poses.append(xf)
+    return frames, hits, poses
+
+
+def test_window_frames_c_and_numpy_agree_and_ghost():
+    from oracle import _oracle as O
+    from oracle import np_oracle as N
+    frames, hits, _ = ghost_sequence()
+    win = O.Window(len(frames[0]))
+    shown = [win.frame(f, h) for f, h in zip(frames, hits)]
+    ref = N.window_frames(frames, hits)
+    for k, (a, b) in enumerate(zip(shown, ref)):
+        assert (a == b).all(), k
+    # frame 0: misses show the zeroed buffer, hits Phong
+    h0 = hits[0] >= 0
+    assert (shown[0][~h0] == 0).all() and (shown[0][h0] == frames[0][h0]).all() and h0.sum() > 50
+    # later frames: every miss pixel shows the previous clean frame; the
+    # object moves, so some of those are last frame's Phong (ghosts)
+    ghosts = 0
+    for k in range(1, len(frames)):
+        hk = hits[k] >= 0
+        assert (shown[k][hk] == frames[k][hk]).all()
+        assert (shown[k][~hk] == frames[k - 1][~hk]).all()
+        ghosts += int(((hits[k - 1] >= 0) & ~hk).sum())
+    assert ghosts > 20

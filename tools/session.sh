@@ -1,0 +1,48 @@
+#!/bin/bash
+# One GPU session from a plan file (replaces round 2's one-off *_session.sh
+# scripts).  Each plan line is `<name> <timeout-s> <command...>`; `#` starts a
+# comment.  Every step runs under its own `timeout -k 10`, writes
+# gpurun_out/<tag>/<name>.log, and the session stops at the first step that
+# faults, aborts or times out (exit codes other than 0, 1 = test failures,
+# 3 = bench device error, 4 = bench frame check).  After the steps, every
+# bench JSON line is summarised.
+#   tools/session.sh <tag> <plan-file>
+# Plan shorthands:
+#   bench <args>            python bench.py <args>
+#   smoke                   __graft_entry__.smoke()
+#   pytest <args>           the GPU test suite (-m gpu -x, 120 s per test)
+#   variant <lib> <args>    bench.py against tools/variants/lib_<lib>.so
+#   pmc <dir> <ctrs> -- <cmd...>   one rocprofv3 --pmc pass (counters only)
+#   stats <dir> -- <cmd...>        rocprofv3 --kernel-trace --stats
+set -u
+TAG=$1; PLAN=$2
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd "$ROOT"
+export TMPDIR=/tmp
+while read -r name to rest; do
+    [ -z "${name:-}" ] && continue
+    case $name in \#*) continue ;; esac
+    set -- $rest
+    case $1 in
+    bench) shift; cmd=(python -u bench.py "$@") ;;
+    smoke) cmd=(python -u -c "import __graft_entry__ as g; g.smoke()") ;;
+    pytest) shift; cmd=(python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread "$@") ;;
+    variant) shift; lib=$1; shift; cmd=(python -u tools/bench_variant.py "tools/variants/lib_$lib.so" "$@") ;;
+    pmc) shift; d=$1; shift; ctrs=(); while [ "$1" != "--" ]; do ctrs+=("$1"); shift; done; shift
+         cmd=(rocprofv3 --pmc "${ctrs[@]}" --output-format csv -d "$OUT/$d" -o run -- "$@") ;;
+    stats) shift; d=$1; shift; [ "$1" = "--" ] && shift
+           cmd=(rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$d" -o run -- "$@") ;;
+    *) cmd=("$@") ;;
+    esac
+    echo "== $name ($to s): ${cmd[*]}"
+    t0=$(date +%s)
+    timeout -k 10 "$to" "${cmd[@]}" > "$OUT/$name.log" 2>&1 < /dev/null
+    rc=$?
+    echo "== $name exit $rc ($(( $(date +%s) - t0 )) s)"
+    tail -n 3 "$OUT/$name.log" | cut -c1-400
+    case $rc in 0|1|3|4) ;; *) echo "stopping: $name exited $rc"; break ;; esac
+done < "$PLAN"
+python3 tools/bench_summary.py "$OUT"/*.log 2>/dev/null
+echo "session $TAG done"
