@@ -506,6 +506,18 @@ def main():
                         stream=sptr)
         torch.cuda.synchronize(dev)
         cnt = cam.counters(reset=True)
+    root_passes = None
+    if a.mode == 0 and not masks:
+        # pixels whose root test passes (kernel 3's counting render with
+        # debug bit 32 stops after the root test: counter [4]); the others'
+        # root visits read no memory (the root box is a kernel argument), so
+        # the roofline also reports the algorithmic bytes without them
+        cam.set_option(_lib.RT_OPT_KERNEL, 3)
+        cam.set_option(_lib.RT_OPT_DEBUG, 32)
+        cam.render_into(scratch, mode=a.mode, flags=R.RT_FLAG_COUNT, tile=tile if multi else None, stream=sptr)
+        torch.cuda.synchronize(dev)
+        root_passes = int(cam.counters(reset=True)[4])
+        cam.set_option(_lib.RT_OPT_DEBUG, 0)
     cam.set_option(_lib.RT_OPT_KERNEL, a.kernel)
     cam.set_option(_lib.RT_OPT_RAYS, a.rays)
     cam.set_option(_lib.RT_OPT_ITEMS, a.items)
@@ -771,14 +783,29 @@ def main():
         achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
         tests = w * h * len(pts)  # flat list: every ray against every triangle
         tflops = FLOPS_PER_TEST * tests / (kern_ms * 1e-3) / 1e12
-        traffic = None
+        # counter-based figures of this configuration from the committed PMC
+        # passes (tools/pmc_plan.py; one frame in flight, the same kernel)
+        traffic, valu_util, pmc_key = None, None, None
         if os.path.exists(a.traffic_json):
             try:
                 tj = json.load(open(a.traffic_json))
-                key = f"{a.scene}_{w}x{h}_m{a.mode}_n{world}"
-                traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
+                key = (f"{a.scene}_{w}x{h}_m{a.mode}_n{world}" + ("_shadow" if a.shadow else "")
+                       + ("" if a.view == "default" else f"_{a.view}"))
+                ent = tj.get(key) or {}
+                traffic = ent.get("hbm_bytes_per_launch")
+                valu_util = ent.get("valu_issue_util")
+                pmc_key = key if ent else None
             except Exception:
-                traffic = None
+                traffic = valu_util = pmc_key = None
+        kern_s = kern_ms * 1e-3
+        util = {
+            "hbm_util": round(traffic / kern_s / (HBM_PEAK_GBS * 1e9), 4) if traffic else None,
+            "valu_issue_util": valu_util,
+            "util_source": (f"profiles/pmc_traffic.json[{pmc_key}]: HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, "
+                            "MI355X_MICROARCH.md) / this run's kernel time / 8 TB/s; SQ_INSTS_VALU x 2 cycles / "
+                            "(1,024 SIMDs x GRBM_GUI_ACTIVE / 8)") if pmc_key else
+                           "no committed PMC passes for this configuration",
+        }
         res = {
             "metric": METRIC,
             "value": round(fps, 2),
@@ -816,6 +843,7 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": round(tflops / VALU_PEAK_TFLOPS, 4),
                 "traffic": None,
+                **util,
                 "kernel": "k_trace_flat",
                 "kernel_form": cam.get_option(_lib.RT_OPT_FLAT),
                 "kernel_ms_avg": round(kern_ms, 5),
@@ -838,6 +866,10 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                **util,
+                **({"frac_excl_root_misses": round((bytes_per_launch - B_INT * (my_pix - root_passes)) / kern_s / 1e9
+                                                   / HBM_PEAK_GBS, 4),
+                    "root_pass_pixels": root_passes} if root_passes is not None and not multi else {}),
                 "kernel": {1: "k_trace_kd", 2: "k_trace_kd2", 3: "k_trace_kd3"}[a.kernel] if a.mode == 0
                           else "k_trace_flat",
                 "kernel_options": {"kernel": a.kernel, "tile_order": a.tile_order,

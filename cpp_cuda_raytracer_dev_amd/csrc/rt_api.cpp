@@ -57,11 +57,13 @@ struct rt_camera {
     int tile_order = 3;              // kOptTileOrder
     // kOptDebug (diagnostics): 1 skip traversal, 2 per-wave stamps, 4 every
     // group coarse, 8 coarse kernel on a side stream, 16 counted shadow walks
-    // stop at occluders, 64 order / cost buffers sized for the current grid only
+    // stop at occluders, 32 counting renders of kernel 3 stop after the root
+    // test, 64 order / cost buffers sized for the current grid only
     int debug = 0;
     int pool_cap = kPoolCapMax;      // kOptPoolCap
     unsigned long long* d_dbg = nullptr;
     int64_t dbg_cap = 0;             // in u64
+    int64_t istamp_off = 0;          // debug bit 128 (RT_ITER_STAMPS builds): stamps' offset in d_dbg, u64
     int32_t* d_order = nullptr;      // the current tile permutation (a slot's buffer)
     int64_t order_key[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
     // Tile permutations live in a ring of slots: a new fine grid (a moving
@@ -852,8 +854,16 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
     p.pool_cap = c->pool_cap;
     p.items = c->items;
     p.dbg = nullptr;
+#if RT_ITER_STAMPS
+    p.istamp = nullptr;
+#endif
     if (c->debug & 2) {
-        const int64_t need = ((int64_t)p.tiles_x * p.block_rows + p.coarse_blocks + p.fill_blocks) * 4 * 3;
+        int64_t need = ((int64_t)p.tiles_x * p.block_rows + p.coarse_blocks + p.fill_blocks) * 4 * 3;
+        c->istamp_off = need;
+#if RT_ITER_STAMPS
+        // debug bit 128: per-iteration stamps of every wave slot after the per-wave records
+        if (c->debug & 128) need += (need / 3) * 4 * kIterStamps;
+#endif
         if (c->dbg_cap < need) {
             dev_free(c->d_dbg);
             int rc = dev_alloc(&c->d_dbg, (size_t)need, "hipMalloc(dbg)");
@@ -861,6 +871,9 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
             c->dbg_cap = need;
         }
         p.dbg = c->d_dbg;
+#if RT_ITER_STAMPS
+        if (c->debug & 128) p.istamp = c->d_dbg + c->istamp_off;
+#endif
         int rc = hip_check(hipMemset(c->d_dbg, 0, sizeof(uint64_t) * (size_t)need), "memset dbg");
         if (rc) return rc;
     }
@@ -1793,6 +1806,7 @@ extern "C" int rt_camera_get_option(const rt_camera* c, int32_t key, int32_t* va
     case kOptFlat: *value = c->flat_variant; return RT_OK;
     case kOptRaysUsed: *value = c->last_rays; return RT_OK;
     case kOptDebug: *value = c->debug; return RT_OK;
+    case kOptStampOffset: *value = (int32_t)c->istamp_off; return RT_OK;
     case kOptShadowOrder: *value = c->shadow_order >= 0 ? c->shadow_order : c->any_best; return RT_OK;
     default: return fail(RT_ERR_INVALID, "rt_camera_get_option: unknown key %d", key);
     }

@@ -51,8 +51,11 @@ enum Option : int32_t {
     kOptRaysUsed = 8,   // get only: pixels per wave of the last kernel-3 render
     kOptDebug = 100,    // diagnostics: 1 = skip traversal, 2 = per-wave timestamps, 4 = every group
                         // coarse, 8 = coarse kernel on a side stream beside the fine one,
-                        // 16 = counted shadow walks stop at occluders (the timed walk's work)
+                        // 16 = counted shadow walks stop at occluders (the timed walk's work),
+                        // 32 = counting renders stop after the root test, 128 = per-iteration
+                        // stamps (RT_ITER_STAMPS builds, with 2)
     kOptPoolCap = 101,  // tests: shrink kernel 3's item pool (66..kPoolCap) to force its fallback
+    kOptStampOffset = 102,  // get only: offset (u64) of the per-iteration stamps in the debug buffer
 };
 constexpr int kPoolCapMax = 640;
 
@@ -140,7 +143,16 @@ struct TraceParams {
     // minima of the chunks, all ones between frames; and the chunk count
     unsigned long long* flat_key;
     int32_t flat_chunks;
+#if RT_ITER_STAMPS
+    // diagnostic builds (-DRT_ITER_STAMPS=1, debug bit 128): per-iteration
+    // shader-clock stamps of kernel 3's pool walk, kIterStamps iterations per
+    // unit, 4 u64 each (tools/diag_iters.py)
+    unsigned long long* istamp;
+#endif
 };
+#if RT_ITER_STAMPS
+constexpr int kIterStamps = 96;
+#endif
 
 }  // namespace rt
 

@@ -1077,8 +1077,14 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
                                           unsigned long long* s_key, uint32_t* s_tri, int n, int lane,
                                           uint32_t& iters, uint32_t& popped, uint32_t& n_int, uint32_t& n_leaf,
                                           uint32_t& n_acc,
-                                          uint32_t& n_desc) {
+                                          uint32_t& n_desc, unsigned long long* st = nullptr) {
     const int cap = min(P.pool_cap, kCap);
+#if RT_ITER_STAMPS
+    // diagnostics: the stamps read a value of each phase (readfirstlane), so
+    // they wait for it; the walk is slower with them, the split is the point
+#define RT_STAMP(v) (__builtin_amdgcn_sched_barrier(0), (void)__builtin_amdgcn_readfirstlane(v), \
+                     __builtin_amdgcn_s_memtime())
+#endif
     const int slack = P.tree_height + 1;
     constexpr bool kTwo = RT_MAX_ITEMS > 1;  // compile-time: one-item builds drop item 1's registers
     const int per = kTwo && P.items > 1 ? 128 : 64;
@@ -1091,6 +1097,10 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
         // (slack = height + 1, height <= 24), so the pool never overflows.
         int take = min(min(n, per), cap - slack - n);
         if (take < 1) take = 1;
+#if RT_ITER_STAMPS
+        const unsigned long long s0 = st ? __builtin_amdgcn_s_memtime() : 0ull;
+        const uint32_t it_no = iters;
+#endif
         iters++;
         popped += (uint32_t)take;
         const int base = n - take;
@@ -1110,12 +1120,18 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
             if (act1 && s_key[it1.w >> 26] == 0ull) act1 = false;
         }
         // both records in flight before either is consumed
+#if RT_ITER_STAMPS
+        const unsigned long long s1 = st ? RT_STAMP(it0.x ^ it1.x) : 0ull;
+#endif
         const float4* p0 = record_of(P, it0.x);
         const float4* p1 = record_of(P, it1.x);
         const float4 a0 = p0[0], a1 = p0[1], a2 = p0[2], a3 = p0[3];
         const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         const float4 b0 = kTwo ? p1[0] : z, b1 = kTwo ? p1[1] : z, b2 = kTwo ? p1[2] : z, b3 = kTwo ? p1[3] : z;
         RT_RECORD_FENCE(a0, a1, a2, a3, b0, b1, b2, b3);
+#if RT_ITER_STAMPS
+        const unsigned long long s2 = st ? RT_STAMP(__float_as_uint(a3.w) ^ __float_as_uint(b3.w)) : 0ull;
+#endif
 #if RT_SEQ_PUSH
         // item 0 is visited, recorded and pushed before item 1 is visited, so
         // its results die before item 1's are made (fewer live VGPRs)
@@ -1129,6 +1145,9 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
             record_candidate<kAny>(s_key, s_tri, it0, v0);
             total += push_children<kAny, (kOrder & 3)>(items, base + total, v0);
         }
+#if RT_ITER_STAMPS
+        const unsigned long long s3 = st ? RT_STAMP(total) : 0ull;
+#endif
         {
             Visit v1;
             v1.ka = v1.kb = false; v1.cand = false;
@@ -1142,6 +1161,16 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
             if (lane == 0) atomicOr(P.err, 2);
             break;
         }
+#if RT_ITER_STAMPS
+        if (st && lane == 0 && it_no < (uint32_t)kIterStamps) {
+            const unsigned long long s4 = RT_STAMP(total);
+            unsigned long long* q = st + 4 * (size_t)it_no;
+            q[0] = s0;
+            q[1] = (s1 - s0) | ((s2 - s1) << 32);
+            q[2] = (s3 - s2) | ((s4 - s3) << 32);
+            q[3] = (unsigned long long)(uint32_t)take | ((unsigned long long)(uint32_t)n << 32);
+        }
+#endif
 #else
         Visit v0, v1;  // children / key fields are read only where nk / cand say so
         v0.ka = v0.kb = false; v0.cand = false;
@@ -1339,13 +1368,22 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
             S_.tri[lane] = kMiss;
         }
         n = seed_root<kCount>(P, items, R0, live, lane, C.n_int, C.n_desc);
+        // diagnostics (debug bit 32, counting renders): stop after the root
+        // test, so counter [4] is the number of pixels whose root test passes
+        // (bench.py's roofline without the root-miss visits)
+        if (kCount && (P.debug & 32)) n = 0;
     }
     if (RT_SPLIT_LEAF && P.items > 1)
         pool_walk_split<kCap, RL::kStride, kTranslated, kCount, false>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters,
                                                                   popped, C.n_int, C.n_leaf, C.n_acc, C.n_desc);
     else
         pool_walk<kCap, RL::kStride, kTranslated, kCount, false>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters, popped,
-                                                            C.n_int, C.n_leaf, C.n_acc, C.n_desc);
+                                                            C.n_int, C.n_leaf, C.n_acc, C.n_desc
+#if RT_ITER_STAMPS
+                                                            , (P.istamp && dbg_slot != kNoDbg)
+                                                                  ? P.istamp + 4 * (size_t)kIterStamps * dbg_slot : nullptr
+#endif
+        );
     float cam[3];
     Ray R;
     {
