@@ -16,6 +16,24 @@
 
 using namespace rt;
 
+// A moving object's screen rectangle changes every frame, so its fine grid
+// did too: every frame got a new tile order slot, and the cost order (tile
+// order 3) never applied (its samples were always of a stale grid).  Renders
+// of a transformed object (an identity transform keeps its exact region:
+// nothing moves, and the margin would turn fused far groups into fine tiles)
+// keep the fine region the camera last chose while the exact one stays
+// inside it and covers at least half of it; a new region is chosen with a
+// margin of 1/8 of its size (at least 2 tile columns and 1 band slot) on
+// every side.  Any region that contains the exact one renders the same frame
+// (a fine tile runs the exact root test; the far groups outside it are the
+// same proof, set_fine_region).  rt_frame_rect derives the gather rectangle
+// without it (every rank alone, no state).  Debug bit 256: off.
+struct Hold {
+    bool valid = false;
+    int32_t key[6] = {0, 0, 0, 0, 0, 0};  // tile_w, tile_h, nranks, rank, groups_x, nslots
+    int32_t tx0 = 0, tx1 = -1, s0 = 0, s1 = -1;
+};
+
 struct rt_scene {
     int device = 0;
     uint32_t ntri = 0;
@@ -64,6 +82,7 @@ struct rt_camera {
     unsigned long long* d_dbg = nullptr;
     int64_t dbg_cap = 0;             // in u64
     int64_t istamp_off = 0;          // debug bit 128 (RT_ITER_STAMPS builds): stamps' offset in d_dbg, u64
+    Hold hold;                       // the fine region renders keep (set_fine_region)
     int32_t* d_order = nullptr;      // the current tile permutation (a slot's buffer)
     int64_t order_key[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
     // Tile permutations live in a ring of slots: a new fine grid (a moving
@@ -593,6 +612,9 @@ struct FrameGeom {
     // groups holding a pixel with a tiny ray component (find_tiny_groups):
     // the camera's cached list, or computed by the caller
     const std::vector<std::pair<int32_t, int32_t>>* tiny = nullptr;
+    // renders only (fill_params): the fine region the camera holds for this
+    // tiling (set_fine_region), or null for the exact region
+    Hold* hold = nullptr;
 };
 
 bool root_rect(const FrameGeom& g, const TraceParams& p, double r[4]) {
@@ -713,6 +735,23 @@ bool set_fine_region(const FrameGeom& c, TraceParams& p, int per_wave, bool fuse
     }
     if (tx1 < tx0 || s1 < s0) {  // nothing of the box on this rank: all coarse
         tx0 = 0; tx1 = -1; s0 = 0; s1 = -1;
+    } else if (c.hold && !p.plain_xf && !(c.debug & (4 | 256))) {
+        Hold& H = *c.hold;
+        const int32_t key[6] = {p.tile_w, p.tile_h, p.nranks, p.rank, p.groups_x, p.nslots};
+        const int64_t area = (int64_t)(tx1 - tx0 + 1) * (s1 - s0 + 1);
+        const int64_t held = (int64_t)(H.tx1 - H.tx0 + 1) * (H.s1 - H.s0 + 1);
+        if (H.valid && std::equal(key, key + 6, H.key) && tx0 >= H.tx0 && tx1 <= H.tx1 && s0 >= H.s0 &&
+            s1 <= H.s1 && 2 * area >= held) {
+            tx0 = H.tx0; tx1 = H.tx1; s0 = H.s0; s1 = H.s1;
+        } else {
+            const int32_t ntx = (c.w + p.tile_w - 1) / p.tile_w;
+            const int32_t mx = std::max(2, (tx1 - tx0 + 1) / 8), ms = std::max(1, (s1 - s0 + 1) / 8);
+            tx0 = std::max(0, tx0 - mx); tx1 = std::min(ntx - 1, tx1 + mx);
+            s0 = std::max(0, s0 - ms); s1 = std::min(p.nslots - 1, s1 + ms);
+            H.valid = true;
+            std::copy(key, key + 6, H.key);
+            H.tx0 = tx0; H.tx1 = tx1; H.s0 = s0; H.s1 = s1;
+        }
     }
     p.fine_tx0 = tx0;
     p.fine_s0 = s0;
@@ -827,7 +866,9 @@ FrameGeom camera_geom(rt_camera* c) {
 }
 
 bool frame_geometry(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t mode, TraceParams& p) {
-    return frame_geometry(camera_geom(c), xform, tile, mode, p);
+    FrameGeom g = camera_geom(c);
+    g.hold = &c->hold;  // renders keep a held fine region (rt_frame_rect does not)
+    return frame_geometry(g, xform, tile, mode, p);
 }
 
 int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t* argb, int64_t* hit,

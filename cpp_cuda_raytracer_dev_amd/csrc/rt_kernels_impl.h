@@ -1351,7 +1351,7 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
     using RL = RayLayout<kRays>;
     uint4* items = S_.items;
     Pixel px;
-    const bool live = unit_pixel(P, U, kRays / 8, lane, px);  // every lane stays for the ballots
+    bool live = unit_pixel(P, U, kRays / 8, lane, px);  // every lane stays for the ballots
     const unsigned long long t_start = P.dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
     uint32_t iters = 0, popped = 0;
 
@@ -1387,12 +1387,13 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
     float cam[3];
     Ray R;
     {
-        // the pixel coordinates pass an empty asm, so the compiler recomputes
-        // the ray rather than keeping the first computation's partial
-        // products live (and spilled) across the walk
-        Pixel pr = px;
-        asm volatile("" : "+v"(pr.x), "+v"(pr.y));
-        camera_ray(P, pr, live, cam, R);
+        // the pixel is recomputed from the lane index behind an empty asm, so
+        // neither the first ray's partial products nor the pixel's output
+        // index stay live (and spilled) across the walk
+        int32_t l2 = lane;
+        asm volatile("" : "+v"(l2));
+        live = unit_pixel(P, U, kRays / 8, l2, px);
+        camera_ray(P, px, live, cam, R);
     }
     const float* X = P.xf;
     unsigned long long kbest = ~0ull;

@@ -48,4 +48,9 @@ while read -r name to rest; do
     case $rc in 0|1|3|4) ;; *) echo "stopping: $name exited $rc"; break ;; esac
 done < "$PLAN"
 python3 tools/bench_summary.py "$OUT"/*.log 2>/dev/null
+# gpurun copies gpurun_out/ back only below 64 MiB: drop the per-dispatch
+# kernel traces (the stats CSVs stay) and compress the counter CSVs
+find "$OUT" -name '*_kernel_trace.csv' -delete 2>/dev/null
+find "$OUT" -name '*_counter_collection.csv' -size +1M -exec gzip -f {} \; 2>/dev/null
+du -sh "$OUT" 2>/dev/null
 echo "session $TAG done"
