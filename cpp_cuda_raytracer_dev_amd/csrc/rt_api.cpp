@@ -138,6 +138,7 @@ struct rt_camera {
     int frames_since = 0;
     uint64_t layout_gen = 0, cost_gen = 0;   // fine-grid generation, and the one h_cost was read for
     uint64_t order_gen = ~0ull;              // generation whose cost order d_order holds
+    int32_t order_split = 0;                 // split tiles at the head of that cost order
     int rays = 0;                    // kOptRays: pixels per wave of kernel 3 (0: auto_rays)
     int last_rays = 0;               // the pixels per wave the last kernel-3 render used
     int items = 2;                   // kOptItems: items per lane per pool iteration
@@ -381,6 +382,7 @@ int ensure_order(rt_camera* c, const TraceParams& p, hipStream_t st) {
     c->ocur = sl;
     c->d_order = o.d;
     c->order_gen = ~0ull;  // no cost order for this grid yet
+    c->order_split = 0;    // nor split tiles
     std::copy(key, key + 8, c->order_key);
     c->centre.swap(order);
     c->layout_gen++;
@@ -551,6 +553,22 @@ int cost_feedback(rt_camera* c, const TraceParams& p, void* stream, int set) {
             same = same && c->h_order[k] == ord[(size_t)k];
             c->h_order[k] = ord[(size_t)k];
         }
+        // Split tiles (order 3, 16-ray units): the tiles costlier than half
+        // the heaviest render as two 8-ray halves, so the heaviest chains
+        // end near the unsplit ones' (a unit's chain is mostly its items:
+        // half the rays, about half the pool iterations); at most a quarter
+        // of the tiles.  Debug bit 512: none.
+        int32_t split = 0;
+        if (c->tile_order == 3 && p.rays == 16 && kd3_waves(16) == 4 && !(c->debug & 512) && n > 0) {
+            auto cost_of = [&](int64_t t) {
+                uint32_t m = 0;
+                for (int k = 0; k < kCostSlots; k++) m = std::max(m, c->h_cost[kCostSlots * (size_t)t + k]);
+                return m;
+            };
+            const uint32_t top = cost_of(ord[0]);
+            while (split < n / 4 && 2 * cost_of(ord[(size_t)split]) > top && top >= 24) split++;
+        }
+        same = same && split == c->order_split;
         if (same && c->order_gen == c->layout_gen) return RT_OK;  // d_order already holds it
         int rc;
         // frames on other streams (frames in flight on the library's lanes,
@@ -574,6 +592,7 @@ int cost_feedback(rt_camera* c, const TraceParams& p, void* stream, int set) {
         c->cost_up_stream = st;
         c->cost_up_valid = true;
         c->order_pending = true;
+        c->order_split = split;  // launches after this upload (stream order) use it
         c->order_gen = c->layout_gen;
         return RT_OK;
     }
@@ -891,6 +910,7 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
     p.tree_height = s->height;
     p.tile_order = c->tile_order;
     p.order = nullptr;
+    p.split = 0;
     p.debug = c->debug;
     p.pool_cap = c->pool_cap;
     p.items = c->items;
@@ -899,7 +919,8 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
     p.istamp = nullptr;
 #endif
     if (c->debug & 2) {
-        int64_t need = ((int64_t)p.tiles_x * p.block_rows + p.coarse_blocks + p.fill_blocks) * 4 * 3;
+        // (fine tiles twice: split tiles add a block each)
+        int64_t need = (2 * (int64_t)p.tiles_x * p.block_rows + p.coarse_blocks + p.fill_blocks) * 4 * 3;
         c->istamp_off = need;
 #if RT_ITER_STAMPS
         // debug bit 128: per-iteration stamps of every wave slot after the per-wave records
@@ -1422,6 +1443,9 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
         if (hipEventQuery(c->order_ev) == hipSuccess) c->cost_up_valid = false;
         else if ((rc = hip_check(hipStreamWaitEvent(st, c->order_ev, 0), "cost order wait"))) return rc;
     }
+    // split tiles of the cost order in d_order (launches are stream-ordered
+    // behind its upload; other streams wait for it above)
+    p.split = (p.order && p.order == c->d_order && p.cost && p.rays == 16 && !(c->debug & 512)) ? c->order_split : 0;
     int cset = 0;
     if (p.cost) {  // this stream's own cost set
         cset = cost_set(c, st);
@@ -1848,6 +1872,7 @@ extern "C" int rt_camera_get_option(const rt_camera* c, int32_t key, int32_t* va
     case kOptRaysUsed: *value = c->last_rays; return RT_OK;
     case kOptDebug: *value = c->debug; return RT_OK;
     case kOptStampOffset: *value = (int32_t)c->istamp_off; return RT_OK;
+    case kOptSplitUsed: *value = c->order_split; return RT_OK;
     case kOptShadowOrder: *value = c->shadow_order >= 0 ? c->shadow_order : c->any_best; return RT_OK;
     default: return fail(RT_ERR_INVALID, "rt_camera_get_option: unknown key %d", key);
     }

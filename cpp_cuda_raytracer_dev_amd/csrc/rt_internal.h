@@ -49,6 +49,7 @@ enum Option : int32_t {
     kOptShadowOrder = 6,  // kernel 3 any-hit push order 0..3, -1 = timed choice (default)
     kOptFlat = 7,       // flat-list kernel: 0 one triangle per iteration, 1 pairs, 2 packed pairs, 3 pipelined
     kOptRaysUsed = 8,   // get only: pixels per wave of the last kernel-3 render
+    kOptSplitUsed = 9,  // get only: split tiles at the head of the current cost order (kernel 3, 16 rays)
     kOptDebug = 100,    // diagnostics: 1 = skip traversal, 2 = per-wave timestamps, 4 = every group
                         // coarse, 8 = coarse kernel on a side stream beside the fine one,
                         // 16 = counted shadow walks stop at occluders (the timed walk's work),
@@ -128,6 +129,7 @@ struct TraceParams {
     int32_t rays;                  // pixels (rays) per wave: 64, 32 or 16
     int32_t tile_order;            // Option kOptTileOrder
     const int32_t* order;          // tile permutation (tile_order 2: centre-out, 3: by cost)
+    int32_t split;                 // kernel 3, 16 rays: order[0..split) render as two 8-ray halves
     uint32_t* cost;                // tile_order 3: pool iterations per fine unit [tile][2], or null
     float root_box[6];             // camera-relative root AABB (t0x,t1x,t0y,t1y,t0z,t1z)
     int32_t pool_cap;              // kernel 3 item-pool capacity in use (<= kPoolCap)

@@ -161,6 +161,18 @@ __device__ __forceinline__ bool unit_pixel(const TraceParams& P, const Unit& u, 
     return lane < rows * 8 && px.x < P.w && px.y < P.h;
 }
 
+// Sub-tile `wave` of the fine tile with index t (in the fine grid).
+__device__ __forceinline__ Unit unit_of_tile(const TraceParams& P, int32_t t, int32_t wave) {
+    int32_t row = t / P.tiles_x;
+    const int32_t tx = t - row * P.tiles_x + P.fine_tx0;
+    row += P.fine_s0 * (kTileH / P.tile_h);
+    const int32_t per_band = kTileH / P.tile_h;
+    const int32_t slot = row / per_band, yin = (row - slot * per_band) * P.tile_h;
+    const int32_t wrows = P.rays >> 3;
+    const int32_t wx = P.tile_w > 8 ? wave * 8 : 0, wy = P.tile_w > 8 ? 0 : wave * wrows;
+    return Unit{tx * P.tile_w + wx, slot, yin + wy};
+}
+
 // Sub-tile `wave` of fine tile b.
 __device__ __forceinline__ Unit unit_of(const TraceParams& P, int32_t b, int32_t wave) {
     int32_t tx, row;
@@ -1347,11 +1359,12 @@ constexpr size_t kNoDbg = ~(size_t)0;
 constexpr int kCoarseMax = 32;  // coarse groups per wave (RT_OPT_COARSE <= 32)
 template <int kRays, int kCap, int kRayVec, bool kTranslated, bool kWriteHit, bool kCount, int kShadow>
 __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, kCap, kRayVec>& S_, const Unit& U,
-                                           int lane, size_t dbg_slot, uint32_t* cost, Counts& C) {
+                                           int lane, size_t dbg_slot, uint32_t* cost, Counts& C,
+                                           int32_t nrows = kRays / 8) {
     using RL = RayLayout<kRays>;
     uint4* items = S_.items;
     Pixel px;
-    bool live = unit_pixel(P, U, kRays / 8, lane, px);  // every lane stays for the ballots
+    bool live = unit_pixel(P, U, nrows, lane, px);  // every lane stays for the ballots
     const unsigned long long t_start = P.dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
     uint32_t iters = 0, popped = 0;
 
@@ -1392,7 +1405,7 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
         // index stay live (and spilled) across the walk
         int32_t l2 = lane;
         asm volatile("" : "+v"(l2));
-        live = unit_pixel(P, U, kRays / 8, l2, px);
+        live = unit_pixel(P, U, nrows, l2, px);
         camera_ray(P, px, live, cam, R);
     }
     const float* X = P.xf;
@@ -1440,7 +1453,9 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
         P.dbg[3 * dbg_slot + 1] = __builtin_amdgcn_s_memrealtime();
         P.dbg[3 * dbg_slot + 2] = iters | ((unsigned long long)popped << 32);
     }
-    if (cost && lane == 0) *cost = iters;  // tile order 3: this unit's pool iterations
+    // tile order 3: this unit's pool iterations (a split unit of half the
+    // rows reports twice its own: the tile's cost as a whole-tile unit, about)
+    if (cost && lane == 0) *cost = iters * (uint32_t)((kRays / 8) / nrows);
     __builtin_amdgcn_wave_barrier();  // LDS of this unit is read; the next unit may overwrite it
     if (!live) return;
     uint32_t argb = kBackground;
@@ -1662,10 +1677,11 @@ __global__ RT_KD3_BOUNDS(64 * kd3_waves(kRays)) void k_trace_kd3(TraceParams P) 
     const int wv = wave_id(), lane = (int)threadIdx.x & 63;
     Counts C;
     const int32_t b = (int32_t)blockIdx.x;
-    if (b >= P.tiles_x * P.block_rows) {
+    const int32_t ntiles = P.tiles_x * P.block_rows;
+    if (b >= ntiles + P.split) {
         // fused far fill: blocks after the fine tiles write the coarse groups,
         // all far by construction (set_fine_region); unrolled as in k_coarse_kd3
-        const int32_t j0 = ((b - P.tiles_x * P.block_rows) * kWaves + wv) * P.coarse_per_wave;
+        const int32_t j0 = ((b - ntiles - P.split) * kWaves + wv) * P.coarse_per_wave;
         const int32_t j1 = min(j0 + P.coarse_per_wave, (int32_t)P.coarse_groups);
         bool ok = true;
 #pragma unroll 8
@@ -1677,14 +1693,22 @@ __global__ RT_KD3_BOUNDS(64 * kd3_waves(kRays)) void k_trace_kd3(TraceParams P) 
         if (kCount) count_flush(P, C);
         return;
     }
-    const int32_t ti = tile_index(P, b);
-    if ((uint32_t)ti >= (uint32_t)(P.tiles_x * P.block_rows)) {  // a stale order: never index past the grid
+    // Split tiles (tile order 3, 16-ray units; the host names the heaviest
+    // P.split tiles of its cost order, order[0..split)): blocks 2k and 2k + 1
+    // render the halves of tile order[k] with one 8-pixel row per wave, which
+    // halves the heaviest units' pool chains; the other tiles follow.
+    const bool split = b < 2 * P.split;
+    const int32_t ti = split ? P.order[b >> 1] : tile_index(P, b - P.split);
+    if ((uint32_t)ti >= (uint32_t)ntiles) {  // a stale order: never index past the grid
         if (lane == 0) atomicOr(P.err, 8);
         return;
     }
     uint32_t* cost = P.cost ? P.cost + kCostSlots * (size_t)ti + wv : nullptr;
-    trace_unit<kRays, kCap, kRayVec, kTranslated, kWriteHit, kCount, kShadow>(P, s_lds[wv], unit_of(P, b, wv), lane,
-                                                                             (size_t)b * kWaves + wv, cost, C);
+    Unit U = unit_of_tile(P, ti, wv);
+    if (split) U.yin = (U.yin - wv * (kRays / 8)) + (b & 1) * kWaves + wv;
+    trace_unit<kRays, kCap, kRayVec, kTranslated, kWriteHit, kCount, kShadow>(P, s_lds[wv], U, lane,
+                                                                             (size_t)b * kWaves + wv, cost, C,
+                                                                             split ? 1 : kRays / 8);
     if (kCount) count_flush(P, C);
 }
 

@@ -391,6 +391,10 @@ int rt_camera_info(const rt_camera* c, int32_t* w, int32_t* h, int32_t* max_dept
  * counting renders take 9). */
 #define RT_OPT_FLAT 7
 #define RT_OPT_RAYS_USED 8 /* get only: the pixels per wave the last kernel-3 render used */
+/* get only: tiles of the current cost order (tile order 3, 16-ray units)
+ * rendered as two 8-ray halves: those costlier than half the heaviest tile,
+ * at most a quarter of the tiles; the frame is the same either way. */
+#define RT_OPT_SPLIT_USED 9
 int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value);
 int rt_camera_get_option(const rt_camera* c, int32_t key, int32_t* value);
 

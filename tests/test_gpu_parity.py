@@ -326,6 +326,37 @@ def test_full_frame_vs_oracle_hash(key):
         _counters_match(cnt, ent["counters"], 3)
 
 
+@pytest.mark.parametrize("key,rays", [("dragon_1920x1080_m0", 0), ("knot_1920x1080_m0", 0), ("knot_960x540_m0", 16),
+                                      ("dragon_1920x1080_m0_shadow", 0)])
+def test_split_tiles_same_frame(key, rays):
+    """Tile order 3 splits the heaviest 16-ray tiles into two 8-ray halves
+    once a cost sample has arrived (RT_OPT_SPLIT_USED > 0): the frame and hit
+    buffer stay the oracle's (committed hashes), with and without shadows."""
+    import hashlib
+    import torch
+    from cpp_cuda_raytracer_dev_amd import _lib
+    ent = H.frame_hashes()[key]
+    if not H.mesh_matches(ent):
+        pytest.skip("stand-in mesh bits differ on this host")
+    w, h = ent["w"], ent["h"]
+    s = H.GpuScene(ent["scene"], w, h, rays=rays)
+    dev = torch.device("cuda:0")
+    out = torch.zeros(w * h, dtype=torch.int32, device=dev)
+    hit = torch.zeros(w * h, dtype=torch.int64, device=dev)
+    flags = R.RT_FLAG_WRITE_HIT | (R.RT_FLAG_SHADOW if ent["shadow"] else 0)
+    for _ in range(64):
+        s.cam.render_into(out, hit, flags=flags)
+    torch.cuda.synchronize()
+    assert s.cam.get_option(_lib.RT_OPT_RAYS_USED) == 16
+    assert s.cam.get_option(_lib.RT_OPT_SPLIT_USED) > 0
+    s.cam.render_into(out, hit, flags=flags)
+    torch.cuda.synchronize()
+    argb = out.cpu().numpy().view(np.uint32)
+    assert hashlib.sha256(argb.tobytes()).hexdigest() == ent["argb_sha"], key
+    assert hashlib.sha256(hit.cpu().numpy().tobytes()).hexdigest() == ent["hit_sha"], key
+    assert s.cam.device_error(reset=True) == 0
+
+
 @pytest.mark.parametrize("w,h", [(960, 540), (1920, 1080)])
 @pytest.mark.parametrize("kernel,order,rays", KERNELS)
 def test_dragon_standin_kd(w, h, kernel, order, rays):
