@@ -408,9 +408,38 @@ struct Ray {
     bool sx, sy, sz;           // r > 0
 };
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// Measured slower: knot 1080p 9.98k -> 9.32k FPS, fill 1080p 765 -> 834 us
+// (r03f); the packed operands cost more register moves than the six
+// multiplies and adds per box they save.
+#ifndef RT_PK_SLAB
+#define RT_PK_SLAB 0
+#endif
+// The leaf test and the child ordering without exec-mask branches: the
+// pool loop's SALU exec bookkeeping is a third of its instructions (knot
+// 1080p 9.98k -> 10.12k FPS, fill 765 -> 759 us, r03f; 78 VGPRs).
+#ifndef RT_BRANCHLESS
+#define RT_BRANCHLESS 1
+#endif
+
 // Slab parameters of one node, TD/Trixel.cu:76-95: entry maxt0, exit mint1.
+// RT_PK_SLAB: each axis's (lo, hi) pair as packed float2 (v_pk_mul_f32 /
+// v_pk_add_f32 round each half as the scalar operation does), the near/far
+// swap by the ray's sign between the multiply and the add.
 __device__ __forceinline__ void slab_vals(const Ray& R, float lx, float hx, float ly, float hy, float lz,
                                           float hz, float& maxt0, float& mint1) {
+    if (RT_PK_SLAB) {
+        const f2v px = f2v{lx, hx} * f2v{R.ix, R.ix};
+        const f2v py = f2v{ly, hy} * f2v{R.iy, R.iy};
+        const f2v pz = f2v{lz, hz} * f2v{R.iz, R.iz};
+        const f2v ax = (R.sx ? px : px.yx) + f2v{R.ox, R.ox};   // (t0x + ox, t1x + ox)
+        const f2v ay = (R.sy ? py : py.yx) + f2v{R.oy, R.oy};
+        const f2v az = (R.sz ? pz : pz.yx) + f2v{R.oz, R.oz};
+        maxt0 = fmaxf(az.x, fmaxf(ax.x, ay.x));
+        mint1 = fminf(az.y, fminf(ax.y, ay.y));
+        return;
+    }
     const float t0x = R.sx ? lx * R.ix : hx * R.ix;
     const float t1x = R.sx ? hx * R.ix : lx * R.ix;
     const float t0y = R.sy ? ly * R.iy : hy * R.iy;
@@ -469,6 +498,19 @@ __device__ __forceinline__ bool leaf_test_cam(const Ray& R, const float4 A, cons
     float qpx, qpy, qpz;
     cross3(qpx, qpy, qpz, R.rx, R.ry, R.rz, e2x, e2y, e2z);
     const float f = dot3(qpx, qpy, qpz, e1x, e1y, e1z);
+    if (RT_BRANCHLESS) {
+        // every lane evaluates the whole test (no exec-mask branches; 1/f of
+        // a rejected f is never used), then selects
+        const float pe1 = 1.0f / f;
+        const float u = pe1 * dot3(qpx, qpy, qpz, tx, ty, tz);
+        const float v = pe1 * dot3(R.rx, R.ry, R.rz, Cq.y, Cq.z, Cq.w);
+        const float w = pe1 * Dq.x;
+        const bool acc = !(f < kEpsF && f > -kEpsF) & (w < d) &
+                         !((u < kEpsF) | (v < kEpsF) | ((u + v) > 1.0f) | (w < kEpsF));
+        d = acc ? w : d;
+        best = acc ? t : best;
+        return acc;
+    }
     if (!(f < kEpsF && f > -kEpsF)) {
         const float pe1 = 1.0f / f;   // == (float)(1.0 / (double)f)
         const float u = pe1 * dot3(qpx, qpy, qpz, tx, ty, tz);
@@ -875,6 +917,14 @@ __device__ __forceinline__ void visit_leaf(const Ray& Q, float4 q4, uint4 it, fl
     uint32_t best = kMiss;
     const bool acc = kTranslated ? leaf_test_rec(Q, r0, r1, r2, it.x & ~kLeafBit, d, best)
                                  : leaf_test_cam(Q, r0, r1, r2, r3, it.x & ~kLeafBit, d, best);
+    if (RT_BRANCHLESS) {
+        const bool c = acc && (!kAny || best != __float_as_uint(q4.w));
+        o.cand = c;
+        o.ctri = best;
+        o.key = kAny ? 0ull : ((unsigned long long)__float_as_uint(d) << 32) | code_key(it.w & kCodeMarkMask);
+        if (kCount) n_acc += c ? 1u : 0u;
+        return;
+    }
     if (acc && (!kAny || best != __float_as_uint(q4.w))) {
         o.cand = true;
         o.ctri = best;
@@ -930,7 +980,12 @@ __device__ __forceinline__ void visit_interior(const Ray& Q, float4 q2, float4 q
     } else {
         if (!kTranslated) s1 = pred::add_eps_ref(r3.x);
         left_first = pred::lt_eps_ref(mx, s2);
-        push_second = left_first ? pred::gt_eps_ref(mn, s2) : (mn < s1 || mx < s1);
+        if (RT_BRANCHLESS) {
+            const bool pa = pred::gt_eps_ref(mn, s2), pb = (mn < s1) | (mx < s1);
+            push_second = (left_first & pa) | (!left_first & pb);
+        } else {
+            push_second = left_first ? pred::gt_eps_ref(mn, s2) : (mn < s1 || mx < s1);
+        }
         lpass = pred::enter_ref(lt0, lt1);
         rpass = pred::enter_ref(rt0, rt1);
     }
@@ -1007,6 +1062,9 @@ __device__ __forceinline__ void record_candidates(unsigned long long* s_key, uin
 #endif
 #ifndef RT_NEAREST_ORDER
 #define RT_NEAREST_ORDER 0
+#endif
+#ifndef RT_SKIP_SLOT1
+#define RT_SKIP_SLOT1 1
 #endif
 // RT_LEAF_FIRST 1 pushes leaf children below interior ones (fewer mixed
 // slots): measured slower for primary rays (dragon 1080p 15.3k -> 14.0k FPS,
@@ -1160,7 +1218,10 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
 #if RT_ITER_STAMPS
         const unsigned long long s3 = st ? RT_STAMP(total) : 0ull;
 #endif
-        {
+        // take is wave-uniform: a pop of at most 64 items leaves slot 1 empty
+        // on every lane, and skipping its bookkeeping (candidate, ballots,
+        // push) outright saves ~300 cycles of such an iteration
+        if (!RT_SKIP_SLOT1 || take > 64) {
             Visit v1;
             v1.ka = v1.kb = false; v1.cand = false;
             if (act1)
@@ -1802,8 +1863,6 @@ __device__ __forceinline__ void flat_accept(float f, float U, float V, float W, 
         }
     }
 }
-
-typedef float f2v __attribute__((ext_vector_type(2)));
 
 // One pair of the flat kernel's pair layout in registers (SGPRs: the loop
 // index is wave-uniform) and its two tests as packed float2 arithmetic.

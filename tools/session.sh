@@ -25,7 +25,7 @@ export TMPDIR=/tmp
 while read -r name to rest; do
     [ -z "${name:-}" ] && continue
     case $name in \#*) continue ;; esac
-    set -- $rest
+    eval "set -- $rest"  # plan lines may quote arguments
     case $1 in
     bench) shift; cmd=(python -u bench.py "$@") ;;
     smoke) cmd=(python -u -c "import __graft_entry__ as g; g.smoke()") ;;
