@@ -536,6 +536,12 @@ int cost_set(rt_camera* c, hipStream_t st) {
     return l;
 }
 
+// Split tiles only while the fine grid holds fewer than this many 16-ray
+// tiles (4 units each): at 1080p (3.4k tiles) the split measured slower with
+// two frames in flight (dragon 16.2k -> 15.6k FPS, knot 10.19k -> 10.08k),
+// at 960x540 (850 tiles) much faster (dragon 33.7k -> 44.5k, r03g).
+constexpr int64_t kSplitMaxTiles = 2048;
+
 int cost_feedback(rt_camera* c, const TraceParams& p, void* stream, int set) {
     hipStream_t st = (hipStream_t)stream;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -559,7 +565,8 @@ int cost_feedback(rt_camera* c, const TraceParams& p, void* stream, int set) {
         // half the rays, about half the pool iterations); at most a quarter
         // of the tiles.  Debug bit 512: none.
         int32_t split = 0;
-        if (c->tile_order == 3 && p.rays == 16 && kd3_waves(16) == 4 && !(c->debug & 512) && n > 0) {
+        if (c->tile_order == 3 && p.rays == 16 && kd3_waves(16) == 4 && !(c->debug & 512) && n > 0 &&
+            n < kSplitMaxTiles) {
             auto cost_of = [&](int64_t t) {
                 uint32_t m = 0;
                 for (int k = 0; k < kCostSlots; k++) m = std::max(m, c->h_cost[kCostSlots * (size_t)t + k]);
@@ -818,8 +825,13 @@ bool set_fine_region(const FrameGeom& c, TraceParams& p, int per_wave, bool fuse
 // rays): 1920x1080 whole 74 vs 139 us, a rank of 2 (6.7k units) 43 vs 70,
 // of 4 (3.4k) 42 vs 36, of 8 (1.7k) 41 vs 24; 960x540 whole (3.4k) 35 vs 38,
 // a rank of 2 34 vs 22.  The 16-ray floor near 41 us is the heaviest unit's
-// chain; 8 rays scale with the work.
-constexpr int64_t kAutoRaysMinUnits = 4096;
+// chain; 8 rays scale with the work.  Round 3 (split tiles, below, shorten
+// the 16-ray chains where few units fill the GPU): 960x540 whole 44.5k FPS
+// with 16 rays + split vs 34.9k with 8 (solo 35.4 vs 38.1 us; knot 30.7k vs
+// 26.3k); per-rank periods at 1080p, two in flight: a rank of 4 (3.4k units)
+// 23.8 us (16 + split) vs 27.9 (8), of 8 (1.7k) 23.6 vs 20.9 (r03g).  So 8
+// rays below 2,048 units.
+constexpr int64_t kAutoRaysMinUnits = 2048;
 
 int auto_rays(const FrameGeom& c, const TraceParams& p) {
     double r[4];
