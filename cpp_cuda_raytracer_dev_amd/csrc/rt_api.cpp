@@ -541,6 +541,17 @@ int cost_set(rt_camera* c, hipStream_t st) {
 // two frames in flight (dragon 16.2k -> 15.6k FPS, knot 10.19k -> 10.08k),
 // at 960x540 (850 tiles) much faster (dragon 33.7k -> 44.5k, r03g).
 constexpr int64_t kSplitMaxTiles = 2048;
+// which tiles split: cost > top / RT_SPLIT_DIV, at most n / RT_SPLIT_CAP_DIV
+#ifndef RT_SPLIT_DIV
+#define RT_SPLIT_DIV 2
+#endif
+#ifndef RT_SPLIT_CAP_DIV
+#define RT_SPLIT_CAP_DIV 4
+#endif
+// 8-ray units split into 4-pixel halves as well
+#ifndef RT_SPLIT8
+#define RT_SPLIT8 0
+#endif
 
 int cost_feedback(rt_camera* c, const TraceParams& p, void* stream, int set) {
     hipStream_t st = (hipStream_t)stream;
@@ -565,15 +576,16 @@ int cost_feedback(rt_camera* c, const TraceParams& p, void* stream, int set) {
         // half the rays, about half the pool iterations); at most a quarter
         // of the tiles.  Debug bit 512: none.
         int32_t split = 0;
-        if (c->tile_order == 3 && p.rays == 16 && kd3_waves(16) == 4 && !(c->debug & 512) && n > 0 &&
-            n < kSplitMaxTiles) {
+        if (c->tile_order == 3 && (p.rays == 16 || (p.rays == 8 && RT_SPLIT8)) && kd3_waves(p.rays) == 4 &&
+            !(c->debug & 512) && n > 0 && n < kSplitMaxTiles) {
             auto cost_of = [&](int64_t t) {
                 uint32_t m = 0;
                 for (int k = 0; k < kCostSlots; k++) m = std::max(m, c->h_cost[kCostSlots * (size_t)t + k]);
                 return m;
             };
             const uint32_t top = cost_of(ord[0]);
-            while (split < n / 4 && 2 * cost_of(ord[(size_t)split]) > top && top >= 24) split++;
+            while (split < n / RT_SPLIT_CAP_DIV && RT_SPLIT_DIV * cost_of(ord[(size_t)split]) > top && top >= 24)
+                split++;
         }
         same = same && split == c->order_split;
         if (same && c->order_gen == c->layout_gen) return RT_OK;  // d_order already holds it
@@ -1457,7 +1469,8 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
     }
     // split tiles of the cost order in d_order (launches are stream-ordered
     // behind its upload; other streams wait for it above)
-    p.split = (p.order && p.order == c->d_order && p.cost && p.rays == 16 && !(c->debug & 512)) ? c->order_split : 0;
+    p.split = (p.order && p.order == c->d_order && p.cost && (p.rays == 16 || (p.rays == 8 && RT_SPLIT8)) &&
+               !(c->debug & 512)) ? c->order_split : 0;
     int cset = 0;
     if (p.cost) {  // this stream's own cost set
         cset = cost_set(c, st);

@@ -150,15 +150,16 @@ struct Unit {
 };
 
 // Lane `lane`'s pixel of a unit (8 pixels per row, row-major); lanes >= rows*8
-// own no pixel.
+// own no pixel, nor do lanes whose column is >= cols (a split 8-ray unit's
+// 4-pixel half).
 __device__ __forceinline__ bool unit_pixel(const TraceParams& P, const Unit& u, int32_t rows, int32_t lane,
-                                           Pixel& px) {
+                                           Pixel& px, int32_t cols = 8) {
     const int32_t band = P.rank + u.slot * P.nranks;
     const int32_t ly = u.yin + (lane >> 3);
     px.x = u.x0 + (lane & 7);
     px.y = band * kTileH + ly;
     px.out = (int64_t)((P.frame_out ? band : u.slot) * kTileH + ly) * P.w + px.x;
-    return lane < rows * 8 && px.x < P.w && px.y < P.h;
+    return lane < rows * 8 && (lane & 7) < cols && px.x < P.w && px.y < P.h;
 }
 
 // Sub-tile `wave` of the fine tile with index t (in the fine grid).
@@ -1421,11 +1422,11 @@ constexpr int kCoarseMax = 32;  // coarse groups per wave (RT_OPT_COARSE <= 32)
 template <int kRays, int kCap, int kRayVec, bool kTranslated, bool kWriteHit, bool kCount, int kShadow>
 __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, kCap, kRayVec>& S_, const Unit& U,
                                            int lane, size_t dbg_slot, uint32_t* cost, Counts& C,
-                                           int32_t nrows = kRays / 8) {
+                                           int32_t nrows = kRays / 8, int32_t ncols = 8) {
     using RL = RayLayout<kRays>;
     uint4* items = S_.items;
     Pixel px;
-    bool live = unit_pixel(P, U, nrows, lane, px);  // every lane stays for the ballots
+    bool live = unit_pixel(P, U, nrows, lane, px, ncols);  // every lane stays for the ballots
     const unsigned long long t_start = P.dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
     uint32_t iters = 0, popped = 0;
 
@@ -1466,7 +1467,7 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
         // index stay live (and spilled) across the walk
         int32_t l2 = lane;
         asm volatile("" : "+v"(l2));
-        live = unit_pixel(P, U, nrows, l2, px);
+        live = unit_pixel(P, U, nrows, l2, px, ncols);
         camera_ray(P, px, live, cam, R);
     }
     const float* X = P.xf;
@@ -1515,8 +1516,8 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
         P.dbg[3 * dbg_slot + 2] = iters | ((unsigned long long)popped << 32);
     }
     // tile order 3: this unit's pool iterations (a split unit of half the
-    // rows reports twice its own: the tile's cost as a whole-tile unit, about)
-    if (cost && lane == 0) *cost = iters * (uint32_t)((kRays / 8) / nrows);
+    // pixels reports twice its own: the tile's cost as a whole-tile unit, about)
+    if (cost && lane == 0) *cost = iters * (uint32_t)(kRays / (nrows * ncols));
     __builtin_amdgcn_wave_barrier();  // LDS of this unit is read; the next unit may overwrite it
     if (!live) return;
     uint32_t argb = kBackground;
@@ -1754,10 +1755,11 @@ __global__ RT_KD3_BOUNDS(64 * kd3_waves(kRays)) void k_trace_kd3(TraceParams P) 
         if (kCount) count_flush(P, C);
         return;
     }
-    // Split tiles (tile order 3, 16-ray units; the host names the heaviest
-    // P.split tiles of its cost order, order[0..split)): blocks 2k and 2k + 1
-    // render the halves of tile order[k] with one 8-pixel row per wave, which
-    // halves the heaviest units' pool chains; the other tiles follow.
+    // Split tiles (tile order 3; the host names the heaviest P.split tiles of
+    // its cost order, order[0..split)): blocks 2k and 2k + 1 render the halves
+    // of tile order[k] -- with 16-ray units one 8-pixel row per wave, with
+    // 8-ray units a 4-pixel half row per wave -- which halves the heaviest
+    // units' pool chains; the other tiles follow.
     const bool split = b < 2 * P.split;
     const int32_t ti = split ? P.order[b >> 1] : tile_index(P, b - P.split);
     if ((uint32_t)ti >= (uint32_t)ntiles) {  // a stale order: never index past the grid
@@ -1766,10 +1768,11 @@ __global__ RT_KD3_BOUNDS(64 * kd3_waves(kRays)) void k_trace_kd3(TraceParams P) 
     }
     uint32_t* cost = P.cost ? P.cost + kCostSlots * (size_t)ti + wv : nullptr;
     Unit U = unit_of_tile(P, ti, wv);
-    if (split) U.yin = (U.yin - wv * (kRays / 8)) + (b & 1) * kWaves + wv;
-    trace_unit<kRays, kCap, kRayVec, kTranslated, kWriteHit, kCount, kShadow>(P, s_lds[wv], U, lane,
-                                                                             (size_t)b * kWaves + wv, cost, C,
-                                                                             split ? 1 : kRays / 8);
+    if (split && kRays == 16) U.yin = (U.yin - wv * (kRays / 8)) + (b & 1) * kWaves + wv;
+    if (split && kRays == 8) U.x0 += (b & 1) * 4;
+    trace_unit<kRays, kCap, kRayVec, kTranslated, kWriteHit, kCount, kShadow>(
+        P, s_lds[wv], U, lane, (size_t)b * kWaves + wv, cost, C, split && kRays == 16 ? 1 : kRays / 8,
+        split && kRays == 8 ? 4 : 8);
     if (kCount) count_flush(P, C);
 }
 
