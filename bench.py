@@ -790,7 +790,7 @@ def main():
             try:
                 tj = json.load(open(a.traffic_json))
                 key = (f"{a.scene}_{w}x{h}_m{a.mode}_n{world}" + ("_shadow" if a.shadow else "")
-                       + ("" if a.view == "default" else f"_{a.view}"))
+                       + ("" if a.view == "default" else f"_{a.view}") + ("_anim" if a.animate else ""))
                 ent = tj.get(key) or {}
                 traffic = ent.get("hbm_bytes_per_launch")
                 valu_util = ent.get("valu_issue_util")

@@ -11,6 +11,7 @@ side is doubled ("hbm_bytes_per_launch"); the raw sum is kept beside it.
 """
 import csv
 import glob
+import gzip
 import json
 import os
 import sys
@@ -21,8 +22,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def load(pass_dir, kernel_sub):
     vals = defaultdict(list)
-    for path in glob.glob(os.path.join(pass_dir, "**", "*counter_collection.csv"), recursive=True):
-        with open(path) as fp:
+    paths = glob.glob(os.path.join(pass_dir, "**", "*counter_collection.csv"), recursive=True)
+    paths += glob.glob(os.path.join(pass_dir, "**", "*counter_collection.csv.gz"), recursive=True)  # session.sh
+    for path in paths:
+        with (gzip.open(path, "rt") if path.endswith(".gz") else open(path)) as fp:
             for row in csv.DictReader(fp):
                 if kernel_sub not in row.get("Kernel_Name", ""):
                     continue
