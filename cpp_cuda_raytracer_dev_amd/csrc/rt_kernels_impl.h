@@ -1067,6 +1067,9 @@ __device__ __forceinline__ void record_candidates(unsigned long long* s_key, uin
 #ifndef RT_SKIP_SLOT1
 #define RT_SKIP_SLOT1 1
 #endif
+#ifndef RT_PRIO_HEAVY
+#define RT_PRIO_HEAVY 0
+#endif
 // RT_LEAF_FIRST 1 pushes leaf children below interior ones (fewer mixed
 // slots): measured slower for primary rays (dragon 1080p 15.3k -> 14.0k FPS,
 // fill 825 -> 927 us), faster only for happy 4K shadows (436 -> 420 us).
@@ -1767,6 +1770,11 @@ __global__ RT_KD3_BOUNDS(64 * kd3_waves(kRays)) void k_trace_kd3(TraceParams P) 
         return;
     }
     uint32_t* cost = P.cost ? P.cost + kCostSlots * (size_t)ti + wv : nullptr;
+    // RT_PRIO_HEAVY (experiment): the heaviest tiles of the cost order (the
+    // split halves, or the first RT_PRIO_HEAVY blocks) issue ahead of the
+    // other waves of their SIMD
+    if (RT_PRIO_HEAVY > 0 && P.cost && P.order && b < max(2 * P.split, (int32_t)RT_PRIO_HEAVY))
+        __builtin_amdgcn_s_setprio(2);
     Unit U = unit_of_tile(P, ti, wv);
     if (split && kRays == 16) U.yin = (U.yin - wv * (kRays / 8)) + (b & 1) * kWaves + wv;
     if (split && kRays == 8) U.x0 += (b & 1) * 4;
