@@ -33,6 +33,7 @@ RT_OPT_RAYS_USED = 8
 RT_OPT_SPLIT_USED = 9
 RT_SCENE_ORDER = 1
 RT_SCENE_TREELET_HEIGHT = 2
+RT_SCENE_TWO_LEVEL_DEPTH = 3
 RT_OPT_DEBUG = 100
 RT_OPT_POOL_CAP = 101
 RT_COMM_ID_BYTES = 128

@@ -52,6 +52,9 @@ struct rt_scene {
     std::vector<int32_t> h_left;
     int record_order = 0;            // RT_SCENE_ORDER: 0 BFS, 1 DFS preorder, 2 treelets
     int treelet_height = 3;          // RT_SCENE_TREELET_HEIGHT
+    // kernel 3's two-level iterations (two_level_depth): the deepest node
+    // depth whose children are interior records at 2i + 1, 2i + 2, or -1
+    int32_t two_depth = -1;
 };
 
 struct rt_camera {
@@ -932,6 +935,8 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
     p.ntri = s->ntri;
     p.max_depth = kMaxDepth;
     p.tree_height = s->height;
+    // debug bit 1024: one-level iterations only
+    p.two_depth = (c->debug & 1024) ? -1 : s->two_depth;
     p.tile_order = c->tile_order;
     p.order = nullptr;
     p.split = 0;
@@ -1081,6 +1086,34 @@ std::vector<int32_t> interior_order(const std::vector<int32_t>& left, int order,
     return ids;
 }
 
+// Kernel 3's two-level iterations load a node's children's records before
+// its own record has arrived, at interior positions 2i + 1 and 2i + 2 of the
+// node's position i.  Returns the deepest depth d such that every interior
+// node at depth <= d has two interior children at exactly those positions
+// (true for the top levels of the reference's tree in BFS record order: its
+// shape depends on n alone, a range of s triangles splitting into ceil(s/2)
+// and floor(s/2), so every node above depth floor(log2 n) - 1 is interior),
+// or -1 when the root's children are not (DFS or treelet orders, tiny trees).
+int32_t two_level_depth(const std::vector<int32_t>& left, const std::vector<int32_t>& ids) {
+    const int64_t n = (int64_t)left.size();
+    if (n == 0 || left[0] < 0) return -1;
+    std::vector<int32_t> pos((size_t)n, -1), depth((size_t)n, 0);
+    for (size_t k = 0; k < ids.size(); k++) pos[(size_t)ids[k]] = (int32_t)k;
+    int32_t bad = INT32_MAX, height = 0;
+    for (int64_t i = 0; i < n; i++) {
+        const int32_t L = left[(size_t)i];
+        if (L < 0) continue;
+        const int32_t R = L + 1, d = depth[(size_t)i];
+        depth[(size_t)L] = depth[(size_t)R] = d + 1;
+        height = std::max(height, d + 1);
+        const bool ok = left[(size_t)L] >= 0 && left[(size_t)R] >= 0 &&
+                        (int64_t)pos[(size_t)L] == 2 * (int64_t)pos[(size_t)i] + 1 &&
+                        (int64_t)pos[(size_t)R] == 2 * (int64_t)pos[(size_t)i] + 2;
+        if (!ok) bad = std::min(bad, d);
+    }
+    return bad == INT32_MAX ? height : bad - 1;
+}
+
 // (Re)builds the interior record order and the node -> ref table (on the
 // device, from the uploaded nodes).
 int relabel(rt_scene* s) {
@@ -1098,6 +1131,7 @@ int relabel(rt_scene* s) {
         (rc = hip_check(hipMemcpy(&s->root_ref, s->d_node_ref, sizeof(uint32_t), hipMemcpyDeviceToHost), "D2H root ref")))
         return rc;
     s->ninterior = (int64_t)ids.size();
+    s->two_depth = two_level_depth(s->h_left, ids);
     s->tree_version++;
     return RT_OK;
 }
@@ -1233,6 +1267,7 @@ extern "C" int rt_scene_get_option(const rt_scene* s, int32_t key, int32_t* valu
     switch (key) {
     case RT_SCENE_ORDER: *value = s->record_order; return RT_OK;
     case RT_SCENE_TREELET_HEIGHT: *value = s->treelet_height; return RT_OK;
+    case RT_SCENE_TWO_LEVEL_DEPTH: *value = s->two_depth; return RT_OK;
     default: return fail(RT_ERR_INVALID, "rt_scene_get_option: unknown key %d", key);
     }
 }

@@ -140,6 +140,9 @@ struct TraceParams {
     uint32_t ntri;
     int32_t max_depth;
     int32_t tree_height;           // the scene tree's height (kernel 3's pool slack is height + 1)
+    // kernel 3's two-level iterations: the deepest node depth whose children
+    // are interior records at positions 2i + 1, 2i + 2 (-1: off)
+    int32_t two_depth;
     int32_t flat_variant;          // Option kOptFlat: flat-list kernel form (0..12)
     // chunked flat forms (10-12, non-counting renders): per-pixel (w bits, triangle)
     // minima of the chunks, all ones between frames; and the chunk count

@@ -934,23 +934,36 @@ __device__ __forceinline__ void visit_leaf(const Ray& Q, float4 q4, uint4 it, fl
     }
 }
 
-// An interior item whose child-box record (r0..r3) has arrived: the node's
-// child ordering (TD/Trixel.cu:146-170) and the children's slab tests.
+// The outcome of an interior node's child ordering (TD/Trixel.cu:146-170):
+// the first- and second-popped children's refs and slab values, whether each
+// is pushed, and whether the left child is the first.
+struct Order {
+    uint32_t first, second;
+    float f0, f1, g0, g1;
+    bool ka, kb, left_first, push_second;
+};
+
+// The reference's visit counters of a node's children (kCount renders):
+// interior children tested, and descended into.
+__device__ __forceinline__ void count_order(const Order& o, uint32_t& n_int, uint32_t& n_desc) {
+    const bool first_leaf = (o.first & kLeafBit) != 0, second_leaf = (o.second & kLeafBit) != 0;
+    n_int += (first_leaf ? 0u : 1u) + ((o.push_second && !second_leaf) ? 1u : 0u);
+    n_desc += ((!first_leaf && o.ka) ? 1u : 0u) + ((o.push_second && !second_leaf && o.kb) ? 1u : 0u);
+}
+
+// The child ordering of an interior node whose own slab values are (t0, t1),
+// from its child-box record's split word r3 and its children's slab values
+// (lt0, lt1) and (rt0, rt1).  kCount: the reference's visit counters of the
+// node's children (when `real`).
 template <bool kTranslated, bool kCount>
-__device__ __forceinline__ void visit_interior(const Ray& Q, float4 q2, float4 q3, float4 q4, uint4 it, float4 r0,
-                                               float4 r1, float4 r2, float4 r3, Visit& o, uint32_t& n_int,
-                                               uint32_t& n_desc) {
-    const uint32_t ray = it.w >> 26;
-    const uint32_t marked = it.w & kCodeMarkMask;
+__device__ __forceinline__ void order_node(float4 q2, float4 q3, float4 q4, float t0, float t1, float4 r3, float lt0,
+                                           float lt1, float rt0, float rt1, bool real, Order& o, uint32_t& n_int,
+                                           uint32_t& n_desc) {
     const uint32_t lw = __float_as_uint(r3.z);
     const uint32_t axis = (lw >> kAxisShift) & 3u;
     const uint32_t L = lw & ~(3u << kAxisShift), Rr = __float_as_uint(r3.w);
     const float dir = axis == 0 ? q2.y : axis == 1 ? q2.z : q2.w;
-    const float mx = __uint_as_float(it.y) * dir, mn = __uint_as_float(it.z) * dir;
-    // children's slab parameters from the boxes in this record
-    float lt0, lt1, rt0, rt1;
-    slab_vals(Q, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, lt0, lt1);
-    slab_vals(Q, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w, rt0, rt1);
+    const float mx = t0 * dir, mn = t1 * dir;
     // The reference's double-promoted epsilon tests (TD/Trixel.cu:146-157);
     // with -DRT_GUARDED_PRED single float compares when every guard of the
     // visit holds (rt_predicates.h, checked on edge sets), else these.
@@ -995,20 +1008,38 @@ __device__ __forceinline__ void visit_interior(const Ray& Q, float4 q2, float4 q
     const bool first_leaf = (first & kLeafBit) != 0, second_leaf = (second & kLeafBit) != 0;
     const bool keep_first = first_leaf || (left_first ? lpass : rpass);
     const bool keep_second = push_second && (second_leaf || (left_first ? rpass : lpass));
-    if (kCount) {
-        n_int += (first_leaf ? 0u : 1u) + ((push_second && !second_leaf) ? 1u : 0u);
-        n_desc += ((!first_leaf && keep_first) ? 1u : 0u) + ((push_second && !second_leaf && keep_second) ? 1u : 0u);
-    }
-    const uint32_t meta_first = (ray << 26) | (marked << 1);
-    const uint32_t meta_second = meta_first | 1u;
-    const float f0 = left_first ? lt0 : rt0, f1 = left_first ? lt1 : rt1;
-    const float g0 = left_first ? rt0 : lt0, g1 = left_first ? rt1 : lt1;
-    const uint4 A = make_uint4(first, __float_as_uint(f0), __float_as_uint(f1), meta_first);
-    const uint4 B = make_uint4(second, __float_as_uint(g0), __float_as_uint(g1), meta_second);
-    o.ca = A;
-    o.cb = B;
+    o.first = first;
+    o.second = second;
+    o.f0 = left_first ? lt0 : rt0; o.f1 = left_first ? lt1 : rt1;
+    o.g0 = left_first ? rt0 : lt0; o.g1 = left_first ? rt1 : lt1;
     o.ka = keep_first;
     o.kb = keep_second;
+    o.left_first = left_first;
+    o.push_second = push_second;
+    if (kCount && real) count_order(o, n_int, n_desc);
+}
+
+// An interior item whose child-box record (r0..r3) has arrived: the node's
+// child ordering (TD/Trixel.cu:146-170) and the children's slab tests.
+template <bool kTranslated, bool kCount>
+__device__ __forceinline__ void visit_interior(const Ray& Q, float4 q2, float4 q3, float4 q4, uint4 it, float4 r0,
+                                               float4 r1, float4 r2, float4 r3, Visit& o, uint32_t& n_int,
+                                               uint32_t& n_desc) {
+    const uint32_t ray = it.w >> 26;
+    const uint32_t marked = it.w & kCodeMarkMask;
+    // children's slab parameters from the boxes in this record
+    float lt0, lt1, rt0, rt1;
+    slab_vals(Q, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, lt0, lt1);
+    slab_vals(Q, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w, rt0, rt1);
+    Order od;
+    order_node<kTranslated, kCount>(q2, q3, q4, __uint_as_float(it.y), __uint_as_float(it.z), r3, lt0, lt1, rt0, rt1,
+                                    true, od, n_int, n_desc);
+    const uint32_t meta_first = (ray << 26) | (marked << 1);
+    const uint32_t meta_second = meta_first | 1u;
+    o.ca = make_uint4(od.first, __float_as_uint(od.f0), __float_as_uint(od.f1), meta_first);
+    o.cb = make_uint4(od.second, __float_as_uint(od.g0), __float_as_uint(od.g1), meta_second);
+    o.ka = od.ka;
+    o.kb = od.kb;
 }
 
 // Visits one item whose record has arrived: a leaf's MT test or an interior
@@ -1140,6 +1171,100 @@ __device__ __forceinline__ int push_children(uint4* items, int at, const Visit& 
     return n1 + n2;
 }
 
+// Two-level pool iterations (RT_TWO_LEVEL, default on; debug bit 1024 or a
+// non-BFS record order turns them off).  A wave's chain of pool iterations is
+// at least the tree's depth, and most iterations pop small pools (24 items on
+// average, r03 stamps), so most lanes idle.  When the pool holds at most 16
+// items every item is popped and handled by a quad of lanes: role 0 visits
+// the item's node as a one-level iteration does (its children's slab tests,
+// their order), and roles 1 and 2 load, in the same memory round trip, the
+// child-box records of the node's left and right child -- for an interior
+// node at depth <= P.two_depth its children are interior records at
+// positions 2i + 1 and 2i + 2 (BFS record order, the shape rt_api.cpp's
+// two_level_depth checks) -- take their own slab values and the node's order
+// from role 0 (DPP quad broadcasts), visit the children the node keeps, and
+// push the grandchildren.  So two tree levels of a small pool take one
+// iteration of about one level's instructions.  The visited (ray, node) items
+// are the reference's, as with any pop order, and so are the counters.
+#ifndef RT_TWO_LEVEL
+#define RT_TWO_LEVEL 1
+#endif
+#ifndef RT_TWO_MAX
+#define RT_TWO_MAX 16
+#endif
+
+// Every lane of a quad receives the value of the quad's lane 0 (DPP
+// quad_perm [0,0,0,0]); the exchange runs with every lane active.
+__device__ __forceinline__ uint32_t quad_bcast0(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x00, 0xF, 0xF, true);
+}
+__device__ __forceinline__ float quad_bcast0(float x) { return __uint_as_float(quad_bcast0(__float_as_uint(x))); }
+
+// One two-level iteration over the whole pool (n <= 16 items); returns the
+// new pool size (<= 4n: an item pushes its two children or its four
+// grandchildren).
+template <int kStride, bool kTranslated, bool kCount, bool kAny, int kOrder>
+__device__ __forceinline__ int two_level_iter(const TraceParams& P, uint4* items, const float2* s_ray,
+                                              unsigned long long* s_key, uint32_t* s_tri, int n, int lane,
+                                              uint32_t& n_int, uint32_t& n_leaf, uint32_t& n_acc, uint32_t& n_desc) {
+    const int k = lane >> 2, role = lane & 3;  // role 0: the item's node; 1 / 2: its left / right child
+    bool act = k < n;
+    const uint4 it = items[act ? k : 0];
+    __builtin_amdgcn_wave_barrier();
+    if (kAny && (!kCount || kOrder >= 4))
+        if (act && s_key[it.w >> 26] == 0ull) act = false;
+    const uint32_t marked = it.w & kCodeMarkMask;
+    const bool interior = (it.x & kLeafBit) == 0;
+    const int depth = 31 - __builtin_clz(marked);
+    const bool el = act && interior && depth <= P.two_depth;  // the same on the quad's lanes
+    const bool child = (role == 1 || role == 2) && el;
+    // role 0 (and the idle role 3): the item's record; roles 1, 2: the child's
+    const float4* pa = child ? P.inode + 4 * (2 * (size_t)it.x + (size_t)role) : record_of(P, it.x);
+    const float4 a0 = pa[0], a1 = pa[1], a2 = pa[2], a3 = pa[3];
+    Ray Q;
+    float4 q2, q3, q4;
+    ray_of<kTranslated, kStride>(s_ray + (size_t)(it.w >> 26), Q, q2, q3, q4);
+    // the slab values of the record's two child boxes (role 0: the node's
+    // children; roles 1, 2: the child's children), then each lane's node's
+    // own values: role 0 the item's, roles 1, 2 what role 0 computed for them
+    float at0, at1, bt0, bt1;
+    slab_vals(Q, a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, at0, at1);
+    slab_vals(Q, a1.z, a1.w, a2.x, a2.y, a2.z, a2.w, bt0, bt1);
+    const float xl0 = quad_bcast0(at0), xl1 = quad_bcast0(at1), xr0 = quad_bcast0(bt0), xr1 = quad_bcast0(bt1);
+    const float t0 = role == 0 ? __uint_as_float(it.y) : role == 1 ? xl0 : xr0;
+    const float t1 = role == 0 ? __uint_as_float(it.z) : role == 1 ? xl1 : xr1;
+    Order o;
+    order_node<kTranslated, kCount>(q2, q3, q4, t0, t1, a3, at0, at1, bt0, bt1, false, o, n_int, n_desc);
+    // role 0's verdict on its node's children, to roles 1 and 2
+    const uint32_t fl = quad_bcast0((o.left_first ? 1u : 0u) | (o.ka ? 2u : 0u) | (o.kb ? 4u : 0u));
+    const bool lfirst = (fl & 1u) != 0;
+    const bool is_first = (role == 1) == lfirst;  // roles 1, 2: whether this child is popped first
+    const bool kept = child && ((fl & (is_first ? 2u : 4u)) != 0);
+    // the node this lane visited: role 0's item, or a child role 0 keeps
+    const bool real = role == 0 ? (act && interior) : kept;
+    if (kCount && real) count_order(o, n_int, n_desc);
+    // role 0 pushes its node's children unless roles 1 and 2 expand them
+    const bool push = role == 0 ? (act && interior && !el) : kept;
+    const uint32_t code = role == 0 ? marked : ((marked << 1) | (is_first ? 0u : 1u));
+    const uint32_t meta = ((it.w >> 26) << 26) | (code << 1);
+    const bool p1 = push && o.ka, p2 = push && o.kb;
+    const unsigned long long m1 = __ballot(p1), m2 = __ballot(p2);
+    const int n1 = __builtin_popcountll(m1);
+    if (p1) items[(int)lanes_below(m1)] = make_uint4(o.first, __float_as_uint(o.f0), __float_as_uint(o.f1), meta);
+    if (p2)
+        items[n1 + (int)lanes_below(m2)] = make_uint4(o.second, __float_as_uint(o.g0), __float_as_uint(o.g1), meta | 1u);
+    {
+        // role 0, a leaf item: the MT test (last: its temporaries and the
+        // orders' are not live together)
+        Visit v;
+        v.ka = v.kb = false; v.cand = false;
+        if (role == 0 && act && !interior)
+            visit_leaf<kTranslated, kCount, kAny>(Q, q4, it, a0, a1, a2, a3, v, n_leaf, n_acc);
+        record_candidate<kAny>(s_key, s_tri, it, v);
+    }
+    return n1 + __builtin_popcountll(m2);
+}
+
 // The pool walk of one wave.  kAny = false: nearest hit per ray, key[ray] =
 // min (w, path code), tri[ray] = its triangle.  kAny = true (shadow rays): any
 // accepted leaf with w < Lmax other than the ray's own hit triangle sets
@@ -1163,6 +1288,18 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
     constexpr bool kTwo = RT_MAX_ITEMS > 1;  // compile-time: one-item builds drop item 1's registers
     const int per = kTwo && P.items > 1 ? 128 : 64;
     while (n > 0) {
+#if RT_TWO_LEVEL
+        // a pool of at most RT_TWO_MAX items (and room for 4 children each
+        // plus the DFS slack): one two-level iteration over all of it
+        if (n <= RT_TWO_MAX && P.two_depth >= 0 && 4 * n <= cap - slack) {
+            iters++;
+            popped += (uint32_t)n;
+            n = two_level_iter<kStride, kTranslated, kCount, kAny, kOrder>(P, items, s_ray, s_key, s_tri, n, lane,
+                                                                          n_int, n_leaf, n_acc, n_desc);
+            __builtin_amdgcn_wave_barrier();
+            continue;
+        }
+#endif
         // Pop as many items as the pool has room for the children of plus
         // the DFS slack below; a single (DFS-like) pop when there is none.
         // Popping k items pushes at most 2k, so a parallel pop leaves

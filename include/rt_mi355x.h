@@ -157,6 +157,12 @@ int rt_scene_read_kd(rt_scene* s, rt_kd_node* nodes, uint64_t nnode);
  * DFS order).  Takes effect at once (cameras re-derive their records). */
 #define RT_SCENE_ORDER 1
 #define RT_SCENE_TREELET_HEIGHT 2
+/* get only: the deepest node depth whose two children are interior records
+ * at positions 2i + 1, 2i + 2 of the node's position i (BFS order: every
+ * depth below floor(log2 ntri) - 1), -1 when none: the wave-cooperative
+ * kernel's two-level iterations load a node's children's records in the same
+ * round trip as its own up to that depth (camera debug bit 1024: off). */
+#define RT_SCENE_TWO_LEVEL_DEPTH 3
 int rt_scene_set_option(rt_scene* s, int32_t key, int32_t value);
 int rt_scene_get_option(const rt_scene* s, int32_t key, int32_t* value);
 

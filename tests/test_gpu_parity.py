@@ -452,6 +452,48 @@ def test_pool_capacity_fallback(cap):
     _counters_match(cnt, ocnt, 3)
 
 
+def test_two_level_depth_option():
+    """The scene's two-level depth: floor(log2 n) - 2 in BFS record order (the
+    top levels of the reference's tree are full), none in DFS order, the top
+    treelet's in treelet order; read only."""
+    from cpp_cuda_raytracer_dev_amd import _lib
+    for name in ("dragon", "rabbit_70k", "tester"):
+        s = H.GpuScene(name, 64, 36)
+        n = len(H.mesh(name)[0])
+        t = s.trixel
+        assert t.get_option(_lib.RT_SCENE_TWO_LEVEL_DEPTH) == int(np.floor(np.log2(n))) - 2, name
+        t.set_option(_lib.RT_SCENE_ORDER, 1)
+        assert t.get_option(_lib.RT_SCENE_TWO_LEVEL_DEPTH) == -1, name
+        t.set_option(_lib.RT_SCENE_TREELET_HEIGHT, 4)
+        t.set_option(_lib.RT_SCENE_ORDER, 2)
+        assert t.get_option(_lib.RT_SCENE_TWO_LEVEL_DEPTH) == min(2, int(np.floor(np.log2(n))) - 2), name
+        t.set_option(_lib.RT_SCENE_ORDER, 0)
+        with pytest.raises(Exception):
+            t.set_option(_lib.RT_SCENE_TWO_LEVEL_DEPTH, 3)
+
+
+@pytest.mark.parametrize("name,w,h", [("dragon", 960, 540), ("knot", 480, 270), ("rabbit_70k", 320, 180)])
+@pytest.mark.parametrize("rays", [16, 8])
+@pytest.mark.parametrize("shadow", [False, True])
+@pytest.mark.parametrize("two_level", [True, False])
+def test_two_level_iterations(name, w, h, rays, shadow, two_level):
+    """Kernel 3's two-level iterations (pools of at most 16 items: a quad of
+    lanes per item, the children's records in the same round trip) and the
+    one-level walk (debug bit 1024) render the oracle's frame with its
+    counters."""
+    from cpp_cuda_raytracer_dev_amd import _lib
+    s = H.GpuScene(name, w, h, kernel=3, rays=rays)
+    if not two_level:
+        s.cam.set_option(_lib.RT_OPT_DEBUG, 1024)
+    argb, hit, cnt = s.render(0, count=True, shadow=shadow)
+    oargb, ohit, ocnt = H.oracle_render(name, w, h, 0, shadow=shadow)
+    _assert_same((argb, hit), (oargb, ohit), f"{name} two-level {two_level}")
+    _counters_match(cnt, ocnt, 3)
+    argb2, hit2, _ = s.render(0, shadow=shadow)
+    _assert_same((argb2, hit2), (oargb, ohit), f"{name} two-level {two_level} (timed instance)")
+    assert s.cam.device_error(reset=True) == 0
+
+
 @pytest.mark.parametrize("w,h", [(81, 45), (1, 1), (33, 9), (7, 130)])
 @pytest.mark.parametrize("kernel,order,rays", KERNELS)
 def test_odd_resolutions(w, h, kernel, order, rays):
