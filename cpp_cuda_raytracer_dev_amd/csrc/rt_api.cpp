@@ -543,10 +543,13 @@ int cost_set(rt_camera* c, hipStream_t st) {
 // tiles (4 units each): at 1080p (3.4k tiles) the split measured slower with
 // two frames in flight (dragon 16.2k -> 15.6k FPS, knot 10.19k -> 10.08k),
 // at 960x540 (850 tiles) much faster (dragon 33.7k -> 44.5k, r03g).
-constexpr int64_t kSplitMaxTiles = 2048;
-// which tiles split: cost > top / RT_SPLIT_DIV, at most n / RT_SPLIT_CAP_DIV
-#ifndef RT_SPLIT_DIV
-#define RT_SPLIT_DIV 2
+#ifndef RT_SPLIT_MAX_TILES
+#define RT_SPLIT_MAX_TILES 2048
+#endif
+constexpr int64_t kSplitMaxTiles = RT_SPLIT_MAX_TILES;
+// which tiles split: cost > RT_SPLIT_PCT % of the top, at most n / RT_SPLIT_CAP_DIV
+#ifndef RT_SPLIT_PCT
+#define RT_SPLIT_PCT 50
 #endif
 #ifndef RT_SPLIT_CAP_DIV
 #define RT_SPLIT_CAP_DIV 4
@@ -587,7 +590,8 @@ int cost_feedback(rt_camera* c, const TraceParams& p, void* stream, int set) {
                 return m;
             };
             const uint32_t top = cost_of(ord[0]);
-            while (split < n / RT_SPLIT_CAP_DIV && RT_SPLIT_DIV * cost_of(ord[(size_t)split]) > top && top >= 24)
+            while (split < n / RT_SPLIT_CAP_DIV && 100ull * cost_of(ord[(size_t)split]) > (uint64_t)RT_SPLIT_PCT * top &&
+                   top >= 24)
                 split++;
         }
         same = same && split == c->order_split;

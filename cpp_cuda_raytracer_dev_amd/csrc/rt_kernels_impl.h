@@ -1207,7 +1207,12 @@ template <int kStride, bool kTranslated, bool kCount, bool kAny, int kOrder>
 __device__ __forceinline__ int two_level_iter(const TraceParams& P, uint4* items, const float2* s_ray,
                                               unsigned long long* s_key, uint32_t* s_tri, int n, int lane,
                                               uint32_t& n_int, uint32_t& n_leaf, uint32_t& n_acc, uint32_t& n_desc) {
-    const int k = lane >> 2, role = lane & 3;  // role 0: the item's node; 1 / 2: its left / right child
+    // the lane's quad and role, recomputed here behind an empty asm so that
+    // they are not hoisted out of the pool loop (live across the one-level
+    // iterations too, they cost the 16-ray instance a spill)
+    int l = lane;
+    asm volatile("" : "+v"(l));
+    const int k = l >> 2, role = l & 3;  // role 0: the item's node; 1 / 2: its left / right child
     bool act = k < n;
     const uint4 it = items[act ? k : 0];
     __builtin_amdgcn_wave_barrier();
@@ -1290,8 +1295,11 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
     while (n > 0) {
 #if RT_TWO_LEVEL
         // a pool of at most RT_TWO_MAX items (and room for 4 children each
-        // plus the DFS slack): one two-level iteration over all of it
-        if (n <= RT_TWO_MAX && P.two_depth >= 0 && 4 * n <= cap - slack) {
+        // plus the DFS slack): one two-level iteration over all of it.
+        // Nearest-hit walks only: an any-hit (shadow) walk stops a ray at its
+        // first occluder, and expanding two levels of every pooled item
+        // reaches it later (knot 1080p + shadows 4.59k -> 3.38k FPS, r03r)
+        if (!kAny && n <= RT_TWO_MAX && P.two_depth >= 0 && 4 * n <= cap - slack) {
             iters++;
             popped += (uint32_t)n;
             n = two_level_iter<kStride, kTranslated, kCount, kAny, kOrder>(P, items, s_ray, s_key, s_tri, n, lane,
@@ -1899,7 +1907,9 @@ __global__ RT_KD3_BOUNDS(64 * kd3_waves(kRays)) void k_trace_kd3(TraceParams P) 
     // its cost order, order[0..split)): blocks 2k and 2k + 1 render the halves
     // of tile order[k] -- with 16-ray units one 8-pixel row per wave, with
     // 8-ray units a 4-pixel half row per wave -- which halves the heaviest
-    // units' pool chains; the other tiles follow.
+    // units' pool chains; the other tiles follow.  (Quarters of the heaviest
+    // tiles, four 4-ray units of a 16-ray unit, measured slower: dragon
+    // 960x540 43.0-45.8k -> 38.0-39.4k FPS, r03s.)
     const bool split = b < 2 * P.split;
     const int32_t ti = split ? P.order[b >> 1] : tile_index(P, b - P.split);
     if ((uint32_t)ti >= (uint32_t)ntiles) {  // a stale order: never index past the grid

@@ -24,6 +24,7 @@ def main():
     rays = int(sys.argv[5]) if len(sys.argv) > 5 else 32
     order = int(sys.argv[6]) if len(sys.argv) > 6 else 2
     items = int(sys.argv[7]) if len(sys.argv) > 7 else 2
+    extra = int(sys.argv[8]) if len(sys.argv) > 8 else 0  # extra debug bits (e.g. 1024: one-level iterations)
     s = H.GpuScene(name, w, h, kernel=kernel, tile_order=order, rays=rays, items=items)
     out = torch.zeros(w * h, dtype=torch.int32, device="cuda:0")
     st = torch.cuda.Stream()
@@ -39,10 +40,12 @@ def main():
         st.synchronize()
         return e0.elapsed_time(e1) / n
 
-    res = {"scene": name, "w": w, "h": h, "kernel": kernel, "rays": rays, "items": items, "full_ms": timed()}
-    s.cam.set_option(_lib.RT_OPT_DEBUG, 1)
+    s.cam.set_option(_lib.RT_OPT_DEBUG, extra)
+    res = {"scene": name, "w": w, "h": h, "kernel": kernel, "rays": rays, "items": items, "debug": extra,
+           "full_ms": timed()}
+    s.cam.set_option(_lib.RT_OPT_DEBUG, 1 | extra)
     res["no_traversal_ms"] = timed()
-    s.cam.set_option(_lib.RT_OPT_DEBUG, 2)
+    s.cam.set_option(_lib.RT_OPT_DEBUG, 2 | extra)
     res["with_stamps_ms"] = timed(5)
     nw = ((w + 7) // 8) * ((h + 7) // 8) * (64 // rays) * 2
     buf = np.zeros(3 * nw, np.uint64)
@@ -64,6 +67,9 @@ def main():
     dur = end - start
     res["span_us"] = float(end.max())
     res["waves"] = int(len(rec))
+    res["iters_total"] = int(vis[vis != 0xFFFFFFFF].sum())
+    res["items_total"] = int(popped[vis != 0xFFFFFFFF].sum())
+    res["wave_us_total"] = float(dur.sum())
     heavy = vis > 1
     res["heavy_waves"] = int(heavy.sum())
     for tag, m in (("light", ~heavy), ("heavy", heavy)):
