@@ -274,7 +274,7 @@ int main(int argc, char** argv) {
                 if (nst > peak) peak = nst;
                 continue;
             }
-            if ((policy == 4 || policy == 5) && nst <= two_max) {
+            if ((policy == 4 || policy == 5 || policy == 6) && nst <= two_max) {
                 /* two-level iteration: item k on lane k (its node's record) and
                  * lane k + 32 (its children's records, implicit BFS positions):
                  * children of an eligible node are expanded in the same
@@ -291,7 +291,9 @@ int main(int argc, char** argv) {
                     item_t kids[2];
                     int nkid = expand_sim(s, rr[it.ray], it, kids);
                     for (int q = 0; q < nkid; q++) {
-                        if (it.depth <= dmax && !s->is_leaf[kids[q].ref]) {
+                        if (policy == 6 && s->is_leaf[kids[q].ref]) {
+                            items++;  /* heap layout: a leaf child's MT test in this iteration */
+                        } else if ((it.depth <= dmax || policy == 6) && !s->is_leaf[kids[q].ref]) {
                             item_t g[2];
                             items++;
                             int ng = expand_sim(s, rr[it.ray], kids[q], g);
