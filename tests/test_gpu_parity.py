@@ -427,6 +427,37 @@ def test_camera_poses_rabbit(pose):
     _assert_same((argb, hit), (oargb, ohit), f"pose {pose}")
 
 
+def _model_poses(name, n=16, seed=7):
+    """SURVEY.md §8d's parity fuzz: n seeded camera poses on a sphere around
+    the model's box centre, 1.5-3.5 box diagonals away, looking at it."""
+    pts = np.asarray(H.mesh(name)[0], np.float32).reshape(-1, 3)
+    lo, hi = pts.min(axis=0), pts.max(axis=0)
+    c, diag = (lo + hi) / 2, float(np.linalg.norm(hi - lo))
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        d = rng.normal(size=3)
+        d /= np.linalg.norm(d)
+        pos = (c + (1.5 + 2.0 * rng.random()) * diag * d).astype(np.float32)
+        out.append(dict(pos=tuple(float(x) for x in pos), look_at=tuple(float(x) for x in c)))
+    return out
+
+
+@pytest.mark.parametrize("name", ["dragon", "happy", "knot", "rabbit_70k"])
+def test_camera_pose_fuzz(name):
+    """16 seeded poses around each model, kernel 3 defaults
+    (two-level iterations, cost order, auto rays): frames and hit indices
+    equal the oracle's at every pose."""
+    for k, pose in enumerate(_model_poses(name)):
+        s = H.GpuScene(name, 160, 90, cam_kw=pose)
+        argb, hit, _ = s.render(0)
+        argb2, hit2, _ = s.render(0)  # a second frame: the cost order of the first applies
+        oargb, ohit, _ = H.oracle_render(name, 160, 90, 0, cam_kw=pose)
+        _assert_same((argb, hit), (oargb, ohit), f"{name} pose {k} {pose}")
+        _assert_same((argb2, hit2), (oargb, ohit), f"{name} pose {k} second frame")
+        assert s.cam.device_error(reset=True) == 0
+
+
 @pytest.mark.parametrize("items", [1, 2])
 @pytest.mark.parametrize("rays", [64, 32, 16, 8])
 @pytest.mark.parametrize("shadow", [False, True])
