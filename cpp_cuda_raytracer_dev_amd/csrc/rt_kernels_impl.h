@@ -423,11 +423,23 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 #ifndef RT_BRANCHLESS
 #define RT_BRANCHLESS 1
 #endif
+// Walks whose rays have no object offset and no zero component skip the
+// slab tests' od/r additions (slab_vals<true>); 0: never.
+#ifndef RT_NO_OFF
+#define RT_NO_OFF 1
+#endif
 
 // Slab parameters of one node, TD/Trixel.cu:76-95: entry maxt0, exit mint1.
 // RT_PK_SLAB: each axis's (lo, hi) pair as packed float2 (v_pk_mul_f32 /
 // v_pk_add_f32 round each half as the scalar operation does), the near/far
 // swap by the ray's sign between the multiply and the add.
+// kNoOff: the walk's rays have no object offset and no zero component, so
+// every od/r term is a signed zero (0/r, r != 0): adding it changes at most
+// the sign of a zero t, which no comparison downstream tells apart (entry
+// and exit tests, the split-plane order, the products t * dir); the six adds
+// per box are skipped.  A ray with a zero component keeps them (0/0 = NaN
+// drops that axis from the reference's test, TD/Trixel.cu:94-95).
+template <bool kNoOff = false>
 __device__ __forceinline__ void slab_vals(const Ray& R, float lx, float hx, float ly, float hy, float lz,
                                           float hz, float& maxt0, float& mint1) {
     if (RT_PK_SLAB) {
@@ -447,6 +459,11 @@ __device__ __forceinline__ void slab_vals(const Ray& R, float lx, float hx, floa
     const float t1y = R.sy ? hy * R.iy : ly * R.iy;
     const float t0z = R.sz ? lz * R.iz : hz * R.iz;
     const float t1z = R.sz ? hz * R.iz : lz * R.iz;
+    if (kNoOff) {
+        maxt0 = fmaxf(t0z, fmaxf(t0x, t0y));
+        mint1 = fminf(t1z, fminf(t1x, t1y));
+        return;
+    }
     maxt0 = fmaxf(t0z + R.oz, fmaxf(t0x + R.ox, t0y + R.oy));
     mint1 = fminf(t1z + R.oz, fminf(t1x + R.ox, t1y + R.oy));
 }
@@ -1021,7 +1038,7 @@ __device__ __forceinline__ void order_node(float4 q2, float4 q3, float4 q4, floa
 
 // An interior item whose child-box record (r0..r3) has arrived: the node's
 // child ordering (TD/Trixel.cu:146-170) and the children's slab tests.
-template <bool kTranslated, bool kCount>
+template <bool kTranslated, bool kCount, bool kNoOff = false>
 __device__ __forceinline__ void visit_interior(const Ray& Q, float4 q2, float4 q3, float4 q4, uint4 it, float4 r0,
                                                float4 r1, float4 r2, float4 r3, Visit& o, uint32_t& n_int,
                                                uint32_t& n_desc) {
@@ -1029,8 +1046,8 @@ __device__ __forceinline__ void visit_interior(const Ray& Q, float4 q2, float4 q
     const uint32_t marked = it.w & kCodeMarkMask;
     // children's slab parameters from the boxes in this record
     float lt0, lt1, rt0, rt1;
-    slab_vals(Q, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, lt0, lt1);
-    slab_vals(Q, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w, rt0, rt1);
+    slab_vals<kNoOff>(Q, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, lt0, lt1);
+    slab_vals<kNoOff>(Q, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w, rt0, rt1);
     Order od;
     order_node<kTranslated, kCount>(q2, q3, q4, __uint_as_float(it.y), __uint_as_float(it.z), r3, lt0, lt1, rt0, rt1,
                                     true, od, n_int, n_desc);
@@ -1044,7 +1061,7 @@ __device__ __forceinline__ void visit_interior(const Ray& Q, float4 q2, float4 q
 
 // Visits one item whose record has arrived: a leaf's MT test or an interior
 // node's child ordering and slab tests.
-template <int kStride, bool kTranslated, bool kCount, bool kAny>
+template <int kStride, bool kTranslated, bool kCount, bool kAny, bool kNoOff = false>
 __device__ __forceinline__ void visit_item(const float2* rd, uint4 it, float4 r0, float4 r1, float4 r2, float4 r3,
                                            Visit& o, uint32_t& n_int, uint32_t& n_leaf, uint32_t& n_acc,
                                            uint32_t& n_desc) {
@@ -1053,13 +1070,13 @@ __device__ __forceinline__ void visit_item(const float2* rd, uint4 it, float4 r0
     if (RT_RAY_HOIST) {
         ray_of<kTranslated, kStride>(rd, Q, q2, q3, q4);
         if (it.x & kLeafBit) visit_leaf<kTranslated, kCount, kAny>(Q, q4, it, r0, r1, r2, r3, o, n_leaf, n_acc);
-        else visit_interior<kTranslated, kCount>(Q, q2, q3, q4, it, r0, r1, r2, r3, o, n_int, n_desc);
+        else visit_interior<kTranslated, kCount, kNoOff>(Q, q2, q3, q4, it, r0, r1, r2, r3, o, n_int, n_desc);
     } else if (it.x & kLeafBit) {
         ray_of<kTranslated, kStride>(rd, Q, q2, q3, q4);
         visit_leaf<kTranslated, kCount, kAny>(Q, q4, it, r0, r1, r2, r3, o, n_leaf, n_acc);
     } else {
         ray_of<kTranslated, kStride>(rd, Q, q2, q3, q4);
-        visit_interior<kTranslated, kCount>(Q, q2, q3, q4, it, r0, r1, r2, r3, o, n_int, n_desc);
+        visit_interior<kTranslated, kCount, kNoOff>(Q, q2, q3, q4, it, r0, r1, r2, r3, o, n_int, n_desc);
     }
 }
 
@@ -1203,7 +1220,7 @@ __device__ __forceinline__ float quad_bcast0(float x) { return __uint_as_float(q
 // One two-level iteration over the whole pool (n <= 16 items); returns the
 // new pool size (<= 4n: an item pushes its two children or its four
 // grandchildren).
-template <int kStride, bool kTranslated, bool kCount, bool kAny, int kOrder>
+template <int kStride, bool kTranslated, bool kCount, bool kAny, int kOrder, bool kNoOff>
 __device__ __forceinline__ int two_level_iter(const TraceParams& P, uint4* items, const float2* s_ray,
                                               unsigned long long* s_key, uint32_t* s_tri, int n, int lane,
                                               uint32_t& n_int, uint32_t& n_leaf, uint32_t& n_acc, uint32_t& n_desc) {
@@ -1233,8 +1250,8 @@ __device__ __forceinline__ int two_level_iter(const TraceParams& P, uint4* items
     // children; roles 1, 2: the child's children), then each lane's node's
     // own values: role 0 the item's, roles 1, 2 what role 0 computed for them
     float at0, at1, bt0, bt1;
-    slab_vals(Q, a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, at0, at1);
-    slab_vals(Q, a1.z, a1.w, a2.x, a2.y, a2.z, a2.w, bt0, bt1);
+    slab_vals<kNoOff>(Q, a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, at0, at1);
+    slab_vals<kNoOff>(Q, a1.z, a1.w, a2.x, a2.y, a2.z, a2.w, bt0, bt1);
     const float xl0 = quad_bcast0(at0), xl1 = quad_bcast0(at1), xr0 = quad_bcast0(bt0), xr1 = quad_bcast0(bt1);
     const float t0 = role == 0 ? __uint_as_float(it.y) : role == 1 ? xl0 : xr0;
     const float t1 = role == 0 ? __uint_as_float(it.z) : role == 1 ? xl1 : xr1;
@@ -1276,7 +1293,7 @@ __device__ __forceinline__ int two_level_iter(const TraceParams& P, uint4* items
 // key[ray] = 0; without counters the items of such rays are dropped.
 // Each lane pops up to P.items (1 or 2) items per iteration and fetches their
 // records together, so a lane keeps two memory round trips in flight.
-template <int kCap, int kStride, bool kTranslated, bool kCount, bool kAny, int kOrder = 0>
+template <int kCap, int kStride, bool kTranslated, bool kCount, bool kAny, int kOrder = 0, bool kNoOff = false>
 __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, const float2* s_ray,
                                           unsigned long long* s_key, uint32_t* s_tri, int n, int lane,
                                           uint32_t& iters, uint32_t& popped, uint32_t& n_int, uint32_t& n_leaf,
@@ -1302,7 +1319,7 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
         if (!kAny && n <= RT_TWO_MAX && P.two_depth >= 0 && 4 * n <= cap - slack) {
             iters++;
             popped += (uint32_t)n;
-            n = two_level_iter<kStride, kTranslated, kCount, kAny, kOrder>(P, items, s_ray, s_key, s_tri, n, lane,
+            n = two_level_iter<kStride, kTranslated, kCount, kAny, kOrder, kNoOff>(P, items, s_ray, s_key, s_tri, n, lane,
                                                                           n_int, n_leaf, n_acc, n_desc);
             __builtin_amdgcn_wave_barrier();
             continue;
@@ -1359,7 +1376,7 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
             Visit v0;
             v0.ka = v0.kb = false; v0.cand = false;
             if (act0)
-                visit_item<kStride, kTranslated, kCount, kAny>(s_ray + (size_t)(it0.w >> 26), it0, a0, a1, a2, a3,
+                visit_item<kStride, kTranslated, kCount, kAny, kNoOff>(s_ray + (size_t)(it0.w >> 26), it0, a0, a1, a2, a3,
                                                             v0, n_int, n_leaf, n_acc, n_desc);
             record_candidate<kAny>(s_key, s_tri, it0, v0);
             total += push_children<kAny, (kOrder & 3)>(items, base + total, v0);
@@ -1374,7 +1391,7 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
             Visit v1;
             v1.ka = v1.kb = false; v1.cand = false;
             if (act1)
-                visit_item<kStride, kTranslated, kCount, kAny>(s_ray + (size_t)(it1.w >> 26), it1, b0, b1, b2, b3,
+                visit_item<kStride, kTranslated, kCount, kAny, kNoOff>(s_ray + (size_t)(it1.w >> 26), it1, b0, b1, b2, b3,
                                                             v1, n_int, n_leaf, n_acc, n_desc);
             record_candidate<kAny>(s_key, s_tri, it1, v1);
             total += push_children<kAny, (kOrder & 3)>(items, base + total, v1);
@@ -1398,10 +1415,10 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
         v0.ka = v0.kb = false; v0.cand = false;
         v1.ka = v1.kb = false; v1.cand = false;
         if (act0)
-            visit_item<kStride, kTranslated, kCount, kAny>(s_ray + (size_t)(it0.w >> 26), it0, a0, a1, a2, a3, v0,
+            visit_item<kStride, kTranslated, kCount, kAny, kNoOff>(s_ray + (size_t)(it0.w >> 26), it0, a0, a1, a2, a3, v0,
                                                         n_int, n_leaf, n_acc, n_desc);
         if (act1)
-            visit_item<kStride, kTranslated, kCount, kAny>(s_ray + (size_t)(it1.w >> 26), it1, b0, b1, b2, b3, v1,
+            visit_item<kStride, kTranslated, kCount, kAny, kNoOff>(s_ray + (size_t)(it1.w >> 26), it1, b0, b1, b2, b3, v1,
                                                         n_int, n_leaf, n_acc, n_desc);
         record_candidates<kAny>(s_key, s_tri, it0, it1, v0, v1);
         // push the children (all first children of item 0, all second ones, then item 1's): ballot compaction
@@ -1579,12 +1596,15 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
     uint32_t iters = 0, popped = 0;
 
     int n;
+    bool no_off;  // the walk may skip the slab tests' od/r terms (slab_vals, kNoOff)
     {
         // the ray goes to LDS for the walk; shading recomputes it afterwards
         // (the same float expressions), so it is not live across the walk
         float cam0[3];
         Ray R0;
         camera_ray(P, px, live, cam0, R0);
+        no_off = !kTranslated && __ballot(live && !(fabsf(R0.rx) > 0.0f && fabsf(R0.ry) > 0.0f &&
+                                                    fabsf(R0.rz) > 0.0f)) == 0ull;
         if (lane < kRays) {
             store_ray(&S_.ray[lane], RL::kStride, R0, kTranslated, 0.0f, 0u);
             S_.key[lane] = ~0ull;
@@ -1599,6 +1619,16 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
     if (RT_SPLIT_LEAF && P.items > 1)
         pool_walk_split<kCap, RL::kStride, kTranslated, kCount, false>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters,
                                                                   popped, C.n_int, C.n_leaf, C.n_acc, C.n_desc);
+    else if (RT_NO_OFF && !kTranslated && no_off)
+        pool_walk<kCap, RL::kStride, kTranslated, kCount, false, 0, true>(P, items, S_.ray, S_.key, S_.tri, n, lane,
+                                                                     iters, popped, C.n_int, C.n_leaf, C.n_acc,
+                                                                     C.n_desc
+#if RT_ITER_STAMPS
+                                                                     , (P.istamp && dbg_slot != kNoDbg)
+                                                                           ? P.istamp + 4 * (size_t)kIterStamps * dbg_slot
+                                                                           : nullptr
+#endif
+        );
     else
         pool_walk<kCap, RL::kStride, kTranslated, kCount, false>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters, popped,
                                                             C.n_int, C.n_leaf, C.n_acc, C.n_desc
