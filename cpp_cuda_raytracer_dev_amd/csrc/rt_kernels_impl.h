@@ -1828,7 +1828,61 @@ __device__ __forceinline__ bool root_certain_miss_xf(const TraceParams& P, int32
     return mint1 < maxt0 - tol || maxt0 < -tol;
 }
 
+// A whole 8x8 group at once (RT_GROUP_MISS): the unnormalised direction
+// D = X3 (n_mod + u_mod fx + v_mod fy) is affine in the pixel, so over the
+// group each D_i lies between its values at the four corners; widened by
+// e_i = 1e-5 sum_j |X_ij| (|n_j| + |u_j| fx_max + |v_j| fy_max) it holds
+// every pixel's float ray divided by its (positive) norm -- the float
+// evaluation of c, the 21-step normalisation and the rotation stay within a
+// few ulps of that sum.  An axis whose interval touches 0 leaves the group to
+// the per-pixel tests (0/0 = NaN drops an axis in the reference).  With the
+// signs fixed, t0_i = (near_i + od_i) / D_i and t1_i = (far_i + od_i) / D_i
+// are monotone in D_i, so every pixel's maxt0 >= L0 = max_i min t0_i and
+// mint1 <= U1 = min_i max t1_i (in the unnormalised scale; the reference's t
+// are these times the norm, a common positive factor, plus float rounding of
+// at most a few ulps of M = (|near| + |far| + |od|) / |D|).  A margin of
+// 1e-4 M_max + 1e-3 (|L0| + |U1|) + 1e-12 above that rounding makes
+// L0 > U1 + margin a miss of every pixel's exact test (mint1 < maxt0 -
+// 1e-16), and U1 < -margin one too (maxt0 <= mint1 + 1e-16 < 0).
+__device__ __forceinline__ bool group_certain_miss(const TraceParams& P, const Unit& G) {
+    const int32_t y0 = (P.rank + G.slot * P.nranks) * kTileH + G.yin;
+    const float fx0 = (float)(uint32_t)G.x0, fx1 = (float)(uint32_t)(G.x0 + 7);
+    const float fy0 = (float)(uint32_t)y0, fy1 = (float)(uint32_t)(y0 + 7);
+    const float* X = P.xf;
+    const float* b = P.root_box;
+    float L0 = -INFINITY, U1 = INFINITY, mmax = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        const float x0 = X[4 * i], x1 = X[4 * i + 1], x2 = X[4 * i + 2], od = X[4 * i + 3];
+        const float A = x0 * P.n_mod[0] + x1 * P.n_mod[1] + x2 * P.n_mod[2];
+        const float B = x0 * P.u_mod[0] + x1 * P.u_mod[1] + x2 * P.u_mod[2];
+        const float Cc = x0 * P.v_mod[0] + x1 * P.v_mod[1] + x2 * P.v_mod[2];
+        const float e = 1e-5f * (fabsf(x0) * (fabsf(P.n_mod[0]) + fabsf(P.u_mod[0]) * fx1 + fabsf(P.v_mod[0]) * fy1) +
+                                 fabsf(x1) * (fabsf(P.n_mod[1]) + fabsf(P.u_mod[1]) * fx1 + fabsf(P.v_mod[1]) * fy1) +
+                                 fabsf(x2) * (fabsf(P.n_mod[2]) + fabsf(P.u_mod[2]) * fx1 + fabsf(P.v_mod[2]) * fy1));
+        const float d00 = A + B * fx0 + Cc * fy0, d01 = A + B * fx0 + Cc * fy1;
+        const float d10 = A + B * fx1 + Cc * fy0, d11 = A + B * fx1 + Cc * fy1;
+        const float dlo = fminf(fminf(d00, d01), fminf(d10, d11)) - e;
+        const float dhi = fmaxf(fmaxf(d00, d01), fmaxf(d10, d11)) + e;
+        if (!(dlo > 0.0f || dhi < 0.0f)) return false;  // touches 0 (or NaN): the per-pixel tests
+        const bool pos = dlo > 0.0f;
+        const float lo = b[2 * i], hi = b[2 * i + 1];
+        const float n0 = (pos ? lo : hi) + od, n1 = (pos ? hi : lo) + od;
+        // t = n / D over D in [dlo, dhi] (one sign): extremes at the ends
+        const float a0 = n0 / dlo, a1 = n0 / dhi, c0 = n1 / dlo, c1 = n1 / dhi;
+        L0 = fmaxf(L0, fminf(a0, a1));
+        U1 = fminf(U1, fmaxf(c0, c1));
+        mmax = fmaxf(mmax, (fabsf(lo) + fabsf(hi) + fabsf(od)) / fminf(fabsf(dlo), fabsf(dhi)));
+    }
+    if (!(fabsf(L0) < 1e30f && fabsf(U1) < 1e30f && mmax < 1e30f)) return false;
+    const float margin = 1e-4f * mmax + 1e-3f * (fabsf(L0) + fabsf(U1)) + 1e-12f;
+    return L0 > U1 + margin || U1 < -margin;
+}
+
 //
+#ifndef RT_GROUP_MISS
+#define RT_GROUP_MISS 1
+#endif
 // Groups at least 2 pixels outside the root box's screen rectangle
 // (P.far_rect, identity transform only) skip even that: the rectangle is the
 // box's exact projection (in double, from the same float basis), a pixel's
@@ -1864,6 +1918,17 @@ __device__ __forceinline__ bool fill_far(const TraceParams& P, const Unit& G, in
         if (kCount) C.n_int += 1u;  // the root visit, which fails
     }
     return true;
+}
+
+// A group known to miss: every pixel background (the root visit fails).
+template <bool kWriteHit, bool kCount>
+__device__ __forceinline__ void fill_background(const TraceParams& P, const Unit& G, int lane, Counts& C) {
+    Pixel px;
+    if (unit_pixel(P, G, 8, lane, px)) {
+        put_pixel(P, px.out, kBackground, false);
+        if (kWriteHit) P.hit[px.out] = (int64_t)-1;
+        if (kCount) C.n_int += 1u;  // the root visit, which fails
+    }
 }
 
 // A coarse group every pixel of which is a certain miss (above) is
@@ -2002,9 +2067,20 @@ __global__ __launch_bounds__(128) void k_coarse_kd3(TraceParams P) {
         const int32_t j = j0 + g;
         if (j < j1 && !(far_ok && fill_far<kWriteHit, kCount>(P, coarse_unit(P, j), lane, C))) pending |= 1u << g;
     }
-    // then the certain-miss test of the rest, unrolled the same way (one
-    // group after another, its rsq / rcp chains cost ~1 us each); the groups
-    // left take the exact root test
+    // the whole-group certain-miss test, one group per lane (RT_GROUP_MISS)
+    if (RT_GROUP_MISS && !(P.root_ref & kLeafBit) && !(P.debug & 1)) {
+        const int32_t jg = j0 + lane;
+        const bool sure = lane < kCoarseMax && jg < j1 && ((pending >> lane) & 1u) &&
+                          group_certain_miss(P, coarse_unit(P, jg));
+        const uint32_t sure_mask = (uint32_t)__ballot(sure);
+#pragma unroll 8
+        for (int g = 0; g < kCoarseMax; g++)
+            if ((sure_mask >> g) & 1u) fill_background<kWriteHit, kCount>(P, coarse_unit(P, j0 + g), lane, C);
+        pending &= ~sure_mask;
+    }
+    // then the per-pixel certain-miss test of the rest, unrolled the same way
+    // (one group after another, its rsq / rcp chains cost ~1 us each); the
+    // groups left take the exact root test
     if (!(P.root_ref & kLeafBit) && !(P.debug & 1)) {
 #pragma unroll 8
         for (int g = 0; g < kCoarseMax; g++)
