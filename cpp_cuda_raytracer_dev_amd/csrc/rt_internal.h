@@ -68,7 +68,11 @@ constexpr int kPoolCapMax = 640;
 #define RT_KD3_WAVES 4
 #endif
 __host__ __device__ constexpr int kd3_waves(int rays) { return rays <= 16 ? RT_KD3_WAVES : 2; }
-constexpr int kCostSlots = 4;   // kernel 3 items per wave (peak measured <= 440, tools/pool_sim.c)
+// Kernel 3's per-tile cost slots (pool iterations): slots 0-3 the waves of a
+// tile, 4-7 the second half's waves of a split tile (zero otherwise), so a
+// split tile's cost is the max over both halves, not whichever half wrote
+// last (that race reordered the heavy tiles at random between samples).
+constexpr int kCostSlots = 8;
 
 // ---------------------------------------------------------------------------
 // Device layouts (all 16-byte aligned, read with dwordx4 loads).

@@ -2027,7 +2027,8 @@ __global__ RT_KD3_BOUNDS(64 * kd3_waves(kRays)) void k_trace_kd3(TraceParams P) 
         if (lane == 0) atomicOr(P.err, 8);
         return;
     }
-    uint32_t* cost = P.cost ? P.cost + kCostSlots * (size_t)ti + wv : nullptr;
+    uint32_t* cost = P.cost ? P.cost + kCostSlots * (size_t)ti + wv + (split ? (b & 1) * 4 : 0) : nullptr;
+    if (cost && !split && lane == 0) cost[4] = 0u;  // no second half
     // RT_PRIO_HEAVY (experiment): the heaviest tiles of the cost order (the
     // split halves, or the first RT_PRIO_HEAVY blocks) issue ahead of the
     // other waves of their SIMD
