@@ -539,10 +539,11 @@ int cost_set(rt_camera* c, hipStream_t st) {
     return l;
 }
 
-// Split tiles only while the fine grid holds fewer than this many 16-ray
-// tiles (4 units each): at 1080p (3.4k tiles) the split measured slower with
-// two frames in flight (dragon 16.2k -> 15.6k FPS, knot 10.19k -> 10.08k),
-// at 960x540 (850 tiles) much faster (dragon 33.7k -> 44.5k, r03g).
+// Grids of fewer than this many 16-ray tiles (4 units each) split the tiles
+// above RT_SPLIT_PCT % of the heaviest, larger ones only those above
+// RT_SPLIT_PCT_LARGE %: at 1080p (3.4k tiles) splitting half the top measured
+// slower with two frames in flight (dragon 16.2k -> 15.6k FPS, knot 10.19k ->
+// 10.08k), at 960x540 (850 tiles) much faster (dragon 33.7k -> 44.5k, r03g).
 #ifndef RT_SPLIT_MAX_TILES
 #define RT_SPLIT_MAX_TILES 2048
 #endif
@@ -550,6 +551,12 @@ constexpr int64_t kSplitMaxTiles = RT_SPLIT_MAX_TILES;
 // which tiles split: cost > RT_SPLIT_PCT % of the top, at most n / RT_SPLIT_CAP_DIV
 #ifndef RT_SPLIT_PCT
 #define RT_SPLIT_PCT 50
+#endif
+// grids of kSplitMaxTiles or more: only tiles above RT_SPLIT_PCT_LARGE % of
+// the top (with deterministic split costs, r03zf: dragon 1080p solo 74.0 ->
+// 71.7 us, knot 107.1 -> 104.7 us, FPS unchanged; 0: no split there)
+#ifndef RT_SPLIT_PCT_LARGE
+#define RT_SPLIT_PCT_LARGE 75
 #endif
 #ifndef RT_SPLIT_CAP_DIV
 #define RT_SPLIT_CAP_DIV 4
@@ -585,14 +592,15 @@ int cost_feedback(rt_camera* c, const TraceParams& p, void* stream, int set) {
         // of the tiles.  Debug bit 512: none.
         int32_t split = 0;
         if (c->tile_order == 3 && (p.rays == 16 || (p.rays == 8 && RT_SPLIT8)) && kd3_waves(p.rays) == 4 &&
-            !(c->debug & 512) && n > 0 && n < kSplitMaxTiles) {
+            !(c->debug & 512) && n > 0 && (n < kSplitMaxTiles || RT_SPLIT_PCT_LARGE > 0)) {
+            const uint64_t pct = n < kSplitMaxTiles ? RT_SPLIT_PCT : RT_SPLIT_PCT_LARGE;
             auto cost_of = [&](int64_t t) {
                 uint32_t m = 0;
                 for (int k = 0; k < kCostSlots; k++) m = std::max(m, c->h_cost[kCostSlots * (size_t)t + k]);
                 return m;
             };
             const uint32_t top = cost_of(ord[0]);
-            while (split < n / RT_SPLIT_CAP_DIV && 100ull * cost_of(ord[(size_t)split]) > (uint64_t)RT_SPLIT_PCT * top &&
+            while (split < n / RT_SPLIT_CAP_DIV && 100ull * cost_of(ord[(size_t)split]) > pct * top &&
                    top >= 24)
                 split++;
         }

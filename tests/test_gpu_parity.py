@@ -332,12 +332,14 @@ def test_full_frame_vs_oracle_hash(key):
 
 @pytest.mark.parametrize("key,rays", [("dragon_960x540_m0", 0), ("knot_960x540_m0", 0), ("knot_960x540_m0", 16),
                                       ("dragon_960x540_m0_shadow", 0), ("dragon_960x540_m0", 8),
-                                      ("knot_960x540_m0", 8), ("dragon_960x540_m0_shadow", 8)])
+                                      ("knot_960x540_m0", 8), ("dragon_960x540_m0_shadow", 8),
+                                      ("dragon_1920x1080_m0", 0), ("knot_1920x1080_m0", 0)])
 def test_split_tiles_same_frame(key, rays):
     """Tile order 3 splits the heaviest 16-ray tiles into two 8-ray halves
     (8-ray units: two 4-pixel halves) once a cost sample has arrived
-    (RT_OPT_SPLIT_USED > 0; grids of fewer than 2,048 tiles): the frame and
-    hit buffer stay the oracle's (committed hashes)."""
+    (RT_OPT_SPLIT_USED > 0; above half the heaviest tile's cost in grids of
+    fewer than 2,048 tiles, above 75 % in larger ones): the frame and hit
+    buffer stay the oracle's (committed hashes)."""
     import hashlib
     import torch
     from cpp_cuda_raytracer_dev_amd import _lib
