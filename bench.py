@@ -913,6 +913,9 @@ def main():
                      "frames_in_flight": inflight if not isinstance(loop, PyLoop) else 1,
                      "what": "host time spent enqueueing the timed frames / steps (rank 0)"},
             "kd_build": build_times,
+            # build provenance: SHA-256 of the library's sources and flags
+            # (rt_build_id; _lib refuses a library whose id is not this tree's)
+            "build_id": _lib.build_id(),
         }
         if frame_check is not None:
             res["frame_check"] = frame_check

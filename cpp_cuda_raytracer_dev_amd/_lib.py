@@ -14,6 +14,7 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "librt_mi355x.so")
+DEFAULT_LIB_PATH = LIB_PATH
 
 RT_OK = 0
 RT_MODE_KD = 0
@@ -147,6 +148,7 @@ SIGNATURES = {
     "rt_camera_destroy": (None, [_P]),
     "rt_last_error_string": (C.c_char_p, []),
     "rt_abi_version": (C.c_int, []),
+    "rt_build_id": (C.c_char_p, []),
 }
 
 _lib = None
@@ -173,8 +175,21 @@ def lib() -> C.CDLL:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        if os.path.abspath(LIB_PATH) == DEFAULT_LIB_PATH:
+            # build provenance: the library must have been built from this
+            # tree's sources and flags (experiment variants are exempt)
+            from . import build
+            want, got = build.source_id(), L.rt_build_id().decode()
+            if got != want:
+                raise ImportError(f"{LIB_PATH} was built from other sources (build id {got[:16]}, this tree "
+                                  f"{want[:16]}): rebuild with `python -m cpp_cuda_raytracer_dev_amd.build`")
         _lib = L
     return _lib
+
+
+def build_id() -> str:
+    """The loaded library's build id (SHA-256 of its sources and flags)."""
+    return lib().rt_build_id().decode()
 
 
 def check(fn: str, code: int) -> int:

@@ -453,6 +453,11 @@ void rt_camera_destroy(rt_camera* c);
 
 const char* rt_last_error_string(void);
 int rt_abi_version(void);
+/* Build provenance: the SHA-256 (hex) of the sources (csrc/, include/) and the
+ * compile/link flags this library was built from (cpp_cuda_raytracer_dev_amd/
+ * build.py source_id); the Python binding refuses a library whose id differs
+ * from the tree's. */
+const char* rt_build_id(void);
 
 #ifdef __cplusplus
 }

@@ -20,6 +20,16 @@ def _built():
     if not os.path.exists(_oracle._LIB_PATH):
         _oracle.build()
     from cpp_cuda_raytracer_dev_amd import _lib, build
-    if not os.path.exists(_lib.LIB_PATH):
+    # (re)build when the library is missing or its embedded build id is not
+    # this tree's (build.source_id); build_lib recompiles only stale objects
+    if not os.path.exists(_lib.LIB_PATH) or _embedded_id(_lib.LIB_PATH) != build.source_id():
         build.build_lib()
     yield
+
+
+def _embedded_id(path):
+    """rt_build_id() of a built library, read without loading it."""
+    import re
+    with open(path, "rb") as fp:
+        m = re.search(rb"generated-id:([0-9a-f]{64})", fp.read())
+    return m.group(1).decode() if m else None

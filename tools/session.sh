@@ -14,6 +14,7 @@
 #   variant <lib> <args>    bench.py against tools/variants/lib_<lib>.so
 #   pmc <dir> <ctrs> -- <cmd...>   one rocprofv3 --pmc pass (counters only)
 #   stats <dir> -- <cmd...>        rocprofv3 --kernel-trace --stats
+#   trace <dir> -- <cmd...>        + --memory-copy-trace; traces kept gzipped (dir must start trace_)
 #   pmcsum <key> <kernel> <dir...>  tools/pmc_traffic.py over pmc dirs of this session
 set -u
 TAG=$1; PLAN=$2
@@ -37,6 +38,8 @@ while read -r name to rest; do
             cmd=(python3 tools/pmc_traffic.py --out "$OUT/pmc_traffic_$k.json" "$k" "$ks" "${ds[@]}") ;;
     stats) shift; d=$1; shift; [ "$1" = "--" ] && shift
            cmd=(rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$d" -o run -- "$@") ;;
+    trace) shift; d=$1; shift; [ "$1" = "--" ] && shift  # kernel + memory-copy trace, kept (gzipped)
+           cmd=(rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/$d" -o run -- "$@") ;;
     *) cmd=("$@") ;;
     esac
     echo "== $name ($to s): ${cmd[*]}"
@@ -50,6 +53,7 @@ done < "$PLAN"
 python3 tools/bench_summary.py "$OUT"/*.log 2>/dev/null
 # gpurun copies gpurun_out/ back only below 64 MiB: drop the per-dispatch
 # kernel traces (the stats CSVs stay) and compress the counter CSVs
+find "$OUT" -path '*trace_*' -name '*_trace.csv' -exec gzip -f {} \; 2>/dev/null
 find "$OUT" -name '*_kernel_trace.csv' -delete 2>/dev/null
 find "$OUT" -name '*_counter_collection.csv' -size +1M -exec gzip -f {} \; 2>/dev/null
 du -sh "$OUT" 2>/dev/null
