@@ -794,8 +794,9 @@ def main():
         tests = w * h * len(pts)  # flat list: every ray against every triangle
         tflops = FLOPS_PER_TEST * tests / (kern_ms * 1e-3) / 1e12
         # counter-based figures of this configuration from the committed PMC
-        # passes (tools/pmc_plan.py; one frame in flight, the same kernel)
-        traffic, valu_util, pmc_key = None, None, None
+        # passes (tools/pmc_plan.py; one frame in flight, the same kernel),
+        # stamped with the build id of the library they measured
+        traffic, valu_util, pmc_key, pmc_build = None, None, None, None
         if os.path.exists(a.traffic_json):
             try:
                 tj = json.load(open(a.traffic_json))
@@ -804,17 +805,31 @@ def main():
                 ent = tj.get(key) or {}
                 traffic = ent.get("hbm_bytes_per_launch")
                 valu_util = ent.get("valu_issue_util")
+                pmc_build = ent.get("build_id")
                 pmc_key = key if ent else None
             except Exception:
-                traffic = valu_util = pmc_key = None
+                traffic = valu_util = pmc_key = pmc_build = None
         kern_s = kern_ms * 1e-3
+        stale = pmc_key is not None and pmc_build != _lib.build_id()
+        hbm_util = traffic / kern_s / (HBM_PEAK_GBS * 1e9) if traffic else None
+        # roofline.frac is the utilisation of the binding resource (VERDICT
+        # r03 item 1): the counter HBM bytes over this run's kernel time
+        # against 8 TB/s, or the VALU issue share of the chip's SIMD cycles,
+        # whichever is higher; the SURVEY.md 8d algorithmic (demand) figure
+        # moves to demand_frac (L1/L2 serve most of those bytes, so it can
+        # exceed 1)
+        phys = [(u, b) for u, b in ((hbm_util, "hbm"), (valu_util, "valu")) if u is not None]
+        binding = max(phys) if phys else (None, None)
         util = {
-            "hbm_util": round(traffic / kern_s / (HBM_PEAK_GBS * 1e9), 4) if traffic else None,
+            "hbm_util": round(hbm_util, 4) if hbm_util is not None else None,
             "valu_issue_util": valu_util,
-            "util_source": (f"profiles/pmc_traffic.json[{pmc_key}]: HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, "
+            "util_source": (("STALE (measured on build " + str(pmc_build)[:16] + ", not this library): " if stale else "")
+                            + f"profiles/pmc_traffic.json[{pmc_key}]: HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, "
                             "MI355X_MICROARCH.md) / this run's kernel time / 8 TB/s; SQ_INSTS_VALU x 2 cycles / "
                             "(1,024 SIMDs x GRBM_GUI_ACTIVE / 8)") if pmc_key else
                            "no committed PMC passes for this configuration",
+            "util_build_id": pmc_build,
+            "util_stale": stale if pmc_key else None,
         }
         res = {
             "metric": METRIC,
@@ -870,15 +885,25 @@ def main():
                 "counts_per_launch": {"leaf_tests": int(cnt[1]), "accept": int(cnt[2]), "hit_pixels": int(cnt[3]),
                                       "pixels": my_pix},
             } if a.mode == 1 else {
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                # the binding resource (see util above); with no committed
+                # counters for this configuration frac is null
+                "bound": binding[1] or "hbm",
+                "achieved": (round(traffic / kern_s / 1e9, 1) if binding[1] == "hbm" else
+                             round(valu_util * VALU_PEAK_TFLOPS, 2) if binding[1] == "valu" else None),
+                "peak": VALU_PEAK_TFLOPS if binding[1] == "valu" else HBM_PEAK_GBS,
+                "unit": "T VALU lane-ops/s" if binding[1] == "valu" else "GB/s",
+                "frac": round(binding[0], 4) if binding[0] is not None else None,
+                "frac_rule": "max(hbm_util, valu_issue_util): counter HBM bytes per launch / kernel time / 8 TB/s, or "
+                             "the VALU issue share (SQ_INSTS_VALU x 2 cycles over 1,024 SIMDs' cycles); a VALU "
+                             "wave64 instruction is 64 lane-ops, 1,024 SIMDs x 2.4 GHz x 64 / 2 = 78.6 T/s",
                 "traffic": traffic,
                 **util,
-                **({"frac_excl_root_misses": round((bytes_per_launch - B_INT * (my_pix - root_passes)) / kern_s / 1e9
-                                                   / HBM_PEAK_GBS, 4),
+                "demand_achieved": round(achieved, 1),
+                "demand_frac": round(achieved / HBM_PEAK_GBS, 4),
+                "demand_unit": "GB/s of SURVEY.md 8d algorithmic bytes (every visited record counted per visit; "
+                               "L1/L2 serve most of them, so this can exceed 1)",
+                **({"demand_frac_excl_root_misses": round((bytes_per_launch - B_INT * (my_pix - root_passes)) / kern_s
+                                                          / 1e9 / HBM_PEAK_GBS, 4),
                     "root_pass_pixels": root_passes} if root_passes is not None and not multi else {}),
                 "kernel": {1: "k_trace_kd", 2: "k_trace_kd2", 3: "k_trace_kd3"}[a.kernel] if a.mode == 0
                           else "k_trace_flat",
@@ -899,8 +924,8 @@ def main():
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 # with frames in flight, launches overlap: the bytes of one
                 # frame over the frame period (elapsed / steps) as well
-                "achieved_per_frame_period": round(bytes_per_launch / (elapsed / a.steps) / 1e9, 1),
-                "frac_per_frame_period": round(bytes_per_launch / (elapsed / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
+                "demand_achieved_per_frame_period": round(bytes_per_launch / (elapsed / a.steps) / 1e9, 1),
+                "demand_frac_per_frame_period": round(bytes_per_launch / (elapsed / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
                 "counts_per_launch": {"interior": int(cnt[0]), "leaf": int(cnt[1]), "accept": int(cnt[2]),
                                       "hit_pixels": int(cnt[3]), "pixels": my_pix},
                 **({"counts_full_shadow_walk": {"interior": int(full_walk[0]), "leaf": int(full_walk[1]),

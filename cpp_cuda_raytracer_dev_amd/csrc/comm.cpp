@@ -15,9 +15,12 @@
 //
 // RCCL is resolved at run time (dlopen of librccl.so.1): a process that
 // already holds PyTorch's RCCL gets that same library (dlopen matches the
-// soname), otherwise ROCm's.  Nothing here runs without a GPU, and the
+// soname), otherwise ROCm's; the environment variable RT_RCCL_LIB names
+// another library with the same entry points (the test-only shim of
+// tests/rccl_shim, which runs N ranks as threads of one process).  Nothing here runs without a GPU, and the
 // library loads on machines without RCCL (rt_comm_* then fail loudly).
 #include <dlfcn.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <mutex>
@@ -56,8 +59,11 @@ std::once_flag g_rccl_once;
 const Rccl* rccl() {
     std::call_once(g_rccl_once, [] {
         const char* names[] = {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"};
-        void* so = dlopen(names[0], RTLD_NOW | RTLD_NOLOAD);
-        for (int k = 0; !so && k < 3; ++k) so = dlopen(names[k], RTLD_NOW | RTLD_LOCAL);
+        // RT_RCCL_LIB: an explicit library instead (tests/rccl_shim: N ranks
+        // as threads of one process on one GPU); it must load, no fallback
+        const char* over = getenv("RT_RCCL_LIB");
+        void* so = over && *over ? dlopen(over, RTLD_NOW | RTLD_LOCAL) : dlopen(names[0], RTLD_NOW | RTLD_NOLOAD);
+        for (int k = 0; !so && !(over && *over) && k < 3; ++k) so = dlopen(names[k], RTLD_NOW | RTLD_LOCAL);
         if (!so) return;
         Rccl r;
         r.so = so;

@@ -234,8 +234,9 @@ int rt_unpack_bands(int device, int32_t w, int32_t h, int32_t nranks,
  * same resolution and options on every rank (message sizes are derived, not
  * exchanged; distributed.NativeFrameGather.verify checks this once).  A rank
  * with no part in the rectangle sends nothing, and rank 0 posts no receive
- * for it.  RCCL is loaded at run time (librccl.so.1); rt_comm_available()
- * says whether it was found. */
+ * for it.  RCCL is loaded at run time (librccl.so.1, or the library the
+ * environment variable RT_RCCL_LIB names, read once per process: the tests'
+ * in-process shim); rt_comm_available() says whether it was found. */
 #define RT_COMM_ID_BYTES 128
 typedef struct rt_comm rt_comm;
 int rt_comm_available(void);

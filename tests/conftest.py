@@ -24,6 +24,8 @@ def _built():
     # this tree's (build.source_id); build_lib recompiles only stale objects
     if not os.path.exists(_lib.LIB_PATH) or _embedded_id(_lib.LIB_PATH) != build.source_id():
         build.build_lib()
+    from tests.rccl_shim import build as shim  # the test-only RCCL stand-in (test_shim_ranks_gather)
+    shim.build()
     yield
 
 

@@ -53,7 +53,12 @@ def main():
         counters.update(c)
         n.update(m)
     data = json.load(open(out_path)) if os.path.exists(out_path) else {}
-    entry = {"kernel": kernel_sub, "counters_per_dispatch": counters, "dispatches": n}
+    sys.path.insert(0, ROOT)
+    from cpp_cuda_raytracer_dev_amd import build
+    # the library the passes measured: this tree's (the binding refuses any
+    # other), so bench.py can tell a stale entry from a current one
+    entry = {"kernel": kernel_sub, "counters_per_dispatch": counters, "dispatches": n,
+             "build_id": build.source_id()}
     if valu_util is not None:
         entry["valu_issue_util"] = round(valu_util, 4)
     if "FETCH_SIZE" in counters and "WRITE_SIZE" in counters:
