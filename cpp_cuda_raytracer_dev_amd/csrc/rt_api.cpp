@@ -141,7 +141,8 @@ struct rt_camera {
     int frames_since = 0;
     uint64_t layout_gen = 0, cost_gen = 0;   // fine-grid generation, and the one h_cost was read for
     uint64_t order_gen = ~0ull;              // generation whose cost order d_order holds
-    int32_t order_split = 0;                 // split tiles at the head of that cost order
+    int32_t order_split = 0;                 // split tiles after the coop tiles of that cost order
+    int32_t order_coop = 0;                  // coop tiles at the head of that cost order
     int rays = 0;                    // kOptRays: pixels per wave of kernel 3 (0: auto_rays)
     int last_rays = 0;               // the pixels per wave the last kernel-3 render used
     int items = 2;                   // kOptItems: items per lane per pool iteration
@@ -386,6 +387,7 @@ int ensure_order(rt_camera* c, const TraceParams& p, hipStream_t st) {
     c->d_order = o.d;
     c->order_gen = ~0ull;  // no cost order for this grid yet
     c->order_split = 0;    // nor split tiles
+    c->order_coop = 0;     // nor coop tiles
     std::copy(key, key + 8, c->order_key);
     c->centre.swap(order);
     c->layout_gen++;
@@ -567,6 +569,21 @@ constexpr int64_t kSplitMaxTiles = RT_SPLIT_MAX_TILES;
 #ifndef RT_SPLIT8
 #define RT_SPLIT8 1
 #endif
+// coop tiles: cost > RT_COOP_PCT % of the top (grids of fewer than
+// kSplitMaxTiles tiles; RT_COOP_PCT_LARGE % for larger ones), at most
+// n / RT_COOP_CAP_DIV and RT_COOP_MAX tiles (each takes 4 blocks)
+#ifndef RT_COOP_PCT
+#define RT_COOP_PCT 60
+#endif
+#ifndef RT_COOP_PCT_LARGE
+#define RT_COOP_PCT_LARGE 70
+#endif
+#ifndef RT_COOP_CAP_DIV
+#define RT_COOP_CAP_DIV 8
+#endif
+#ifndef RT_COOP_MAX
+#define RT_COOP_MAX 256
+#endif
 
 int cost_feedback(rt_camera* c, const TraceParams& p, void* stream, int set) {
     hipStream_t st = (hipStream_t)stream;
@@ -590,21 +607,34 @@ int cost_feedback(rt_camera* c, const TraceParams& p, void* stream, int set) {
         // end near the unsplit ones' (a unit's chain is mostly its items:
         // half the rays, about half the pool iterations); at most a quarter
         // of the tiles.  Debug bit 512: none.
-        int32_t split = 0;
+        // Coop tiles (kernel 3, 16- and 8-ray units): the tiles costlier than
+        // RT_COOP_PCT % of the heaviest (at most n / RT_COOP_CAP_DIV and
+        // RT_COOP_MAX) head the order and render each unit with a whole
+        // block on one pool (k_trace_kd3's trace_unit_coop); debug bit 2048:
+        // none.
+        int32_t split = 0, coop = 0;
+        auto cost_of = [&](int64_t t) {
+            uint32_t m = 0;
+            for (int k = 0; k < kCostSlots; k++) m = std::max(m, c->h_cost[kCostSlots * (size_t)t + k]);
+            return m;
+        };
+        const uint32_t top = n > 0 ? cost_of(ord[0]) : 0;
+        if (c->tile_order == 3 && (p.rays == 16 || p.rays == 8) && kd3_waves(p.rays) == 4 && !(c->debug & 2048) &&
+            n > 0 && RT_COOP_PCT > 0) {
+            const int64_t pct = n < kSplitMaxTiles ? RT_COOP_PCT : RT_COOP_PCT_LARGE;
+            while (coop < std::min<int64_t>(n / RT_COOP_CAP_DIV, RT_COOP_MAX) &&
+                   100ull * cost_of(ord[(size_t)coop]) > (uint64_t)pct * top && top >= 24)
+                coop++;
+            if (c->debug & 4096) coop = (int32_t)n;  // tests: every tile a coop tile
+        }
         if (c->tile_order == 3 && (p.rays == 16 || (p.rays == 8 && RT_SPLIT8)) && kd3_waves(p.rays) == 4 &&
             !(c->debug & 512) && n > 0 && (n < kSplitMaxTiles || RT_SPLIT_PCT_LARGE > 0)) {
             const uint64_t pct = n < kSplitMaxTiles ? RT_SPLIT_PCT : RT_SPLIT_PCT_LARGE;
-            auto cost_of = [&](int64_t t) {
-                uint32_t m = 0;
-                for (int k = 0; k < kCostSlots; k++) m = std::max(m, c->h_cost[kCostSlots * (size_t)t + k]);
-                return m;
-            };
-            const uint32_t top = cost_of(ord[0]);
-            while (split < n / RT_SPLIT_CAP_DIV && 100ull * cost_of(ord[(size_t)split]) > pct * top &&
+            while (coop + split < n / RT_SPLIT_CAP_DIV && 100ull * cost_of(ord[(size_t)(coop + split)]) > pct * top &&
                    top >= 24)
                 split++;
         }
-        same = same && split == c->order_split;
+        same = same && split == c->order_split && coop == c->order_coop;
         if (same && c->order_gen == c->layout_gen) return RT_OK;  // d_order already holds it
         int rc;
         // frames on other streams (frames in flight on the library's lanes,
@@ -629,6 +659,7 @@ int cost_feedback(rt_camera* c, const TraceParams& p, void* stream, int set) {
         c->cost_up_valid = true;
         c->order_pending = true;
         c->order_split = split;  // launches after this upload (stream order) use it
+        c->order_coop = coop;
         c->order_gen = c->layout_gen;
         return RT_OK;
     }
@@ -962,8 +993,8 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
     p.istamp = nullptr;
 #endif
     if (c->debug & 2) {
-        // (fine tiles twice: split tiles add a block each)
-        int64_t need = (2 * (int64_t)p.tiles_x * p.block_rows + p.coarse_blocks + p.fill_blocks) * 4 * 3;
+        // (fine tiles four times: a split tile adds a block, a coop tile three)
+        int64_t need = (4 * (int64_t)p.tiles_x * p.block_rows + p.coarse_blocks + p.fill_blocks) * 4 * 3;
         c->istamp_off = need;
 #if RT_ITER_STAMPS
         // debug bit 128: per-iteration stamps of every wave slot after the per-wave records
@@ -1520,6 +1551,14 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
     // behind its upload; other streams wait for it above)
     p.split = (p.order && p.order == c->d_order && p.cost && (p.rays == 16 || (p.rays == 8 && RT_SPLIT8)) &&
                !(c->debug & 512)) ? c->order_split : 0;
+    p.coop = (p.order && p.order == c->d_order && p.cost && (p.rays == 16 || p.rays == 8) && !(c->debug & 2048))
+                 ? c->order_coop : 0;
+    if (p.coop && (flags & RT_FLAG_SHADOW)) {
+        // shadow walks have no coop form: the coop tiles render as split
+        // tiles (halves) there, ahead of the order's split tiles
+        if (!(c->debug & 512)) p.split += p.coop;
+        p.coop = 0;
+    }
     int cset = 0;
     if (p.cost) {  // this stream's own cost set
         cset = cost_set(c, st);
@@ -1947,6 +1986,7 @@ extern "C" int rt_camera_get_option(const rt_camera* c, int32_t key, int32_t* va
     case kOptDebug: *value = c->debug; return RT_OK;
     case kOptStampOffset: *value = (int32_t)c->istamp_off; return RT_OK;
     case kOptSplitUsed: *value = c->order_split; return RT_OK;
+    case kOptCoopUsed: *value = c->order_coop; return RT_OK;
     case kOptShadowOrder: *value = c->shadow_order >= 0 ? c->shadow_order : c->any_best; return RT_OK;
     default: return fail(RT_ERR_INVALID, "rt_camera_get_option: unknown key %d", key);
     }

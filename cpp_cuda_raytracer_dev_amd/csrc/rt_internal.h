@@ -49,12 +49,15 @@ enum Option : int32_t {
     kOptShadowOrder = 6,  // kernel 3 any-hit push order 0..3, -1 = timed choice (default)
     kOptFlat = 7,       // flat-list kernel: 0 one triangle per iteration, 1 pairs, 2 packed pairs, 3 pipelined
     kOptRaysUsed = 8,   // get only: pixels per wave of the last kernel-3 render
-    kOptSplitUsed = 9,  // get only: split tiles at the head of the current cost order (kernel 3, 16 rays)
+    kOptSplitUsed = 9,  // get only: split tiles after the coop tiles of the current cost order (kernel 3)
+    kOptCoopUsed = 10,  // get only: coop tiles at the head of the current cost order (kernel 3)
     kOptDebug = 100,    // diagnostics: 1 = skip traversal, 2 = per-wave timestamps, 4 = every group
                         // coarse, 8 = coarse kernel on a side stream beside the fine one,
                         // 16 = counted shadow walks stop at occluders (the timed walk's work),
                         // 32 = counting renders stop after the root test, 128 = per-iteration
-                        // stamps (RT_ITER_STAMPS builds, with 2)
+                        // stamps (RT_ITER_STAMPS builds, with 2), 512 = no split tiles,
+                        // 1024 = no two-level iterations, 2048 = no coop tiles, 4096 = every
+                        // tile of a cost order a coop tile (tests)
     kOptPoolCap = 101,  // tests: shrink kernel 3's item pool (66..kPoolCap) to force its fallback
     kOptStampOffset = 102,  // get only: offset (u64) of the per-iteration stamps in the debug buffer
 };
@@ -133,7 +136,11 @@ struct TraceParams {
     int32_t rays;                  // pixels (rays) per wave: 64, 32 or 16
     int32_t tile_order;            // Option kOptTileOrder
     const int32_t* order;          // tile permutation (tile_order 2: centre-out, 3: by cost)
-    int32_t split;                 // kernel 3, 16 rays: order[0..split) render as two 8-ray halves
+    // kernel 3, tile order 3 (16- and 8-ray units): order[0..coop) render each
+    // unit with a whole block on one pool (4 blocks per tile), then
+    // order[coop..coop + split) as two halves (2 blocks per tile)
+    int32_t coop;
+    int32_t split;
     uint32_t* cost;                // tile_order 3: pool iterations per fine unit [tile][2], or null
     float root_box[6];             // camera-relative root AABB (t0x,t1x,t0y,t1y,t0z,t1z)
     int32_t pool_cap;              // kernel 3 item-pool capacity in use (<= kPoolCap)

@@ -88,7 +88,7 @@ int launch_trace(const TraceParams& p, uint32_t mode, uint32_t flags, int kernel
         // the coarse groups first, then the fine tiles (or just one of them)
         const bool coarse = pass == 0;
         if ((coarse && part == kPartFine) || (!coarse && part == kPartCoarse)) continue;
-        const unsigned grid = coarse ? (unsigned)p.coarse_blocks : fine + (unsigned)p.split + (unsigned)p.fill_blocks;
+        const unsigned grid = coarse ? (unsigned)p.coarse_blocks : fine + 3u * (unsigned)p.coop + (unsigned)p.split + (unsigned)p.fill_blocks;
         if (grid == 0) continue;
         TraceFn fn;
         if (tr) fn = wh ? (cnt ? kd_kernel_111(v, r, sh, coarse) : kd_kernel_110(v, r, sh, coarse))

@@ -1597,6 +1597,34 @@ struct Counts {
     uint32_t n_int = 0, n_leaf = 0, n_acc = 0, n_desc = 0, n_hit = 0;
 };
 
+// A traced pixel's output: Phong of its nearest hit (color_cam_cuda,
+// TD/Camera.cu:27-60), black when its shadow ray is occluded, else the
+// background; and the hit index.
+template <bool kWriteHit, bool kCount>
+__device__ __forceinline__ void shade_out(const TraceParams& P, const Pixel& px, const Ray& R, const float cam[3],
+                                          unsigned long long kbest, uint32_t best, bool shadowed, Counts& C) {
+    const float* X = P.xf;
+    uint32_t argb = kBackground;
+    if (shadowed) {
+        argb = 0x00000000u;  // point_rad stays 0: 0/0 -> (u8)NaN = 0 (H14)
+    } else if (best != kMiss) {
+        const float d = __uint_as_float((uint32_t)(kbest >> 32));
+        const float4 N = P.shade[2 * (size_t)best];
+        const float4 M = P.shade[2 * (size_t)best + 1];
+        const float pnt[3] = {d * R.rx + R.odx, d * R.ry + R.ody, d * R.rz + R.odz};
+        // norm.device_rotate(rot_m, i, -1), TD/vector.cuh:23-33
+        const float ax = -1 * N.x, ay = -1 * N.y, az = -1 * N.z;
+        const float nrm[3] = {(ax * X[0] + ay * X[1] + az * X[2]) * -1,
+                              (ax * X[4] + ay * X[5] + az * X[6]) * -1,
+                              (ax * X[8] + ay * X[9] + az * X[10]) * -1};
+        const float rad[3] = {M.x, M.y, M.z};
+        argb = phong(pnt, nrm, cam, rad);
+    }
+    put_pixel(P, px.out, argb, best != kMiss);
+    if (kWriteHit) P.hit[px.out] = best == kMiss ? (int64_t)-1 : (int64_t)best;
+    if (kCount && best != kMiss) C.n_hit++;
+}
+
 // One wave's unit of work: the kRays pixels (8 x kRays/8) of unit U.
 constexpr size_t kNoDbg = ~(size_t)0;
 constexpr int kCoarseMax = 32;  // coarse groups per wave (RT_OPT_COARSE <= 32)
@@ -1664,7 +1692,6 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
         live = unit_pixel(P, U, nrows, l2, px, ncols);
         camera_ray(P, px, live, cam, R);
     }
-    const float* X = P.xf;
     unsigned long long kbest = ~0ull;
     uint32_t best = kMiss;
     if (lane < kRays) {
@@ -1714,25 +1741,7 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
     if (cost && lane == 0) *cost = iters * (uint32_t)(kRays / (nrows * ncols));
     __builtin_amdgcn_wave_barrier();  // LDS of this unit is read; the next unit may overwrite it
     if (!live) return;
-    uint32_t argb = kBackground;
-    if (shadowed) {
-        argb = 0x00000000u;  // point_rad stays 0: 0/0 -> (u8)NaN = 0 (H14)
-    } else if (best != kMiss) {
-        const float d = __uint_as_float((uint32_t)(kbest >> 32));
-        const float4 N = P.shade[2 * (size_t)best];
-        const float4 M = P.shade[2 * (size_t)best + 1];
-        const float pnt[3] = {d * R.rx + R.odx, d * R.ry + R.ody, d * R.rz + R.odz};
-        // norm.device_rotate(rot_m, i, -1), TD/vector.cuh:23-33
-        const float ax = -1 * N.x, ay = -1 * N.y, az = -1 * N.z;
-        const float nrm[3] = {(ax * X[0] + ay * X[1] + az * X[2]) * -1,
-                              (ax * X[4] + ay * X[5] + az * X[6]) * -1,
-                              (ax * X[8] + ay * X[9] + az * X[10]) * -1};
-        const float rad[3] = {M.x, M.y, M.z};
-        argb = phong(pnt, nrm, cam, rad);
-    }
-    put_pixel(P, px.out, argb, best != kMiss);
-    if (kWriteHit) P.hit[px.out] = best == kMiss ? (int64_t)-1 : (int64_t)best;
-    if (kCount && best != kMiss) C.n_hit++;
+    shade_out<kWriteHit, kCount>(P, px, R, cam, kbest, best, shadowed, C);
 }
 
 __device__ __forceinline__ void count_flush(const TraceParams& P, const Counts& C) {
@@ -1968,6 +1977,280 @@ __device__ __forceinline__ unsigned long long coarse_root(const TraceParams& P, 
     return b;
 }
 
+// ---------------------------------------------------------------------------
+// Block-cooperative units.  A frame ends with the pool
+// chains of its heaviest units: 3,000-6,000 items popped at most 128 per
+// iteration by one wave (knot 1080p: 75 iterations for the heaviest 16-ray
+// unit, tools/sched_sim.c).  The host names the heaviest P.coop tiles of its
+// cost order (order[0..coop)); each of their units is rendered by a whole
+// 4-wave block popping ONE LDS pool: up to 4 x 128 items per iteration, and
+// two-level iterations while the pool holds at most 4 x 16 items -- the
+// simulated chain of the heaviest unit drops from 75 to 23 iterations (knot
+// 1080p), 24 to 18 (dragon 960x540, against the split 8-ray halves).
+//
+// One iteration: every wave takes its share of the top `take` items (wave w:
+// items base + 64w + lane, slot 1 base + 256 + 64w + lane), issues their
+// records, and meets the others at barrier A (every popped item is in
+// registers, and the shared push counter holds `base`); each wave then visits
+// its items and appends their children at offsets it reserves with one LDS
+// atomic add on the counter; barrier B, and every wave reads the new pool
+// size.  The visited (ray, node) items are the reference's whatever the pop
+// order, as in the per-wave pool.  Nearest-candidate bookkeeping stays per
+// wave (each wave its own (w, path code) minimum per ray, race-free as in the
+// per-wave pool); the unit's result is the minimum over the four rows, the
+// reference's winner (keys are unique per ray and leaf).
+// ---------------------------------------------------------------------------
+#ifndef RT_COOP
+#define RT_COOP 1
+#endif
+// a coop unit reports its tile's cost as at least popped / RT_COOP_COST_DIV
+// (see trace_unit_coop)
+#ifndef RT_COOP_COST_DIV
+#define RT_COOP_COST_DIV 64
+#endif
+constexpr int kCoopWaves = 4;
+
+template <int kRays, int kRayVec>
+struct CoopHead {
+    float2 ray[kRays * kRayVec * 2];
+    unsigned long long key[kCoopWaves][kRays];
+    uint32_t tri[kCoopWaves][kRays];
+    // pool size / push counter, double-buffered: iteration i pushes through
+    // top[i & 1] while a slow wave may still read top[(i - 1) & 1]
+    int32_t top[2];
+    int32_t pad[2];
+};
+
+// The coop pool takes the LDS of the block's four wave pools.
+template <int kRays, int kCap, int kRayVec>
+constexpr int coop_cap() {
+    return (int)((sizeof(WaveLds<kRays, kCap, kRayVec>) * kCoopWaves - sizeof(CoopHead<kRays, kRayVec>)) /
+                 sizeof(uint4));
+}
+
+template <int kRays, int kCap, int kRayVec>
+struct CoopLds {
+    uint4 items[coop_cap<kRays, kCap, kRayVec>()];
+    CoopHead<kRays, kRayVec> h;
+};
+
+// Workgroup barrier for the coop pool: this wave's LDS operations complete,
+// then s_barrier; the memory clobber keeps the compiler from moving LDS
+// accesses across it (outstanding global loads stay in flight).
+__device__ __forceinline__ void coop_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// `count` pool slots for this wave's pushes (wave-uniform count, all lanes
+// active): the offset of the first.
+__device__ __forceinline__ int coop_reserve(int32_t* top, int count, int lane) {
+    int at = 0;
+    if (count > 0 && lane == 0) at = atomicAdd(top, count);
+    return __builtin_amdgcn_readfirstlane(at);
+}
+
+// A two-level iteration (see two_level_iter) over the coop pool: wave w takes
+// items [16w, 16w + 16) of the n <= 64 pooled items, one quad per item;
+// pushes are reserved on the shared counter (reset to 0 by wave 0 before the
+// barrier, since the whole pool is popped).
+template <int kStride, bool kTranslated, bool kCount, bool kNoOff>
+__device__ __forceinline__ void two_level_coop(const TraceParams& P, uint4* items, int32_t* top, const float2* s_ray,
+                                               unsigned long long* s_key, uint32_t* s_tri, int n, int wv, int lane,
+                                               uint32_t& n_int, uint32_t& n_leaf, uint32_t& n_acc, uint32_t& n_desc) {
+    int l = lane;
+    asm volatile("" : "+v"(l));
+    const int k = wv * 16 + (l >> 2), role = l & 3;
+    bool act = k < n;
+    const uint4 it = items[act ? k : 0];
+    if (wv == 0 && lane == 0) *top = 0;
+    const uint32_t marked = it.w & kCodeMarkMask;
+    const bool interior = (it.x & kLeafBit) == 0;
+    const int depth = 31 - __builtin_clz(marked);
+    const bool el = act && interior && depth <= P.two_depth;
+    const bool child = (role == 1 || role == 2) && el;
+    const float4* pa = child ? P.inode + 4 * (2 * (size_t)it.x + (size_t)role) : record_of(P, it.x);
+    const float4 a0 = pa[0], a1 = pa[1], a2 = pa[2], a3 = pa[3];
+    coop_barrier();  // A: every wave holds its items; the pool may be overwritten
+    Ray Q;
+    float4 q2, q3, q4;
+    ray_of<kTranslated, kStride>(s_ray + (size_t)(it.w >> 26), Q, q2, q3, q4);
+    float at0, at1, bt0, bt1;
+    slab_vals<kNoOff>(Q, a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, at0, at1);
+    slab_vals<kNoOff>(Q, a1.z, a1.w, a2.x, a2.y, a2.z, a2.w, bt0, bt1);
+    const float xl0 = quad_bcast0(at0), xl1 = quad_bcast0(at1), xr0 = quad_bcast0(bt0), xr1 = quad_bcast0(bt1);
+    const float t0 = role == 0 ? __uint_as_float(it.y) : role == 1 ? xl0 : xr0;
+    const float t1 = role == 0 ? __uint_as_float(it.z) : role == 1 ? xl1 : xr1;
+    Order o;
+    order_node<kTranslated, kCount>(q2, q3, q4, t0, t1, a3, at0, at1, bt0, bt1, false, o, n_int, n_desc);
+    const uint32_t fl = quad_bcast0((o.left_first ? 1u : 0u) | (o.ka ? 2u : 0u) | (o.kb ? 4u : 0u));
+    const bool lfirst = (fl & 1u) != 0;
+    const bool is_first = (role == 1) == lfirst;
+    const bool kept = child && ((fl & (is_first ? 2u : 4u)) != 0);
+    const bool real = role == 0 ? (act && interior) : kept;
+    if (kCount && real) count_order(o, n_int, n_desc);
+    const bool push = role == 0 ? (act && interior && !el) : kept;
+    const uint32_t code = role == 0 ? marked : ((marked << 1) | (is_first ? 0u : 1u));
+    const uint32_t meta = ((it.w >> 26) << 26) | (code << 1);
+    const bool p1 = push && o.ka, p2 = push && o.kb;
+    const unsigned long long m1 = __ballot(p1), m2 = __ballot(p2);
+    const int n1 = __builtin_popcountll(m1);
+    const int at = coop_reserve(top, n1 + __builtin_popcountll(m2), lane);
+    if (p1) items[at + (int)lanes_below(m1)] = make_uint4(o.first, __float_as_uint(o.f0), __float_as_uint(o.f1), meta);
+    if (p2)
+        items[at + n1 + (int)lanes_below(m2)] =
+            make_uint4(o.second, __float_as_uint(o.g0), __float_as_uint(o.g1), meta | 1u);
+    {
+        Visit v;
+        v.ka = v.kb = false; v.cand = false;
+        if (role == 0 && act && !interior) visit_leaf<kTranslated, kCount, false>(Q, q4, it, a0, a1, a2, a3, v, n_leaf, n_acc);
+        record_candidate<false>(s_key, s_tri, it, v);
+    }
+}
+
+// The coop pool walk of one unit (nearest hit; every wave of the block runs
+// it, the loop is uniform across them since n is read from LDS after each
+// barrier B).  Returns the iterations and items popped.
+template <int kCap, int kStride, bool kTranslated, bool kCount, bool kNoOff>
+__device__ __forceinline__ void pool_walk_coop(const TraceParams& P, uint4* items, int32_t* tops, const float2* s_ray,
+                                               unsigned long long* s_key, uint32_t* s_tri, int n, int wv, int lane,
+                                               uint32_t& iters, uint32_t& popped, uint32_t& n_int, uint32_t& n_leaf,
+                                               uint32_t& n_acc, uint32_t& n_desc) {
+    const int cap = min(kCoopWaves * P.pool_cap, kCap);
+    const int slack = P.tree_height + 1;
+    constexpr int per = kCoopWaves * 128;
+    int par = 0;  // tops[0] holds the seeded size
+    while (n > 0) {
+        iters++;
+        par ^= 1;
+        int32_t* top = tops + par;
+        if (RT_TWO_LEVEL && n <= kCoopWaves * RT_TWO_MAX && P.two_depth >= 0 && 4 * n <= cap - slack) {
+            popped += (uint32_t)n;
+            two_level_coop<kStride, kTranslated, kCount, kNoOff>(P, items, top, s_ray, s_key, s_tri, n, wv, lane, n_int,
+                                                                n_leaf, n_acc, n_desc);
+        } else {
+            int take = min(min(n, per), cap - slack - n);
+            if (take < 1) take = 1;
+            popped += (uint32_t)take;
+            const int base = n - take;
+            const int i0 = wv * 64 + lane, i1 = kCoopWaves * 64 + wv * 64 + lane;
+            const bool act0 = i0 < take, act1 = i1 < take;
+            const uint4 it0 = items[base + (act0 ? i0 : 0)];
+            const uint4 it1 = items[base + (act1 ? i1 : 0)];
+            if (wv == 0 && lane == 0) *top = base;
+            const float4* p0 = record_of(P, it0.x);
+            const float4* p1 = record_of(P, it1.x);
+            const float4 a0 = p0[0], a1 = p0[1], a2 = p0[2], a3 = p0[3];
+            const bool two = kCoopWaves * 64 + wv * 64 < take;  // wave-uniform: this wave's slot 1 holds items
+            const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            float4 b0 = z, b1 = z, b2 = z, b3 = z;
+            if (two) { b0 = p1[0]; b1 = p1[1]; b2 = p1[2]; b3 = p1[3]; }
+            coop_barrier();  // A: every wave holds its items; the counter holds base
+            {
+                Visit v0;
+                v0.ka = v0.kb = false; v0.cand = false;
+                if (act0)
+                    visit_item<kStride, kTranslated, kCount, false, kNoOff>(s_ray + (size_t)(it0.w >> 26), it0, a0, a1,
+                                                                           a2, a3, v0, n_int, n_leaf, n_acc, n_desc);
+                record_candidate<false>(s_key, s_tri, it0, v0);
+                const int c0 = __builtin_popcountll(__ballot(v0.ka)) + __builtin_popcountll(__ballot(v0.kb));
+                push_children<false, 0>(items, coop_reserve(top, c0, lane), v0);
+            }
+            if (two) {
+                Visit v1;
+                v1.ka = v1.kb = false; v1.cand = false;
+                if (act1)
+                    visit_item<kStride, kTranslated, kCount, false, kNoOff>(s_ray + (size_t)(it1.w >> 26), it1, b0, b1,
+                                                                           b2, b3, v1, n_int, n_leaf, n_acc, n_desc);
+                record_candidate<false>(s_key, s_tri, it1, v1);
+                const int c1 = __builtin_popcountll(__ballot(v1.ka)) + __builtin_popcountll(__ballot(v1.kb));
+                push_children<false, 0>(items, coop_reserve(top, c1, lane), v1);
+            }
+        }
+        coop_barrier();  // B: every push has landed
+        n = __builtin_amdgcn_readfirstlane(*(volatile int32_t*)top);
+        if (n > cap) {  // unreachable by the pop rule; guard anyway (uniform)
+            if (lane == 0 && wv == 0) atomicOr(P.err, 2);
+            break;
+        }
+    }
+}
+
+// One unit rendered by the whole block (all kCoopWaves waves call it).
+template <int kRays, int kCap, int kRayVec, bool kTranslated, bool kWriteHit, bool kCount>
+__device__ __forceinline__ void trace_unit_coop(const TraceParams& P, CoopLds<kRays, kCap, kRayVec>& S,
+                                                const Unit& U, int wv, int lane, size_t dbg_slot, uint32_t* cost,
+                                                Counts& C) {
+    using RL = RayLayout<kRays>;
+    constexpr int kCoopCap = coop_cap<kRays, kCap, kRayVec>();
+    Pixel px;
+    bool live = unit_pixel(P, U, kRays / 8, lane, px);
+    const unsigned long long t_start = P.dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    uint32_t iters = 0, popped = 0;
+    int n = 0;
+    bool no_off;
+    {
+        float cam0[3];
+        Ray R0;
+        camera_ray(P, px, live, cam0, R0);
+        no_off = !kTranslated && __ballot(live && !(fabsf(R0.rx) > 0.0f && fabsf(R0.ry) > 0.0f &&
+                                                    fabsf(R0.rz) > 0.0f)) == 0ull;
+        if (lane < kRays) {
+            S.h.key[wv][lane] = ~0ull;
+            S.h.tri[wv][lane] = kMiss;
+        }
+        if (wv == 0) {
+            if (lane < kRays) store_ray(&S.h.ray[lane], RL::kStride, R0, kTranslated, 0.0f, 0u);
+            n = seed_root<kCount>(P, S.items, R0, live, lane, C.n_int, C.n_desc);
+            if (kCount && (P.debug & 32)) n = 0;
+            if (lane == 0) S.h.top[0] = n;
+        }
+    }
+    coop_barrier();
+    n = __builtin_amdgcn_readfirstlane(*(volatile int32_t*)&S.h.top[0]);
+    if (RT_NO_OFF && !kTranslated && no_off)
+        pool_walk_coop<kCoopCap, RL::kStride, kTranslated, kCount, true>(P, S.items, S.h.top, S.h.ray, S.h.key[wv],
+                                                                        S.h.tri[wv], n, wv, lane, iters, popped,
+                                                                        C.n_int, C.n_leaf, C.n_acc, C.n_desc);
+    else
+        pool_walk_coop<kCoopCap, RL::kStride, kTranslated, kCount, false>(P, S.items, S.h.top, S.h.ray, S.h.key[wv],
+                                                                         S.h.tri[wv], n, wv, lane, iters, popped,
+                                                                         C.n_int, C.n_leaf, C.n_acc, C.n_desc);
+    // every candidate of every wave has landed (the walk ends after a barrier
+    // B); wave 0 shades the unit
+    if (wv != 0) return;
+    if (P.dbg && lane == 0 && dbg_slot != kNoDbg) {
+        P.dbg[3 * dbg_slot] = t_start;
+        P.dbg[3 * dbg_slot + 1] = __builtin_amdgcn_s_memrealtime();
+        P.dbg[3 * dbg_slot + 2] = iters | ((unsigned long long)popped << 32);
+    }
+    // the tile's cost in the per-wave pool's terms (its iterations), so the
+    // cost order does not change with the rendering: at least this walk's
+    // iterations, and the items a single wave would pop at ~64 per iteration
+    // (heavy 16-ray waves pop ~85: an over-estimate keeps a coop tile in the
+    // coop set rather than alternating)
+    if (cost && lane == 0) *cost = max(iters, (popped + RT_COOP_COST_DIV - 1) / RT_COOP_COST_DIV);
+    float cam[3];
+    Ray R;
+    {
+        int32_t l2 = lane;
+        asm volatile("" : "+v"(l2));
+        live = unit_pixel(P, U, kRays / 8, l2, px);
+        camera_ray(P, px, live, cam, R);
+    }
+    unsigned long long kbest = ~0ull;
+    uint32_t best = kMiss;
+    if (lane < kRays) {
+#pragma unroll
+        for (int w = 0; w < kCoopWaves; w++) {
+            const unsigned long long k = S.h.key[w][lane];
+            if (k < kbest) {
+                kbest = k;
+                best = S.h.tri[w][lane];
+            }
+        }
+    }
+    if (!live) return;
+    shade_out<kWriteHit, kCount>(P, px, R, cam, kbest, best, false, C);
+}
+
 // kRays pixels per wave (64: 8x8; 32: 8x4; 16: 8x2; 8: 8x1): fewer rays per wave
 // spread a heavy tile's items over more SIMDs, the other lanes only help.
 // kShadow: a second pool walk traces one shadow ray per hit (SURVEY.md §8a
@@ -1997,12 +2280,15 @@ __global__ RT_KD3_BOUNDS(64 * kd3_waves(kRays)) void k_trace_kd3(TraceParams P) 
     __shared__ WaveLds<kRays, kCap, kRayVec> s_lds[kWaves];
     const int wv = wave_id(), lane = (int)threadIdx.x & 63;
     Counts C;
-    const int32_t b = (int32_t)blockIdx.x;
     const int32_t ntiles = P.tiles_x * P.block_rows;
-    if (b >= ntiles + P.split) {
+    // blocks: 4 per coop tile, 2 per split tile, 1 per other fine tile, then
+    // the far fill
+    const int32_t head = 3 * P.coop + P.split;
+    int32_t b = (int32_t)blockIdx.x;
+    if (b >= ntiles + head) {
         // fused far fill: blocks after the fine tiles write the coarse groups,
         // all far by construction (set_fine_region); unrolled as in k_coarse_kd3
-        const int32_t j0 = ((b - ntiles - P.split) * kWaves + wv) * P.coarse_per_wave;
+        const int32_t j0 = ((b - ntiles - head) * kWaves + wv) * P.coarse_per_wave;
         const int32_t j1 = min(j0 + P.coarse_per_wave, (int32_t)P.coarse_groups);
         bool ok = true;
 #pragma unroll 8
@@ -2021,8 +2307,29 @@ __global__ RT_KD3_BOUNDS(64 * kd3_waves(kRays)) void k_trace_kd3(TraceParams P) 
     // units' pool chains; the other tiles follow.  (Quarters of the heaviest
     // tiles, four 4-ray units of a 16-ray unit, measured slower: dragon
     // 960x540 43.0-45.8k -> 38.0-39.4k FPS, r03s.)
+    // Coop tiles (the host's heaviest P.coop of its cost order, order[0..coop)):
+    // block 4k + u renders unit u of tile order[k] with all four waves.
+    if constexpr (RT_COOP && kWaves == kCoopWaves && kRays <= 16 && kShadow == 0) {
+        if (b < 4 * P.coop) {
+            const int32_t ti = P.order[b >> 2];
+            if ((uint32_t)ti >= (uint32_t)ntiles) {  // a stale order: never index past the grid
+                if (lane == 0 && wv == 0) atomicOr(P.err, 8);
+                return;
+            }
+            const int u = b & 3;
+            uint32_t* cost = P.cost ? P.cost + kCostSlots * (size_t)ti + u : nullptr;
+            if (cost && wv == 0 && lane == 0) cost[4] = 0u;  // no second half
+            static_assert(sizeof(CoopLds<kRays, kCap, kRayVec>) <= sizeof(s_lds), "coop pool exceeds the block's LDS");
+            trace_unit_coop<kRays, kCap, kRayVec, kTranslated, kWriteHit, kCount>(
+                P, *reinterpret_cast<CoopLds<kRays, kCap, kRayVec>*>(s_lds), unit_of_tile(P, ti, u), wv, lane,
+                (size_t)blockIdx.x * kWaves + wv, cost, C);
+            if (kCount) count_flush(P, C);
+            return;
+        }
+    }
+    b -= 4 * P.coop;  // the split tiles order[coop..coop + split), then the rest
     const bool split = b < 2 * P.split;
-    const int32_t ti = split ? P.order[b >> 1] : tile_index(P, b - P.split);
+    const int32_t ti = split ? P.order[P.coop + (b >> 1)] : tile_index(P, b - P.split + P.coop);
     if ((uint32_t)ti >= (uint32_t)ntiles) {  // a stale order: never index past the grid
         if (lane == 0) atomicOr(P.err, 8);
         return;
@@ -2038,7 +2345,7 @@ __global__ RT_KD3_BOUNDS(64 * kd3_waves(kRays)) void k_trace_kd3(TraceParams P) 
     if (split && kRays == 16) U.yin = (U.yin - wv * (kRays / 8)) + (b & 1) * kWaves + wv;
     if (split && kRays == 8) U.x0 += (b & 1) * 4;
     trace_unit<kRays, kCap, kRayVec, kTranslated, kWriteHit, kCount, kShadow>(
-        P, s_lds[wv], U, lane, (size_t)b * kWaves + wv, cost, C, split && kRays == 16 ? 1 : kRays / 8,
+        P, s_lds[wv], U, lane, (size_t)blockIdx.x * kWaves + wv, cost, C, split && kRays == 16 ? 1 : kRays / 8,
         split && kRays == 8 ? 4 : 8);
     if (kCount) count_flush(P, C);
 }

@@ -371,6 +371,76 @@ def test_split_tiles_same_frame(key, rays):
     assert s.cam.device_error(reset=True) == 0
 
 
+@pytest.mark.parametrize("key,rays,debug", [("dragon_960x540_m0", 0, 0), ("knot_960x540_m0", 0, 0),
+                                            ("knot_960x540_m0", 8, 0), ("dragon_1920x1080_m0", 0, 0),
+                                            ("knot_1920x1080_m0", 0, 0), ("dragon_960x540_m0", 0, 4096),
+                                            ("dragon_960x540_m0", 8, 4096), ("rabbit_70k_960x540_m0", 0, 4096),
+                                            ("tester_320x180_m0", 0, 4096)])
+def test_coop_tiles_same_frame(key, rays, debug):
+    """Block-cooperative units: once a cost sample has
+    arrived, the heaviest tiles of the cost order render each 16- or 8-ray
+    unit with a whole 4-wave block on one LDS pool (RT_OPT_COOP_USED > 0);
+    debug bit 4096 makes every tile a coop tile.  The frame and hit buffer
+    stay the oracle's (committed hashes), and a counting render's visit
+    counters equal the oracle's."""
+    import hashlib
+    import torch
+    from cpp_cuda_raytracer_dev_amd import _lib
+    ent = H.frame_hashes()[key]
+    if not H.mesh_matches(ent):
+        pytest.skip("stand-in mesh bits differ on this host")
+    w, h = ent["w"], ent["h"]
+    s = H.GpuScene(ent["scene"], w, h, rays=rays, debug=debug or None)
+    dev = torch.device("cuda:0")
+    out = torch.zeros(w * h, dtype=torch.int32, device=dev)
+    hit = torch.zeros(w * h, dtype=torch.int64, device=dev)
+    st = torch.cuda.Stream(device=dev)
+    for _ in range(64):
+        s.cam.render_into(out, hit, flags=R.RT_FLAG_WRITE_HIT, stream=st.cuda_stream)
+    torch.cuda.synchronize()
+    assert s.cam.get_option(_lib.RT_OPT_COOP_USED) > 0
+    out.fill_(0x7BADBEEF)
+    s.cam.render_into(out, hit, flags=R.RT_FLAG_WRITE_HIT, stream=st.cuda_stream)
+    torch.cuda.synchronize()
+    argb = out.cpu().numpy().view(np.uint32)
+    assert hashlib.sha256(argb.tobytes()).hexdigest() == ent["argb_sha"], key
+    assert hashlib.sha256(hit.cpu().numpy().tobytes()).hexdigest() == ent["hit_sha"], key
+    s.cam.render_into(out, hit, flags=R.RT_FLAG_WRITE_HIT | R.RT_FLAG_COUNT, stream=st.cuda_stream)
+    torch.cuda.synchronize()
+    _counters_match(s.cam.counters(reset=True), ent["counters"], 3)
+    assert hashlib.sha256(out.cpu().numpy().view(np.uint32).tobytes()).hexdigest() == ent["argb_sha"], key
+    assert s.cam.device_error(reset=True) == 0
+
+
+@pytest.mark.parametrize("pose", [1, 3, 4])
+def test_coop_tiles_moved_pose(pose):
+    """Coop tiles under an object transform (the translated kernel instance,
+    coarse far groups): every tile a coop tile (debug 4096) and the default
+    selection, against the oracle at the pose; also with the item pool shrunk
+    so the coop walk's single-pop fallback runs."""
+    import torch
+    from cpp_cuda_raytracer_dev_amd import _lib
+    xfs = {1: _rot_y(3.0), 3: _rot_y(-4.0, (0.01, 0.0, 0.0)), 4: _rot_y(1.5, (0.0, 0.004, 0.0))}
+    xf = np.asarray(xfs[pose], np.float32).reshape(12)
+    w, h = 960, 540
+    oargb, ohit, _ = H.oracle_render("dragon", w, h, 0, xform=xf.reshape(3, 4))
+    dev = torch.device("cuda:0")
+    for debug, cap in ((4096, 0), (0, 0), (4096, 89)):
+        s = H.GpuScene("dragon", w, h, debug=debug or None)
+        if cap:
+            s.cam.set_option(_lib.RT_OPT_POOL_CAP, cap)
+        out = torch.zeros(w * h, dtype=torch.int32, device=dev)
+        hit = torch.zeros(w * h, dtype=torch.int64, device=dev)
+        st = torch.cuda.Stream(device=dev)
+        for _ in range(40):
+            s.cam.render_into(out, hit, xform=xf, flags=R.RT_FLAG_WRITE_HIT, stream=st.cuda_stream)
+        torch.cuda.synchronize()
+        assert s.cam.get_option(_lib.RT_OPT_COOP_USED) > 0
+        _assert_same((out.cpu().numpy().view(np.uint32), hit.cpu().numpy()), (oargb, ohit),
+                     f"pose {pose} debug {debug} cap {cap}")
+        assert s.cam.device_error(reset=True) == 0
+
+
 @pytest.mark.parametrize("w,h", [(960, 540), (1920, 1080)])
 @pytest.mark.parametrize("kernel,order,rays", KERNELS)
 def test_dragon_standin_kd(w, h, kernel, order, rays):

@@ -198,6 +198,10 @@ int main(int argc, char** argv) {
     const int three_max = tm3 ? atoi(tm3) : 8;
     const char* tcs = getenv("TL_COST");
     tl_cost = tcs ? atof(tcs) : 1.6;
+    /* BLOCK_WAVES=W: a block of W waves pops one shared pool (W x 128 items
+     * per iteration; cap is then the block's pool) */
+    const char* bws = getenv("BLOCK_WAVES");
+    const int bw = bws ? atoi(bws) : 1;
     float* pts; uint32_t n; orc_leaf* lf;
     if (orc_read_ply(mesh, mode, &pts, &n, &lf)) { fprintf(stderr, "read fail\n"); return 1; }
     orc_node* nodes = (orc_node*)malloc(sizeof(orc_node) * (2 * (size_t)n - 1));
@@ -223,8 +227,8 @@ int main(int argc, char** argv) {
     double* cost_of = (double*)calloc((size_t)nu, sizeof(double));
 #pragma omp parallel for schedule(dynamic, 64) reduction(+ : tot_items, tot_iters, mixed, slots, tot2, tot2s) reduction(max : peak)
     for (long long u = 0; u < nu; u++) {
-        item_t* st = (item_t*)malloc(sizeof(item_t) * 4096);
-        item_t pop[128], kid1[128], kid2[128];
+        item_t* st = (item_t*)malloc(sizeof(item_t) * 16384);
+        item_t pop[128 * 8], kid1[128], kid2[128];
         float rr[64][3];
         long long nst = 0, iters = 0, items = 0, iters2 = 0, iters_two_slot = 0;
         for (int l = 0; l < rays; l++) {
@@ -307,7 +311,7 @@ int main(int argc, char** argv) {
                 if (nst > peak) peak = nst;
                 continue;
             }
-            long long take = nst < 128 ? nst : 128;
+            long long take = nst < 128 * bw ? nst : 128 * bw;
             if (take > cap - slack - nst) take = cap - slack - nst;
             int lifo = policy == 0 || policy >= 4;
             if (take < 1) { take = 1; lifo = 1; }
@@ -332,7 +336,7 @@ int main(int argc, char** argv) {
             }
             iters++;
             if (take > 64) iters_two_slot++;
-            for (int sl = 0; sl < 2; sl++) {
+            for (int sl = 0; sl < 2 * bw; sl++) {
                 int n1 = 0, n2 = 0, nleaf = 0, nint = 0;
                 for (int k = sl * 64; k < take && k < sl * 64 + 64; k++) {
                     item_t it = pop[k];
