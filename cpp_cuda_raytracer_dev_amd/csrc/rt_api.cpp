@@ -745,6 +745,44 @@ bool root_rect(const FrameGeom& g, const TraceParams& p, double r[4]) {
     return true;
 }
 
+// Whether the (translated) root box lies behind the eye for every pixel's ray
+// (a moving object carried past the camera).  A pixel's
+// ray is R = X3 (n_mod + u_mod x + v_mod y), normalised by a positive factor,
+// and the slab test of TD/Trixel.cu:76-95 sees the box B + od from the
+// origin; if every corner c of B + od has c . R < 0, the whole box lies in
+// the half-space x . R < 0, so any t with t R in the box has t |R|^2 < 0: the
+// exact entry and exit parameters are negative and the test (maxt0 > -1e-16
+// and mint1 >= maxt0 - 1e-16) fails.  An axis the reference drops (0/0 = NaN
+// when a component of R is zero) leaves the projections on the other axes,
+// for which the same holds since R has no component on the dropped one.
+// R over the frame's pixels is a convex combination of the four corner
+// pixels' directions (affine in x, y, then linear), so testing the 8 x 4
+// corner pairs with a relative margin of 1e-4 (the kernel's rays deviate
+// from these by ~1e-6) covers every pixel.
+bool box_behind(const FrameGeom& g, const TraceParams& p) {
+    const float* X = p.xf;
+    double D[4][3];
+    for (int k = 0; k < 4; k++) {
+        const double fx = (k & 1) ? (double)(g.w - 1) : 0.0, fy = (k & 2) ? (double)(g.h - 1) : 0.0;
+        double cam[3];
+        for (int j = 0; j < 3; j++) cam[j] = (double)g.n_mod[j] + (double)g.u_mod[j] * fx + (double)g.v_mod[j] * fy;
+        for (int i = 0; i < 3; i++)
+            D[k][i] = (double)X[4 * i] * cam[0] + (double)X[4 * i + 1] * cam[1] + (double)X[4 * i + 2] * cam[2];
+    }
+    const double od[3] = {X[3], X[7], X[11]};
+    for (int m = 0; m < 8; m++) {
+        const double cc[3] = {p.root_box[(m & 1) ? 1 : 0] + od[0], p.root_box[(m & 2) ? 3 : 2] + od[1],
+                              p.root_box[(m & 4) ? 5 : 4] + od[2]};
+        const double cn = sqrt(cc[0] * cc[0] + cc[1] * cc[1] + cc[2] * cc[2]);
+        for (int k = 0; k < 4; k++) {
+            const double dn = sqrt(D[k][0] * D[k][0] + D[k][1] * D[k][1] + D[k][2] * D[k][2]);
+            const double dot = cc[0] * D[k][0] + cc[1] * D[k][1] + cc[2] * D[k][2];
+            if (!(dot < -1e-4 * cn * dn) || !std::isfinite(dot)) return false;
+        }
+    }
+    return true;
+}
+
 // Splits this rank's tiles into the fine region (one kRays unit per wave)
 // around the root box's screen rectangle and coarse 8x8 groups elsewhere
 // (`per_wave` to a wave; 0 = everything fine).
@@ -781,7 +819,7 @@ void find_tiny_groups(rt_camera* c) {
 // blocks; the fine region then covers every group that is not far, and
 // fusion is refused (returns false, region set as unfused) when a tiny-ray
 // group would fall outside it.
-bool set_fine_region(const FrameGeom& c, TraceParams& p, int per_wave, bool fused) {
+bool set_fine_region(const FrameGeom& c, TraceParams& p, int per_wave, bool fused, bool behind_ok = false) {
     const int32_t nbands = (c.h + kTileH - 1) / kTileH;
     const int32_t per_band = kTileH / p.tile_h;
     p.groups_x = (c.w + 7) / 8;
@@ -796,9 +834,25 @@ bool set_fine_region(const FrameGeom& c, TraceParams& p, int per_wave, bool fuse
     p.far_rect[0] = p.far_rect[2] = INT32_MIN / 2;
     p.far_rect[1] = p.far_rect[3] = INT32_MAX / 2;
     p.fill_blocks = 0;
+    p.far_all = 0;
     double r[4];
     // coarse groups are indexed in 32 bits (k_coarse_kd3)
-    if (per_wave <= 0 || (int64_t)p.nslots * p.groups_x >= ((int64_t)1 << 31) || !root_rect(c, p, r)) return false;
+    if (per_wave <= 0 || (int64_t)p.nslots * p.groups_x >= ((int64_t)1 << 31)) return false;
+    if (!root_rect(c, p, r)) {
+        if (!behind_ok || !box_behind(c, p)) return false;
+        // the box behind the eye for every pixel: no fine tiles, every group
+        // background (far_all), filled by the fine kernel's blocks under any
+        // transform
+        p.tiles_x = p.block_rows = 0;
+        p.cg_x0 = p.cg_x1 = 0;
+        p.cs0 = p.cs1 = 0;
+        p.coarse_per_wave = per_wave;
+        p.coarse_groups = (int64_t)p.nslots * p.groups_x;
+        const int64_t waves = (p.coarse_groups + per_wave - 1) / per_wave;
+        p.fill_blocks = (int32_t)((waves + kd3_waves(p.rays) - 1) / kd3_waves(p.rays));
+        p.far_all = 1;
+        return true;
+    }
     // r is the projection widened by a pixel; far groups lie 2 more outside
     auto clampi = [](double v) { return (int32_t)std::max(-1e9, std::min(1e9, v)); };
     p.far_rect[0] = clampi(r[0] - 2); p.far_rect[1] = clampi(r[1] + 2);
@@ -933,8 +987,9 @@ bool frame_geometry(const FrameGeom& g, const float* xform, const rt_tile* tile,
     // Far groups go to the fine kernel's extra blocks when every coarse group
     // can be far (identity transform, interior root, no diagnostics);
     // otherwise to k_coarse_kd3.
-    const bool fuse = kernel == 3 && p.plain_xf && !g.root_leaf && !(g.debug & (1 | 4 | 8));
-    return set_fine_region(g, p, kernel == 3 ? g.coarse : 0, fuse);
+    // A box behind the eye makes every group background under any transform.
+    const bool can_fuse = kernel == 3 && !g.root_leaf && !(g.debug & (1 | 4 | 8));
+    return set_fine_region(g, p, kernel == 3 ? g.coarse : 0, can_fuse && p.plain_xf, can_fuse);
 }
 
 // The geometry inputs of a device camera (its object prepared).
@@ -985,6 +1040,7 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
     p.tile_order = c->tile_order;
     p.order = nullptr;
     p.split = 0;
+    p.coop = 0;
     p.debug = c->debug;
     p.pool_cap = c->pool_cap;
     p.items = c->items;

@@ -132,6 +132,7 @@ struct TraceParams {
     int64_t coarse_groups;         // total coarse groups
     int32_t plain_xf;              // object transform is the identity (rotation 1, offset 0)
     int32_t far_rect[4];           // root box's screen rectangle + 2 px (x0, x1, y0, y1; frame pixels)
+    int32_t far_all;               // every group background: the box lies behind the eye (box_behind)
     int32_t tile_w, tile_h;        // pixels per block (tile_h divides the 8-row band)
     int32_t rays;                  // pixels (rays) per wave: 64, 32 or 16
     int32_t tile_order;            // Option kOptTileOrder

@@ -1917,10 +1917,12 @@ __device__ __forceinline__ bool ray_has_tiny_component(const TraceParams& P, int
 // writes it and returns true; otherwise returns false and writes nothing.
 template <bool kWriteHit, bool kCount>
 __device__ __forceinline__ bool fill_far(const TraceParams& P, const Unit& G, int lane, Counts& C) {
-    if (!far_group(P, G)) return false;
+    // P.far_all: the host proved the box behind the eye for every pixel
+    // (rt_api.cpp box_behind, any transform, zero components included)
+    if (!P.far_all && !far_group(P, G)) return false;
     Pixel px;
     const bool live = unit_pixel(P, G, 8, lane, px);
-    if (__ballot(live && ray_has_tiny_component(P, px.x, px.y)) != 0ull) return false;
+    if (!P.far_all && __ballot(live && ray_has_tiny_component(P, px.x, px.y)) != 0ull) return false;
     if (live) {
         put_pixel(P, px.out, kBackground, false);
         if (kWriteHit) P.hit[px.out] = (int64_t)-1;

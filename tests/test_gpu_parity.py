@@ -1386,3 +1386,59 @@ def test_shim_ranks_gather():
         assert g["device_err"] == [0] * g["nranks"], g
         assert all(s["equal"] for s in g["sets"]), g
         assert {s["pose"] for s in g["sets"]} - {0}, "a moved pose is checked"
+
+
+def test_far_along_key_sequence_background():
+    """bench.py --animate R+W.Q.T.W carries the object past
+    the camera after ~500 ticks (the oracle shows background only).  The host
+    then proves the box behind the eye for every pixel (rt_api.cpp
+    box_behind): no fine tiles, every group filled as background by the fine
+    kernel's blocks (far_all), and the N > 1 gather rectangle is empty.  The
+    frames equal the oracle's at those poses (and at poses where the object is
+    still in view, where the proof must not fire), for 1 and 4 ranks."""
+    import bench
+    import torch
+    from cpp_cuda_raytracer_dev_amd import _lib
+    from oracle import motion as M
+    from oracle import np_oracle as N
+    w, h = 640, 360
+    masks = bench.key_masks("R+W.Q.T.W")
+    cam = N.camera(w, h)
+    ref = M.Motion(cam["pos"], cam["n"], cam["u"])
+    s = H.GpuScene("dragon", w, h)
+    dev = torch.device("cuda:0")
+    out = torch.zeros(w * h, dtype=torch.int32, device=dev)
+    hit = torch.zeros(w * h, dtype=torch.int64, device=dev)
+    checked = {"visible": 0, "behind": 0}
+    for i in range(1201):
+        ref.tick(masks[i % len(masks)])
+        if i not in (10, 40, 120, 400, 600, 1200):
+            continue
+        xf = np.asarray(ref.xform(), np.float32).reshape(12)
+        oargb, ohit, _ = H.oracle_render("dragon", w, h, 0, xform=xf.reshape(3, 4))
+        out.fill_(0x7BADBEEF)
+        s.cam.render_into(out, hit, xform=xf, flags=R.RT_FLAG_WRITE_HIT)
+        torch.cuda.synchronize()
+        _assert_same((out.cpu().numpy().view(np.uint32), hit.cpu().numpy()), (oargb, ohit), f"tick {i}")
+        rect = np.zeros(4, np.int32)
+        _lib.call("rt_frame_rect", s.cam._h, _lib.ptr(xf), 0, 4, _lib.ptr(rect))
+        if (ohit >= 0).any():
+            checked["visible"] += 1
+            assert rect[1] > rect[0]
+        elif tuple(rect) == (0, 0, 0, 0):
+            checked["behind"] += 1
+        # the ranks' bands of the same pose
+        for r in range(4):
+            loc = torch.full((R.packed_pixels(w, h, 4),), 0x5EEDF00D, dtype=torch.int32, device=dev)
+            s.cam.render_into(loc, xform=xf, tile=(4, r))
+            torch.cuda.synchronize()
+            from cpp_cuda_raytracer_dev_amd.distributed import pack_bands_numpy
+            want = pack_bands_numpy(oargb, w, h, 4, r)
+            got = loc.cpu().numpy().view(np.uint32)
+            # rows of the slots that hold a band of the frame (slot j: band r + 4j)
+            rows = np.array([r + 4 * (y // 8) < (h + 7) // 8 and (r + 4 * (y // 8)) * 8 + y % 8 < h
+                             for y in range(len(got) // w)])
+            sel = np.repeat(rows, w)
+            assert (got[sel] == want[sel]).all(), f"tick {i} rank {r}"
+    assert checked["visible"] >= 2 and checked["behind"] >= 2, checked
+    assert s.cam.device_error(reset=True) == 0
