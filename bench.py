@@ -833,6 +833,11 @@ def main():
         }
         res = {
             "metric": METRIC,
+            #  the metric string is BASELINE.json's; since round 3
+            # the default workload is the knot stand-in, named in
+            # config.workload (the displaced-sphere blob is --scene dragon)
+            "metric_workload": (f"{a.scene}{' stand-in' if a.scene in scenes.STANDINS else ''} {w}x{h}"
+                                + ("" if a.view == "default" else f" {a.view} view")),
             "value": round(fps, 2),
             "unit": "frames/s",
             "mray_per_s": round(fps * rays_per_frame / 1e6, 2),

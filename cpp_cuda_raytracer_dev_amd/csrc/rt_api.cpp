@@ -129,6 +129,7 @@ struct rt_camera {
     uint32_t* d_cost = nullptr;      // [cost set][tile][kCostSlots] iterations
     int64_t cost_cap = 0;            // u32 per cost set
     hipStream_t cost_stream[RT_LOOP_MAX_LANES] = {};   // the stream that owns each cost set
+    bool cost_owned[RT_LOOP_MAX_LANES] = {};           // whether it is owned (the null stream can own one)
     int cost_next = 0;                                 // the set reclaimed next when all are owned
     hipEvent_t slot_join_ev[8] = {};  // cost-order upload: joins the streams that read the slot
     hipStream_t cost_up_stream = nullptr;   // the last cost-order upload's stream ...
@@ -530,9 +531,10 @@ std::vector<int32_t> cost_order(const rt_camera* c, const TraceParams& p, bool x
 // worst a dispatch order, never a frame).
 int cost_set(rt_camera* c, hipStream_t st) {
     for (int l = 0; l < RT_LOOP_MAX_LANES; l++)
-        if (c->cost_stream[l] == st) return l;
+        if (c->cost_owned[l] && c->cost_stream[l] == st) return l;
     for (int l = 0; l < RT_LOOP_MAX_LANES; l++)
-        if (!c->cost_stream[l]) {
+        if (!c->cost_owned[l]) {
+            c->cost_owned[l] = true;
             c->cost_stream[l] = st;
             return l;
         }
@@ -1734,6 +1736,9 @@ extern "C" int rt_camera_frame_geometry(rt_camera* c, rt_frame_geometry* out) {
     DeviceGuard g(c->device);
     int rc;
     if ((rc = prepare_camera_object(c))) return rc;
+    // the host rectangle (rt_frame_rect_host) assumes a KD tree, as the
+    // device rectangle does only when the scene has one
+    if (!c->obj->d_nodes) return fail(RT_ERR_STATE, "rt_camera_frame_geometry: the scene has no KD tree");
     const FrameGeom f = camera_geom(c);
     out->w = f.w;
     out->h = f.h;

@@ -142,7 +142,7 @@ struct TraceParams {
     // order[coop..coop + split) as two halves (2 blocks per tile)
     int32_t coop;
     int32_t split;
-    uint32_t* cost;                // tile_order 3: pool iterations per fine unit [tile][2], or null
+    uint32_t* cost;                // tile_order 3: pool iterations per fine unit [tile][kCostSlots], or null
     float root_box[6];             // camera-relative root AABB (t0x,t1x,t0y,t1y,t0z,t1z)
     int32_t pool_cap;              // kernel 3 item-pool capacity in use (<= kPoolCap)
     int32_t items;                 // kernel 3 items per lane per iteration (1 or 2)

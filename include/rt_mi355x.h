@@ -271,7 +271,8 @@ int rt_unpack_rect(int device, int32_t w, int32_t h, int32_t nranks, const int32
  * RT_OPT_RAYS, RT_OPT_COARSE, RT_OPT_DEBUG).  rt_frame_rect_host(g, ...)
  * equals rt_frame_rect(cam, ...) whenever rt_camera_frame_geometry(cam, g)
  * filled g, so every rank (any process, no GPU needed) derives the same
- * message sizes.  rt_pack_rect_host / rt_unpack_rect_host: rt_pack_rect /
+ * message sizes; rt_camera_frame_geometry fails with RT_ERR_STATE when the
+ * camera's scene has no KD tree (the host rectangle assumes one).  rt_pack_rect_host / rt_unpack_rect_host: rt_pack_rect /
  * rt_unpack_rect on host buffers (local0 distinct from frame). */
 typedef struct rt_frame_geometry {
     int32_t w, h;
@@ -308,7 +309,9 @@ void rt_comm_destroy(rt_comm* c);
  * already queued on render_stream / comm_stream, and those streams wait for
  * the lanes before the call returns.  Frames that share a buffer set are
  * ordered (a set is rendered again once its last frame, or its gather, is
- * done), so without comm nbuf must be a multiple of inflight.  Frames are
+ * done), so nbuf must be a multiple of inflight whenever inflight > 1, with or
+ * without comm (round 3 extended the rule to comm loops: a set is always
+ * rendered by the same lane, so its frames stay ordered).  Frames are
  * independent reads of the scene; a frame's tail overlaps the next frame's
  * start, where one frame leaves most CUs idle.  Timing events then bracket
  * renders that share the GPU with another frame. */
@@ -398,10 +401,19 @@ int rt_camera_info(const rt_camera* c, int32_t* w, int32_t* h, int32_t* max_dept
  * counting renders take 9). */
 #define RT_OPT_FLAT 7
 #define RT_OPT_RAYS_USED 8 /* get only: the pixels per wave the last kernel-3 render used */
-/* get only: tiles of the current cost order (tile order 3, 16-ray units)
- * rendered as two 8-ray halves: those costlier than half the heaviest tile,
- * at most a quarter of the tiles; the frame is the same either way. */
+/* get only: tiles of the current cost order (tile order 3, 16- and 8-ray
+ * units) rendered as two halves (a 16-ray unit as two 8-ray rows, an 8-ray
+ * unit as two 4-pixel halves): after the coop tiles, those costlier than 50 %
+ * of the heaviest tile in grids of fewer than 2,048 tiles and 75 % in larger
+ * ones, at most a quarter of the tiles counting the coop ones.  Costs are
+ * pool iterations per unit (8 slots per tile: the 4 units and the second
+ * halves).  The frame is the same either way. */
 #define RT_OPT_SPLIT_USED 9
+/* get only: tiles at the head of the current cost order whose units each
+ * render with a whole 4-wave block on one item pool (block-cooperative
+ * units): costlier than 60 % of the heaviest tile (70 % in grids of 2,048
+ * tiles or more), at most an eighth of the tiles; the frame is the same. */
+#define RT_OPT_COOP_USED 10
 int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value);
 int rt_camera_get_option(const rt_camera* c, int32_t key, int32_t* value);
 
