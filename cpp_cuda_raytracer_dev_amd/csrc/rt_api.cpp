@@ -2150,12 +2150,18 @@ extern "C" int rt_run_frames(rt_camera* c, rt_comm* comm, const rt_frame_loop* a
         }
         c->loop_ev.push_back(e);
     }
-    // lanes start after the caller's queued work (fork) ...
+    // lanes start after the caller's queued work (fork) ...  A stream with
+    // nothing queued needs no fork: its marker and the lanes' waits on it
+    // would only delay the first frame by a cross-queue hop (~10 us).
     if (L > 1) {
         hipEvent_t fork = c->lane_ev[0];
-        rc = hip_check(hipEventRecord(fork, rs), "lane fork");
-        for (int l = 0; !rc && l < L; l++) rc = hip_check(hipStreamWaitEvent(lane[l], fork, 0), "lane fork wait");
-        if (!rc && comm && (rc = hip_check(hipEventRecord(fork, cs), "lane fork")) == RT_OK)
+        rc = RT_OK;
+        if (hipStreamQuery(rs) != hipSuccess) {
+            rc = hip_check(hipEventRecord(fork, rs), "lane fork");
+            for (int l = 0; !rc && l < L; l++) rc = hip_check(hipStreamWaitEvent(lane[l], fork, 0), "lane fork wait");
+        }
+        if (!rc && comm && hipStreamQuery(cs) != hipSuccess &&
+            (rc = hip_check(hipEventRecord(fork, cs), "lane fork")) == RT_OK)
             rc = hip_check(hipStreamWaitEvent(gs, fork, 0), "lane fork wait");
         if (rc) {
             cleanup();
@@ -2222,20 +2228,15 @@ extern "C" int rt_run_frames(rt_camera* c, rt_comm* comm, const rt_frame_loop* a
         used[k] = true;
     }
     if (host_ms) *host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
-    // ... and the caller's streams wait for the lanes (join)
-    if (!rc && L > 1) {
-        for (int l = 0; l < L && !rc; l++) {
-            rc = hip_check(hipEventRecord(c->lane_ev[l], lane[l]), "lane join");
-            if (!rc) rc = hip_check(hipStreamWaitEvent(rs, c->lane_ev[l], 0), "lane join wait");
-        }
-        if (!rc && comm) {
-            rc = hip_check(hipEventRecord(c->lane_ev[RT_LOOP_MAX_LANES], gs), "lane join");
-            if (!rc) rc = hip_check(hipStreamWaitEvent(cs, c->lane_ev[RT_LOOP_MAX_LANES], 0), "lane join wait");
-        }
-    }
+    // ... and the call returns once every lane has drained: the lanes
+    // themselves are synchronised (a join into the caller's streams and a
+    // wait on those would add a cross-queue hop to the last frame), so the
+    // caller's later work is ordered after the loop
     c->nactive = 0;
-    if (!rc) rc = hip_check(hipStreamSynchronize(rs), "loop sync");
-    if (!rc && comm) rc = hip_check(hipStreamSynchronize(cs), "loop sync");
+    for (int l = 0; !rc && l < L; l++) rc = hip_check(hipStreamSynchronize(lane[l]), "loop sync");
+    if (!rc && comm) rc = hip_check(hipStreamSynchronize(gs), "loop sync");
+    if (!rc && L > 1) rc = hip_check(hipStreamSynchronize(rs), "loop sync");  // the fork's marker, if any
+    if (!rc && L > 1 && comm) rc = hip_check(hipStreamSynchronize(cs), "loop sync");
     if (rc) (void)hipDeviceSynchronize();  // nothing of this loop may still use the events
     cleanup();
     if (rc) return rc;

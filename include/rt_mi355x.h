@@ -306,8 +306,9 @@ void rt_comm_destroy(rt_comm* c);
  * renders on the library's render lane j % inflight (streams of the camera,
  * created once, each on a hardware queue of its own while queues are free),
  * the gather on the library's comm lane; the lanes start after the work
- * already queued on render_stream / comm_stream, and those streams wait for
- * the lanes before the call returns.  Frames that share a buffer set are
+ * already queued on render_stream / comm_stream (no fork when nothing is
+ * queued there), and every lane has drained when the call returns (it
+ * synchronises them).  Frames that share a buffer set are
  * ordered (a set is rendered again once its last frame, or its gather, is
  * done), so nbuf must be a multiple of inflight whenever inflight > 1, with or
  * without comm (round 3 extended the rule to comm loops: a set is always

@@ -23,6 +23,21 @@ OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd "$ROOT"
 export TMPDIR=/tmp
+# the pushed library must be this tree's build (rt_build_id); rebuild here if not
+python3 - <<'PYEOF' || { echo "stopping: library build failed"; exit 1; }
+import os, re, sys
+sys.path.insert(0, os.getcwd())
+from cpp_cuda_raytracer_dev_amd import _lib, build
+want = build.source_id()
+got = None
+if os.path.exists(_lib.LIB_PATH):
+    m = re.search(rb"generated-id:([0-9a-f]{64})", open(_lib.LIB_PATH, "rb").read())
+    got = m.group(1).decode() if m else None
+print("library build id", (got or "missing")[:16], "tree", want[:16], flush=True)
+if got != want:
+    print("rebuilding the library for this tree", flush=True)
+    build.build_lib()
+PYEOF
 while read -r name to rest; do
     [ -z "${name:-}" ] && continue
     case $name in \#*) continue ;; esac
