@@ -362,7 +362,9 @@ def test_split_tiles_same_frame(key, rays):
         s.cam.render_into(out, hit, flags=flags)
     torch.cuda.synchronize()
     assert s.cam.get_option(_lib.RT_OPT_RAYS_USED) == (rays or 16)
-    assert s.cam.get_option(_lib.RT_OPT_SPLIT_USED) > 0
+    # (since round 4 the heaviest tiles may be coop tiles instead; shadow
+    # renders take those as split tiles too)
+    assert s.cam.get_option(_lib.RT_OPT_SPLIT_USED) + s.cam.get_option(_lib.RT_OPT_COOP_USED) > 0
     s.cam.render_into(out, hit, flags=flags)
     torch.cuda.synchronize()
     argb = out.cpu().numpy().view(np.uint32)
