@@ -10,6 +10,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <mutex>
+#include <string>
 #include <vector>
 
 #include "rt_internal.h"
@@ -587,6 +589,21 @@ constexpr int64_t kSplitMaxTiles = RT_SPLIT_MAX_TILES;
 #define RT_COOP_MAX 256
 #endif
 
+// Experiments: a tuning constant from the environment (read once), else
+// the compiled default.  RT_TUNE_COOP_PCT, RT_TUNE_COOP_PCT_LARGE,
+// RT_TUNE_COOP_CAP_DIV, RT_TUNE_SPLIT_PCT, RT_TUNE_SPLIT_PCT_LARGE.
+int tune(const char* name, int dflt) {
+    static std::mutex m;
+    static std::vector<std::pair<std::string, int>> cache;
+    std::lock_guard<std::mutex> lk(m);
+    for (const auto& kv : cache)
+        if (kv.first == name) return kv.second;
+    const char* v = getenv(name);
+    const int x = v && *v ? atoi(v) : dflt;
+    cache.emplace_back(name, x);
+    return x;
+}
+
 int cost_feedback(rt_camera* c, const TraceParams& p, void* stream, int set) {
     hipStream_t st = (hipStream_t)stream;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -623,15 +640,17 @@ int cost_feedback(rt_camera* c, const TraceParams& p, void* stream, int set) {
         const uint32_t top = n > 0 ? cost_of(ord[0]) : 0;
         if (c->tile_order == 3 && (p.rays == 16 || p.rays == 8) && kd3_waves(p.rays) == 4 && !(c->debug & 2048) &&
             n > 0 && RT_COOP_PCT > 0) {
-            const int64_t pct = n < kSplitMaxTiles ? RT_COOP_PCT : RT_COOP_PCT_LARGE;
-            while (coop < std::min<int64_t>(n / RT_COOP_CAP_DIV, RT_COOP_MAX) &&
+            const int64_t pct = n < kSplitMaxTiles ? tune("RT_TUNE_COOP_PCT", RT_COOP_PCT)
+                                                   : tune("RT_TUNE_COOP_PCT_LARGE", RT_COOP_PCT_LARGE);
+            while (coop < std::min<int64_t>(n / tune("RT_TUNE_COOP_CAP_DIV", RT_COOP_CAP_DIV), RT_COOP_MAX) &&
                    100ull * cost_of(ord[(size_t)coop]) > (uint64_t)pct * top && top >= 24)
                 coop++;
             if (c->debug & 4096) coop = (int32_t)n;  // tests: every tile a coop tile
         }
         if (c->tile_order == 3 && (p.rays == 16 || (p.rays == 8 && RT_SPLIT8)) && kd3_waves(p.rays) == 4 &&
             !(c->debug & 512) && n > 0 && (n < kSplitMaxTiles || RT_SPLIT_PCT_LARGE > 0)) {
-            const uint64_t pct = n < kSplitMaxTiles ? RT_SPLIT_PCT : RT_SPLIT_PCT_LARGE;
+            const uint64_t pct = n < kSplitMaxTiles ? tune("RT_TUNE_SPLIT_PCT", RT_SPLIT_PCT)
+                                                    : tune("RT_TUNE_SPLIT_PCT_LARGE", RT_SPLIT_PCT_LARGE);
             while (coop + split < n / RT_SPLIT_CAP_DIV && 100ull * cost_of(ord[(size_t)(coop + split)]) > pct * top &&
                    top >= 24)
                 split++;

@@ -2005,11 +2005,7 @@ __device__ __forceinline__ unsigned long long coarse_root(const TraceParams& P, 
 #ifndef RT_COOP
 #define RT_COOP 1
 #endif
-// a coop unit reports its tile's cost as at least popped / RT_COOP_COST_DIV
-// (see trace_unit_coop)
-#ifndef RT_COOP_COST_DIV
-#define RT_COOP_COST_DIV 64
-#endif
+
 constexpr int kCoopWaves = 4;
 
 template <int kRays, int kRayVec>
@@ -2223,12 +2219,7 @@ __device__ __forceinline__ void trace_unit_coop(const TraceParams& P, CoopLds<kR
         P.dbg[3 * dbg_slot + 1] = __builtin_amdgcn_s_memrealtime();
         P.dbg[3 * dbg_slot + 2] = iters | ((unsigned long long)popped << 32);
     }
-    // the tile's cost in the per-wave pool's terms (its iterations), so the
-    // cost order does not change with the rendering: at least this walk's
-    // iterations, and the items a single wave would pop at ~64 per iteration
-    // (heavy 16-ray waves pop ~85: an over-estimate keeps a coop tile in the
-    // coop set rather than alternating)
-    if (cost && lane == 0) *cost = max(iters, (popped + RT_COOP_COST_DIV - 1) / RT_COOP_COST_DIV);
+    if (cost && lane == 0) *cost = iters;  // (the kernel passes none: see k_trace_kd3)
     float cam[3];
     Ray R;
     {
@@ -2319,8 +2310,10 @@ __global__ RT_KD3_BOUNDS(64 * kd3_waves(kRays)) void k_trace_kd3(TraceParams P) 
                 return;
             }
             const int u = b & 3;
-            uint32_t* cost = P.cost ? P.cost + kCostSlots * (size_t)ti + u : nullptr;
-            if (cost && wv == 0 && lane == 0) cost[4] = 0u;  // no second half
+            // a coop unit leaves its tile's cost slots as the tile's last
+            // per-wave render wrote them (the coop chain is no measure of the
+            // single-wave cost the order and the thresholds compare)
+            uint32_t* cost = nullptr;
             static_assert(sizeof(CoopLds<kRays, kCap, kRayVec>) <= sizeof(s_lds), "coop pool exceeds the block's LDS");
             trace_unit_coop<kRays, kCap, kRayVec, kTranslated, kWriteHit, kCount>(
                 P, *reinterpret_cast<CoopLds<kRays, kCap, kRayVec>*>(s_lds), unit_of_tile(P, ti, u), wv, lane,
