@@ -192,6 +192,9 @@ struct rt_camera {
     // rt_run_frames: events kept across calls (the timed call reuses the
     // warm-up call's), pairs bracketing sampled frames' renders
     std::vector<hipEvent_t> loop_ev;
+    // the frame period of the last loop with frames in flight (its timed
+    // frames' bracketed time / lanes), for the next loop's lane stagger
+    double frame_us_est = 0.0;
     struct RectCache {
         bool valid = false;
         uint64_t gen = 0, tree = 0;
@@ -587,6 +590,11 @@ constexpr int64_t kSplitMaxTiles = RT_SPLIT_MAX_TILES;
 #endif
 #ifndef RT_COOP_MAX
 #define RT_COOP_MAX 256
+#endif
+// rt_run_frames: lane 1 of two starts RT_STAGGER_PCT % of the last frame
+// period after lane 0
+#ifndef RT_STAGGER_PCT
+#define RT_STAGGER_PCT 50
 #endif
 
 // Experiments: a tuning constant from the environment (read once), else
@@ -2189,6 +2197,22 @@ extern "C" int rt_run_frames(rt_camera* c, rt_comm* comm, const rt_frame_loop* a
         c->nactive = L;
         for (int l = 0; l < L; l++) c->active[l] = lane[l];
     }
+    // Stagger: lanes 1.. start their first frame a fraction of a frame
+    // period after lane 0 (k_delay), so that each frame's tail overlaps the
+    // next lane's bulk from the first frame on.  Two lanes started together
+    // stay in lockstep (r04c trace of the driver's 20-frame run: both lanes'
+    // kernels 210-219 us, start to start within 12 us, 109.7 us per frame,
+    // against 97 us per frame once a long run has drifted out of phase).
+    // RT_TUNE_STAGGER_PCT: percent of the last loop's frame period (0: off).
+    if (L > 1 && c->frame_us_est > 0.0) {
+        const int pct = tune("RT_TUNE_STAGGER_PCT", RT_STAGGER_PCT);
+        for (int l = 1; !rc && l < L && pct > 0; l++)
+            rc = launch_delay(c->frame_us_est * pct / 100.0 * l / (L - 1), lane[l]);
+        if (rc) {
+            cleanup();
+            return rc;
+        }
+    }
     const rt_tile* tile = a->tile.nranks > 0 ? &a->tile : nullptr;
     // rank 0 renders its bands straight into the frame it assembles (its
     // part of the frame is never copied); the gather places the peers' parts
@@ -2268,6 +2292,7 @@ extern "C" int rt_run_frames(rt_camera* c, rt_comm* comm, const rt_frame_loop* a
             cnt++;
         }
     }
+    if (cnt && L > 1) c->frame_us_est = 1e3 * sum / cnt / L;  // bracketed frames share the GPU with L - 1 others
     if (kernel_ms_avg) *kernel_ms_avg = cnt ? sum / cnt : 0.0;
     if (kernel_ms_frames) *kernel_ms_frames = cnt;
     return RT_OK;

@@ -206,6 +206,8 @@ int launch_node_ref(const rt_kd_node* d_nodes, int64_t nnode, const int32_t* d_i
                     uint32_t* d_ref, void* stream);
 // rt_kd_build's input checks: tri indices a permutation of [0, n), no NaN bound.
 int validate_leafs(const rt_leaf_aabb* leafs, uint32_t n, const char* what);
+// One wave on `stream` sleeping `us` microseconds (a lane's start offset).
+int launch_delay(double us, void* stream);
 int launch_unpack(int32_t w, int32_t h, int32_t nranks, const uint32_t* gathered,
                   uint32_t* frame, void* stream);
 // Slots s of `rank` whose band rank + s*nranks lies in [b0, b1): [s0, s1).

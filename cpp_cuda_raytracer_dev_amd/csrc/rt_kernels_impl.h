@@ -3011,6 +3011,16 @@ __global__ void k_unpack_rect(int32_t w, int32_t nranks, int32_t x0, int32_t x1,
     }
 }
 
+// A lane's start offset (rt_run_frames' stagger): one wave sleeps until
+// `ticks` of the 100 MHz real-time counter have passed.  Frames in flight on
+// two lanes that start together stay in lockstep, so their tails (a few
+// heavy units on an otherwise idle GPU) coincide; a lane started half a frame
+// later overlaps each frame's tail with the other lane's bulk.
+__global__ __launch_bounds__(64) void k_delay(uint64_t ticks) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(32);
+}
+
 template <class K>
 int check_launch(const char* what) {
     hipError_t e = hipGetLastError();
