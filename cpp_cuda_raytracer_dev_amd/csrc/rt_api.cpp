@@ -143,6 +143,16 @@ struct rt_camera {
     bool cost_pending = false, order_pending = false;
     int frames_since = 0;
     uint64_t layout_gen = 0, cost_gen = 0;   // fine-grid generation, and the one h_cost was read for
+    // The order ranks tiles by the cost of one wave per unit (pool
+    // iterations).  Coop tiles write no cost (their walk is no measure of
+    // it) and split halves report an estimate, so each tile's cost as last
+    // measured unsplit and not coop is remembered (per grid) and used while
+    // it renders split or coop: sample_mode holds, per tile, how the sampled
+    // frame rendered it (0 whole, 1 coop, 2 split; taken when the sample is
+    // queued).
+    std::vector<uint8_t> sample_coop;
+    std::vector<uint32_t> cost_mem;
+    uint64_t mem_gen = ~0ull;
     uint64_t order_gen = ~0ull;              // generation whose cost order d_order holds
     int32_t order_split = 0;                 // split tiles after the coop tiles of that cost order
     int32_t order_coop = 0;                  // coop tiles at the head of that cost order
@@ -192,9 +202,13 @@ struct rt_camera {
     // rt_run_frames: events kept across calls (the timed call reuses the
     // warm-up call's), pairs bracketing sampled frames' renders
     std::vector<hipEvent_t> loop_ev;
-    // the frame period of the last loop with frames in flight (its timed
-    // frames' bracketed time / lanes), for the next loop's lane stagger
-    double frame_us_est = 0.0;
+    // rt_run_frames' dispatch gate: per lane, the count of started blocks
+    // of its kernel-3 frames (device, zeroed once) and how many it will reach
+    // once every frame launched so far has dispatched (host)
+    unsigned long long* d_started = nullptr;
+    hipStream_t copy_st = nullptr;   // cost samples' D2H copies (cost_feedback)
+    hipEvent_t copy_ev = nullptr;
+    unsigned long long started_cum[RT_LOOP_MAX_LANES] = {};
     struct RectCache {
         bool valid = false;
         uint64_t gen = 0, tree = 0;
@@ -591,11 +605,7 @@ constexpr int64_t kSplitMaxTiles = RT_SPLIT_MAX_TILES;
 #ifndef RT_COOP_MAX
 #define RT_COOP_MAX 256
 #endif
-// rt_run_frames: lane 1 of two starts RT_STAGGER_PCT % of the last frame
-// period after lane 0
-#ifndef RT_STAGGER_PCT
-#define RT_STAGGER_PCT 50
-#endif
+
 
 // Experiments: a tuning constant from the environment (read once), else
 // the compiled default.  RT_TUNE_COOP_PCT, RT_TUNE_COOP_PCT_LARGE,
@@ -623,7 +633,27 @@ int cost_feedback(rt_camera* c, const TraceParams& p, void* stream, int set) {
         c->cost_pending = c->order_pending = false;
         c->frames_since = 0;
         if (c->cost_gen != c->layout_gen || (int64_t)c->centre.size() != n) return RT_OK;  // stale sample
-        const std::vector<int32_t> ord = cost_order(c, p, c->tile_order == 4, c->h_cost);
+        // the sampled costs with each coop tile's remembered single-wave cost
+        // (its slots hold whatever this stream's set last had for it)
+        if (c->mem_gen != c->layout_gen || (int64_t)c->cost_mem.size() != n) {
+            c->cost_mem.assign((size_t)n, 0u);
+            c->mem_gen = c->layout_gen;
+        }
+        std::vector<uint32_t> eff(c->h_cost, c->h_cost + kCostSlots * (size_t)n);
+        const bool have_flags = (int64_t)c->sample_coop.size() == n;
+        for (int64_t t = 0; t < n; t++) {
+            uint32_t* e = eff.data() + kCostSlots * (size_t)t;
+            uint32_t m = 0;
+            for (int k = 0; k < kCostSlots; k++) m = std::max(m, e[k]);
+            const uint8_t mode = have_flags ? c->sample_coop[(size_t)t] : 0;
+            if (mode && c->cost_mem[(size_t)t] > 0) {
+                for (int k = 0; k < kCostSlots; k++) e[k] = 0u;
+                e[0] = c->cost_mem[(size_t)t];
+            } else if (!mode) {
+                c->cost_mem[(size_t)t] = m;
+            }
+        }
+        const std::vector<int32_t> ord = cost_order(c, p, c->tile_order == 4, eff.data());
         bool same = true;
         for (int64_t k = 0; k < n; k++) {
             same = same && c->h_order[k] == ord[(size_t)k];
@@ -642,7 +672,7 @@ int cost_feedback(rt_camera* c, const TraceParams& p, void* stream, int set) {
         int32_t split = 0, coop = 0;
         auto cost_of = [&](int64_t t) {
             uint32_t m = 0;
-            for (int k = 0; k < kCostSlots; k++) m = std::max(m, c->h_cost[kCostSlots * (size_t)t + k]);
+            for (int k = 0; k < kCostSlots; k++) m = std::max(m, eff[kCostSlots * (size_t)t + k]);
             return m;
         };
         const uint32_t top = n > 0 ? cost_of(ord[0]) : 0;
@@ -694,13 +724,33 @@ int cost_feedback(rt_camera* c, const TraceParams& p, void* stream, int set) {
     }
     if (++c->frames_since < kCostPeriod) return RT_OK;
     int rc;
-    if ((rc = hip_check(hipMemcpyAsync(c->h_cost, c->d_cost + (size_t)set * c->cost_cap,
-                                       sizeof(uint32_t) * kCostSlots * (size_t)n, hipMemcpyDeviceToHost, st),
+    // The copy runs on the camera's copy stream after this frame, beside the
+    // stream's next frames: on the render stream it was a blit kernel that
+    // shared the GPU with two frames in flight and held the lane's next frame
+    // back by 38-46 us (r04c / r04e traces).  A later frame of this stream
+    // may overwrite the set while it is read: its costs are the same tiles'
+    // (a mixed sample costs at worst a dispatch order, never a frame).
+    if (!c->copy_st && (rc = hip_check(hipStreamCreateWithFlags(&c->copy_st, hipStreamNonBlocking), "copy stream")))
+        return rc;
+    if (!c->copy_ev && (rc = hip_check(hipEventCreateWithFlags(&c->copy_ev, hipEventDisableTiming), "copy event")))
+        return rc;
+    if ((rc = hip_check(hipEventRecord(c->copy_ev, st), "cost sample fork")) ||
+        (rc = hip_check(hipStreamWaitEvent(c->copy_st, c->copy_ev, 0), "cost sample wait")) ||
+        (rc = hip_check(hipMemcpyAsync(c->h_cost, c->d_cost + (size_t)set * c->cost_cap,
+                                       sizeof(uint32_t) * kCostSlots * (size_t)n, hipMemcpyDeviceToHost, c->copy_st),
                         "D2H cost")) ||
-        (rc = hip_check(hipEventRecord(c->cost_ev, st), "cost event")))
+        (rc = hip_check(hipEventRecord(c->cost_ev, c->copy_st), "cost event")))
         return rc;
     c->cost_pending = true;
     c->cost_gen = c->layout_gen;
+    // how the order this frame launched with rendered each tile (render_common:
+    // coop tiles order[0..coop), split tiles order[coop..coop + split))
+    c->sample_coop.assign((size_t)n, 0);
+    if (c->order_gen == c->layout_gen)
+        for (int32_t k = 0; k < p.coop + p.split && k < n; k++) {
+            const int32_t t = c->h_order[k];
+            if (t >= 0 && t < n) c->sample_coop[(size_t)t] = k < p.coop ? 1 : 2;
+        }
     return RT_OK;
 }
 
@@ -1074,6 +1124,7 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
     p.pool_cap = c->pool_cap;
     p.items = c->items;
     p.dbg = nullptr;
+    p.started = nullptr;
 #if RT_ITER_STAMPS
     p.istamp = nullptr;
 #endif
@@ -1555,7 +1606,8 @@ static int flat_keys_for(rt_camera* c, hipStream_t stream, int64_t npix, unsigne
 }
 
 static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32_t flags, const rt_tile* tile,
-                         uint32_t* argb, int64_t* hit, void* stream, uint32_t* display = nullptr) {
+                         uint32_t* argb, int64_t* hit, void* stream, uint32_t* display = nullptr,
+                         unsigned long long* started = nullptr, int64_t* blocks = nullptr) {
     if (!c) return fail(RT_ERR_INVALID, "rt_render: null camera");
     if (mode != RT_MODE_KD && mode != RT_MODE_FLAT) return fail(RT_ERR_INVALID, "rt_render: mode %u", mode);
     int rc = check_tile(tile);
@@ -1649,6 +1701,10 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
         cset = cost_set(c, st);
         p.cost = c->d_cost + (size_t)cset * c->cost_cap;
     }
+    // kernel 3 counts its started blocks for rt_run_frames' dispatch gate
+    const bool kd3 = mode == RT_MODE_KD && effective_kernel(c) == 3;
+    p.started = kd3 ? started : nullptr;
+    if (blocks) *blocks = kd3 && started ? (int64_t)fine_grid_blocks(p) : 0;
     if ((rc = launch_split(c, p, mode, flags, stream))) return rc;
     if (p.order) {  // the streams that read the current order slot
         note_order_stream(c, st);
@@ -1989,6 +2045,7 @@ extern "C" void rt_camera_destroy(rt_camera* c) {
     }
     c->d_order = nullptr;
     dev_free(c->d_dbg);
+    dev_free(c->d_started);
     for (auto& k : c->flat_keys) dev_free(k.d);
     dev_free(c->d_cost);
     for (hipEvent_t e : c->slot_join_ev)
@@ -2004,6 +2061,8 @@ extern "C" void rt_camera_destroy(rt_camera* c) {
     for (hipEvent_t e : c->loop_ev)
         if (e) (void)hipEventDestroy(e);
     if (c->side) (void)hipStreamDestroy(c->side);
+    if (c->copy_st) (void)hipStreamDestroy(c->copy_st);
+    if (c->copy_ev) (void)hipEventDestroy(c->copy_ev);
     for (int k = 0; k <= RT_LOOP_MAX_LANES; k++) {
         if (c->lanes[k]) (void)hipStreamDestroy(c->lanes[k]);
         if (c->lane_ev[k]) (void)hipEventDestroy(c->lane_ev[k]);
@@ -2119,6 +2178,13 @@ static int ensure_lanes(rt_camera* c, int L, bool comm) {
         if (!c->lane_ev[k] && (rc = hip_check(hipEventCreateWithFlags(&c->lane_ev[k], hipEventDisableTiming), "lane event")))
             return rc;
     }
+    if (!c->d_started) {  // the dispatch gate's counters (rt_run_frames)
+        if ((rc = dev_alloc(&c->d_started, RT_LOOP_MAX_LANES, "hipMalloc(started)")) ||
+            (rc = hip_check(hipMemset(c->d_started, 0, sizeof(unsigned long long) * RT_LOOP_MAX_LANES), "memset started")) ||
+            (rc = hip_check(hipDeviceSynchronize(), "started init")))
+            return rc;
+        for (auto& v : c->started_cum) v = 0;
+    }
     return RT_OK;
 }
 
@@ -2197,22 +2263,12 @@ extern "C" int rt_run_frames(rt_camera* c, rt_comm* comm, const rt_frame_loop* a
         c->nactive = L;
         for (int l = 0; l < L; l++) c->active[l] = lane[l];
     }
-    // Stagger: lanes 1.. start their first frame a fraction of a frame
-    // period after lane 0 (k_delay), so that each frame's tail overlaps the
-    // next lane's bulk from the first frame on.  Two lanes started together
-    // stay in lockstep (r04c trace of the driver's 20-frame run: both lanes'
-    // kernels 210-219 us, start to start within 12 us, 109.7 us per frame,
-    // against 97 us per frame once a long run has drifted out of phase).
-    // RT_TUNE_STAGGER_PCT: percent of the last loop's frame period (0: off).
-    if (L > 1 && c->frame_us_est > 0.0) {
-        const int pct = tune("RT_TUNE_STAGGER_PCT", RT_STAGGER_PCT);
-        for (int l = 1; !rc && l < L && pct > 0; l++)
-            rc = launch_delay(c->frame_us_est * pct / 100.0 * l / (L - 1), lane[l]);
-        if (rc) {
-            cleanup();
-            return rc;
-        }
-    }
+    // The dispatch gate (k_gate): frame j > 0 of the call starts on its lane
+    // once every block of frame j - 1 (on the previous lane) has started, so
+    // the lanes never run in lockstep; KD frames of kernel 3 only (its blocks
+    // count themselves).  RT_TUNE_GATE=0 turns it off (A/B).
+    const bool gated = L > 1 && a->mode == RT_MODE_KD && effective_kernel(c) == 3 && c->d_started &&
+                       tune("RT_TUNE_GATE", 1) != 0;
     const rt_tile* tile = a->tile.nranks > 0 ? &a->tile : nullptr;
     // rank 0 renders its bands straight into the frame it assembles (its
     // part of the frame is never copied); the gather places the peers' parts
@@ -2244,11 +2300,21 @@ extern "C" int rt_run_frames(rt_camera* c, rt_comm* comm, const rt_frame_loop* a
         if (linked && used[k] && hipEventQuery(sent[k]) != hipSuccess &&
             (rc = hip_check(hipStreamWaitEvent(ls, sent[k], 0), "render wait")))
             break;
+        const int ln = j % L;
+        if (gated && j > 0) {
+            const int pl = (j - 1) % L;
+            rc = launch_gate(c->d_started + pl, c->started_cum[pl], 2000.0, ls);
+            if (rc) break;
+        }
         const bool timed = every > 0 && j % every == 0;
         const int64_t t = every > 0 ? j / every : 0;
         rc = timed ? hip_check(hipEventRecord(c->loop_ev[(size_t)(2 * t)], ls), "loop timing") : RT_OK;
         uint32_t* target = direct ? a->d_frame[k] : a->d_local[k];
-        if (!rc) rc = render_common(c, xf, a->mode, a->flags | (direct ? RT_FLAG_FRAME_OUT : 0u), tile, target, nullptr, ls);
+        int64_t blocks = 0;
+        if (!rc)
+            rc = render_common(c, xf, a->mode, a->flags | (direct ? RT_FLAG_FRAME_OUT : 0u), tile, target, nullptr, ls,
+                               nullptr, gated ? c->d_started + ln : nullptr, &blocks);
+        if (!rc && gated) c->started_cum[ln] += (unsigned long long)blocks;
         if (!rc && timed) rc = hip_check(hipEventRecord(c->loop_ev[(size_t)(2 * t + 1)], ls), "loop timing");
         if (!rc && comm) {
             if (linked) {
@@ -2292,7 +2358,6 @@ extern "C" int rt_run_frames(rt_camera* c, rt_comm* comm, const rt_frame_loop* a
             cnt++;
         }
     }
-    if (cnt && L > 1) c->frame_us_est = 1e3 * sum / cnt / L;  // bracketed frames share the GPU with L - 1 others
     if (kernel_ms_avg) *kernel_ms_avg = cnt ? sum / cnt : 0.0;
     if (kernel_ms_frames) *kernel_ms_frames = cnt;
     return RT_OK;

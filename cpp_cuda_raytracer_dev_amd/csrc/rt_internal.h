@@ -148,6 +148,7 @@ struct TraceParams {
     int32_t items;                 // kernel 3 items per lane per iteration (1 or 2)
     int32_t debug;                 // diagnostic builds only: 1 = skip traversal
     unsigned long long* dbg;       // per-wave (t_start, t_end, visits) when non-null
+    unsigned long long* started;   // kernel 3: count of started blocks (rt_run_frames' dispatch gate), or null
     uint32_t root_ref;
     uint32_t ntri;
     int32_t max_depth;
@@ -170,6 +171,11 @@ struct TraceParams {
 #if RT_ITER_STAMPS
 constexpr int kIterStamps = 96;
 #endif
+
+// Blocks of k_trace_kd3's grid (fine tiles, coop and split extras, far fill).
+inline unsigned fine_grid_blocks(const TraceParams& p) {
+    return (unsigned)(p.tiles_x * p.block_rows) + 3u * (unsigned)p.coop + (unsigned)p.split + (unsigned)p.fill_blocks;
+}
 
 }  // namespace rt
 
@@ -206,8 +212,9 @@ int launch_node_ref(const rt_kd_node* d_nodes, int64_t nnode, const int32_t* d_i
                     uint32_t* d_ref, void* stream);
 // rt_kd_build's input checks: tri indices a permutation of [0, n), no NaN bound.
 int validate_leafs(const rt_leaf_aabb* leafs, uint32_t n, const char* what);
-// One wave on `stream` sleeping `us` microseconds (a lane's start offset).
-int launch_delay(double us, void* stream);
+// rt_run_frames' dispatch gate: one wave on `stream` until *started >= target
+// (blocks of another lane's frames that have started) or timeout_us passed.
+int launch_gate(const unsigned long long* started, unsigned long long target, double timeout_us, void* stream);
 int launch_unpack(int32_t w, int32_t h, int32_t nranks, const uint32_t* gathered,
                   uint32_t* frame, void* stream);
 // Slots s of `rank` whose band rank + s*nranks lies in [b0, b1): [s0, s1).

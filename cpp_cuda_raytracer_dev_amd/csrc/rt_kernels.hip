@@ -88,7 +88,7 @@ int launch_trace(const TraceParams& p, uint32_t mode, uint32_t flags, int kernel
         // the coarse groups first, then the fine tiles (or just one of them)
         const bool coarse = pass == 0;
         if ((coarse && part == kPartFine) || (!coarse && part == kPartCoarse)) continue;
-        const unsigned grid = coarse ? (unsigned)p.coarse_blocks : fine + 3u * (unsigned)p.coop + (unsigned)p.split + (unsigned)p.fill_blocks;
+        const unsigned grid = coarse ? (unsigned)p.coarse_blocks : fine_grid_blocks(p);
         if (grid == 0) continue;
         TraceFn fn;
         if (tr) fn = wh ? (cnt ? kd_kernel_111(v, r, sh, coarse) : kd_kernel_110(v, r, sh, coarse))
@@ -102,10 +102,9 @@ int launch_trace(const TraceParams& p, uint32_t mode, uint32_t flags, int kernel
     return RT_OK;
 }
 
-int launch_delay(double us, void* stream) {
-    if (!(us > 0.0)) return RT_OK;
-    k_delay<<<1, 64, 0, (hipStream_t)stream>>>((uint64_t)(us * 100.0));  // 100 MHz counter
-    return check_launch<void>("k_delay");
+int launch_gate(const unsigned long long* started, unsigned long long target, double timeout_us, void* stream) {
+    k_gate<<<1, 64, 0, (hipStream_t)stream>>>(started, target, (uint64_t)(timeout_us * 100.0));  // 100 MHz counter
+    return check_launch<void>("k_gate");
 }
 
 int launch_unpack(int32_t w, int32_t h, int32_t nranks, const uint32_t* gathered, uint32_t* frame,

@@ -2272,6 +2272,7 @@ __global__ RT_KD3_BOUNDS(64 * kd3_waves(kRays)) void k_trace_kd3(TraceParams P) 
     constexpr int kRayVec = (kTranslated || kShadow) ? 5 : 3;  // float4s of per-ray data in LDS
     __shared__ WaveLds<kRays, kCap, kRayVec> s_lds[kWaves];
     const int wv = wave_id(), lane = (int)threadIdx.x & 63;
+    if (P.started && threadIdx.x == 0) atomicAdd(P.started, 1ull);  // the dispatch gate's count (k_gate)
     Counts C;
     const int32_t ntiles = P.tiles_x * P.block_rows;
     // blocks: 4 per coop tile, 2 per split tile, 1 per other fine tile, then
@@ -3011,14 +3012,24 @@ __global__ void k_unpack_rect(int32_t w, int32_t nranks, int32_t x0, int32_t x1,
     }
 }
 
-// A lane's start offset (rt_run_frames' stagger): one wave sleeps until
-// `ticks` of the 100 MHz real-time counter have passed.  Frames in flight on
-// two lanes that start together stay in lockstep, so their tails (a few
-// heavy units on an otherwise idle GPU) coincide; a lane started half a frame
-// later overlaps each frame's tail with the other lane's bulk.
-__global__ __launch_bounds__(64) void k_delay(uint64_t ticks) {
+// The dispatch gate of frames in flight (rt_run_frames): one lane waits
+// until every block of the other lane's previous frame has started, so the
+// next frame's blocks fill the CUs the previous frame's tail frees, and two
+// frames never run in lockstep (their tails would coincide: r04c/r04e traces
+// of the driver's 20-frame run, both lanes' kernels 210-230 us, start to
+// start within 12 us).  k_trace_kd3 counts its started blocks (P.started);
+// the gate polls that count with vector loads (a VGPR address) and gives up
+// after `timeout` ticks of the 100 MHz counter, so it always ends.
+__global__ __launch_bounds__(64) void k_gate(const unsigned long long* started, unsigned long long target,
+                                           uint64_t timeout) {
+    if (threadIdx.x != 0) return;
+    int z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    const unsigned long long* q = started + z;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(32);
+    while (__hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target &&
+           __builtin_amdgcn_s_memrealtime() - t0 < timeout)
+        __builtin_amdgcn_s_sleep(2);
 }
 
 template <class K>

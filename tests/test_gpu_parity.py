@@ -397,8 +397,10 @@ def test_coop_tiles_same_frame(key, rays, debug):
     out = torch.zeros(w * h, dtype=torch.int32, device=dev)
     hit = torch.zeros(w * h, dtype=torch.int64, device=dev)
     st = torch.cuda.Stream(device=dev)
-    for _ in range(64):
+    for k in range(64):
         s.cam.render_into(out, hit, flags=R.RT_FLAG_WRITE_HIT, stream=st.cuda_stream)
+        if k % 8 == 7:  # let cost samples arrive (they are only queried, never waited for)
+            st.synchronize()
     torch.cuda.synchronize()
     assert s.cam.get_option(_lib.RT_OPT_COOP_USED) > 0
     out.fill_(0x7BADBEEF)
@@ -434,8 +436,10 @@ def test_coop_tiles_moved_pose(pose):
         out = torch.zeros(w * h, dtype=torch.int32, device=dev)
         hit = torch.zeros(w * h, dtype=torch.int64, device=dev)
         st = torch.cuda.Stream(device=dev)
-        for _ in range(40):
+        for k in range(48):
             s.cam.render_into(out, hit, xform=xf, flags=R.RT_FLAG_WRITE_HIT, stream=st.cuda_stream)
+            if k % 8 == 7:  # let cost samples arrive (they are only queried, never waited for)
+                st.synchronize()
         torch.cuda.synchronize()
         if debug & 4096:  # (the default selection may pick none for the lighter 8-ray units here)
             assert s.cam.get_option(_lib.RT_OPT_COOP_USED) > 0
