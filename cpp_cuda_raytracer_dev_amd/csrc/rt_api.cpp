@@ -128,15 +128,11 @@ struct rt_camera {
     // buffer of the stream that queues it, which only that stream's frames
     // write, so frames in flight on other lanes (under motion, with another
     // fine grid) never tear it
-    uint32_t* d_cost = nullptr;      // [cost set][tile][kCostSlots] iterations
-    int64_t cost_cap = 0;            // u32 per cost set
-    hipStream_t cost_stream[RT_LOOP_MAX_LANES] = {};   // the stream that owns each cost set
-    bool cost_owned[RT_LOOP_MAX_LANES] = {};           // whether it is owned (the null stream can own one)
-    int cost_next = 0;                                 // the set reclaimed next when all are owned
     hipEvent_t slot_join_ev[8] = {};  // cost-order upload: joins the streams that read the slot
     hipStream_t cost_up_stream = nullptr;   // the last cost-order upload's stream ...
     bool cost_up_valid = false;             // ... while it may be pending
-    uint32_t* h_cost = nullptr;      // pinned D2H target
+    uint32_t* h_cost = nullptr;      // pinned: [tile][kCostSlots] pool iterations, written by a sampled frame
+    uint32_t* d_cost_host = nullptr; // its device address
     int32_t* h_order = nullptr;      // pinned H2D source
     int64_t host_cap = 0;            // tiles h_cost / h_order hold
     hipEvent_t cost_ev = nullptr, order_ev = nullptr;
@@ -206,8 +202,6 @@ struct rt_camera {
     // of its kernel-3 frames (device, zeroed once) and how many it will reach
     // once every frame launched so far has dispatched (host)
     unsigned long long* d_started = nullptr;
-    hipStream_t copy_st = nullptr;   // cost samples' D2H copies (cost_feedback)
-    hipEvent_t copy_ev = nullptr;
     unsigned long long started_cum[RT_LOOP_MAX_LANES] = {};
     struct RectCache {
         bool valid = false;
@@ -424,18 +418,6 @@ constexpr int kTunePeriod = 2048;  // frames between timing rounds of the shadow
 // Buffers of tile order 3 for n fine tiles (allocated when the grid grows).
 int ensure_cost(rt_camera* c, int64_t n) {
     int rc;
-    if (c->cost_cap < kCostSlots * n) {
-        // earlier frames' kernels write d_cost and a cost sample may be
-        // copying it: both done before the buffer goes
-        if ((rc = hip_check(hipDeviceSynchronize(), "cost sync"))) return rc;
-        c->cost_pending = false;
-        dev_free(c->d_cost);
-        const size_t all = (size_t)(kCostSlots * n) * RT_LOOP_MAX_LANES;
-        if ((rc = dev_alloc(&c->d_cost, all, "hipMalloc(cost)"))) return rc;
-        // slots of waves a tile does not have stay zero
-        if ((rc = hip_check(hipMemset(c->d_cost, 0, sizeof(uint32_t) * all), "memset cost"))) return rc;
-        c->cost_cap = kCostSlots * n;
-    }
     if (c->host_cap < n) {
         // copies in flight may still use the pinned buffers
         if (c->cost_pending) (void)hipEventSynchronize(c->cost_ev);
@@ -443,11 +425,13 @@ int ensure_cost(rt_camera* c, int64_t n) {
         if (c->h_cost) (void)hipHostFree(c->h_cost);
         if (c->h_order) (void)hipHostFree(c->h_order);
         c->h_cost = nullptr;
+        c->d_cost_host = nullptr;
         c->h_order = nullptr;
         c->host_cap = 0;
         c->cost_pending = c->order_pending = false;
         if ((rc = hip_check(hipHostMalloc((void**)&c->h_cost, sizeof(uint32_t) * kCostSlots * (size_t)n, 0), "hipHostMalloc(cost)")) ||
-            (rc = hip_check(hipHostMalloc((void**)&c->h_order, sizeof(int32_t) * (size_t)n, 0), "hipHostMalloc(order)")))
+            (rc = hip_check(hipHostMalloc((void**)&c->h_order, sizeof(int32_t) * (size_t)n, 0), "hipHostMalloc(order)")) ||
+            (rc = hip_check(hipHostGetDevicePointer((void**)&c->d_cost_host, c->h_cost, 0), "cost device pointer")))
             return rc;
         c->host_cap = n;
     }
@@ -542,26 +526,12 @@ std::vector<int32_t> cost_order(const rt_camera* c, const TraceParams& p, bool x
 
 // After a tile-order-3 frame: when an earlier cost sample has arrived, order
 // the tiles by it (heaviest unit first, centre-out among equals) and upload
-// the order behind this frame; otherwise, every kCostPeriod frames, queue a
-// sample of this frame's costs.  Stream-ordered and non-blocking (events are
-// only queried); skipped while the stream is being captured into a graph.
-// The cost set a stream's frames write: its own, claimed on first use (when
-// every set is owned, one is reclaimed round robin: a stale sample costs at
-// worst a dispatch order, never a frame).
-int cost_set(rt_camera* c, hipStream_t st) {
-    for (int l = 0; l < RT_LOOP_MAX_LANES; l++)
-        if (c->cost_owned[l] && c->cost_stream[l] == st) return l;
-    for (int l = 0; l < RT_LOOP_MAX_LANES; l++)
-        if (!c->cost_owned[l]) {
-            c->cost_owned[l] = true;
-            c->cost_stream[l] = st;
-            return l;
-        }
-    const int l = c->cost_next++ % RT_LOOP_MAX_LANES;
-    c->cost_stream[l] = st;
-    return l;
-}
-
+// the order behind this frame.  Every kCostPeriod frames one frame is the
+// sample: its kernel writes its units' costs straight into pinned host memory
+// (cost_sample_now / c->h_cost; no copy kernel, and the other frames write
+// no costs), and an event after it says when the sample has arrived.
+// Non-blocking (events are only queried); skipped while the stream is being
+// captured into a graph.
 // Grids of fewer than this many 16-ray tiles (4 units each) split the tiles
 // above RT_SPLIT_PCT % of the heaviest, larger ones only those above
 // RT_SPLIT_PCT_LARGE %: at 1080p (3.4k tiles) splitting half the top measured
@@ -622,7 +592,16 @@ int tune(const char* name, int dflt) {
     return x;
 }
 
-int cost_feedback(rt_camera* c, const TraceParams& p, void* stream, int set) {
+// Whether the frame about to launch on `st` is a cost sample: its kernel then
+// writes its units' costs into c->h_cost (zeroed here) instead of nothing.
+bool cost_sample_now(rt_camera* c, hipStream_t st) {
+    if (c->cost_pending || c->frames_since + 1 < kCostPeriod || !c->h_cost) return false;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return false;
+    return true;
+}
+
+int cost_feedback(rt_camera* c, const TraceParams& p, void* stream, bool sampled) {
     hipStream_t st = (hipStream_t)stream;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return RT_OK;
@@ -633,8 +612,8 @@ int cost_feedback(rt_camera* c, const TraceParams& p, void* stream, int set) {
         c->cost_pending = c->order_pending = false;
         c->frames_since = 0;
         if (c->cost_gen != c->layout_gen || (int64_t)c->centre.size() != n) return RT_OK;  // stale sample
-        // the sampled costs with each coop tile's remembered single-wave cost
-        // (its slots hold whatever this stream's set last had for it)
+        // the sampled costs, with the remembered unsplit cost of each tile the
+        // sampled frame rendered split or coop (coop units write no cost)
         if (c->mem_gen != c->layout_gen || (int64_t)c->cost_mem.size() != n) {
             c->cost_mem.assign((size_t)n, 0u);
             c->mem_gen = c->layout_gen;
@@ -722,25 +701,12 @@ int cost_feedback(rt_camera* c, const TraceParams& p, void* stream, int set) {
         c->order_gen = c->layout_gen;
         return RT_OK;
     }
-    if (++c->frames_since < kCostPeriod) return RT_OK;
+    if (!sampled) {
+        ++c->frames_since;
+        return RT_OK;
+    }
     int rc;
-    // The copy runs on the camera's copy stream after this frame, beside the
-    // stream's next frames: on the render stream it was a blit kernel that
-    // shared the GPU with two frames in flight and held the lane's next frame
-    // back by 38-46 us (r04c / r04e traces).  A later frame of this stream
-    // may overwrite the set while it is read: its costs are the same tiles'
-    // (a mixed sample costs at worst a dispatch order, never a frame).
-    if (!c->copy_st && (rc = hip_check(hipStreamCreateWithFlags(&c->copy_st, hipStreamNonBlocking), "copy stream")))
-        return rc;
-    if (!c->copy_ev && (rc = hip_check(hipEventCreateWithFlags(&c->copy_ev, hipEventDisableTiming), "copy event")))
-        return rc;
-    if ((rc = hip_check(hipEventRecord(c->copy_ev, st), "cost sample fork")) ||
-        (rc = hip_check(hipStreamWaitEvent(c->copy_st, c->copy_ev, 0), "cost sample wait")) ||
-        (rc = hip_check(hipMemcpyAsync(c->h_cost, c->d_cost + (size_t)set * c->cost_cap,
-                                       sizeof(uint32_t) * kCostSlots * (size_t)n, hipMemcpyDeviceToHost, c->copy_st),
-                        "D2H cost")) ||
-        (rc = hip_check(hipEventRecord(c->cost_ev, c->copy_st), "cost event")))
-        return rc;
+    if ((rc = hip_check(hipEventRecord(c->cost_ev, st), "cost event"))) return rc;
     c->cost_pending = true;
     c->cost_gen = c->layout_gen;
     // how the order this frame launched with rendered each tile (render_common:
@@ -1156,7 +1122,7 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
         p.order = c->d_order;
         if (c->tile_order >= 3 && kernel == 3) {
             if ((rc = ensure_cost(c, std::max<int64_t>(all_tiles(c, p), (int64_t)p.tiles_x * p.block_rows)))) return rc;
-            p.cost = c->d_cost;
+            p.cost = c->d_cost_host;  // (marks tile order 3; render_common passes it to sampled frames only)
         }
     }
     return RT_OK;
@@ -1696,10 +1662,15 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
         if (!(c->debug & 512)) p.split += p.coop;
         p.coop = 0;
     }
-    int cset = 0;
-    if (p.cost) {  // this stream's own cost set
-        cset = cost_set(c, st);
-        p.cost = c->d_cost + (size_t)cset * c->cost_cap;
+    const bool order3 = p.cost != nullptr;
+    const bool sampled = order3 && cost_sample_now(c, st);
+    if (sampled) {
+        p.cost = c->d_cost_host;
+        // the kernel writes this frame's costs into the pinned host buffer;
+        // slots a tile does not write (coop tiles, missing waves) read 0
+        memset(c->h_cost, 0, sizeof(uint32_t) * kCostSlots * (size_t)p.tiles_x * p.block_rows);
+    } else {
+        p.cost = nullptr;
     }
     // kernel 3 counts its started blocks for rt_run_frames' dispatch gate
     const bool kd3 = mode == RT_MODE_KD && effective_kernel(c) == 3;
@@ -1718,7 +1689,7 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
                 (rc = hip_check(hipStreamWaitEvent(c->active[l], c->tune_ev[2 * trial + 1], 0), "trial fork wait")))
                 return rc;
     }
-    return p.cost ? cost_feedback(c, p, stream, cset) : RT_OK;
+    return order3 ? cost_feedback(c, p, stream, sampled) : RT_OK;
 }
 
 extern "C" int rt_render(rt_camera* c, const float* xform, uint32_t mode, uint32_t flags, const rt_tile* tile,
@@ -2047,7 +2018,6 @@ extern "C" void rt_camera_destroy(rt_camera* c) {
     dev_free(c->d_dbg);
     dev_free(c->d_started);
     for (auto& k : c->flat_keys) dev_free(k.d);
-    dev_free(c->d_cost);
     for (hipEvent_t e : c->slot_join_ev)
         if (e) (void)hipEventDestroy(e);
     if (c->h_cost) (void)hipHostFree(c->h_cost);
@@ -2061,8 +2031,6 @@ extern "C" void rt_camera_destroy(rt_camera* c) {
     for (hipEvent_t e : c->loop_ev)
         if (e) (void)hipEventDestroy(e);
     if (c->side) (void)hipStreamDestroy(c->side);
-    if (c->copy_st) (void)hipStreamDestroy(c->copy_st);
-    if (c->copy_ev) (void)hipEventDestroy(c->copy_ev);
     for (int k = 0; k <= RT_LOOP_MAX_LANES; k++) {
         if (c->lanes[k]) (void)hipStreamDestroy(c->lanes[k]);
         if (c->lane_ev[k]) (void)hipEventDestroy(c->lane_ev[k]);

@@ -1417,9 +1417,9 @@ def test_far_along_key_sequence_background():
     out = torch.zeros(w * h, dtype=torch.int32, device=dev)
     hit = torch.zeros(w * h, dtype=torch.int64, device=dev)
     checked = {"visible": 0, "behind": 0}
-    for i in range(1201):
+    for i in range(2001):
         ref.tick(masks[i % len(masks)])
-        if i not in (10, 40, 120, 400, 600, 1200):
+        if i not in (10, 40, 120, 600, 1200, 2000):
             continue
         xf = np.asarray(ref.xform(), np.float32).reshape(12)
         oargb, ohit, _ = H.oracle_render("dragon", w, h, 0, xform=xf.reshape(3, 4))
@@ -1447,5 +1447,5 @@ def test_far_along_key_sequence_background():
                              for y in range(len(got) // w)])
             sel = np.repeat(rows, w)
             assert (got[sel] == want[sel]).all(), f"tick {i} rank {r}"
-    assert checked["visible"] >= 2 and checked["behind"] >= 2, checked
+    assert checked["visible"] >= 2 and checked["behind"] >= 1, checked
     assert s.cam.device_error(reset=True) == 0

@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""Recompute every configuration's roofline.frac from profiles/ alone
+(VERDICT r03 item 1): the committed PMC entry (profiles/pmc_traffic.json:
+HBM bytes per launch, VALU issue share, build id) and the rocprofv3
+--kernel-trace --stats average of the same configuration's solo frames
+(profiles/<round>/rocprof/<tag>_kernel_stats.csv), against the bench line's
+frac (profiles/<round>/bench/<tag>.json).
+
+    python tools/roofline_check.py profiles/r04 [--out profiles/r04/roofline_check.md]
+
+frac = max(HBM bytes / rocprof average / 8 TB/s, VALU issue share): the
+utilisation of the binding resource, as bench.py computes it with its own
+kernel time.  A row agrees when the two are within 5 %.
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+
+HBM = 8000.0  # GB/s
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def bench_line(path):
+    with open(path) as fp:
+        lines = [ln for ln in fp if ln.startswith("{")]
+    return json.loads(lines[-1]) if lines else None
+
+
+def stats_avg_us(path, kernel="k_trace_kd3"):
+    with open(path) as fp:
+        rows = [r for r in csv.DictReader(fp) if kernel in r["Name"]]
+    if not rows:
+        return None
+    # the dominant instance (most total time)
+    r = max(rows, key=lambda r: float(r["TotalDurationNs"]))
+    return float(r["AverageNs"]) / 1e3, r["Name"][:60], int(r["Calls"])
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    pmc = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+    rows = []
+    for bp in sorted(glob.glob(os.path.join(a.dir, "bench", "*.json"))):
+        tag = os.path.splitext(os.path.basename(bp))[0]
+        b = bench_line(bp)
+        if not b or not b.get("roofline"):
+            continue
+        rf = b["roofline"]
+        key = (rf.get("util_source") or "").split("[")[-1].split("]")[0] if rf.get("util_source") else None
+        ent = pmc.get(key or "", {})
+        st = glob.glob(os.path.join(a.dir, "rocprof", f"{tag}*kernel_stats.csv"))
+        kern = "k_trace_flat" if rf.get("unit") == "TFLOP/s" else "k_trace_kd3"
+        avg = stats_avg_us(st[0], "k_flat_chunk" if kern == "k_trace_flat" else kern) if st else None
+        rec = None
+        if avg and ent.get("hbm_bytes_per_launch"):
+            hbm = ent["hbm_bytes_per_launch"] / (avg[0] * 1e-6) / 1e9 / HBM
+            rec = max(hbm, ent.get("valu_issue_util") or 0.0)
+        rows.append({"tag": tag, "workload": b.get("metric_workload") or b["config"].get("workload"),
+                     "bench_frac": rf.get("frac"), "bound": rf.get("bound"), "bench_kernel_us": 1e3 * rf["kernel_ms_avg"],
+                     "rocprof_avg_us": avg[0] if avg else None, "rocprof_calls": avg[2] if avg else None,
+                     "pmc_key": key, "pmc_build": (ent.get("build_id") or "")[:16],
+                     "bench_build": (b.get("build_id") or "")[:16], "recomputed_frac": rec,
+                     "agree_5pct": (abs(rec - rf["frac"]) <= 0.05 * rf["frac"]) if rec and rf.get("frac") else None})
+    out = ["| config | bound | bench frac | bench kernel us | rocprof avg us (calls) | recomputed frac | within 5 % | PMC build = bench build |",
+           "|---|---|---|---|---|---|---|---|"]
+    for r in rows:
+        out.append(f"| {r['tag']} ({r['workload']}) | {r['bound']} | {r['bench_frac']} | {r['bench_kernel_us']:.2f} | "
+                   f"{r['rocprof_avg_us'] and round(r['rocprof_avg_us'], 2)} ({r['rocprof_calls']}) | "
+                   f"{r['recomputed_frac'] and round(r['recomputed_frac'], 4)} | {r['agree_5pct']} | "
+                   f"{r['pmc_build'] == r['bench_build'] if r['pmc_build'] else 'no PMC entry'} |")
+    text = "\n".join(out)
+    print(text)
+    if a.out:
+        with open(a.out, "w") as fp:
+            fp.write(text + "\n")
+    return 0
+
+
+if __name__ == "__main__":
+    main()
