@@ -203,6 +203,7 @@ struct rt_camera {
     // once every frame launched so far has dispatched (host)
     unsigned long long* d_started = nullptr;
     unsigned long long started_cum[RT_LOOP_MAX_LANES] = {};
+    unsigned long long started_last[RT_LOOP_MAX_LANES] = {};  // blocks of each lane's last gated frame
     struct RectCache {
         bool valid = false;
         uint64_t gen = 0, tree = 0;
@@ -574,6 +575,11 @@ constexpr int64_t kSplitMaxTiles = RT_SPLIT_MAX_TILES;
 #endif
 #ifndef RT_COOP_MAX
 #define RT_COOP_MAX 256
+#endif
+// rt_run_frames' dispatch gate: a lane's frame starts once the previous
+// frame (other lane) has started RT_GATE_PCT % of its blocks
+#ifndef RT_GATE_PCT
+#define RT_GATE_PCT 50
 #endif
 
 
@@ -2152,6 +2158,7 @@ static int ensure_lanes(rt_camera* c, int L, bool comm) {
             (rc = hip_check(hipDeviceSynchronize(), "started init")))
             return rc;
         for (auto& v : c->started_cum) v = 0;
+        for (auto& v : c->started_last) v = 0;
     }
     return RT_OK;
 }
@@ -2235,8 +2242,9 @@ extern "C" int rt_run_frames(rt_camera* c, rt_comm* comm, const rt_frame_loop* a
     // once every block of frame j - 1 (on the previous lane) has started, so
     // the lanes never run in lockstep; KD frames of kernel 3 only (its blocks
     // count themselves).  RT_TUNE_GATE=0 turns it off (A/B).
+    const int gate_pct = tune("RT_TUNE_GATE_PCT", RT_GATE_PCT);
     const bool gated = L > 1 && a->mode == RT_MODE_KD && effective_kernel(c) == 3 && c->d_started &&
-                       tune("RT_TUNE_GATE", 1) != 0;
+                       tune("RT_TUNE_GATE", 1) != 0 && gate_pct > 0;
     const rt_tile* tile = a->tile.nranks > 0 ? &a->tile : nullptr;
     // rank 0 renders its bands straight into the frame it assembles (its
     // part of the frame is never copied); the gather places the peers' parts
@@ -2270,8 +2278,11 @@ extern "C" int rt_run_frames(rt_camera* c, rt_comm* comm, const rt_frame_loop* a
             break;
         const int ln = j % L;
         if (gated && j > 0) {
+            // frame j - 1 (lane pl) has started gate_pct % of its blocks
             const int pl = (j - 1) % L;
-            rc = launch_gate(c->d_started + pl, c->started_cum[pl], 2000.0, ls);
+            const unsigned long long prev = c->started_last[pl];
+            const unsigned long long target = c->started_cum[pl] - prev + (prev * (unsigned)gate_pct + 99) / 100;
+            rc = launch_gate(c->d_started + pl, target, 2000.0, ls);
             if (rc) break;
         }
         const bool timed = every > 0 && j % every == 0;
@@ -2282,7 +2293,10 @@ extern "C" int rt_run_frames(rt_camera* c, rt_comm* comm, const rt_frame_loop* a
         if (!rc)
             rc = render_common(c, xf, a->mode, a->flags | (direct ? RT_FLAG_FRAME_OUT : 0u), tile, target, nullptr, ls,
                                nullptr, gated ? c->d_started + ln : nullptr, &blocks);
-        if (!rc && gated) c->started_cum[ln] += (unsigned long long)blocks;
+        if (!rc && gated) {
+            c->started_cum[ln] += (unsigned long long)blocks;
+            c->started_last[ln] = (unsigned long long)blocks;
+        }
         if (!rc && timed) rc = hip_check(hipEventRecord(c->loop_ev[(size_t)(2 * t + 1)], ls), "loop timing");
         if (!rc && comm) {
             if (linked) {
