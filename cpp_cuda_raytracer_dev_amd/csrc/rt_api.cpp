@@ -564,11 +564,17 @@ constexpr int64_t kSplitMaxTiles = RT_SPLIT_MAX_TILES;
 // coop tiles: cost > RT_COOP_PCT % of the top (grids of fewer than
 // kSplitMaxTiles tiles; RT_COOP_PCT_LARGE % for larger ones), at most
 // n / RT_COOP_CAP_DIV and RT_COOP_MAX tiles (each takes 4 blocks)
+// Measured (round 4, r04d-r04h): coop tiles shorten the heaviest units'
+// chains (dragon 960x540: 25-27 -> 17-18 iterations) but their extra waves
+// slow the other heavy units' iterations (1.10 -> 1.25 us), and the frame
+// lost: C3 47.8k -> 43.2k FPS, knot 960x540 31.0k -> 30.2k, dragon 1080p
+// 16.48k -> 16.36k.  Off by default (0); debug bit 8192 selects them at
+// 60 % / 70 % (tests), 4096 makes every tile a coop tile.
 #ifndef RT_COOP_PCT
-#define RT_COOP_PCT 60
+#define RT_COOP_PCT 0
 #endif
 #ifndef RT_COOP_PCT_LARGE
-#define RT_COOP_PCT_LARGE 70
+#define RT_COOP_PCT_LARGE 0
 #endif
 #ifndef RT_COOP_CAP_DIV
 #define RT_COOP_CAP_DIV 8
@@ -578,8 +584,13 @@ constexpr int64_t kSplitMaxTiles = RT_SPLIT_MAX_TILES;
 #endif
 // rt_run_frames' dispatch gate: a lane's frame starts once the previous
 // frame (other lane) has started RT_GATE_PCT % of its blocks
+// Measured (r04g, r04h: knot 1080p, the driver's 20 frames / 1000 frames):
+// gate off 8.90k / 10.32k FPS, at 70 % 8.83k, 50 % 8.29-8.58k / 9.82k, 30 %
+// 8.22k / 9.36k, 15 % 8.02-8.21k / 9.37k, at 100 % (every block started)
+// 7.63-7.75k / 8.44k: the free-running lanes overlap more than any gate
+// lets them.  Off by default (0).
 #ifndef RT_GATE_PCT
-#define RT_GATE_PCT 50
+#define RT_GATE_PCT 0
 #endif
 
 
@@ -661,10 +672,12 @@ int cost_feedback(rt_camera* c, const TraceParams& p, void* stream, bool sampled
             return m;
         };
         const uint32_t top = n > 0 ? cost_of(ord[0]) : 0;
+        const bool sel8192 = (c->debug & 8192) != 0;
+        const int64_t cpct = n < kSplitMaxTiles ? (sel8192 ? 60 : tune("RT_TUNE_COOP_PCT", RT_COOP_PCT))
+                                                : (sel8192 ? 70 : tune("RT_TUNE_COOP_PCT_LARGE", RT_COOP_PCT_LARGE));
         if (c->tile_order == 3 && (p.rays == 16 || p.rays == 8) && kd3_waves(p.rays) == 4 && !(c->debug & 2048) &&
-            n > 0 && RT_COOP_PCT > 0) {
-            const int64_t pct = n < kSplitMaxTiles ? tune("RT_TUNE_COOP_PCT", RT_COOP_PCT)
-                                                   : tune("RT_TUNE_COOP_PCT_LARGE", RT_COOP_PCT_LARGE);
+            n > 0 && (cpct > 0 || (c->debug & 4096))) {
+            const int64_t pct = cpct;
             while (coop < std::min<int64_t>(n / tune("RT_TUNE_COOP_CAP_DIV", RT_COOP_CAP_DIV), RT_COOP_MAX) &&
                    100ull * cost_of(ord[(size_t)coop]) > (uint64_t)pct * top && top >= 24)
                 coop++;

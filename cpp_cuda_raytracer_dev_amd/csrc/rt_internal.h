@@ -57,7 +57,8 @@ enum Option : int32_t {
                         // 32 = counting renders stop after the root test, 128 = per-iteration
                         // stamps (RT_ITER_STAMPS builds, with 2), 512 = no split tiles,
                         // 1024 = no two-level iterations, 2048 = no coop tiles, 4096 = every
-                        // tile of a cost order a coop tile (tests)
+                        // tile of a cost order a coop tile (tests), 8192 = coop tiles above
+                        // 60 % / 70 % of the heaviest tile (tests; off by default)
     kOptPoolCap = 101,  // tests: shrink kernel 3's item pool (66..kPoolCap) to force its fallback
     kOptStampOffset = 102,  // get only: offset (u64) of the per-iteration stamps in the debug buffer
 };

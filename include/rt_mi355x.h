@@ -412,8 +412,10 @@ int rt_camera_info(const rt_camera* c, int32_t* w, int32_t* h, int32_t* max_dept
 #define RT_OPT_SPLIT_USED 9
 /* get only: tiles at the head of the current cost order whose units each
  * render with a whole 4-wave block on one item pool (block-cooperative
- * units): costlier than 60 % of the heaviest tile (70 % in grids of 2,048
- * tiles or more), at most an eighth of the tiles; the frame is the same. */
+ * units).  Off by default (measured slower with frames in flight, DESIGN.md
+ * §4 round 4); diagnostics bit 8192 selects the tiles costlier than 60 % of
+ * the heaviest (70 % in grids of 2,048 tiles or more, at most an eighth of
+ * the tiles), bit 4096 every tile.  The frame is the same. */
 #define RT_OPT_COOP_USED 10
 int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value);
 int rt_camera_get_option(const rt_camera* c, int32_t key, int32_t* value);

@@ -373,16 +373,18 @@ def test_split_tiles_same_frame(key, rays):
     assert s.cam.device_error(reset=True) == 0
 
 
-@pytest.mark.parametrize("key,rays,debug", [("dragon_960x540_m0", 0, 0), ("knot_960x540_m0", 0, 0),
-                                            ("knot_960x540_m0", 8, 0), ("dragon_1920x1080_m0", 0, 0),
-                                            ("knot_1920x1080_m0", 0, 0), ("dragon_960x540_m0", 0, 4096),
+@pytest.mark.parametrize("key,rays,debug", [("dragon_960x540_m0", 0, 8192), ("knot_960x540_m0", 0, 8192),
+                                            ("knot_960x540_m0", 8, 8192), ("dragon_1920x1080_m0", 0, 8192),
+                                            ("knot_1920x1080_m0", 0, 8192), ("dragon_960x540_m0", 0, 4096),
                                             ("dragon_960x540_m0", 8, 4096), ("rabbit_70k_960x540_m0", 0, 4096),
                                             ("tester_320x180_m0", 0, 4096)])
 def test_coop_tiles_same_frame(key, rays, debug):
     """Block-cooperative units: once a cost sample has
     arrived, the heaviest tiles of the cost order render each 16- or 8-ray
-    unit with a whole 4-wave block on one LDS pool (RT_OPT_COOP_USED > 0);
-    debug bit 4096 makes every tile a coop tile.  The frame and hit buffer
+    unit with a whole 4-wave block on one LDS pool (RT_OPT_COOP_USED > 0;
+    off by default since it measured slower, debug bit 8192 selects them as
+    the round-4 experiment did); debug bit 4096 makes every tile a coop
+    tile.  The frame and hit buffer
     stay the oracle's (committed hashes), and a counting render's visit
     counters equal the oracle's."""
     import hashlib
@@ -429,7 +431,7 @@ def test_coop_tiles_moved_pose(pose):
     w, h = 960, 540
     oargb, ohit, _ = H.oracle_render("dragon", w, h, 0, xform=xf.reshape(3, 4))
     dev = torch.device("cuda:0")
-    for debug, cap in ((4096, 0), (0, 0), (4096, 89)):
+    for debug, cap in ((4096, 0), (8192, 0), (4096, 89)):
         s = H.GpuScene("dragon", w, h, debug=debug or None)
         if cap:
             s.cam.set_option(_lib.RT_OPT_POOL_CAP, cap)

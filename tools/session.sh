@@ -15,6 +15,7 @@
 #   pmc <dir> <ctrs> -- <cmd...>   one rocprofv3 --pmc pass (counters only)
 #   stats <dir> -- <cmd...>        rocprofv3 --kernel-trace --stats
 #   trace <dir> -- <cmd...>        + --memory-copy-trace; traces kept gzipped (dir must start trace_)
+#   setenv VAR VALUE / unsetenv VAR  environment of the following steps
 #   pmcsum <key> <kernel> <dir...>  tools/pmc_traffic.py over pmc dirs of this session
 set -u
 TAG=$1; PLAN=$2
@@ -42,6 +43,13 @@ while read -r name to rest; do
     [ -z "${name:-}" ] && continue
     case $name in \#*) continue ;; esac
     eval "set -- $rest"  # plan lines may quote arguments
+    # `setenv VAR VALUE` / `unsetenv VAR`: the environment of the steps that
+    # follow (never put `env` after rocprofv3's `--`: the profiled program must
+    # be the program itself)
+    case $name in
+    setenv) export "$to=$1"; echo "== setenv $to=$1"; continue ;;
+    unsetenv) unset "$to"; echo "== unsetenv $to"; continue ;;
+    esac
     case $1 in
     bench) shift; cmd=(python -u bench.py "$@") ;;
     smoke) cmd=(python -u -c "import __graft_entry__ as g; g.smoke()") ;;
