@@ -535,7 +535,10 @@ def main():
     bytes_per_launch = B_INT * int(cnt[0]) + B_LEAF * int(cnt[1]) + B_HIT * int(cnt[2]) + B_PIX * my_pix
 
     loop_kind = a.loop
-    inflight = max(1, a.inflight) if loop_kind == "native" else 1
+    # --inflight -1: the persistent frame loop (RT_LOOP_PERSISTENT; one kernel
+    # takes many frames' blocks in frame order; N = 1, static scene)
+    persistent = loop_kind == "native" and a.inflight == -1 and not multi and not a.animate
+    inflight = (2 if persistent else max(1, a.inflight)) if loop_kind == "native" else 1
     if a.event_every <= 0:
         a.event_every = 8 if (multi or inflight > 1) else 1
     collective = a.collective
@@ -667,7 +670,7 @@ def main():
             return R.FrameLoop(cam, ng.local if ng is not None else outs, xform=xf, mode=a.mode, flags=sflag,
                                tile=tile if multi else None, render_stream=sptr, comm=ng,
                                comm_stream=cstream.cuda_stream if ng is not None else None,
-                               event_every=a.event_every, inflight=inflight,
+                               event_every=a.event_every, inflight=-1 if persistent else inflight,
                                xforms=anim_xfs if masks else None)
         return PyLoop()
 
@@ -734,7 +737,8 @@ def main():
         kern_ms, n_ev = solo
     kern_label = (f"median over {len(batch_ms)} batches of the mean period of {n_ev} solo frames back to back before "
                   f"the timed region (one in flight; kernel + the launch gap, an upper bound of the kernel time); the "
-                  f"timed frames keep {inflight} in flight"
+                  + (f"timed frames keep {inflight} in flight" if not persistent else
+                     "timed frames run in persistent launches (RT_LOOP_PERSISTENT)")
                   if solo is not None else
                   f"{n_ev} of {a.steps} timed frames (every {max(1, a.event_every)})")
     kern_extra = ({"kernel_ms_solo_batches": [round(b, 5) for b in batch_ms],
@@ -940,7 +944,7 @@ def main():
             "device_err": errs if multi else dev_err,
             "host": {"us_per_frame": round(host_us_per_frame, 2), "loop": "native (rt_run_frames)"
                      if not isinstance(loop, PyLoop) else "python",
-                     "frames_in_flight": inflight if not isinstance(loop, PyLoop) else 1,
+                     "frames_in_flight": ("persistent" if persistent else inflight) if not isinstance(loop, PyLoop) else 1,
                      "what": "host time spent enqueueing the timed frames / steps (rank 0)"},
             "kd_build": build_times,
             # build provenance: SHA-256 of the library's sources and flags

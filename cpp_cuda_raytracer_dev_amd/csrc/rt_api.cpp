@@ -202,6 +202,7 @@ struct rt_camera {
     // of its kernel-3 frames (device, zeroed once) and how many it will reach
     // once every frame launched so far has dispatched (host)
     unsigned long long* d_started = nullptr;
+    int32_t* d_pf_next = nullptr;    // the persistent frame loop's work counter
     unsigned long long started_cum[RT_LOOP_MAX_LANES] = {};
     unsigned long long started_last[RT_LOOP_MAX_LANES] = {};  // blocks of each lane's last gated frame
     struct RectCache {
@@ -1590,9 +1591,18 @@ static int flat_keys_for(rt_camera* c, hipStream_t stream, int64_t npix, unsigne
     return RT_OK;
 }
 
+// rt_run_frames' persistent frame loop: `frames` frames in one launch, frame
+// f into argb[(seq0 + f) % nbuf].
+struct PersistArgs {
+    int32_t frames, seq0, nbuf;
+    uint32_t* const* argb;
+};
+
 static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32_t flags, const rt_tile* tile,
                          uint32_t* argb, int64_t* hit, void* stream, uint32_t* display = nullptr,
-                         unsigned long long* started = nullptr, int64_t* blocks = nullptr) {
+                         unsigned long long* started = nullptr, int64_t* blocks = nullptr,
+                         const PersistArgs* pf = nullptr, int32_t* rendered = nullptr) {
+    if (rendered) *rendered = 1;
     if (!c) return fail(RT_ERR_INVALID, "rt_render: null camera");
     if (mode != RT_MODE_KD && mode != RT_MODE_FLAT) return fail(RT_ERR_INVALID, "rt_render: mode %u", mode);
     int rc = check_tile(tile);
@@ -1682,7 +1692,25 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
         p.coop = 0;
     }
     const bool order3 = p.cost != nullptr;
-    const bool sampled = order3 && cost_sample_now(c, st);
+    // the persistent loop (KD kernel 3, fused far fill, no per-frame
+    // outputs beyond the frame): one launch for pf->frames frames, no cost
+    // sample inside it
+    const bool persist = pf && pf->frames > 1 && mode == RT_MODE_KD && effective_kernel(c) == 3 && p.coarse_blocks == 0 &&
+                         flags == 0 && !display && (p.rays == 16 || p.rays == 8) &&
+                         p.xf[3] == 0.0f && p.xf[7] == 0.0f && p.xf[11] == 0.0f;  // k_trace_kd3_pf: untranslated
+    p.pf_frames = 0;
+    if (persist) {
+        if (!c->d_pf_next && (rc = dev_alloc(&c->d_pf_next, 1, "hipMalloc(pf_next)"))) return rc;
+        if ((rc = hip_check(hipMemsetAsync(c->d_pf_next, 0, sizeof(int32_t), st), "pf counter reset"))) return rc;
+        p.pf_frames = pf->frames;
+        p.pf_blocks = (int32_t)fine_grid_blocks(p);
+        p.pf_nbuf = pf->nbuf;
+        p.pf_seq0 = pf->seq0 % pf->nbuf;
+        p.pf_next = c->d_pf_next;
+        for (int k = 0; k < RT_LOOP_MAX_BUF; k++) p.pf_argb[k] = k < pf->nbuf ? pf->argb[k] : nullptr;
+        if (rendered) *rendered = pf->frames;
+    }
+    const bool sampled = order3 && !persist && cost_sample_now(c, st);
     if (sampled) {
         p.cost = c->d_cost_host;
         // the kernel writes this frame's costs into the pinned host buffer;
@@ -2036,6 +2064,7 @@ extern "C" void rt_camera_destroy(rt_camera* c) {
     c->d_order = nullptr;
     dev_free(c->d_dbg);
     dev_free(c->d_started);
+    dev_free(c->d_pf_next);
     for (auto& k : c->flat_keys) dev_free(k.d);
     for (hipEvent_t e : c->slot_join_ev)
         if (e) (void)hipEventDestroy(e);
@@ -2176,11 +2205,84 @@ static int ensure_lanes(rt_camera* c, int L, bool comm) {
     return RT_OK;
 }
 
+// rt_run_frames with RT_LOOP_PERSISTENT: frames in launches of up to
+// kPersistChunk frames, each a persistent k_trace_kd3 whose resident blocks
+// take (frame, block) pairs from one counter (render_common's PersistArgs).
+// Until a cost order exists (tile order 3) frames launch one at a time, so
+// that cost samples are taken; persistent launches take none.
+constexpr int32_t kPersistChunk = 128;
+
+static int run_frames_persistent(rt_camera* c, const rt_frame_loop* a, int32_t nframes, int64_t* seq,
+                                 double* kernel_ms_avg, int32_t* kernel_ms_frames, double* host_ms) {
+    hipStream_t rs = (hipStream_t)a->render_stream;
+    const rt_tile* tile = a->tile.nranks > 0 ? &a->tile : nullptr;
+    std::vector<std::pair<int, int32_t>> timed;  // (event pair, frames) of bracketed launches
+    int rc = RT_OK;
+    const int every = a->event_every;
+    const auto h0 = std::chrono::steady_clock::now();
+    for (int32_t j = 0; j < nframes && !rc;) {
+        const bool have_order = c->tile_order != 3 || c->order_gen == c->layout_gen;
+        const int32_t chunk = have_order ? std::min(nframes - j, kPersistChunk) : 1;
+        const bool time_it = every > 0;
+        const int pair = (int)timed.size();
+        if (time_it && (int64_t)c->loop_ev.size() < 2 * (pair + 1)) {
+            hipEvent_t e0 = nullptr, e1 = nullptr;
+            if ((rc = hip_check(hipEventCreate(&e0), "loop timing event")) ||
+                (rc = hip_check(hipEventCreate(&e1), "loop timing event")))
+                break;
+            c->loop_ev.push_back(e0);
+            c->loop_ev.push_back(e1);
+        }
+        if (time_it && (rc = hip_check(hipEventRecord(c->loop_ev[(size_t)(2 * pair)], rs), "loop timing"))) break;
+        const PersistArgs pf{chunk, (int32_t)((*seq) % a->nbuf), a->nbuf, a->d_local};
+        const int k = (int)((*seq) % a->nbuf);
+        int32_t done = 1;
+        rc = render_common(c, a->xform, a->mode, a->flags, tile, a->d_local[k], nullptr, rs, nullptr, nullptr, nullptr,
+                           chunk > 1 ? &pf : nullptr, &done);
+        if (rc) break;
+        if (time_it) {
+            if ((rc = hip_check(hipEventRecord(c->loop_ev[(size_t)(2 * pair + 1)], rs), "loop timing"))) break;
+            timed.emplace_back(pair, done);
+        }
+        j += done;
+        *seq += done;
+    }
+    if (host_ms) *host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
+    c->nactive = 0;
+    if (!rc) rc = hip_check(hipStreamSynchronize(rs), "loop sync");
+    if (rc) {
+        (void)hipDeviceSynchronize();
+        return rc;
+    }
+    double sum = 0.0;
+    int32_t cnt = 0;
+    for (const auto& tp : timed) {
+        float ms = 0.0f;
+        if (hipEventElapsedTime(&ms, c->loop_ev[(size_t)(2 * tp.first)], c->loop_ev[(size_t)(2 * tp.first + 1)]) ==
+            hipSuccess) {
+            sum += ms;
+            cnt += tp.second;
+        }
+    }
+    // per frame: the launches' bracketed time over the frames they rendered
+    if (kernel_ms_avg) *kernel_ms_avg = cnt ? sum / cnt : 0.0;
+    if (kernel_ms_frames) *kernel_ms_frames = cnt;
+    return RT_OK;
+}
+
 extern "C" int rt_run_frames(rt_camera* c, rt_comm* comm, const rt_frame_loop* a, int32_t nframes, int64_t* seq,
                              double* kernel_ms_avg, int32_t* kernel_ms_frames, double* host_ms) {
-    if (!c || !a || !seq || nframes < 0 || a->nbuf < 1 || a->nbuf > RT_LOOP_MAX_BUF || a->inflight < 0 ||
-        a->inflight > RT_LOOP_MAX_LANES)
+    if (!c || !a || !seq || nframes < 0 || a->nbuf < 1 || a->nbuf > RT_LOOP_MAX_BUF ||
+        (a->inflight < 0 && a->inflight != RT_LOOP_PERSISTENT) || a->inflight > RT_LOOP_MAX_LANES)
         return fail(RT_ERR_INVALID, "rt_run_frames: bad argument");
+    if (a->inflight == RT_LOOP_PERSISTENT) {
+        if (comm || a->nxforms > 0)
+            return fail(RT_ERR_INVALID, "rt_run_frames: the persistent loop renders a static scene without a gather");
+        for (int k = 0; k < a->nbuf; k++)
+            if (!a->d_local[k]) return fail(RT_ERR_INVALID, "rt_run_frames: missing buffer of set %d", k);
+        DeviceGuard g(c->device);
+        return run_frames_persistent(c, a, nframes, seq, kernel_ms_avg, kernel_ms_frames, host_ms);
+    }
     if (a->nxforms < 0 || (a->nxforms > 0 && !a->xforms))
         return fail(RT_ERR_INVALID, "rt_run_frames: bad transform sequence");
     const int L = std::max(1, (int)a->inflight);

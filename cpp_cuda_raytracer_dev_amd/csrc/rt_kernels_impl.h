@@ -111,9 +111,14 @@ __device__ __forceinline__ uint32_t phong(const float pnt[3], const float nrm[3]
 // window's buffer is overwritten by color_cam_cuda only where rmi >= 0,
 // TD/Camera.cu:27-61, and reset to background + Phong by the SET pass after
 // the blit, TD/WinMain.cpp:212-237, TD/Camera.cu:77-84).
+// The persistent frame loop's output buffer of the (frame, block) a block is
+// rendering (k_trace_kd3; set by its thread 0 before each block).
+__shared__ uint32_t* s_pf_argb;
+
 __device__ __forceinline__ void put_pixel(const TraceParams& P, int64_t out, uint32_t argb, bool hit) {
     if (P.display) P.display[out] = hit ? argb : P.argb[out];
-    P.argb[out] = argb;
+    uint32_t* base = P.pf_frames > 0 ? s_pf_argb : P.argb;
+    base[out] = argb;
 }
 
 __device__ __forceinline__ int32_t tile_index(const TraceParams& P, int32_t b) {
@@ -2265,20 +2270,18 @@ __device__ __forceinline__ void trace_unit_coop(const TraceParams& P, CoopLds<kR
 #else
 #define RT_KD3_BOUNDS(threads) __launch_bounds__(threads)
 #endif
-template <int kRays, bool kTranslated, bool kWriteHit, bool kCount, int kShadow>
-__global__ RT_KD3_BOUNDS(64 * kd3_waves(kRays)) void k_trace_kd3(TraceParams P) {
+// One block of k_trace_kd3's grid: block index b (blockIdx.x, or the virtual
+// index of the persistent frame loop below).
+template <int kRays, bool kTranslated, bool kWriteHit, bool kCount, int kShadow, int kCap, int kRayVec>
+__device__ __forceinline__ void kd3_block(const TraceParams& P, WaveLds<kRays, kCap, kRayVec>* s_lds, int32_t b,
+                                          int wv, int lane) {
     constexpr int kWaves = kd3_waves(kRays);
-    constexpr int kCap = pool_cap_for<kRays>();
-    constexpr int kRayVec = (kTranslated || kShadow) ? 5 : 3;  // float4s of per-ray data in LDS
-    __shared__ WaveLds<kRays, kCap, kRayVec> s_lds[kWaves];
-    const int wv = wave_id(), lane = (int)threadIdx.x & 63;
-    if (P.started && threadIdx.x == 0) atomicAdd(P.started, 1ull);  // the dispatch gate's count (k_gate)
     Counts C;
     const int32_t ntiles = P.tiles_x * P.block_rows;
+    const int32_t bslot = b;  // diagnostics slot of this block
     // blocks: 4 per coop tile, 2 per split tile, 1 per other fine tile, then
     // the far fill
     const int32_t head = 3 * P.coop + P.split;
-    int32_t b = (int32_t)blockIdx.x;
     if (b >= ntiles + head) {
         // fused far fill: blocks after the fine tiles write the coarse groups,
         // all far by construction (set_fine_region); unrolled as in k_coarse_kd3
@@ -2315,10 +2318,11 @@ __global__ RT_KD3_BOUNDS(64 * kd3_waves(kRays)) void k_trace_kd3(TraceParams P) 
             // per-wave render wrote them (the coop chain is no measure of the
             // single-wave cost the order and the thresholds compare)
             uint32_t* cost = nullptr;
-            static_assert(sizeof(CoopLds<kRays, kCap, kRayVec>) <= sizeof(s_lds), "coop pool exceeds the block's LDS");
+            static_assert(sizeof(CoopLds<kRays, kCap, kRayVec>) <= kWaves * sizeof(WaveLds<kRays, kCap, kRayVec>),
+                          "coop pool exceeds the block's LDS");
             trace_unit_coop<kRays, kCap, kRayVec, kTranslated, kWriteHit, kCount>(
                 P, *reinterpret_cast<CoopLds<kRays, kCap, kRayVec>*>(s_lds), unit_of_tile(P, ti, u), wv, lane,
-                (size_t)blockIdx.x * kWaves + wv, cost, C);
+                (size_t)bslot * kWaves + wv, cost, C);
             if (kCount) count_flush(P, C);
             return;
         }
@@ -2341,9 +2345,50 @@ __global__ RT_KD3_BOUNDS(64 * kd3_waves(kRays)) void k_trace_kd3(TraceParams P) 
     if (split && kRays == 16) U.yin = (U.yin - wv * (kRays / 8)) + (b & 1) * kWaves + wv;
     if (split && kRays == 8) U.x0 += (b & 1) * 4;
     trace_unit<kRays, kCap, kRayVec, kTranslated, kWriteHit, kCount, kShadow>(
-        P, s_lds[wv], U, lane, (size_t)blockIdx.x * kWaves + wv, cost, C, split && kRays == 16 ? 1 : kRays / 8,
+        P, s_lds[wv], U, lane, (size_t)bslot * kWaves + wv, cost, C, split && kRays == 16 ? 1 : kRays / 8,
         split && kRays == 8 ? 4 : 8);
     if (kCount) count_flush(P, C);
+}
+
+// Kernel 3: one frame, one block per grid slot.
+template <int kRays, bool kTranslated, bool kWriteHit, bool kCount, int kShadow>
+__global__ RT_KD3_BOUNDS(64 * kd3_waves(kRays)) void k_trace_kd3(TraceParams P) {
+    constexpr int kCap = pool_cap_for<kRays>();
+    constexpr int kRayVec = (kTranslated || kShadow) ? 5 : 3;  // float4s of per-ray data in LDS
+    __shared__ WaveLds<kRays, kCap, kRayVec> s_lds[kd3_waves(kRays)];
+    const int wv = wave_id(), lane = (int)threadIdx.x & 63;
+    if (P.started && threadIdx.x == 0) atomicAdd(P.started, 1ull);  // the dispatch gate's count (k_gate)
+    kd3_block<kRays, kTranslated, kWriteHit, kCount, kShadow, kCap, kRayVec>(P, s_lds, (int32_t)blockIdx.x, wv, lane);
+}
+
+// Kernel 3's persistent frame loop (rt_run_frames with RT_LOOP_PERSISTENT;
+// P.pf_frames > 0): as many blocks as are resident, each taking the next
+// (frame, block) from one counter, frame-major, so frame f + 1's heaviest
+// tiles start on the CUs frame f's tail frees, with no launch between frames
+// and no two frames in lockstep.  Frame f writes P.pf_argb[(P.pf_seq0 + f) %
+// P.pf_nbuf] (static scenes: every frame is the same frame).  Its own kernel:
+// the loop around the block body raises register pressure (a loop in
+// k_trace_kd3 itself cost the 16-ray instance 26 spilled VGPRs).
+template <int kRays>
+__global__ RT_KD3_BOUNDS(64 * kd3_waves(kRays)) void k_trace_kd3_pf(TraceParams P) {
+    constexpr int kCap = pool_cap_for<kRays>();
+    constexpr int kRayVec = 3;
+    __shared__ WaveLds<kRays, kCap, kRayVec> s_lds[kd3_waves(kRays)];
+    __shared__ int32_t s_t;
+    const int wv = wave_id(), lane = (int)threadIdx.x & 63;
+    const int32_t total = P.pf_frames * P.pf_blocks;
+    for (;;) {
+        if (threadIdx.x == 0) {
+            const int32_t t = atomicAdd(P.pf_next, 1);
+            s_t = t;
+            if (t < total) s_pf_argb = P.pf_argb[(P.pf_seq0 + t / P.pf_blocks) % P.pf_nbuf];
+        }
+        __syncthreads();
+        const int32_t t = s_t;
+        if (t >= total) break;  // the same t on every wave: the whole block ends
+        kd3_block<kRays, false, false, false, 0, kCap, kRayVec>(P, s_lds, t % P.pf_blocks, wv, lane);
+        __syncthreads();  // the block's LDS and s_t are free for the next (frame, block)
+    }
 }
 
 // The coarse groups (every 8x8 group of this rank outside the fine tiles),

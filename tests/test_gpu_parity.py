@@ -1451,3 +1451,43 @@ def test_far_along_key_sequence_background():
             assert (got[sel] == want[sel]).all(), f"tick {i} rank {r}"
     assert checked["visible"] >= 2 and checked["behind"] >= 1, checked
     assert s.cam.device_error(reset=True) == 0
+
+
+@pytest.mark.parametrize("key", ["dragon_960x540_m0", "knot_1920x1080_m0", "dragon_1920x1080_m0"])
+def test_persistent_frame_loop(key):
+    """rt_run_frames with RT_LOOP_PERSISTENT: launches of up to 128 frames,
+    each one kernel whose resident blocks take (frame, block) pairs from one
+    counter (k_trace_kd3_pf).  Every buffer set holds the oracle's frame
+    (committed hash) after 1, 3, 20 and 200 frames, with 2 and 3 sets; the
+    first frames before a cost order exists launch one at a time.  A moving
+    object or a gather is rejected."""
+    import hashlib
+    import torch
+    from cpp_cuda_raytracer_dev_amd import _lib
+    ent = H.frame_hashes()[key]
+    if not H.mesh_matches(ent):
+        pytest.skip("stand-in mesh bits differ on this host")
+    w, h = ent["w"], ent["h"]
+    s = H.GpuScene(ent["scene"], w, h)
+    dev = torch.device("cuda:0")
+    st = torch.cuda.Stream(device=dev)
+    for nbuf in (2, 3):
+        bufs = [torch.full((w * h,), 0x7BADBEEF, dtype=torch.int32, device=dev) for _ in range(nbuf)]
+        loop = R.FrameLoop(s.cam, bufs, mode=0, render_stream=st.cuda_stream, event_every=1,
+                           inflight=_lib.RT_LOOP_PERSISTENT)
+        for n in (1, 3, 20, 200):
+            for b in bufs:
+                b.fill_(0x7BADBEEF)
+            torch.cuda.synchronize()
+            ms, cnt, host = loop.run(n)
+            torch.cuda.synchronize()
+            assert cnt == n and ms > 0
+            # every set the loop wrote holds the frame (the loop's sets rotate from its sequence number)
+            shas = {hashlib.sha256(b.cpu().numpy().view(np.uint32).tobytes()).hexdigest() for b in bufs}
+            assert ent["argb_sha"] in shas
+            if n >= nbuf:
+                assert shas == {ent["argb_sha"]}, (key, nbuf, n)
+        assert s.cam.device_error(reset=True) == 0
+    with pytest.raises(_lib.RtError):
+        R.FrameLoop(s.cam, bufs, mode=0, render_stream=st.cuda_stream, inflight=_lib.RT_LOOP_PERSISTENT,
+                    xforms=np.stack([np.eye(3, 4, dtype=np.float32).reshape(12)] * 2)).run(4)
