@@ -202,7 +202,6 @@ struct rt_camera {
     // of its kernel-3 frames (device, zeroed once) and how many it will reach
     // once every frame launched so far has dispatched (host)
     unsigned long long* d_started = nullptr;
-    int32_t* d_pf_next = nullptr;    // the persistent frame loop's work counter
     unsigned long long started_cum[RT_LOOP_MAX_LANES] = {};
     unsigned long long started_last[RT_LOOP_MAX_LANES] = {};  // blocks of each lane's last gated frame
     struct RectCache {
@@ -1591,8 +1590,8 @@ static int flat_keys_for(rt_camera* c, hipStream_t stream, int64_t npix, unsigne
     return RT_OK;
 }
 
-// rt_run_frames' persistent frame loop: `frames` frames in one launch, frame
-// f into argb[(seq0 + f) % nbuf].
+// rt_run_frames' multi-frame launches: `frames` frames in one grid, frame f
+// into argb[(seq0 + f) % nbuf].
 struct PersistArgs {
     int32_t frames, seq0, nbuf;
     uint32_t* const* argb;
@@ -1696,17 +1695,13 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
     // outputs beyond the frame): one launch for pf->frames frames, no cost
     // sample inside it
     const bool persist = pf && pf->frames > 1 && mode == RT_MODE_KD && effective_kernel(c) == 3 && p.coarse_blocks == 0 &&
-                         flags == 0 && !display && (p.rays == 16 || p.rays == 8) &&
-                         p.xf[3] == 0.0f && p.xf[7] == 0.0f && p.xf[11] == 0.0f;  // k_trace_kd3_pf: untranslated
+                         flags == 0 && !display;
     p.pf_frames = 0;
     if (persist) {
-        if (!c->d_pf_next && (rc = dev_alloc(&c->d_pf_next, 1, "hipMalloc(pf_next)"))) return rc;
-        if ((rc = hip_check(hipMemsetAsync(c->d_pf_next, 0, sizeof(int32_t), st), "pf counter reset"))) return rc;
         p.pf_frames = pf->frames;
         p.pf_blocks = (int32_t)fine_grid_blocks(p);
         p.pf_nbuf = pf->nbuf;
         p.pf_seq0 = pf->seq0 % pf->nbuf;
-        p.pf_next = c->d_pf_next;
         for (int k = 0; k < RT_LOOP_MAX_BUF; k++) p.pf_argb[k] = k < pf->nbuf ? pf->argb[k] : nullptr;
         if (rendered) *rendered = pf->frames;
     }
@@ -2064,7 +2059,6 @@ extern "C" void rt_camera_destroy(rt_camera* c) {
     c->d_order = nullptr;
     dev_free(c->d_dbg);
     dev_free(c->d_started);
-    dev_free(c->d_pf_next);
     for (auto& k : c->flat_keys) dev_free(k.d);
     for (hipEvent_t e : c->slot_join_ev)
         if (e) (void)hipEventDestroy(e);
@@ -2206,8 +2200,8 @@ static int ensure_lanes(rt_camera* c, int L, bool comm) {
 }
 
 // rt_run_frames with RT_LOOP_PERSISTENT: frames in launches of up to
-// kPersistChunk frames, each a persistent k_trace_kd3 whose resident blocks
-// take (frame, block) pairs from one counter (render_common's PersistArgs).
+// kPersistChunk frames, each one k_trace_kd3 grid of every frame's blocks,
+// frame-major (render_common's PersistArgs).
 // Until a cost order exists (tile order 3) frames launch one at a time, so
 // that cost samples are taken; persistent launches take none.
 constexpr int32_t kPersistChunk = 128;

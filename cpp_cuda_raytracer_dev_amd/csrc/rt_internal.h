@@ -150,12 +150,10 @@ struct TraceParams {
     int32_t debug;                 // diagnostic builds only: 1 = skip traversal
     unsigned long long* dbg;       // per-wave (t_start, t_end, visits) when non-null
     unsigned long long* started;   // kernel 3: count of started blocks (rt_run_frames' dispatch gate), or null
-    // The persistent frame loop (kernel 3; pf_frames > 0): pf_frames frames of
-    // pf_blocks blocks each, taken in order from the counter *pf_next (zeroed
-    // before the launch) by the launch's resident blocks; frame f writes
+    // A multi-frame launch (kernel 3; pf_frames > 0): pf_frames frames of
+    // pf_blocks blocks each, frame-major in one grid; frame f writes
     // pf_argb[(pf_seq0 + f) % pf_nbuf].
     int32_t pf_frames, pf_blocks, pf_seq0, pf_nbuf;
-    int32_t* pf_next;
     uint32_t* pf_argb[RT_LOOP_MAX_BUF];
     uint32_t root_ref;
     uint32_t ntri;

@@ -1,10 +1,6 @@
 // rt_kernels.hip -- the launchers of the gfx950 kernels (rt_kernels_impl.h).
 // The KD kernels' instances live in rt_kd_dispatch.hip, compiled once per
 // (translated, write-hit, count) combination (build.py).
-#include <algorithm>
-#include <mutex>
-#include <vector>
-
 #include "rt_kernels_impl.h"
 
 namespace rt {
@@ -64,24 +60,6 @@ int launch_pair_tri(const float4* trec, uint32_t ntri, float4* tpair, void* stre
     return check_launch<void>("k_pair_tri");
 }
 
-// Blocks of `fn` resident on the whole device at once (occupancy x CUs),
-// cached per kernel; 0 when the runtime cannot say.
-unsigned resident_blocks(const void* fn, unsigned threads) {
-    static std::mutex m;
-    static std::vector<std::pair<const void*, unsigned>> cache;
-    std::lock_guard<std::mutex> lk(m);
-    for (const auto& e : cache)
-        if (e.first == fn) return e.second;
-    int dev = 0, cus = 0, per = 0;
-    unsigned res = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, (int)threads, 0) == hipSuccess && per > 0 && cus > 0)
-        res = (unsigned)(per * cus);
-    cache.emplace_back(fn, res);
-    return res;
-}
-
 int launch_trace(const TraceParams& p, uint32_t mode, uint32_t flags, int kernel_version, void* stream, int part) {
     hipStream_t s = (hipStream_t)stream;
     const bool wh = (flags & RT_FLAG_WRITE_HIT) != 0, cnt = (flags & RT_FLAG_COUNT) != 0;
@@ -117,14 +95,7 @@ int launch_trace(const TraceParams& p, uint32_t mode, uint32_t flags, int kernel
                         : (cnt ? kd_kernel_101(v, r, sh, coarse) : kd_kernel_100(v, r, sh, coarse));
         else fn = wh ? (cnt ? kd_kernel_011(v, r, sh, coarse) : kd_kernel_010(v, r, sh, coarse))
                      : (cnt ? kd_kernel_001(v, r, sh, coarse) : kd_kernel_000(v, r, sh, coarse));
-        if (!coarse && p.pf_frames > 0) {
-            // the persistent frame loop (plain untranslated walks only: the
-            // caller checks): as many blocks as are resident
-            fn = r == 8 ? k_trace_kd3_pf<8> : k_trace_kd3_pf<16>;
-            const unsigned res = resident_blocks((const void*)fn, threads);
-            const unsigned long long total = (unsigned long long)grid * (unsigned)p.pf_frames;
-            grid = (unsigned)std::min<unsigned long long>(total, res ? res : grid);
-        }
+        if (!coarse && p.pf_frames > 0) grid *= (unsigned)p.pf_frames;  // a multi-frame launch, frame-major
         fn<<<grid, coarse ? 128u : threads, 0, s>>>(p);
         int rc = check_launch<void>(coarse ? "k_coarse_kd3" : "k_trace_kd");
         if (rc) return rc;

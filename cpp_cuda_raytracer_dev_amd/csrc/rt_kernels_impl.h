@@ -111,8 +111,8 @@ __device__ __forceinline__ uint32_t phong(const float pnt[3], const float nrm[3]
 // window's buffer is overwritten by color_cam_cuda only where rmi >= 0,
 // TD/Camera.cu:27-61, and reset to background + Phong by the SET pass after
 // the blit, TD/WinMain.cpp:212-237, TD/Camera.cu:77-84).
-// The persistent frame loop's output buffer of the (frame, block) a block is
-// rendering (k_trace_kd3; set by its thread 0 before each block).
+// A multi-frame launch's output buffer of the frame a block renders
+// (k_trace_kd3; stored by each wave's lane 0 at the block's start).
 __shared__ uint32_t* s_pf_argb;
 
 __device__ __forceinline__ void put_pixel(const TraceParams& P, int64_t out, uint32_t argb, bool hit) {
@@ -2350,7 +2350,13 @@ __device__ __forceinline__ void kd3_block(const TraceParams& P, WaveLds<kRays, k
     if (kCount) count_flush(P, C);
 }
 
-// Kernel 3: one frame, one block per grid slot.
+// Kernel 3: one frame, one block per grid slot.  A multi-frame launch
+// (rt_run_frames with RT_LOOP_PERSISTENT; P.pf_frames > 0) has pf_frames x
+// pf_blocks blocks, frame-major: block i renders block i % pf_blocks of frame
+// i / pf_blocks into P.pf_argb[(P.pf_seq0 + frame) % P.pf_nbuf].  Blocks are
+// dispatched in index order, so frame f + 1's heaviest tiles start on the CUs
+// frame f's tail frees, with no launch between frames and no two frames in
+// lockstep (static scenes: every frame is the same frame).
 template <int kRays, bool kTranslated, bool kWriteHit, bool kCount, int kShadow>
 __global__ RT_KD3_BOUNDS(64 * kd3_waves(kRays)) void k_trace_kd3(TraceParams P) {
     constexpr int kCap = pool_cap_for<kRays>();
@@ -2358,37 +2364,15 @@ __global__ RT_KD3_BOUNDS(64 * kd3_waves(kRays)) void k_trace_kd3(TraceParams P) 
     __shared__ WaveLds<kRays, kCap, kRayVec> s_lds[kd3_waves(kRays)];
     const int wv = wave_id(), lane = (int)threadIdx.x & 63;
     if (P.started && threadIdx.x == 0) atomicAdd(P.started, 1ull);  // the dispatch gate's count (k_gate)
-    kd3_block<kRays, kTranslated, kWriteHit, kCount, kShadow, kCap, kRayVec>(P, s_lds, (int32_t)blockIdx.x, wv, lane);
-}
-
-// Kernel 3's persistent frame loop (rt_run_frames with RT_LOOP_PERSISTENT;
-// P.pf_frames > 0): as many blocks as are resident, each taking the next
-// (frame, block) from one counter, frame-major, so frame f + 1's heaviest
-// tiles start on the CUs frame f's tail frees, with no launch between frames
-// and no two frames in lockstep.  Frame f writes P.pf_argb[(P.pf_seq0 + f) %
-// P.pf_nbuf] (static scenes: every frame is the same frame).  Its own kernel:
-// the loop around the block body raises register pressure (a loop in
-// k_trace_kd3 itself cost the 16-ray instance 26 spilled VGPRs).
-template <int kRays>
-__global__ RT_KD3_BOUNDS(64 * kd3_waves(kRays)) void k_trace_kd3_pf(TraceParams P) {
-    constexpr int kCap = pool_cap_for<kRays>();
-    constexpr int kRayVec = 3;
-    __shared__ WaveLds<kRays, kCap, kRayVec> s_lds[kd3_waves(kRays)];
-    __shared__ int32_t s_t;
-    const int wv = wave_id(), lane = (int)threadIdx.x & 63;
-    const int32_t total = P.pf_frames * P.pf_blocks;
-    for (;;) {
-        if (threadIdx.x == 0) {
-            const int32_t t = atomicAdd(P.pf_next, 1);
-            s_t = t;
-            if (t < total) s_pf_argb = P.pf_argb[(P.pf_seq0 + t / P.pf_blocks) % P.pf_nbuf];
-        }
-        __syncthreads();
-        const int32_t t = s_t;
-        if (t >= total) break;  // the same t on every wave: the whole block ends
-        kd3_block<kRays, false, false, false, 0, kCap, kRayVec>(P, s_lds, t % P.pf_blocks, wv, lane);
-        __syncthreads();  // the block's LDS and s_t are free for the next (frame, block)
+    int32_t b = (int32_t)blockIdx.x;
+    if (P.pf_frames > 0) {
+        const int32_t f = b / P.pf_blocks;
+        b -= f * P.pf_blocks;
+        // every wave's lane 0 stores the same pointer, then its own lanes read it
+        if (lane == 0) s_pf_argb = P.pf_argb[(P.pf_seq0 + f) % P.pf_nbuf];
+        __builtin_amdgcn_wave_barrier();
     }
+    kd3_block<kRays, kTranslated, kWriteHit, kCount, kShadow, kCap, kRayVec>(P, s_lds, b, wv, lane);
 }
 
 // The coarse groups (every 8x8 group of this rank outside the fine tiles),

@@ -319,8 +319,8 @@ void rt_comm_destroy(rt_comm* c);
 #define RT_LOOP_MAX_BUF 8
 #define RT_LOOP_MAX_LANES 4
 /* inflight = RT_LOOP_PERSISTENT: a static scene's frames (no comm, no xforms)
- * in launches of up to 128 frames, each one kernel whose resident blocks take
- * (frame, block) pairs in frame order from one counter, so frame j + 1's
+ * in launches of up to 128 frames, each one grid of every frame's blocks in
+ * frame order (blocks are dispatched in index order), so frame j + 1's
  * heaviest tiles start on the CUs frame j's tail frees; frame j writes set
  * j % nbuf (every frame of a static scene is the same frame).  KD mode with
  * kernel 3, flags 0 and the fused far fill; otherwise (and until a cost order
