@@ -88,8 +88,11 @@ def parse():
     ap.add_argument("--loop", default="native", choices=["native", "python"],
                     help="frame loop: native = rt_run_frames (C++, the render + RCCL gather enqueued per frame "
                          "without Python), python = the same calls from Python (torch collectives, --animate)")
-    ap.add_argument("--inflight", type=int, default=2,
-                    help="native loop: frames in flight on the library's render lanes (rt_frame_loop.inflight; "
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="native loop: 0 = automatic (multi-frame launches for frames below 1920x1080 pixels at one "
+                         "GPU, else 2), -1 = multi-frame launches (RT_LOOP_MULTIFRAME: one grid of many frames' "
+                         "blocks, frame-major; static scene, N = 1), else frames in flight on the library's render "
+                         "lanes (rt_frame_loop.inflight; "
                          "1 = one frame at a time).  The roofline's kernel time comes from a separate pass of "
                          "solo frames (one in flight), since overlapped launches share the GPU")
     ap.add_argument("--solo-frames", type=int, default=200,
@@ -535,10 +538,16 @@ def main():
     bytes_per_launch = B_INT * int(cnt[0]) + B_LEAF * int(cnt[1]) + B_HIT * int(cnt[2]) + B_PIX * my_pix
 
     loop_kind = a.loop
-    # --inflight -1: the persistent frame loop (RT_LOOP_PERSISTENT; one kernel
-    # takes many frames' blocks in frame order; N = 1, static scene)
-    persistent = loop_kind == "native" and a.inflight == -1 and not multi and not a.animate
-    inflight = (2 if persistent else max(1, a.inflight)) if loop_kind == "native" else 1
+    # --inflight -1: multi-frame launches (RT_LOOP_MULTIFRAME: one grid holds
+    # many frames' blocks, frame-major; N = 1, static scene, KD mode, no
+    # shadow rays).  0 (auto) takes them for frames below 1920x1080, where
+    # they measured faster than two lanes (dragon 960x540 48.7k -> 50.5k FPS,
+    # knot 960x540 31.0k -> 34.3k); at 1920x1080 two lanes stay (knot 10.44k
+    # vs 10.31k, dragon 16.59k vs 16.26k; r04i)
+    can_mf = loop_kind == "native" and not multi and not a.animate and a.mode == 0 and not a.shadow
+    multiframe = can_mf and (a.inflight == -1 or (a.inflight == 0 and w * h < 1920 * 1080))
+    persistent = multiframe
+    inflight = (2 if multiframe or a.inflight <= 0 else a.inflight) if loop_kind == "native" else 1
     if a.event_every <= 0:
         a.event_every = 8 if (multi or inflight > 1) else 1
     collective = a.collective
@@ -738,7 +747,7 @@ def main():
     kern_label = (f"median over {len(batch_ms)} batches of the mean period of {n_ev} solo frames back to back before "
                   f"the timed region (one in flight; kernel + the launch gap, an upper bound of the kernel time); the "
                   + (f"timed frames keep {inflight} in flight" if not persistent else
-                     "timed frames run in persistent launches (RT_LOOP_PERSISTENT)")
+                     "timed frames run in multi-frame launches (RT_LOOP_MULTIFRAME)")
                   if solo is not None else
                   f"{n_ev} of {a.steps} timed frames (every {max(1, a.event_every)})")
     kern_extra = ({"kernel_ms_solo_batches": [round(b, 5) for b in batch_ms],
@@ -944,7 +953,8 @@ def main():
             "device_err": errs if multi else dev_err,
             "host": {"us_per_frame": round(host_us_per_frame, 2), "loop": "native (rt_run_frames)"
                      if not isinstance(loop, PyLoop) else "python",
-                     "frames_in_flight": ("persistent" if persistent else inflight) if not isinstance(loop, PyLoop) else 1,
+                     "frames_in_flight": ("multi-frame launches" if persistent else inflight)
+                     if not isinstance(loop, PyLoop) else 1,
                      "what": "host time spent enqueueing the timed frames / steps (rank 0)"},
             "kd_build": build_times,
             # build provenance: SHA-256 of the library's sources and flags

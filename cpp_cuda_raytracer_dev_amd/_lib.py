@@ -70,7 +70,7 @@ class RtTile(C.Structure):
 
 RT_LOOP_MAX_BUF = 8
 RT_LOOP_MAX_LANES = 4
-RT_LOOP_PERSISTENT = -1
+RT_LOOP_MULTIFRAME = -1
 
 
 class RtFrameLoop(C.Structure):

@@ -1691,7 +1691,7 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
         p.coop = 0;
     }
     const bool order3 = p.cost != nullptr;
-    // the persistent loop (KD kernel 3, fused far fill, no per-frame
+    // a multi-frame launch (KD kernel 3, fused far fill, no per-frame
     // outputs beyond the frame): one launch for pf->frames frames, no cost
     // sample inside it
     const bool persist = pf && pf->frames > 1 && mode == RT_MODE_KD && effective_kernel(c) == 3 && p.coarse_blocks == 0 &&
@@ -2199,14 +2199,14 @@ static int ensure_lanes(rt_camera* c, int L, bool comm) {
     return RT_OK;
 }
 
-// rt_run_frames with RT_LOOP_PERSISTENT: frames in launches of up to
+// rt_run_frames with RT_LOOP_MULTIFRAME: frames in launches of up to
 // kPersistChunk frames, each one k_trace_kd3 grid of every frame's blocks,
 // frame-major (render_common's PersistArgs).
 // Until a cost order exists (tile order 3) frames launch one at a time, so
-// that cost samples are taken; persistent launches take none.
+// that cost samples are taken; multi-frame launches take none.
 constexpr int32_t kPersistChunk = 128;
 
-static int run_frames_persistent(rt_camera* c, const rt_frame_loop* a, int32_t nframes, int64_t* seq,
+static int run_frames_multiframe(rt_camera* c, const rt_frame_loop* a, int32_t nframes, int64_t* seq,
                                  double* kernel_ms_avg, int32_t* kernel_ms_frames, double* host_ms) {
     hipStream_t rs = (hipStream_t)a->render_stream;
     const rt_tile* tile = a->tile.nranks > 0 ? &a->tile : nullptr;
@@ -2267,15 +2267,15 @@ static int run_frames_persistent(rt_camera* c, const rt_frame_loop* a, int32_t n
 extern "C" int rt_run_frames(rt_camera* c, rt_comm* comm, const rt_frame_loop* a, int32_t nframes, int64_t* seq,
                              double* kernel_ms_avg, int32_t* kernel_ms_frames, double* host_ms) {
     if (!c || !a || !seq || nframes < 0 || a->nbuf < 1 || a->nbuf > RT_LOOP_MAX_BUF ||
-        (a->inflight < 0 && a->inflight != RT_LOOP_PERSISTENT) || a->inflight > RT_LOOP_MAX_LANES)
+        (a->inflight < 0 && a->inflight != RT_LOOP_MULTIFRAME) || a->inflight > RT_LOOP_MAX_LANES)
         return fail(RT_ERR_INVALID, "rt_run_frames: bad argument");
-    if (a->inflight == RT_LOOP_PERSISTENT) {
+    if (a->inflight == RT_LOOP_MULTIFRAME) {
         if (comm || a->nxforms > 0)
-            return fail(RT_ERR_INVALID, "rt_run_frames: the persistent loop renders a static scene without a gather");
+            return fail(RT_ERR_INVALID, "rt_run_frames: multi-frame launches render a static scene without a gather");
         for (int k = 0; k < a->nbuf; k++)
             if (!a->d_local[k]) return fail(RT_ERR_INVALID, "rt_run_frames: missing buffer of set %d", k);
         DeviceGuard g(c->device);
-        return run_frames_persistent(c, a, nframes, seq, kernel_ms_avg, kernel_ms_frames, host_ms);
+        return run_frames_multiframe(c, a, nframes, seq, kernel_ms_avg, kernel_ms_frames, host_ms);
     }
     if (a->nxforms < 0 || (a->nxforms > 0 && !a->xforms))
         return fail(RT_ERR_INVALID, "rt_run_frames: bad transform sequence");

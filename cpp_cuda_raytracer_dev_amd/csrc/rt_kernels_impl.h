@@ -2271,7 +2271,7 @@ __device__ __forceinline__ void trace_unit_coop(const TraceParams& P, CoopLds<kR
 #define RT_KD3_BOUNDS(threads) __launch_bounds__(threads)
 #endif
 // One block of k_trace_kd3's grid: block index b (blockIdx.x, or the virtual
-// index of the persistent frame loop below).
+// index within a multi-frame launch, below).
 template <int kRays, bool kTranslated, bool kWriteHit, bool kCount, int kShadow, int kCap, int kRayVec>
 __device__ __forceinline__ void kd3_block(const TraceParams& P, WaveLds<kRays, kCap, kRayVec>* s_lds, int32_t b,
                                           int wv, int lane) {
@@ -2351,7 +2351,7 @@ __device__ __forceinline__ void kd3_block(const TraceParams& P, WaveLds<kRays, k
 }
 
 // Kernel 3: one frame, one block per grid slot.  A multi-frame launch
-// (rt_run_frames with RT_LOOP_PERSISTENT; P.pf_frames > 0) has pf_frames x
+// (rt_run_frames with RT_LOOP_MULTIFRAME; P.pf_frames > 0) has pf_frames x
 // pf_blocks blocks, frame-major: block i renders block i % pf_blocks of frame
 // i / pf_blocks into P.pf_argb[(P.pf_seq0 + frame) % P.pf_nbuf].  Blocks are
 // dispatched in index order, so frame f + 1's heaviest tiles start on the CUs

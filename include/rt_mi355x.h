@@ -318,7 +318,7 @@ void rt_comm_destroy(rt_comm* c);
  * renders that share the GPU with another frame. */
 #define RT_LOOP_MAX_BUF 8
 #define RT_LOOP_MAX_LANES 4
-/* inflight = RT_LOOP_PERSISTENT: a static scene's frames (no comm, no xforms)
+/* inflight = RT_LOOP_MULTIFRAME: a static scene's frames (no comm, no xforms)
  * in launches of up to 128 frames, each one grid of every frame's blocks in
  * frame order (blocks are dispatched in index order), so frame j + 1's
  * heaviest tiles start on the CUs frame j's tail frees; frame j writes set
@@ -326,7 +326,7 @@ void rt_comm_destroy(rt_comm* c);
  * kernel 3, flags 0 and the fused far fill; otherwise (and until a cost order
  * exists) frames launch one at a time.  event_every > 0 brackets each launch;
  * *kernel_ms_avg is then their time per frame. */
-#define RT_LOOP_PERSISTENT (-1)
+#define RT_LOOP_MULTIFRAME (-1)
 typedef struct rt_frame_loop {
     const float* xform;
     uint32_t mode, flags;

@@ -1454,10 +1454,9 @@ def test_far_along_key_sequence_background():
 
 
 @pytest.mark.parametrize("key", ["dragon_960x540_m0", "knot_1920x1080_m0", "dragon_1920x1080_m0"])
-def test_persistent_frame_loop(key):
-    """rt_run_frames with RT_LOOP_PERSISTENT: launches of up to 128 frames,
-    each one kernel whose resident blocks take (frame, block) pairs from one
-    counter (k_trace_kd3_pf).  Every buffer set holds the oracle's frame
+def test_multiframe_launch_loop(key):
+    """rt_run_frames with RT_LOOP_MULTIFRAME: launches of up to 128 frames,
+    each one k_trace_kd3 grid holding every frame's blocks, frame-major.  Every buffer set holds the oracle's frame
     (committed hash) after 1, 3, 20 and 200 frames, with 2 and 3 sets; the
     first frames before a cost order exists launch one at a time.  A moving
     object or a gather is rejected."""
@@ -1474,7 +1473,7 @@ def test_persistent_frame_loop(key):
     for nbuf in (2, 3):
         bufs = [torch.full((w * h,), 0x7BADBEEF, dtype=torch.int32, device=dev) for _ in range(nbuf)]
         loop = R.FrameLoop(s.cam, bufs, mode=0, render_stream=st.cuda_stream, event_every=1,
-                           inflight=_lib.RT_LOOP_PERSISTENT)
+                           inflight=_lib.RT_LOOP_MULTIFRAME)
         for n in (1, 3, 20, 200):
             for b in bufs:
                 b.fill_(0x7BADBEEF)
@@ -1489,5 +1488,5 @@ def test_persistent_frame_loop(key):
                 assert shas == {ent["argb_sha"]}, (key, nbuf, n)
         assert s.cam.device_error(reset=True) == 0
     with pytest.raises(_lib.RtError):
-        R.FrameLoop(s.cam, bufs, mode=0, render_stream=st.cuda_stream, inflight=_lib.RT_LOOP_PERSISTENT,
+        R.FrameLoop(s.cam, bufs, mode=0, render_stream=st.cuda_stream, inflight=_lib.RT_LOOP_MULTIFRAME,
                     xforms=np.stack([np.eye(3, 4, dtype=np.float32).reshape(12)] * 2)).run(4)
