@@ -98,6 +98,9 @@ def parse():
     ap.add_argument("--solo-frames", type=int, default=200,
                     help="inflight > 1: solo frames (one in flight, every one bracketed by events) before the "
                          "timed region, for the roofline's kernel time")
+    ap.add_argument("--solo-when", default="before", choices=["before", "after"],
+                    help="solo frames (the roofline's kernel time) run just before the warm-up-to-timed handover, "
+                         "or after the timed frames")
     ap.add_argument("--pipeline", type=int, default=2,
                     help="rccl: buffer sets in flight (frame i+1 renders while frame i is gathered)")
     ap.add_argument("--kernel", type=int, default=3,
@@ -698,8 +701,12 @@ def main():
         loop = PyLoop()
         loop.run(a.warmup, False)
         torch.cuda.synchronize(dev)
-    solo = None
-    if not isinstance(loop, PyLoop) and inflight > 1 and a.solo_frames > 0:
+    solo, batch_ms = None, []
+
+    def measure_solo():
+        """(median batch mean ms, frames per batch) of solo frames, or None."""
+        if isinstance(loop, PyLoop) or inflight <= 1 or a.solo_frames <= 0:
+            return None
         # the roofline's kernel time: solo frames (one in flight) back to
         # back, untimed, one event pair around the batch (per-frame event
         # pairs add ~5 us of queue time to each bracketed launch); the timed
@@ -715,7 +722,7 @@ def main():
         # (one batch of C3's 35 us frames is 7 ms, and batch means spread by
         # 10-30 % from run to run on one box)
         nbatch = 1 if masks else 5
-        batch_ms = []
+        batch_ms.clear()
         for _ in range(nbatch):
             sl.seq.value = 0
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -724,10 +731,18 @@ def main():
             e1.record(stream)
             torch.cuda.synchronize(dev)
             batch_ms.append(e0.elapsed_time(e1) / nsolo)
-        solo = (float(np.median(batch_ms)), nsolo)
+        return float(np.median(batch_ms)), nsolo
+
+    if a.solo_when == "before":
+        solo = measure_solo()
+    # the GPU's idle time between the last untimed frame and the timed
+    # region's start (diagnostic: clocks may fall in a long idle gap)
+    g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    g0.record(stream)
     if multi:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    g1.record(stream)
     t0 = time.perf_counter()
     if isinstance(loop, PyLoop):
         kern_ms, n_ev, host_ms = loop.run(a.steps, True)
@@ -738,13 +753,16 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    pre_timed_idle_us = 1e3 * g0.elapsed_time(g1)
+    if a.solo_when == "after":
+        solo = measure_solo()
     host_us_per_frame = 1e3 * host_ms / max(1, a.steps)
     if masks and not isinstance(loop, PyLoop):
         xf = anim_xfs[-1]  # the last timed frame's pose
     kern_ms_timed, n_ev_timed = kern_ms, n_ev
     if solo is not None:
         kern_ms, n_ev = solo
-    kern_label = (f"median over {len(batch_ms)} batches of the mean period of {n_ev} solo frames back to back before "
+    kern_label = (f"median over {len(batch_ms)} batches of the mean period of {n_ev} solo frames back to back {a.solo_when} "
                   f"the timed region (one in flight; kernel + the launch gap, an upper bound of the kernel time); the "
                   + (f"timed frames keep {inflight} in flight" if not persistent else
                      "timed frames run in multi-frame launches (RT_LOOP_MULTIFRAME)")
@@ -951,7 +969,7 @@ def main():
                 "bytes_model": "36*V_int + 40*V_leaf + 24*H + 4*P (SURVEY.md 8d)",
             }),
             "device_err": errs if multi else dev_err,
-            "host": {"us_per_frame": round(host_us_per_frame, 2), "loop": "native (rt_run_frames)"
+            "host": {"us_per_frame": round(host_us_per_frame, 2), "pre_timed_idle_us": round(pre_timed_idle_us, 1), "loop": "native (rt_run_frames)"
                      if not isinstance(loop, PyLoop) else "python",
                      "frames_in_flight": ("multi-frame launches" if persistent else inflight)
                      if not isinstance(loop, PyLoop) else 1,

@@ -3,7 +3,8 @@
 (VERDICT r03 item 1): the committed PMC entry (profiles/pmc_traffic.json:
 HBM bytes per launch, VALU issue share, build id) and the rocprofv3
 --kernel-trace --stats average of the same configuration's solo frames
-(profiles/<round>/rocprof/<tag>_kernel_stats.csv), against the bench line's
+(profiles/<round>/rocprof/<tag>_solo_kernel_stats.csv: the bench arguments
+with --inflight 1, so every launch is one frame), against the bench line's
 frac (profiles/<round>/bench/<tag>.json).
 
     python tools/roofline_check.py profiles/r04 [--out profiles/r04/roofline_check.md]
@@ -53,7 +54,10 @@ def main():
         rf = b["roofline"]
         key = (rf.get("util_source") or "").split("[")[-1].split("]")[0] if rf.get("util_source") else None
         ent = pmc.get(key or "", {})
-        st = glob.glob(os.path.join(a.dir, "rocprof", f"{tag}*kernel_stats.csv"))
+        # the solo-frame profile of the same arguments (`--inflight 1`: every
+        # launch one frame, as bench.py's kernel time) when there is one
+        st = (glob.glob(os.path.join(a.dir, "rocprof", f"{tag}_solo*kernel_stats.csv"))
+              or glob.glob(os.path.join(a.dir, "rocprof", f"{tag}*kernel_stats.csv")))
         kern = "k_trace_flat" if rf.get("unit") == "TFLOP/s" else "k_trace_kd3"
         avg = stats_avg_us(st[0], "k_flat_chunk" if kern == "k_trace_flat" else kern) if st else None
         rec = None

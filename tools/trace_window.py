@@ -34,6 +34,8 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--last", type=int, default=20)
     ap.add_argument("--kernel", default="k_trace_kd3")
+    ap.add_argument("--skip", type=int, default=0,
+                    help="renders after the window (bench --solo-when after: 20 + 5 x 200 solo frames follow it)")
     a = ap.parse_args()
     kt = rows(find(a.dir, "kernel_trace"))
     ev = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "K " + r["Kernel_Name"][:60],
@@ -44,7 +46,8 @@ def main():
             ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
                        "C " + r.get("Direction", r.get("Operation", "copy")) + f" {r.get('Size', '?')} B", "dma"))
     ev.sort()
-    rend = [e for e in ev if e[2].startswith("K") and a.kernel in e[2]][-a.last:]
+    rend = [e for e in ev if e[2].startswith("K") and a.kernel in e[2]]
+    rend = rend[len(rend) - a.last - a.skip:len(rend) - a.skip]
     t0, t1 = rend[0][0], rend[-1][1]
     win = [e for e in ev if e[1] >= t0 and e[0] <= t1]
     print(f"window: {a.last} renders, {(t1 - t0) / 1e3:.1f} us first start -> last end "
