@@ -38,6 +38,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -101,6 +102,9 @@ def parse():
     ap.add_argument("--solo-when", default="before", choices=["before", "after"],
                     help="solo frames (the roofline's kernel time) run just before the warm-up-to-timed handover, "
                          "or after the timed frames")
+    ap.add_argument("--settle-ms", type=float, default=40.0,
+                    help="untimed frames of the timed loop itself for about this much time right before the timed "
+                         "region (a moving object: native loop only, the timed frames then restart at pose W; 0: none)")
     ap.add_argument("--pipeline", type=int, default=2,
                     help="rccl: buffer sets in flight (frame i+1 renders while frame i is gathered)")
     ap.add_argument("--kernel", type=int, default=3,
@@ -735,6 +739,34 @@ def main():
 
     if a.solo_when == "before":
         solo = measure_solo()
+    # Settle frames: the timed loop itself, untimed, for about --settle-ms of
+    # GPU time right before the timed region.  Two frames in flight reach their
+    # steady period only after ~20-35 ms of that load: knot 1080p pairs of
+    # frames take 214 us at first and 186 us from ~35 ms on, while solo
+    # frames stay at 105 us throughout (kernel traces r04e / r04k), so a
+    # 20-frame window timed straight after the solo pass ran at 9.0-9.2k
+    # FPS against 10.5k over 1000 frames (r04j, r04k).
+    def run_untimed(n):
+        loop.run(n, False) if isinstance(loop, PyLoop) else loop.run(n)
+
+    settle = 0
+    # (a moving object: native loop only, whose frame k renders pose k; the
+    # timed frames then start again at pose W)
+    if a.settle_ms > 0 and (not masks or not isinstance(loop, PyLoop)):
+        ts = time.perf_counter()
+        run_untimed(50)
+        torch.cuda.synchronize(dev)
+        per = (time.perf_counter() - ts) / 50
+        n = int(math.ceil(a.settle_ms * 1e-3 / max(per, 1e-6)))
+        if multi:  # every rank renders (and gathers) the same frames
+            tn = torch.tensor([n], dtype=torch.int64, device=dev)
+            dist.all_reduce(tn, op=dist.ReduceOp.MAX)
+            n = int(tn[0])
+        run_untimed(n)
+        settle = 50 + n
+        if masks:
+            torch.cuda.synchronize(dev)
+            loop.seq.value = a.warmup
     # the GPU's idle time between the last untimed frame and the timed
     # region's start (diagnostic: clocks may fall in a long idle gap)
     g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -969,7 +1001,8 @@ def main():
                 "bytes_model": "36*V_int + 40*V_leaf + 24*H + 4*P (SURVEY.md 8d)",
             }),
             "device_err": errs if multi else dev_err,
-            "host": {"us_per_frame": round(host_us_per_frame, 2), "pre_timed_idle_us": round(pre_timed_idle_us, 1), "loop": "native (rt_run_frames)"
+            "host": {"us_per_frame": round(host_us_per_frame, 2), "pre_timed_idle_us": round(pre_timed_idle_us, 1),
+                     "settle_frames": settle, "loop": "native (rt_run_frames)"
                      if not isinstance(loop, PyLoop) else "python",
                      "frames_in_flight": ("multi-frame launches" if persistent else inflight)
                      if not isinstance(loop, PyLoop) else 1,

@@ -34,6 +34,8 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--last", type=int, default=20)
     ap.add_argument("--kernel", default="k_trace_kd3")
+    ap.add_argument("--chunks", type=int, default=0,
+                    help="instead: every render launch of the trace in chunks of this many, mean duration and start")
     ap.add_argument("--skip", type=int, default=0,
                     help="renders after the window (bench --solo-when after: 20 + 5 x 200 solo frames follow it)")
     a = ap.parse_args()
@@ -47,6 +49,13 @@ def main():
                        "C " + r.get("Direction", r.get("Operation", "copy")) + f" {r.get('Size', '?')} B", "dma"))
     ev.sort()
     rend = [e for e in ev if e[2].startswith("K") and a.kernel in e[2]]
+    if a.chunks > 0:
+        t00 = rend[0][0]
+        print(f"{len(rend)} render launches; per chunk of {a.chunks}: first start (ms), mean / min duration (us)")
+        for i in range(0, len(rend), a.chunks):
+            d = [(e - s) / 1e3 for s, e, _, _ in rend[i:i + a.chunks]]
+            print(f"  {i:6d} {(rend[i][0] - t00) / 1e6:9.2f} {np.mean(d):8.1f} {min(d):8.1f}")
+        return
     rend = rend[len(rend) - a.last - a.skip:len(rend) - a.skip]
     t0, t1 = rend[0][0], rend[-1][1]
     win = [e for e in ev if e[1] >= t0 and e[0] <= t1]
