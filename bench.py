@@ -102,6 +102,8 @@ def parse():
     ap.add_argument("--solo-when", default="before", choices=["before", "after"],
                     help="solo frames (the roofline's kernel time) run just before the warm-up-to-timed handover, "
                          "or after the timed frames")
+    ap.add_argument("--frame-group", type=int, default=0,
+                    help="multi-frame launches: frames per interleaved group (RT_OPT_FRAME_GROUP; 0 = library default)")
     ap.add_argument("--settle-ms", type=float, default=40.0,
                     help="untimed frames of the timed loop itself for about this much time right before the timed "
                          "region (a moving object: native loop only, the timed frames then restart at pose W; 0: none)")
@@ -532,6 +534,7 @@ def main():
     cam.set_option(_lib.RT_OPT_RAYS, a.rays)
     cam.set_option(_lib.RT_OPT_ITEMS, a.items)
     cam.set_option(_lib.RT_OPT_COARSE, a.coarse)
+    cam.set_option(_lib.RT_OPT_FRAME_GROUP, a.frame_group)
     cam.set_option(_lib.RT_OPT_SHADOW_ORDER, a.shadow_order)
     if a.flat >= 0:
         cam.set_option(_lib.RT_OPT_FLAT, a.flat)
@@ -1002,7 +1005,8 @@ def main():
             }),
             "device_err": errs if multi else dev_err,
             "host": {"us_per_frame": round(host_us_per_frame, 2), "pre_timed_idle_us": round(pre_timed_idle_us, 1),
-                     "settle_frames": settle, "loop": "native (rt_run_frames)"
+                     "settle_frames": settle,
+                     **({"frame_group": cam.get_option(_lib.RT_OPT_FRAME_GROUP)} if persistent else {}), "loop": "native (rt_run_frames)"
                      if not isinstance(loop, PyLoop) else "python",
                      "frames_in_flight": ("multi-frame launches" if persistent else inflight)
                      if not isinstance(loop, PyLoop) else 1,

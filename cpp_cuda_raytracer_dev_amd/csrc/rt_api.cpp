@@ -113,6 +113,7 @@ struct rt_camera {
     int noused = 0;
     bool oused_overflow = false;
     int coarse = 8;                  // kOptCoarse: coarse groups per wave (0 = off)
+    int frame_group = 0;             // kOptFrameGroup: multi-frame launches' group (0 = RT_PF_GROUP)
     std::vector<int32_t> centre;     // centre-out permutation of the current fine grid (host copy)
     // 8x8 groups (x / 8, y / 8) holding a pixel whose primary ray has a zero
     // or tiny component (computed once, as the kernels compute the rays)
@@ -591,6 +592,10 @@ constexpr int64_t kSplitMaxTiles = RT_SPLIT_MAX_TILES;
 // lets them.  Off by default (0).
 #ifndef RT_GATE_PCT
 #define RT_GATE_PCT 0
+#endif
+// multi-frame launches: frames per interleaved group (1: frame-major)
+#ifndef RT_PF_GROUP
+#define RT_PF_GROUP 1
 #endif
 
 
@@ -1702,6 +1707,7 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
         p.pf_blocks = (int32_t)fine_grid_blocks(p);
         p.pf_nbuf = pf->nbuf;
         p.pf_seq0 = pf->seq0 % pf->nbuf;
+        p.pf_group = std::max(1, std::min(pf->frames, c->frame_group > 0 ? c->frame_group : RT_PF_GROUP));
         for (int k = 0; k < RT_LOOP_MAX_BUF; k++) p.pf_argb[k] = k < pf->nbuf ? pf->argb[k] : nullptr;
         if (rendered) *rendered = pf->frames;
     }
@@ -2125,6 +2131,10 @@ extern "C" int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value) {
         if (value < 0 || value > 4) return fail(RT_ERR_INVALID, "tile order %d (0..4)", value);
         c->tile_order = value;
         return RT_OK;
+    case kOptFrameGroup:
+        if (value < 0 || value > 8) return fail(RT_ERR_INVALID, "frames per group %d (0 default, 1..8)", value);
+        c->frame_group = value;
+        return RT_OK;
     default:
         return fail(RT_ERR_INVALID, "rt_camera_set_option: unknown key %d", key);
     }
@@ -2144,6 +2154,7 @@ extern "C" int rt_camera_get_option(const rt_camera* c, int32_t key, int32_t* va
     case kOptStampOffset: *value = (int32_t)c->istamp_off; return RT_OK;
     case kOptSplitUsed: *value = c->order_split; return RT_OK;
     case kOptCoopUsed: *value = c->order_coop; return RT_OK;
+    case kOptFrameGroup: *value = c->frame_group > 0 ? c->frame_group : RT_PF_GROUP; return RT_OK;
     case kOptShadowOrder: *value = c->shadow_order >= 0 ? c->shadow_order : c->any_best; return RT_OK;
     default: return fail(RT_ERR_INVALID, "rt_camera_get_option: unknown key %d", key);
     }

@@ -51,6 +51,7 @@ enum Option : int32_t {
     kOptRaysUsed = 8,   // get only: pixels per wave of the last kernel-3 render
     kOptSplitUsed = 9,  // get only: split tiles after the coop tiles of the current cost order (kernel 3)
     kOptCoopUsed = 10,  // get only: coop tiles at the head of the current cost order (kernel 3)
+    kOptFrameGroup = 11,  // multi-frame launches: frames per interleaved group (0 = default)
     kOptDebug = 100,    // diagnostics: 1 = skip traversal, 2 = per-wave timestamps, 4 = every group
                         // coarse, 8 = coarse kernel on a side stream beside the fine one,
                         // 16 = counted shadow walks stop at occluders (the timed walk's work),
@@ -151,9 +152,9 @@ struct TraceParams {
     unsigned long long* dbg;       // per-wave (t_start, t_end, visits) when non-null
     unsigned long long* started;   // kernel 3: count of started blocks (rt_run_frames' dispatch gate), or null
     // A multi-frame launch (kernel 3; pf_frames > 0): pf_frames frames of
-    // pf_blocks blocks each, frame-major in one grid; frame f writes
-    // pf_argb[(pf_seq0 + f) % pf_nbuf].
-    int32_t pf_frames, pf_blocks, pf_seq0, pf_nbuf;
+    // pf_blocks blocks each in one grid, in groups of pf_group frames whose
+    // blocks interleave; frame f writes pf_argb[(pf_seq0 + f) % pf_nbuf].
+    int32_t pf_frames, pf_blocks, pf_seq0, pf_nbuf, pf_group;
     uint32_t* pf_argb[RT_LOOP_MAX_BUF];
     uint32_t root_ref;
     uint32_t ntri;

@@ -2355,8 +2355,10 @@ __device__ __forceinline__ void kd3_block(const TraceParams& P, WaveLds<kRays, k
 // pf_blocks blocks, frame-major: block i renders block i % pf_blocks of frame
 // i / pf_blocks into P.pf_argb[(P.pf_seq0 + frame) % P.pf_nbuf].  Blocks are
 // dispatched in index order, so frame f + 1's heaviest tiles start on the CUs
-// frame f's tail frees, with no launch between frames and no two frames in
-// lockstep (static scenes: every frame is the same frame).
+// frame f's tail frees, with no launch between frames (static scenes: every
+// frame is the same frame).  With pf_group G > 1 the frames go in groups of
+// G whose blocks interleave (block i of a group renders block i / G of its
+// frame i % G): G frames dispatch side by side, as G lanes' frames do.
 template <int kRays, bool kTranslated, bool kWriteHit, bool kCount, int kShadow>
 __global__ RT_KD3_BOUNDS(64 * kd3_waves(kRays)) void k_trace_kd3(TraceParams P) {
     constexpr int kCap = pool_cap_for<kRays>();
@@ -2366,8 +2368,14 @@ __global__ RT_KD3_BOUNDS(64 * kd3_waves(kRays)) void k_trace_kd3(TraceParams P) 
     if (P.started && threadIdx.x == 0) atomicAdd(P.started, 1ull);  // the dispatch gate's count (k_gate)
     int32_t b = (int32_t)blockIdx.x;
     if (P.pf_frames > 0) {
-        const int32_t f = b / P.pf_blocks;
-        b -= f * P.pf_blocks;
+        // frames in groups of pf_group, frame-major across groups and
+        // interleaved block by block inside one (the last group may be short)
+        const int32_t gsz = P.pf_group * P.pf_blocks;
+        const int32_t grp = b / gsz;
+        const int32_t r = b - grp * gsz;
+        const int32_t gc = min(P.pf_group, P.pf_frames - grp * P.pf_group);
+        const int32_t f = grp * P.pf_group + r % gc;
+        b = r / gc;
         // every wave's lane 0 stores the same pointer, then its own lanes read it
         if (lane == 0) s_pf_argb = P.pf_argb[(P.pf_seq0 + f) % P.pf_nbuf];
         __builtin_amdgcn_wave_barrier();

@@ -426,6 +426,12 @@ int rt_camera_info(const rt_camera* c, int32_t* w, int32_t* h, int32_t* max_dept
  * the heaviest (70 % in grids of 2,048 tiles or more, at most an eighth of
  * the tiles), bit 4096 every tile.  The frame is the same. */
 #define RT_OPT_COOP_USED 10
+/* multi-frame launches (RT_LOOP_MULTIFRAME): frames per group, 0 = the
+ * default, 1..8.  A launch renders its frames in groups of this many whose
+ * blocks interleave (the group's frames dispatch side by side, as frames on
+ * separate lanes do); 1 renders them one after another (frame-major).  The
+ * frames are the same either way. */
+#define RT_OPT_FRAME_GROUP 11
 int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value);
 int rt_camera_get_option(const rt_camera* c, int32_t key, int32_t* value);
 

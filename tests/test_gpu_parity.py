@@ -1456,7 +1456,9 @@ def test_far_along_key_sequence_background():
 @pytest.mark.parametrize("key", ["dragon_960x540_m0", "knot_1920x1080_m0", "dragon_1920x1080_m0"])
 def test_multiframe_launch_loop(key):
     """rt_run_frames with RT_LOOP_MULTIFRAME: launches of up to 128 frames,
-    each one k_trace_kd3 grid holding every frame's blocks, frame-major.  Every buffer set holds the oracle's frame
+    each one k_trace_kd3 grid holding every frame's blocks, frame-major
+    (RT_OPT_FRAME_GROUP 1) or in interleaved groups of 2 and 3 frames (the
+    last group of a launch short).  Every buffer set holds the oracle's frame
     (committed hash) after 1, 3, 20 and 200 frames, with 2 and 3 sets; the
     first frames before a cost order exists launch one at a time.  A moving
     object or a gather is rejected."""
@@ -1470,7 +1472,9 @@ def test_multiframe_launch_loop(key):
     s = H.GpuScene(ent["scene"], w, h)
     dev = torch.device("cuda:0")
     st = torch.cuda.Stream(device=dev)
-    for nbuf in (2, 3):
+    for group, nbuf in ((1, 2), (1, 3), (2, 2), (2, 3), (3, 2), (3, 3)):
+        s.cam.set_option(_lib.RT_OPT_FRAME_GROUP, group)
+        assert s.cam.get_option(_lib.RT_OPT_FRAME_GROUP) == group
         bufs = [torch.full((w * h,), 0x7BADBEEF, dtype=torch.int32, device=dev) for _ in range(nbuf)]
         loop = R.FrameLoop(s.cam, bufs, mode=0, render_stream=st.cuda_stream, event_every=1,
                            inflight=_lib.RT_LOOP_MULTIFRAME)
@@ -1485,8 +1489,9 @@ def test_multiframe_launch_loop(key):
             shas = {hashlib.sha256(b.cpu().numpy().view(np.uint32).tobytes()).hexdigest() for b in bufs}
             assert ent["argb_sha"] in shas
             if n >= nbuf:
-                assert shas == {ent["argb_sha"]}, (key, nbuf, n)
+                assert shas == {ent["argb_sha"]}, (key, group, nbuf, n)
         assert s.cam.device_error(reset=True) == 0
+    s.cam.set_option(_lib.RT_OPT_FRAME_GROUP, 0)
     with pytest.raises(_lib.RtError):
         R.FrameLoop(s.cam, bufs, mode=0, render_stream=st.cuda_stream, inflight=_lib.RT_LOOP_MULTIFRAME,
                     xforms=np.stack([np.eye(3, 4, dtype=np.float32).reshape(12)] * 2)).run(4)
