@@ -773,6 +773,7 @@ def main():
     # the GPU's idle time between the last untimed frame and the timed
     # region's start (diagnostic: clocks may fall in a long idle gap)
     g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(dev)  # (the lanes' frames are not on `stream`)
     g0.record(stream)
     if multi:
         dist.barrier()
