@@ -90,8 +90,8 @@ def parse():
                     help="frame loop: native = rt_run_frames (C++, the render + RCCL gather enqueued per frame "
                          "without Python), python = the same calls from Python (torch collectives, --animate)")
     ap.add_argument("--inflight", type=int, default=0,
-                    help="native loop: 0 = automatic (multi-frame launches for frames below 1920x1080 pixels at one "
-                         "GPU, else 2), -1 = multi-frame launches (RT_LOOP_MULTIFRAME: one grid of many frames' "
+                    help="native loop: 0 = automatic (multi-frame launches for a static KD scene without shadow rays "
+                         "at one GPU, else 2), -1 = multi-frame launches (RT_LOOP_MULTIFRAME: one grid of many frames' "
                          "blocks, frame-major; static scene, N = 1), else frames in flight on the library's render "
                          "lanes (rt_frame_loop.inflight; "
                          "1 = one frame at a time).  The roofline's kernel time comes from a separate pass of "
@@ -550,12 +550,16 @@ def main():
     loop_kind = a.loop
     # --inflight -1: multi-frame launches (RT_LOOP_MULTIFRAME: one grid holds
     # many frames' blocks, frame-major; N = 1, static scene, KD mode, no
-    # shadow rays).  0 (auto) takes them for frames below 1920x1080, where
-    # they measured faster than two lanes (dragon 960x540 48.7k -> 50.5k FPS,
-    # knot 960x540 31.0k -> 34.3k); at 1920x1080 two lanes stay (knot 10.44k
-    # vs 10.31k, dragon 16.59k vs 16.26k; r04i)
+    # shadow rays).  0 (auto, the default) takes them wherever they apply.
+    # Against two lanes on one box (r04i, r04m, r04n): dragon 960x540 48.7k
+    # -> 50.5k FPS over 1,000 frames (r04i, both without the settle); at
+    # 1920x1080 the driver's 20 frames 10.11-10.20k -> 10.23-10.30k (knot),
+    # 15.71k -> 15.96k (dragon), while over 1,000 frames two lanes stay 1-3 %
+    # ahead (knot 10.60k vs 10.43-10.49k, dragon 16.90k vs 16.38k): the
+    # second lane's first frame often cannot start before the first lane's
+    # first frame ends (kernel traces), which a short window pays for
     can_mf = loop_kind == "native" and not multi and not a.animate and a.mode == 0 and not a.shadow
-    multiframe = can_mf and (a.inflight == -1 or (a.inflight == 0 and w * h < 1920 * 1080))
+    multiframe = can_mf and a.inflight in (-1, 0)
     persistent = multiframe
     inflight = (2 if multiframe or a.inflight <= 0 else a.inflight) if loop_kind == "native" else 1
     if a.event_every <= 0:

@@ -597,11 +597,6 @@ constexpr int64_t kSplitMaxTiles = RT_SPLIT_MAX_TILES;
 #ifndef RT_PF_GROUP
 #define RT_PF_GROUP 1
 #endif
-// rt_run_frames: the lanes' first frames wait for a sleep of this many
-// microseconds on the caller's stream (0: they start as queued)
-#ifndef RT_LANE_START_US
-#define RT_LANE_START_US 0
-#endif
 
 
 // Experiments: a tuning constant from the environment (read once), else
@@ -2346,19 +2341,13 @@ extern "C" int rt_run_frames(rt_camera* c, rt_comm* comm, const rt_frame_loop* a
     // lanes start after the caller's queued work (fork) ...  A stream with
     // nothing queued needs no fork: its marker and the lanes' waits on it
     // would only delay the first frame by a cross-queue hop (~10 us).
-    // With the caller's stream idle the lanes' first frames would start as
-    // they are queued: the first one takes every CU before the second one
-    // arrives, and the second then waited for the whole first frame in 1 of
-    // 4 calls (r04l trace: a 129 us start offset, against 9-37 us in
-    // others).  A short sleep on the caller's stream (RT_LANE_START_US)
-    // holds every lane's first frame until all of them are queued.
-    const int start_us = tune("RT_TUNE_LANE_START_US", RT_LANE_START_US);
+    // (The second lane's first frame often starts only when the first lane's
+    // first frame ends, 9-129 us after it in kernel traces; holding both
+    // behind one event after a short sleep did not change that, r04n.)
     if (L > 1) {
         hipEvent_t fork = c->lane_ev[0];
         rc = RT_OK;
-        const bool busy = hipStreamQuery(rs) != hipSuccess;
-        if (!busy && start_us > 0) rc = launch_delay((double)start_us, rs);
-        if (!rc && (busy || start_us > 0)) {
+        if (hipStreamQuery(rs) != hipSuccess) {
             rc = hip_check(hipEventRecord(fork, rs), "lane fork");
             for (int l = 0; !rc && l < L; l++) rc = hip_check(hipStreamWaitEvent(lane[l], fork, 0), "lane fork wait");
         }

@@ -222,7 +222,6 @@ int validate_leafs(const rt_leaf_aabb* leafs, uint32_t n, const char* what);
 // rt_run_frames' dispatch gate: one wave on `stream` until *started >= target
 // (blocks of another lane's frames that have started) or timeout_us passed.
 int launch_gate(const unsigned long long* started, unsigned long long target, double timeout_us, void* stream);
-int launch_delay(double us, void* stream);
 int launch_unpack(int32_t w, int32_t h, int32_t nranks, const uint32_t* gathered,
                   uint32_t* frame, void* stream);
 // Slots s of `rank` whose band rank + s*nranks lies in [b0, b1): [s0, s1).

@@ -108,11 +108,6 @@ int launch_gate(const unsigned long long* started, unsigned long long target, do
     return check_launch<void>("k_gate");
 }
 
-int launch_delay(double us, void* stream) {
-    k_delay<<<1, 64, 0, (hipStream_t)stream>>>((uint64_t)(us * 100.0));  // 100 MHz counter
-    return check_launch<void>("k_delay");
-}
-
 int launch_unpack(int32_t w, int32_t h, int32_t nranks, const uint32_t* gathered, uint32_t* frame,
                   void* stream) {
     const int32_t nbands = (h + kTileH - 1) / kTileH;

@@ -3069,14 +3069,6 @@ __global__ __launch_bounds__(64) void k_gate(const unsigned long long* started, 
         __builtin_amdgcn_s_sleep(2);
 }
 
-// rt_run_frames' lane start: one wave sleeps for `ticks` of the 100 MHz
-// real-time counter, so that the first frames of every lane (queued behind
-// it) are all visible to the dispatcher when they become ready.
-__global__ __launch_bounds__(64) void k_delay(uint64_t ticks) {
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
-}
-
 template <class K>
 int check_launch(const char* what) {
     hipError_t e = hipGetLastError();
