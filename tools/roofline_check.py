@@ -43,10 +43,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--out", default="")
+    ap.add_argument("--session", default="r04o", help="the bench session whose lines are checked")
     a = ap.parse_args()
     pmc = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
     rows = []
-    for bp in sorted(glob.glob(os.path.join(a.dir, "bench", "*.json"))):
+    for bp in sorted(glob.glob(os.path.join(a.dir, "bench", f"{a.session}_*.json"))):
         tag = os.path.splitext(os.path.basename(bp))[0]
         b = bench_line(bp)
         if not b or not b.get("roofline"):
@@ -56,8 +57,9 @@ def main():
         ent = pmc.get(key or "", {})
         # the solo-frame profile of the same arguments (`--inflight 1`: every
         # launch one frame, as bench.py's kernel time) when there is one
-        st = (glob.glob(os.path.join(a.dir, "rocprof", f"{tag}_solo*kernel_stats.csv"))
-              or glob.glob(os.path.join(a.dir, "rocprof", f"{tag}*kernel_stats.csv")))
+        # (bench/<session>_<config>.json pairs with rocprof/<session>_<config>_solo_*: any session, the latest)
+        name = tag.split("_", 1)[1] if "_" in tag else tag
+        st = sorted(glob.glob(os.path.join(a.dir, "rocprof", f"*_{name}_solo_kernel_stats.csv")))[-1:]
         kern = "k_trace_flat" if rf.get("unit") == "TFLOP/s" else "k_trace_kd3"
         avg = stats_avg_us(st[0], "k_flat_chunk" if kern == "k_trace_flat" else kern) if st else None
         rec = None
