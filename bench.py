@@ -106,7 +106,7 @@ def parse():
                     help="multi-frame launches: frames per interleaved group (RT_OPT_FRAME_GROUP; 0 = library default)")
     ap.add_argument("--settle-ms", type=float, default=40.0,
                     help="untimed frames of the timed loop itself for about this much time right before the timed "
-                         "region (a moving object: native loop only, the timed frames then restart at pose W; 0: none)")
+                         "region (a moving object: one pass over the timed poses, native loop only; 0: none)")
     ap.add_argument("--pipeline", type=int, default=2,
                     help="rccl: buffer sets in flight (frame i+1 renders while frame i is gathered)")
     ap.add_argument("--kernel", type=int, default=3,
@@ -757,9 +757,15 @@ def main():
         loop.run(n, False) if isinstance(loop, PyLoop) else loop.run(n)
 
     settle = 0
-    # (a moving object: native loop only, whose frame k renders pose k; the
-    # timed frames then start again at pose W)
-    if a.settle_ms > 0 and (not masks or not isinstance(loop, PyLoop)):
+    if a.settle_ms > 0 and masks and not isinstance(loop, PyLoop):
+        # a moving object (native loop, whose frame k renders pose k): one
+        # pass over the timed poses themselves, then the timed frames start
+        # again at pose W (so a profile of the run averages the same poses)
+        run_untimed(a.steps)
+        torch.cuda.synchronize(dev)
+        loop.seq.value = a.warmup
+        settle = a.steps
+    elif a.settle_ms > 0 and not masks:
         ts = time.perf_counter()
         run_untimed(50)
         torch.cuda.synchronize(dev)
@@ -771,9 +777,6 @@ def main():
             n = int(tn[0])
         run_untimed(n)
         settle = 50 + n
-        if masks:
-            torch.cuda.synchronize(dev)
-            loop.seq.value = a.warmup
     # the GPU's idle time between the last untimed frame and the timed
     # region's start (diagnostic: clocks may fall in a long idle gap)
     g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -872,7 +875,7 @@ def main():
             try:
                 tj = json.load(open(a.traffic_json))
                 key = (f"{a.scene}_{w}x{h}_m{a.mode}_n{world}" + ("_shadow" if a.shadow else "")
-                       + ("" if a.view == "default" else f"_{a.view}") + ("_anim" if a.animate else ""))
+                       + ("" if a.view == "default" else f"_{a.view}") + (f"_anim{a.steps}" if a.animate else ""))
                 ent = tj.get(key) or {}
                 traffic = ent.get("hbm_bytes_per_launch")
                 valu_util = ent.get("valu_issue_util")

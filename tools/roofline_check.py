@@ -59,11 +59,17 @@ def main():
         # launch one frame, as bench.py's kernel time) when there is one
         # (bench/<session>_<config>.json pairs with rocprof/<session>_<config>_solo_*: any session, the latest)
         name = tag.split("_", 1)[1] if "_" in tag else tag
+        # repeats and variants of a configuration share its solo profile
+        name = {"drv": "knot", "drv2": "knot", "drv_lanes": "knot", "knot_lanes": "knot", "trace_drv": "knot",
+                "rehearse": "knot", "anim2": "anim", "anim3": "anim"}.get(name, name)
         st = sorted(glob.glob(os.path.join(a.dir, "rocprof", f"*_{name}_solo_kernel_stats.csv")))[-1:]
         kern = "k_trace_flat" if rf.get("unit") == "TFLOP/s" else "k_trace_kd3"
         avg = stats_avg_us(st[0], "k_flat_chunk" if kern == "k_trace_flat" else kern) if st else None
         rec = None
-        if avg and ent.get("hbm_bytes_per_launch"):
+        if avg and rf.get("unit") == "TFLOP/s" and rf.get("flops_per_launch"):
+            # the flat kernel: the FLOP model's rate over the profiled kernel time
+            rec = rf["flops_per_launch"] / (avg[0] * 1e-6) / 1e12 / rf["peak"]
+        elif avg and ent.get("hbm_bytes_per_launch"):
             hbm = ent["hbm_bytes_per_launch"] / (avg[0] * 1e-6) / 1e9 / HBM
             rec = max(hbm, ent.get("valu_issue_util") or 0.0)
         rows.append({"tag": tag, "workload": b.get("metric_workload") or b["config"].get("workload"),
