@@ -803,18 +803,27 @@ def main():
     if masks and not isinstance(loop, PyLoop):
         xf = anim_xfs[-1]  # the last timed frame's pose
     kern_ms_timed, n_ev_timed = kern_ms, n_ev
-    if solo is not None:
+    if solo is not None and not persistent:
         kern_ms, n_ev = solo
-    kern_label = (f"median over {len(batch_ms)} batches of the mean period of {n_ev} solo frames back to back {a.solo_when} "
-                  f"the timed region (one in flight; kernel + the launch gap, an upper bound of the kernel time); the "
-                  + (f"timed frames keep {inflight} in flight" if not persistent else
-                     "timed frames run in multi-frame launches (RT_LOOP_MULTIFRAME)")
-                  if solo is not None else
-                  f"{n_ev} of {a.steps} timed frames (every {max(1, a.event_every)})")
-    kern_extra = ({"kernel_ms_solo_batches": [round(b, 5) for b in batch_ms],
+    if persistent:
+        # multi-frame launches do not overlap (one stream): the kernel time
+        # is the timed launches' own, measured live -- every launch between
+        # a pair of HIP events, their sum over the frames they rendered
+        kern_label = (f"the timed region's multi-frame launches (RT_LOOP_MULTIFRAME), each between a pair of HIP events "
+                      f"on the render stream: their total duration / the {n_ev} frames they rendered (kernel time per "
+                      f"frame); kernel_ms_solo is one frame alone")
+    elif solo is not None:
+        kern_label = (f"median over {len(batch_ms)} batches of the mean period of {n_ev} solo frames back to back "
+                      f"{a.solo_when} the timed region (one in flight; kernel + the launch gap, an upper bound of the "
+                      f"kernel time); the timed frames keep {inflight} in flight")
+    else:
+        kern_label = f"{n_ev} of {a.steps} timed frames (every {max(1, a.event_every)})"
+    kern_extra = ({"kernel_ms_solo": round(solo[0], 5),
+                   "kernel_ms_solo_batches": [round(b, 5) for b in batch_ms],
                    "kernel_ms_avg_timed": round(kern_ms_timed, 5),
-                   "kernel_ms_timed_frames": f"{n_ev_timed} of {a.steps} timed frames (every {a.event_every}), "
-                                             f"each sharing the GPU with the other frames in flight"}
+                   "kernel_ms_timed_frames": (f"{n_ev_timed} timed frames in multi-frame launches" if persistent else
+                                              f"{n_ev_timed} of {a.steps} timed frames (every {a.event_every}), "
+                                              f"each sharing the GPU with the other frames in flight")}
                   if solo is not None else {})
     # the device error word of this rank's timed frames (stack / pool
     # overflow, a far-group proof that failed): reported, and fatal below
@@ -868,21 +877,26 @@ def main():
         tests = w * h * len(pts)  # flat list: every ray against every triangle
         tflops = FLOPS_PER_TEST * tests / (kern_ms * 1e-3) / 1e12
         # counter-based figures of this configuration from the committed PMC
-        # passes (tools/pmc_plan.py; one frame in flight, the same kernel),
+        # passes (tools/pmc_plan.py: one frame in flight, or with --own the
+        # multi-frame launches of this loop, key suffix _mf; the same kernel),
         # stamped with the build id of the library they measured
         traffic, valu_util, pmc_key, pmc_build = None, None, None, None
         if os.path.exists(a.traffic_json):
             try:
                 tj = json.load(open(a.traffic_json))
                 key = (f"{a.scene}_{w}x{h}_m{a.mode}_n{world}" + ("_shadow" if a.shadow else "")
-                       + ("" if a.view == "default" else f"_{a.view}") + (f"_anim{a.steps}" if a.animate else ""))
+                       + ("" if a.view == "default" else f"_{a.view}") + (f"_anim{a.steps}" if a.animate else "")
+                       + ("_mf" if persistent else ""))  # multi-frame launches: passes of that loop
                 ent = tj.get(key) or {}
-                traffic = ent.get("hbm_bytes_per_launch")
+                # HBM bytes per frame (older entries: per launch of one frame)
+                traffic = ent.get("hbm_bytes_per_frame", ent.get("hbm_bytes_per_launch"))
+                pmc_fpd = ent.get("frames_per_dispatch", 1.0)
                 valu_util = ent.get("valu_issue_util")
                 pmc_build = ent.get("build_id")
                 pmc_key = key if ent else None
             except Exception:
                 traffic = valu_util = pmc_key = pmc_build = None
+                pmc_fpd = None
         kern_s = kern_ms * 1e-3
         stale = pmc_key is not None and pmc_build != _lib.build_id()
         hbm_util = traffic / kern_s / (HBM_PEAK_GBS * 1e9) if traffic else None
@@ -898,9 +912,10 @@ def main():
             "hbm_util": round(hbm_util, 4) if hbm_util is not None else None,
             "valu_issue_util": valu_util,
             "util_source": (("STALE (measured on build " + str(pmc_build)[:16] + ", not this library): " if stale else "")
-                            + f"profiles/pmc_traffic.json[{pmc_key}]: HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, "
-                            "MI355X_MICROARCH.md) / this run's kernel time / 8 TB/s; SQ_INSTS_VALU x 2 cycles / "
-                            "(1,024 SIMDs x GRBM_GUI_ACTIVE / 8)") if pmc_key else
+                            + f"profiles/pmc_traffic.json[{pmc_key}]: HBM bytes per frame (FETCH_SIZE x2 + WRITE_SIZE, "
+                            "MI355X_MICROARCH.md) / this run's kernel time per frame / 8 TB/s; SQ_INSTS_VALU x 2 "
+                            "cycles / (1,024 SIMDs x GRBM_GUI_ACTIVE / 8), over the passes' launches of this loop "
+                            f"({pmc_fpd} frames per launch)") if pmc_key else
                            "no committed PMC passes for this configuration",
             "util_build_id": pmc_build,
             "util_stale": stale if pmc_key else None,

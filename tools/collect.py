@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Copy a session's results from gpurun_out/<tag>/ into profiles/<round>/:
 every bench JSON line -> bench/<tag>_<step>.json, every rocprofv3 --stats
-summary -> rocprof/<tag>_<dir>_kernel_stats.csv, every pmc_traffic_*.json ->
+summary -> rocprof/<tag>_<dir>_kernel_stats.csv (and a trace_* directory's
+gzipped kernel trace beside it), every pmc_traffic_*.json ->
 pmc/, tool JSON outputs (ranks_*, anim_*) -> ranks/ or anim/, and the GPU
 test-suite tail -> pytest_gpu_<tag>.txt.
 
@@ -43,6 +44,10 @@ def main():
     for st in sorted(glob.glob(os.path.join(src, "*", "*kernel_stats.csv"))):
         d = os.path.basename(os.path.dirname(st))
         shutil.copy(st, os.path.join(dst, "rocprof", f"{a.tag}_{d}_kernel_stats.csv"))
+        n += 1
+    for kt in sorted(glob.glob(os.path.join(src, "trace_*", "*kernel_trace.csv.gz"))):
+        d = os.path.basename(os.path.dirname(kt))
+        shutil.copy(kt, os.path.join(dst, "rocprof", f"{a.tag}_{d}_kernel_trace.csv.gz"))
         n += 1
     for pj in sorted(glob.glob(os.path.join(src, "pmc_traffic_*.json"))):
         key = os.path.basename(pj)[len("pmc_traffic_"):-len(".json")]

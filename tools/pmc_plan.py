@@ -3,13 +3,15 @@
 bench.py configuration (replaces round 2's pmc_*.sh scripts), then
 summarises them into profiles/pmc_traffic.json with tools/pmc_traffic.py.
 
-    python tools/pmc_plan.py <key> <kernel-substring> [bench args...] > plan
+    python tools/pmc_plan.py [--own] <key> <kernel-substring> [bench args...] > plan
     tools/session.sh <tag> plan
 
 One pass per counter group (rocprofv3 --pmc, counters only, no trace
 domains), each within the gfx950 slot limits (SQ 8, TCC 4 with FETCH_SIZE
 taking 3 and WRITE_SIZE 2, TCP 4, GRBM 2).  The bench runs one frame in
-flight (--inflight 1) so every dispatch is a whole frame on its own.
+flight (--inflight 1) so every dispatch is a whole frame on its own, or with
+--own its default loop (multi-frame launches where they apply: the passes
+then count per frame, tools/pmc_traffic.py) without the solo pass.
 """
 import shlex
 import sys
@@ -27,12 +29,16 @@ PASSES = [
 
 
 def main():
-    if len(sys.argv) < 3:
+    if len(sys.argv) < 3 or (sys.argv[1] == "--own" and len(sys.argv) < 4):
         print(__doc__, file=sys.stderr)
         return 2
-    key, ksub, args = sys.argv[1], sys.argv[2], sys.argv[3:]
-    bench = "python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline --inflight 1 " + " ".join(
-        shlex.quote(a) for a in args)
+    argv = sys.argv[1:]
+    own = argv[0] == "--own"  # the bench's own frame loop (multi-frame launches), without its solo pass
+    if own:
+        argv = argv[1:]
+    key, ksub, args = argv[0], argv[1], argv[2:]
+    bench = ("python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline "
+             + ("--solo-frames 0 " if own else "--inflight 1 ") + " ".join(shlex.quote(a) for a in args))
     print(f"# PMC passes of [{key}] ({ksub}): bench.py {' '.join(args)}")
     for name, ctrs in PASSES:
         print(f"pmc_{key}_{name} 120 pmc pmc_{key}_{name} {ctrs} -- {bench}")

@@ -3,8 +3,9 @@
     python tools/pmc_traffic.py [--out file.json] <key> <kernel-substring> <pass_dir> [<pass_dir> ...]
 
 Each pass directory holds one rocprofv3 --pmc run (counters collected in
-separate passes: FETCH_SIZE and WRITE_SIZE do not fit one TCC pass).  Per
-dispatch of the matching kernel, counters are averaged.  HBM bytes per launch
+separate passes: FETCH_SIZE and WRITE_SIZE do not fit one TCC pass).  The
+matching kernel's counters are summed and divided by the frames the
+dispatches rendered (a multi-frame launch renders many; see load()).  HBM bytes per launch
 follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB, and on
 gfx950 FETCH_SIZE reports half the bytes of 16-B-per-lane reads, so the read
 side is doubled ("hbm_bytes_per_launch"); the raw sum is kept beside it.
@@ -21,16 +22,39 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def load(pass_dir, kernel_sub):
-    vals = defaultdict(list)
+    """Per frame: every counter summed over the matching dispatches and
+    divided by the frames they rendered.  A multi-frame launch
+    (RT_LOOP_MULTIFRAME) renders Grid_Size / (one frame's grid) frames, one
+    frame's grid being the most common of the small dispatches (the frames a
+    run renders one at a time); when a run has multi-frame launches only
+    those count (the mode bench.py times), else every dispatch is a frame."""
+    rows = []
     paths = glob.glob(os.path.join(pass_dir, "**", "*counter_collection.csv"), recursive=True)
     paths += glob.glob(os.path.join(pass_dir, "**", "*counter_collection.csv.gz"), recursive=True)  # session.sh
     for path in paths:
         with (gzip.open(path, "rt") if path.endswith(".gz") else open(path)) as fp:
             for row in csv.DictReader(fp):
-                if kernel_sub not in row.get("Kernel_Name", ""):
-                    continue
-                vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in vals.items() if v}, {k: len(v) for k, v in vals.items()}
+                if kernel_sub in row.get("Kernel_Name", ""):
+                    rows.append(row)
+    if not rows:
+        return {}, {}, 1.0
+    grids = [int(r["Grid_Size"]) for r in rows if r.get("Grid_Size")]
+    frames_of = lambda r: 1
+    if grids:
+        g0 = min(grids)
+        small = [g for g in grids if g < 1.5 * g0]
+        one = max(set(small), key=small.count)
+        frames_of = lambda r: max(1, int(round(int(r["Grid_Size"]) / one)))
+        if any(frames_of(r) > 1 for r in rows):
+            rows = [r for r in rows if frames_of(r) > 1]
+    vals, nfr, ndisp = defaultdict(float), defaultdict(int), defaultdict(int)
+    for r in rows:
+        vals[r["Counter_Name"]] += float(r["Counter_Value"])
+        nfr[r["Counter_Name"]] += frames_of(r)
+        ndisp[r["Counter_Name"]] += 1
+    per_frame = {k: v / nfr[k] for k, v in vals.items() if nfr[k]}
+    fpd = max(nfr[k] / ndisp[k] for k in ndisp) if ndisp else 1.0
+    return per_frame, dict(ndisp), fpd
 
 
 def main():
@@ -41,8 +65,10 @@ def main():
     key, kernel_sub, dirs = argv[0], argv[1], argv[2:]
     counters, n = {}, {}
     valu_util = None
+    fpd = 1.0
     for d in dirs:
-        c, m = load(d, kernel_sub)
+        c, m, f = load(d, kernel_sub)
+        fpd = max(fpd, f)
         if "SQ_INSTS_VALU" in c and c.get("GRBM_GUI_ACTIVE"):
             # VALU issue share of the chip's SIMD cycles in this pass: a wave64
             # VALU instruction issues over 2 cycles of a SIMD-32
@@ -57,14 +83,16 @@ def main():
     from cpp_cuda_raytracer_dev_amd import build
     # the library the passes measured: this tree's (the binding refuses any
     # other), so bench.py can tell a stale entry from a current one
-    entry = {"kernel": kernel_sub, "counters_per_dispatch": counters, "dispatches": n,
-             "build_id": build.source_id()}
+    entry = {"kernel": kernel_sub, "counters_per_frame": counters, "dispatches": n,
+             "frames_per_dispatch": round(fpd, 2), "build_id": build.source_id()}
     if valu_util is not None:
         entry["valu_issue_util"] = round(valu_util, 4)
     if "FETCH_SIZE" in counters and "WRITE_SIZE" in counters:
         fetch, write = counters["FETCH_SIZE"] * 1024.0, counters["WRITE_SIZE"] * 1024.0
+        # per frame (one frame per launch unless multi-frame launches)
         entry["hbm_bytes_per_launch_raw"] = fetch + write
         entry["hbm_bytes_per_launch"] = 2.0 * fetch + write
+        entry["hbm_bytes_per_frame"] = 2.0 * fetch + write
     if "TCC_HIT_sum" in counters and "TCC_MISS_sum" in counters:
         h, m = counters["TCC_HIT_sum"], counters["TCC_MISS_sum"]
         entry["l2_hit_rate"] = h / (h + m) if h + m else None

@@ -16,6 +16,7 @@ kernel time.  A row agrees when the two are within 5 %.
 import argparse
 import csv
 import glob
+import gzip
 import json
 import os
 
@@ -37,6 +38,28 @@ def stats_avg_us(path, kernel="k_trace_kd3"):
     # the dominant instance (most total time)
     r = max(rows, key=lambda r: float(r["TotalDurationNs"]))
     return float(r["AverageNs"]) / 1e3, r["Name"][:60], int(r["Calls"])
+
+
+def trace_per_frame_us(path, kernel="k_trace_kd3"):
+    """Multi-frame launches in a kernel trace (the bench's own run): their
+    total duration over the frames they rendered (Grid_Size / one frame's
+    grid, one frame's grid the most common small dispatch), in us."""
+    with (gzip.open(path, "rt") if path.endswith(".gz") else open(path)) as fp:
+        rows = [r for r in csv.DictReader(fp) if kernel in r["Kernel_Name"] and "true" not in r["Kernel_Name"][:60]]
+    if not rows:
+        return None
+    gkey = "Grid_Size" if "Grid_Size" in rows[0] else "Grid_Size_X"
+    grids = [int(r[gkey]) for r in rows]
+    g0 = min(grids)
+    small = [g for g in grids if g < 1.5 * g0]
+    one = max(set(small), key=small.count)
+    dur = frames = 0
+    for r, g in zip(rows, grids):
+        f = int(round(g / one))
+        if f > 1:
+            dur += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            frames += f
+    return (dur / frames / 1e3, frames) if frames else None
 
 
 def main():
@@ -65,6 +88,12 @@ def main():
         st = sorted(glob.glob(os.path.join(a.dir, "rocprof", f"*_{name}_solo_kernel_stats.csv")))[-1:]
         kern = "k_trace_flat" if rf.get("unit") == "TFLOP/s" else "k_trace_kd3"
         avg = stats_avg_us(st[0], "k_flat_chunk" if kern == "k_trace_flat" else kern) if st else None
+        if key and key.endswith("_mf"):
+            # multi-frame launches: the per-frame time of the launches in a
+            # kernel trace of the bench's own command (no solo profile)
+            tr = sorted(glob.glob(os.path.join(a.dir, "rocprof", f"*_trace_{name}_mf_kernel_trace.csv*")))[-1:]
+            pf = trace_per_frame_us(tr[0]) if tr else None
+            avg = (pf[0], "multi-frame launches", pf[1]) if pf else None
         rec = None
         if avg and rf.get("unit") == "TFLOP/s" and rf.get("flops_per_launch"):
             # the flat kernel: the FLOP model's rate over the profiled kernel time
@@ -75,14 +104,16 @@ def main():
         rows.append({"tag": tag, "workload": b.get("metric_workload") or b["config"].get("workload"),
                      "bench_frac": rf.get("frac"), "bound": rf.get("bound"), "bench_kernel_us": 1e3 * rf["kernel_ms_avg"],
                      "rocprof_avg_us": avg[0] if avg else None, "rocprof_calls": avg[2] if avg else None,
+                     "rocprof_source": "per frame of multi-frame launches (kernel trace)" if key and key.endswith("_mf")
+                     else "solo frames (--stats average)",
                      "pmc_key": key, "pmc_build": (ent.get("build_id") or "")[:16],
                      "bench_build": (b.get("build_id") or "")[:16], "recomputed_frac": rec,
                      "agree_5pct": (abs(rec - rf["frac"]) <= 0.05 * rf["frac"]) if rec and rf.get("frac") else None})
-    out = ["| config | bound | bench frac | bench kernel us | rocprof avg us (calls) | recomputed frac | within 5 % | PMC build = bench build |",
-           "|---|---|---|---|---|---|---|---|"]
+    out = ["| config | bound | bench frac | bench kernel us | rocprof us (calls or frames) | rocprof source | recomputed frac | within 5 % | PMC build = bench build |",
+           "|---|---|---|---|---|---|---|---|---|"]
     for r in rows:
         out.append(f"| {r['tag']} ({r['workload']}) | {r['bound']} | {r['bench_frac']} | {r['bench_kernel_us']:.2f} | "
-                   f"{r['rocprof_avg_us'] and round(r['rocprof_avg_us'], 2)} ({r['rocprof_calls']}) | "
+                   f"{r['rocprof_avg_us'] and round(r['rocprof_avg_us'], 2)} ({r['rocprof_calls']}) | {r['rocprof_source']} | "
                    f"{r['recomputed_frac'] and round(r['recomputed_frac'], 4)} | {r['agree_5pct']} | "
                    f"{r['pmc_build'] == r['bench_build'] if r['pmc_build'] else 'no PMC entry'} |")
     text = "\n".join(out)
