@@ -114,6 +114,7 @@ struct rt_camera {
     bool oused_overflow = false;
     int coarse = 8;                  // kOptCoarse: coarse groups per wave (0 = off)
     int frame_group = 0;             // kOptFrameGroup: multi-frame launches' group (0 = RT_PF_GROUP)
+    bool multiframe = false;         // inside rt_run_frames' multi-frame launches (auto_rays)
     std::vector<int32_t> centre;     // centre-out permutation of the current fine grid (host copy)
     // 8x8 groups (x / 8, y / 8) holding a pixel whose primary ray has a zero
     // or tiny component (computed once, as the kernels compute the rays)
@@ -764,6 +765,7 @@ struct FrameGeom {
     float root_box[6] = {0, 0, 0, 0, 0, 0};  // camera-relative root box
     bool root_leaf = false;
     int kernel = 3, rays = 0, coarse = 8, debug = 0;
+    bool multiframe = false;  // renders of rt_run_frames' multi-frame launches (auto_rays)
     // groups holding a pixel with a tiny ray component (find_tiny_groups):
     // the camera's cached list, or computed by the caller
     const std::vector<std::pair<int32_t, int32_t>>* tiny = nullptr;
@@ -1015,6 +1017,15 @@ bool set_fine_region(const FrameGeom& c, TraceParams& p, int per_wave, bool fuse
 // 23.8 us (16 + split) vs 27.9 (8), of 8 (1.7k) 23.6 vs 20.9 (r03g).  So 8
 // rays below 2,048 units.
 constexpr int64_t kAutoRaysMinUnits = 2048;
+// Multi-frame launches (round 4): frames overlap inside one grid, so the
+// per-wave work counts for more than the heaviest unit's chain, and fine
+// regions of fewer than this many 16-ray units render 32 rays per wave.
+// Measured (r04u, r04v, 1,000 frames, one box; 16 -> 32 rays): dragon
+// 960x540 (3.4k units) 54.3k -> 65.9k FPS, knot 960x540 36.3k -> 37.3k;
+// at 1920x1080 (13.4k units) dragon 16.5k -> 17.7k, fill 1,351 -> 1,396,
+// but knot 10.43k -> 9.91k; 64 rays lose everywhere (C3 55.5k, knot
+// 960x540 29.5k, knot 1080p 8.1k).
+constexpr int64_t kAutoRaysMfMaxUnits = 8192;
 
 int auto_rays(const FrameGeom& c, const TraceParams& p) {
     double r[4];
@@ -1023,6 +1034,7 @@ int auto_rays(const FrameGeom& c, const TraceParams& p) {
     const double y0 = std::max(r[2] - 2, 0.0), y1 = std::min(r[3] + 2, (double)c.h - 1);
     if (x1 < x0 || y1 < y0) return 16;
     const double px = (x1 - x0 + 1) * (y1 - y0 + 1) / p.nranks;
+    if (c.multiframe) return px / 16 < (double)kAutoRaysMfMaxUnits ? 32 : 16;
     return px / 16 < (double)kAutoRaysMinUnits ? 8 : 16;
 }
 
@@ -1073,6 +1085,7 @@ FrameGeom camera_geom(rt_camera* c) {
     g.root_leaf = (c->obj->root_ref & kLeafBit) != 0;
     g.kernel = effective_kernel(c);
     g.rays = c->rays;
+    g.multiframe = c->multiframe;
     g.coarse = c->coarse;
     g.debug = c->debug;
     find_tiny_groups(c);
@@ -2219,6 +2232,15 @@ constexpr int32_t kPersistChunk = 128;
 
 static int run_frames_multiframe(rt_camera* c, const rt_frame_loop* a, int32_t nframes, int64_t* seq,
                                  double* kernel_ms_avg, int32_t* kernel_ms_frames, double* host_ms) {
+    // the frames of this call take the multi-frame rays-per-wave rule
+    // (auto_rays); a change of rule is a change of launch geometry
+    struct MfScope {
+        rt_camera* c;
+        explicit MfScope(rt_camera* cam) : c(cam) {
+            if (!c->multiframe) { c->multiframe = true; c->geom_gen++; }
+        }
+        ~MfScope() { c->multiframe = false; c->geom_gen++; }
+    } mf_scope(c);
     hipStream_t rs = (hipStream_t)a->render_stream;
     const rt_tile* tile = a->tile.nranks > 0 ? &a->tile : nullptr;
     std::vector<std::pair<int, int32_t>> timed;  // (event pair, frames) of bracketed launches
