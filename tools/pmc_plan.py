@@ -42,7 +42,8 @@ def main():
     print(f"# PMC passes of [{key}] ({ksub}): bench.py {' '.join(args)}")
     for name, ctrs in PASSES:
         print(f"pmc_{key}_{name} 120 pmc pmc_{key}_{name} {ctrs} -- {bench}")
-    print(f"pmc_{key}_summary 60 pmcsum {key} {shlex.quote(ksub)} " + " ".join(f"pmc_{key}_{n}" for n, _ in PASSES))
+    print(f"pmc_{key}_summary 60 pmcsum {key} {shlex.quote(ksub)} " + " ".join(f"pmc_{key}_{n}" for n, _ in PASSES)
+          + ("" if own else " --one"))
     return 0
 
 

@@ -1,6 +1,6 @@
 """Summarise rocprofv3 --pmc passes of bench.py into profiles/pmc_traffic.json.
 
-    python tools/pmc_traffic.py [--out file.json] <key> <kernel-substring> <pass_dir> [<pass_dir> ...]
+    python tools/pmc_traffic.py [--out file.json] [--one] <key> <kernel-substring> <pass_dir> [<pass_dir> ...]
 
 Each pass directory holds one rocprofv3 --pmc run (counters collected in
 separate passes: FETCH_SIZE and WRITE_SIZE do not fit one TCC pass).  The
@@ -21,7 +21,7 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def load(pass_dir, kernel_sub):
+def load(pass_dir, kernel_sub, one_frame=False):
     """Per frame: every counter summed over the matching dispatches and
     divided by the frames they rendered.  A multi-frame launch
     (RT_LOOP_MULTIFRAME) renders Grid_Size / (one frame's grid) frames, one
@@ -40,7 +40,7 @@ def load(pass_dir, kernel_sub):
         return {}, {}, 1.0
     grids = [int(r["Grid_Size"]) for r in rows if r.get("Grid_Size")]
     frames_of = lambda r: 1
-    if grids:
+    if grids and not one_frame:
         g0 = min(grids)
         small = [g for g in grids if g < 1.5 * g0]
         one = max(set(small), key=small.count)
@@ -62,12 +62,17 @@ def main():
     out_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if argv and argv[0] == "--out":
         out_path, argv = argv[1], argv[2:]
+    # --one: every dispatch is one frame (passes of --inflight 1 runs, whose
+    # grids vary with a moving object's fine region)
+    one_frame = bool(argv) and argv[0] == "--one"
+    if one_frame:
+        argv = argv[1:]
     key, kernel_sub, dirs = argv[0], argv[1], argv[2:]
     counters, n = {}, {}
     valu_util = None
     fpd = 1.0
     for d in dirs:
-        c, m, f = load(d, kernel_sub)
+        c, m, f = load(d, kernel_sub, one_frame)
         fpd = max(fpd, f)
         if "SQ_INSTS_VALU" in c and c.get("GRBM_GUI_ACTIVE"):
             # VALU issue share of the chip's SIMD cycles in this pass: a wave64

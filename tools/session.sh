@@ -16,7 +16,7 @@
 #   stats <dir> -- <cmd...>        rocprofv3 --kernel-trace --stats
 #   trace <dir> -- <cmd...>        + --memory-copy-trace; traces kept gzipped (dir must start trace_)
 #   setenv VAR VALUE / unsetenv VAR  environment of the following steps
-#   pmcsum <key> <kernel> <dir...>  tools/pmc_traffic.py over pmc dirs of this session
+#   pmcsum <key> <kernel> <dir...> [--one]  tools/pmc_traffic.py over pmc dirs of this session
 set -u
 TAG=$1; PLAN=$2
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -57,8 +57,9 @@ while read -r name to rest; do
     variant) shift; lib=$1; shift; cmd=(python -u tools/bench_variant.py "tools/variants/lib_$lib.so" "$@") ;;
     pmc) shift; d=$1; shift; ctrs=(); while [ "$1" != "--" ]; do ctrs+=("$1"); shift; done; shift
          cmd=(rocprofv3 --pmc "${ctrs[@]}" --output-format csv -d "$OUT/$d" -o run -- "$@") ;;
-    pmcsum) shift; k=$1; ks=$2; shift 2; ds=(); for d in "$@"; do ds+=("$OUT/$d"); done
-            cmd=(python3 tools/pmc_traffic.py --out "$OUT/pmc_traffic_$k.json" "$k" "$ks" "${ds[@]}") ;;
+    pmcsum) shift; k=$1; ks=$2; shift 2; ds=(); one=()
+            for d in "$@"; do if [ "$d" = "--one" ]; then one=(--one); else ds+=("$OUT/$d"); fi; done
+            cmd=(python3 tools/pmc_traffic.py --out "$OUT/pmc_traffic_$k.json" ${one[@]+"${one[@]}"} "$k" "$ks" "${ds[@]}") ;;
     stats) shift; d=$1; shift; [ "$1" = "--" ] && shift
            cmd=(rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$d" -o run -- "$@") ;;
     trace) shift; d=$1; shift; [ "$1" = "--" ] && shift  # kernel + memory-copy trace, kept (gzipped)
