@@ -807,7 +807,8 @@ constexpr int pool_cap_for() {
 // shadow walks: Lmax, hit triangle).
 // Per-ray data of the pool walk in a wave's LDS: six float2 fields per ray
 // (ten for translated and shadow walks), field-major -- field k of ray r at
-// ray[k * kRays + r] -- so that every read of a field by the lanes of a wave
+// ray[k * stride + r], stride kRays (48 for 32 rays, RayLayout) -- so that
+// every read of a field by the lanes of a wave
 // (items of up to kRays distinct rays) hits distinct banks, whatever width
 // the compiler reads it with: for kRays <= 16 a ds_read_b64 (64 banks) and a
 // ds_read_b32 / ds_read2_b32 (32 banks) of one component both spread the
@@ -826,9 +827,16 @@ constexpr int pool_cap_for() {
 #ifndef RT_RAY_HOIST
 #define RT_RAY_HOIST 0
 #endif
+// The 32-ray instance (multi-frame launches of small frames, auto_rays)
+// spaces its fields 48 float2s apart, so that two fields of one ray read
+// together do not share banks: C3 65.6-65.7k -> 66.9-67.0k FPS, knot
+// 960x540 37.1k -> 37.7k (r04va; 40 gave the same).
+#ifndef RT_RAY_STRIDE32
+#define RT_RAY_STRIDE32 48
+#endif
 template <int kRays>
 struct RayLayout {
-    static constexpr int kStride = kRays;  // float2s between the fields of one ray
+    static constexpr int kStride = kRays == 32 ? RT_RAY_STRIDE32 : kRays;  // float2s between the fields of one ray
 };
 
 __device__ __forceinline__ void store_ray(float2* rd, int stride, const Ray& R, bool translated, float lmax,
@@ -1593,7 +1601,7 @@ __device__ __forceinline__ void pool_walk_split(const TraceParams& P, uint4* ite
 template <int kRays, int kCap, int kRayVec>
 struct WaveLds {
     uint4 items[kCap];
-    float2 ray[kRays * kRayVec * 2];
+    float2 ray[RayLayout<kRays>::kStride * kRayVec * 2];
     unsigned long long key[kRays];
     uint32_t tri[kRays];
 };
@@ -2015,7 +2023,7 @@ constexpr int kCoopWaves = 4;
 
 template <int kRays, int kRayVec>
 struct CoopHead {
-    float2 ray[kRays * kRayVec * 2];
+    float2 ray[RayLayout<kRays>::kStride * kRayVec * 2];
     unsigned long long key[kCoopWaves][kRays];
     uint32_t tri[kCoopWaves][kRays];
     // pool size / push counter, double-buffered: iteration i pushes through
