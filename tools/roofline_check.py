@@ -82,6 +82,8 @@ def main():
         # launch one frame, as bench.py's kernel time) when there is one
         # (bench/<session>_<config>.json pairs with rocprof/<session>_<config>_solo_*: any session, the latest)
         name = tag.split("_", 1)[1] if "_" in tag else tag
+        if name.startswith("trace_") and name.endswith("_mf"):
+            continue  # the profiled runs themselves (their traces are the reference)
         # repeats and variants of a configuration share its solo profile
         name = {"drv": "knot", "drv2": "knot", "drv_lanes": "knot", "knot_lanes": "knot", "trace_drv": "knot",
                 "rehearse": "knot", "anim2": "anim", "anim3": "anim"}.get(name, name)
