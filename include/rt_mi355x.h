@@ -385,13 +385,16 @@ int rt_camera_info(const rt_camera* c, int32_t* w, int32_t* h, int32_t* max_dept
  * node-own box records; 2: per-lane DFS, child-box records; 3: wave-
  * cooperative item pool, default), key 2 = tile dispatch order (0: XCD-
  * contiguous, 1: natural, 2: centre-out, 3: heaviest first by the cost an
- * earlier frame measured, default; kernel 3 reads the costs back with
- * stream-ordered async copies, skipped while the stream is captured).
+ * earlier frame measured, default; every 16th frame of kernel 3 writes
+ * its units' costs into page-locked host memory, read once that frame's
+ * event has completed; no samples while the stream is captured).
  * Every setting renders the identical frame. */
 #define RT_OPT_KERNEL 1
 #define RT_OPT_TILE_ORDER 2
 #define RT_OPT_RAYS 3 /* kernel 3: pixels per wave (64, 32, 16, 8; 0 = auto, default: 8 when this rank's
-                         share of the object's screen rectangle is too small to fill the GPU with 16) */
+                         share of the object's screen rectangle is too small to fill the GPU with 16,
+                         else 16; inside rt_run_frames' multi-frame launches (RT_LOOP_MULTIFRAME) 32
+                         when that rectangle holds fewer than 8,192 16-pixel units, else 16) */
 #define RT_OPT_ITEMS 4 /* kernel 3: items each lane pops per iteration (1, 2 default) */
 #define RT_OPT_COARSE 5 /* kernel 3: 8x8 groups per wave outside the root box's screen rectangle (0..32, 8 default, 0 = off) */
 /* kernel 3, shadow rays: the order the any-hit walk pushes children in (0..3;
