@@ -66,7 +66,11 @@ B_INT, B_LEAF, B_HIT, B_PIX = 36, 40, 24, 4
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs (ranks); N > 1 without torch.distributed.run starts its own N rank processes")
+    ap.add_argument("--launch-dry-run", action="store_true",
+                    help="with --gpus N: start the N rank processes, each of which prints its rank environment "
+                         "as JSON and exits without touching a GPU (tests the launcher on CPU)")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--scene", default="knot", choices=["dragon", "happy", "rabbit_70k", "tester", "big", "knot"],
@@ -418,8 +422,73 @@ def key_masks(spec: str) -> list:
     return out
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(a) -> int:
+    """`--gpus N` (N > 1) without torch.distributed.run (WORLD_SIZE unset):
+    start N fresh rank processes of this script with RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_ADDR (127.0.0.1) / MASTER_PORT set, one per GPU, and
+    wait for them.  This process never touches a GPU:
+    it only counts the visible devices (torch.cuda.device_count() does not
+    initialise HIP on this image) and fails fast when there are fewer than N.
+    Rank 0 prints the JSON line.  When a rank fails the others get 60 s to
+    finish, then are killed (by PID); the first failing rank's exit code is
+    returned."""
+    import subprocess
+    n = a.gpus
+    if not a.launch_dry_run:
+        import torch
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py: --gpus {n} but only {have} GPU(s) visible", file=sys.stderr, flush=True)
+            return 2
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RT_BENCH_LAUNCHED="1")
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rc, deadline = 0, None
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if bad and not rc:
+            rc = bad[0][1]
+            print(f"bench.py: rank {bad[0][0]} exited {rc}", file=sys.stderr, flush=True)
+            deadline = time.monotonic() + 60.0
+        if all(c is not None for c in codes):
+            break
+        if deadline is not None and time.monotonic() > deadline:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+            for p in procs:
+                p.wait()
+            break
+        time.sleep(0.1)
+    return rc if rc >= 0 else 128 - rc  # a rank killed by signal s: 128 + s, as a shell reports it
+
+
 def main():
     a = parse()
+    if a.launch_dry_run and os.environ.get("WORLD_SIZE"):
+        # a launched rank of --launch-dry-run: report the rank environment, no GPU
+        # (one write per line: the ranks share the parent's stdout)
+        sys.stdout.write(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                                                     "MASTER_PORT", "RT_BENCH_LAUNCHED")}) + "\n")
+        sys.stdout.flush()
+        # (tests: RT_BENCH_DRY_FAIL=r:code makes rank r exit with that code)
+        fail = os.environ.get("RT_BENCH_DRY_FAIL", "")
+        if fail and fail.split(":")[0] == os.environ.get("RANK"):
+            return int(fail.split(":")[1])
+        return 0
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ and not a.cpu_only:
+        return launch_ranks(a)
     if os.environ.get("RT_BENCH_WATCHDOG"):
         # diagnostics: dump every thread's Python stack and exit if the run
         # takes longer than this many seconds
@@ -833,12 +902,36 @@ def main():
         last = outs[loop.last_set()] if not isinstance(loop, PyLoop) else out
         frame_check = frame_check_n1(last.cpu().numpy().view(np.uint32), pts, nodes, cam_kw, a,
                                      xform=xf if masks else None)
+    ranks_info = None
     if multi:
         ok = gathered_frame_ok(loop)
         if rank == 0:
             frame_check = {"gathered_equals_single_gpu_frame": ok,
                            "collective": collective + (f", {len(ng.local)} buffer sets" if ng is not None else ""),
                            **({"note": gather_note} if gather_note else {})}
+        # per rank: the rank count the communicator
+        # reports, this rank's kernel time, and its gather alone -- 50
+        # gathers of its last rendered buffer set back to back on the comm
+        # stream, untimed, between one pair of HIP events (every rank takes
+        # part in each: rank 0 receives, the peers pack and send)
+        gather_us, comm_ranks = None, None
+        if ng is not None:
+            comm_ranks = ng.info()[0]
+            k = loop.last_set()
+            torch.cuda.synchronize(dev)
+            dist.barrier()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(cstream)
+            for _ in range(50):
+                ng.gather(k, cam, xf, a.mode, cstream.cuda_stream)
+            e1.record(cstream)
+            torch.cuda.synchronize(dev)
+            gather_us = 1e3 * e0.elapsed_time(e1) / 50
+        mine = {"rank": rank, "comm_ranks": comm_ranks, "kernel_us": round(1e3 * kern_ms, 2),
+                "gather_us": round(gather_us, 2) if gather_us is not None else None,
+                "host_us_per_frame": round(host_us_per_frame, 2)}
+        ranks_info = [None] * world
+        dist.all_gather_object(ranks_info, mine)
     full_walk = None
     if a.shadow and not masks:
         # shadow walks stop at their first occluder; the counting frame above
@@ -870,6 +963,16 @@ def main():
     # rays per frame: every pixel's primary ray, plus a shadow ray per hit
     rays_per_frame = w * h + (hits_all if a.shadow else 0)
 
+    solo_before = (20 + len(batch_ms) * solo[1]) if (solo is not None and a.solo_when == "before") else 0
+    if persistent:
+        loop_label = ("multi-frame launches (RT_LOOP_MULTIFRAME): up to 128 copies of the same static frame per "
+                      "k_trace_kd3 launch, frame-major; a batching mode for a static scene, not a per-frame loop")
+    elif isinstance(loop, PyLoop):
+        loop_label = "per-frame loop from Python, one frame at a time" + (" + gather" if multi else "")
+    else:
+        loop_label = (f"per-frame loop (rt_run_frames), {inflight} frame(s) in flight on the library's render lanes"
+                      + (" + RCCL gather to rank 0 on the comm lane" if ng is not None else
+                         " + torch gather" if multi else ""))
     rc = 0
     if rank == 0:
         fps = a.steps / elapsed
@@ -933,6 +1036,11 @@ def main():
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
+            # every untimed frame of the timed loop and the solo pass that ran
+            # before the timed region
+            "warmup_effective": a.warmup + settle + solo_before,
+            "warmup_breakdown": {"warmup": a.warmup, "settle": settle, "solo_pass": solo_before},
+            "loop": loop_label,
             "ms_per_step": round(1e3 * elapsed / a.steps, 5),
             "higher_is_better": True,
             "scaling": "strong",
@@ -1027,6 +1135,7 @@ def main():
                 "bytes_model": "36*V_int + 40*V_leaf + 24*H + 4*P (SURVEY.md 8d)",
             }),
             "device_err": errs if multi else dev_err,
+            **({"ranks": ranks_info} if ranks_info is not None else {}),
             "host": {"us_per_frame": round(host_us_per_frame, 2), "pre_timed_idle_us": round(pre_timed_idle_us, 1),
                      "settle_frames": settle,
                      **({"frame_group": cam.get_option(_lib.RT_OPT_FRAME_GROUP)} if persistent else {}), "loop": "native (rt_run_frames)"
@@ -1059,10 +1168,29 @@ def main():
             rc = 4
     if multi:
         dist.barrier()
-        if ng is not None:
-            ng.close()
+    # explicit teardown: every device object this run
+    # made is released here, after a device-wide synchronisation, while the
+    # HIP runtime and any profiler tool are fully alive -- not by finalisers
+    # at interpreter exit (the raytracer finalisers are no-ops then)
+    torch.cuda.synchronize(dev)
+    release(ng, cam, obj, trixel)
+    torch.cuda.synchronize(dev)
+    if multi:
         dist.destroy_process_group()
+    maps = os.environ.get("RT_BENCH_MAPS")
+    if maps:  # diagnostics: this process's mappings, to symbolise a crash report's addresses
+        with open(maps, "w") as fp, open("/proc/self/maps") as src:
+            fp.write(src.read())
     return rc
+
+
+def release(ng, cam, obj, trixel):
+    """Closes the run's library handles in dependency order: the RCCL
+    communicator, the camera (its streams, events, buffers), the object's
+    motion state, then the scene."""
+    for h in (ng, cam, getattr(obj, "motion", None), trixel):
+        if h is not None:
+            h.close()
 
 
 if __name__ == "__main__":

@@ -1716,13 +1716,18 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
                          flags == 0 && !display;
     p.pf_frames = 0;
     if (persist) {
-        p.pf_frames = pf->frames;
         p.pf_blocks = (int32_t)fine_grid_blocks(p);
+        // one dispatch holds at most 2^32 - 1 work-items (and 2^31 - 1
+        // blocks): fewer frames per launch for large frames (a
+        // 4K frame of 8-ray units is ~259k blocks of 256 threads)
+        const int64_t threads = 64 * (int64_t)kd3_waves(p.rays);
+        const int64_t max_blocks = std::min<int64_t>(0xFFFFFFFFll / threads, 0x7FFFFFFFll);
+        p.pf_frames = (int32_t)std::max<int64_t>(1, std::min<int64_t>(pf->frames, max_blocks / std::max(1, p.pf_blocks)));
         p.pf_nbuf = pf->nbuf;
         p.pf_seq0 = pf->seq0 % pf->nbuf;
-        p.pf_group = std::max(1, std::min(pf->frames, c->frame_group > 0 ? c->frame_group : RT_PF_GROUP));
+        p.pf_group = std::max(1, std::min(p.pf_frames, c->frame_group > 0 ? c->frame_group : RT_PF_GROUP));
         for (int k = 0; k < RT_LOOP_MAX_BUF; k++) p.pf_argb[k] = k < pf->nbuf ? pf->argb[k] : nullptr;
-        if (rendered) *rendered = pf->frames;
+        if (rendered) *rendered = p.pf_frames;
     }
     const bool sampled = order3 && !persist && cost_sample_now(c, st);
     if (sampled) {

@@ -157,6 +157,14 @@ class NativeFrameGather:
         _lib.call("rt_frame_rect", cam._h, _lib.ptr(xf), mode, self.world, _lib.ptr(rect))
         return tuple(int(v) for v in rect)
 
+    def info(self) -> tuple:
+        """(ranks, rank) the communicator itself reports (rt_comm_info)."""
+        import ctypes as C
+        from . import _lib
+        n, r = C.c_int32(), C.c_int32()
+        _lib.call("rt_comm_info", self._h, C.byref(n), C.byref(r))
+        return n.value, r.value
+
     def close(self) -> None:
         from . import _lib
         if self._h:

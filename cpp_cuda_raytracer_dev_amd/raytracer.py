@@ -20,6 +20,7 @@ reference (0 = success); failures of the device path raise ``RtError``.
 from __future__ import annotations
 
 import ctypes as C
+import sys
 
 import numpy as np
 
@@ -36,6 +37,22 @@ ROTATE_TRI_PY, ROTATE_TRI_NY = 10, 11                 # TD/platform_common.h:19-
 #: Held-key bits of ObjectMotion.tick / Object.key_tick (TD/WinMain.cpp:186-209).
 KEY_R, KEY_W, KEY_S, KEY_Q, KEY_E, KEY_T = 1, 2, 4, 8, 16, 32
 CAM_SPEED = np.float32(.005)  # TD/WinMain.cpp:170
+
+
+def _finalize(owner) -> None:
+    """__del__ of a handle owner: close it, unless the interpreter is shutting
+    down.  Then the HIP runtime (and a profiler's tool library) may already be
+    finalising, and releasing device memory from a finaliser can fault
+    (a SIGSEGV in __cxa_finalize after bench.py's line
+    under rocprofv3); the process's exit returns the memory anyway.  Owners
+    close their handles explicitly (bench.py, smoke(), the tests' scenes)."""
+    if sys.is_finalizing():
+        return
+    try:
+        owner.close()
+    except Exception:
+        pass
+
 
 #: Material of every triangle in the reference demo (TD/WinMain.cpp:117-121).
 DEFAULT_RAD = (np.float32(0.1), np.float32(0.55), np.float32(0.2))
@@ -169,10 +186,7 @@ class ObjectMotion:
             self._h = C.c_void_p()
 
     def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
+        _finalize(self)
 
 
 class Trixel:
@@ -251,10 +265,7 @@ class Trixel:
             self._h = C.c_void_p()
 
     def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
+        _finalize(self)
 
 
 class Object:
@@ -403,10 +414,7 @@ class Camera:
             self._h = C.c_void_p()
 
     def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
+        _finalize(self)
 
 
 class FrameLoop:
@@ -501,10 +509,7 @@ class PinnedFrames:
         self._ptrs = []
 
     def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
+        _finalize(self)
 
 
 __all__ = ["read_ply", "assemble_mesh", "kd_build", "film_w", "camera_basis", "Quaternion", "Trixel", "Object",

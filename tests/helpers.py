@@ -109,6 +109,12 @@ class GpuScene:
         cnt = self.cam.counters() if count else None
         return self.cam.h_color.copy(), self.cam.h_rmi.copy(), cnt
 
+    def close(self):
+        """Releases the camera, the motion state and the scene (in that order)."""
+        for h in (self.cam, self.obj.motion, self.trixel):
+            if h is not None:
+                h.close()
+
 
 def golden():
     return np.load(GOLDEN, allow_pickle=False)

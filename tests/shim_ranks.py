@@ -83,7 +83,7 @@ POSES = [rot_y_xform(0.0), rot_y_xform(3.0), rot_y_xform(0.0, (0.01, 0.0, 0.0)),
          rot_y_xform(1.5, (0.0, 0.004, 0.0))]
 
 
-def run_group(n, scene, w, h, frames, inflight, nbuf, trixel, oracle_frame):
+def run_group(n, scene, w, h, frames, inflight, nbuf, trixel, oracle_frame, poses, flags):
     import torch
     from cpp_cuda_raytracer_dev_amd import raytracer as R, scenes
     from cpp_cuda_raytracer_dev_amd.distributed import NativeFrameGather
@@ -109,9 +109,9 @@ def run_group(n, scene, w, h, frames, inflight, nbuf, trixel, oracle_frame):
                 loc.fill_(0x5EEDF00D)
             rect = ng.verify(cam, None, 0)
             rs, cs = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
-            loop = R.FrameLoop(cam, ng.local, mode=0, tile=(n, r), render_stream=rs.cuda_stream, comm=ng,
-                               comm_stream=cs.cuda_stream, event_every=8, inflight=inflight,
-                               xforms=np.stack(POSES))
+            loop = R.FrameLoop(cam, ng.local, mode=0, flags=flags, tile=(n, r), render_stream=rs.cuda_stream,
+                               comm=ng, comm_stream=cs.cuda_stream, event_every=8, inflight=inflight,
+                               xforms=np.stack(poses))
             torch.cuda.synchronize(dev)
             d.barrier()
             t0 = time.perf_counter()
@@ -137,7 +137,7 @@ def run_group(n, scene, w, h, frames, inflight, nbuf, trixel, oracle_frame):
     ok = True
     for k in range(nbuf):
         j = max(i for i in range(frames) if i % nbuf == k)  # the set's last frame
-        p = j % len(POSES)
+        p = j % len(poses)
         got = ng0.frames[k].cpu().numpy().view(np.uint32)
         ref, how = oracle_frame(p)  # a frame, or the SHA-256 of one
         sha = hashlib.sha256(got.tobytes()).hexdigest()
@@ -150,8 +150,10 @@ def run_group(n, scene, w, h, frames, inflight, nbuf, trixel, oracle_frame):
     out = {"nranks": n, "ok": ok, "device_err": errs, "frames": frames, "inflight": inflight, "nbuf": nbuf,
            "rect_identity": list(state[0]["rect"]), "sets": sets,
            "seconds_per_rank": [round(s["seconds"], 4) for s in state]}
-    for s in state:
-        s["ng"].close()
+    for s in state:  # explicit release, in dependency order
+        for k in ("ng", "cam"):
+            s[k].close()
+        s["obj"].motion.close()
     return out
 
 
@@ -164,6 +166,8 @@ def main():
     ap.add_argument("--frames", type=int, default=24)
     ap.add_argument("--inflight", type=int, default=2)
     ap.add_argument("--nbuf", type=int, default=4)
+    ap.add_argument("--shadow", action="store_true", help="one shadow ray per hit (config C5)")
+    ap.add_argument("--identity-only", action="store_true", help="every frame at the identity pose")
     a = ap.parse_args()
     if not os.environ.get("RT_RCCL_LIB"):
         print("shim_ranks.py: RT_RCCL_LIB must name tests/rccl_shim/librccl_shim.so", file=sys.stderr)
@@ -179,7 +183,9 @@ def main():
     trixel = R.Trixel(len(pts), pts, device=0)
     trixel.set_kd_nodes(nodes)
     cam_kw = scenes.view(a.scene, "default")
-    ent = H.frame_hashes().get(f"{a.scene}_{w}x{h}_m0")
+    ent = H.frame_hashes().get(f"{a.scene}_{w}x{h}_m0" + ("_shadow" if a.shadow else ""))
+    poses = POSES[:1] if a.identity_only else POSES
+    flags = R.RT_FLAG_SHADOW if a.shadow else 0
     cache = {}
 
     def oracle_frame(p):
@@ -192,15 +198,17 @@ def main():
                 for k in nodes.dtype.names:
                     on[k] = nodes[k]
                 s = O.Scene(pts, O.default_rad(len(pts)), on, O.camera(w, h, **cam_kw))
-                ref, _, _ = s.render(0, xform=POSES[p].reshape(3, 4), nthreads=H.ORACLE_THREADS, want_hit=False)
+                ref, _, _ = s.render(0, xform=poses[p].reshape(3, 4), nthreads=H.ORACLE_THREADS, want_hit=False,
+                                     shadow=a.shadow)
                 s.close()
                 cache[p] = (ref, "oracle render at the pose")
         return cache[p]
 
-    results = [run_group(int(n), a.scene, w, h, a.frames, a.inflight, a.nbuf, trixel, oracle_frame)
+    results = [run_group(int(n), a.scene, w, h, a.frames, a.inflight, a.nbuf, trixel, oracle_frame, poses, flags)
                for n in a.nranks.split(",")]
+    trixel.close()
     ok = all(r["ok"] for r in results)
-    print(json.dumps({"ok": ok, "scene": a.scene, "resolution": [w, h], "build_id": _lib.build_id(),
+    print(json.dumps({"ok": ok, "scene": a.scene, "resolution": [w, h], "shadow": a.shadow, "build_id": _lib.build_id(),
                       "rccl": os.environ["RT_RCCL_LIB"], "groups": results}), flush=True)
     return 0 if ok else 1
 

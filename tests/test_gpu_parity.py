@@ -1397,6 +1397,38 @@ def test_shim_ranks_gather():
         assert {s["pose"] for s in g["sets"]} - {0}, "a moved pose is checked"
 
 
+@pytest.mark.gpu
+def test_shim_ranks_gather_c5():
+    """BASELINE config C5 (happy stand-in 3840x2160, one
+    shadow ray per hit, 8 ranks) through the library's own N > 1 gather
+    (csrc/comm.cpp) via the test-only RCCL shim: 4K rectangle parts of up to
+    4.1 MB per rank and shadowed frames go through rank 0's ncclRecv loop and
+    assembly.  Identity pose; every buffer set rank 0 assembled hashes to the
+    committed oracle frame happy_3840x2160_m0_shadow, every rank's device
+    error word is 0.  Not an N > 1 hardware measurement."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from tests.rccl_shim import build as shim
+    ent = H.frame_hashes()["happy_3840x2160_m0_shadow"]
+    if not H.mesh_matches(ent):
+        pytest.skip("the happy stand-in's mesh differs on this host (numpy transcendentals)")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, RT_RCCL_LIB=shim.build())
+    r = subprocess.run([sys.executable, "-u", os.path.join(root, "tests", "shim_ranks.py"), "--nranks", "8",
+                        "--scene", "happy", "--width", "3840", "--height", "2160", "--shadow", "--identity-only",
+                        "--frames", "16"], cwd=root, env=env, capture_output=True, text=True, timeout=110)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert lines, f"no result (exit {r.returncode}): {r.stdout[-2000:]} {r.stderr[-2000:]}"
+    out = json.loads(lines[-1])
+    print(json.dumps(out))
+    assert r.returncode == 0 and out["ok"], out
+    (g,) = out["groups"]
+    assert g["nranks"] == 8 and g["device_err"] == [0] * 8, g
+    assert all(s["equal"] and s["method"].startswith("sha256") for s in g["sets"]), g
+
+
 def test_far_along_key_sequence_background():
     """bench.py --animate R+W.Q.T.W carries the object past
     the camera after ~500 ticks (the oracle shows background only).  The host
@@ -1451,6 +1483,34 @@ def test_far_along_key_sequence_background():
             assert (got[sel] == want[sel]).all(), f"tick {i} rank {r}"
     assert checked["visible"] >= 2 and checked["behind"] >= 1, checked
     assert s.cam.device_error(reset=True) == 0
+
+
+@pytest.mark.gpu
+def test_multiframe_launch_grid_limit():
+    """a multi-frame launch holds at most 2^32 - 1 work-items.
+    The dragon fill view at 3840x2160 with 8-ray units is ~259k blocks of 256
+    threads per frame, so 128 frames per launch would exceed it; the library
+    takes fewer frames per launch.  Every buffer set equals a single-frame
+    render of the same frame (itself checked against the oracle elsewhere)."""
+    import torch
+    from cpp_cuda_raytracer_dev_amd import _lib, scenes
+    w, h = 3840, 2160
+    s = H.GpuScene("dragon", w, h, cam_kw=scenes.view("dragon", "fill"), rays=8)
+    dev = torch.device("cuda:0")
+    st = torch.cuda.Stream(device=dev)
+    ref = torch.zeros(w * h, dtype=torch.int32, device=dev)
+    s.cam.render_into(ref, stream=st.cuda_stream)
+    bufs = [torch.full((w * h,), 0x7BADBEEF, dtype=torch.int32, device=dev) for _ in range(2)]
+    loop = R.FrameLoop(s.cam, bufs, mode=0, render_stream=st.cuda_stream, event_every=1,
+                       inflight=_lib.RT_LOOP_MULTIFRAME)
+    ms, cnt, _ = loop.run(300)
+    torch.cuda.synchronize()
+    assert s.cam.get_option(_lib.RT_OPT_RAYS_USED) == 8
+    assert cnt == 300 and ms > 0
+    for b in bufs:
+        assert torch.equal(b, ref)
+    assert s.cam.device_error(reset=True) == 0
+    s.close()
 
 
 @pytest.mark.parametrize("key", ["dragon_960x540_m0", "knot_1920x1080_m0", "dragon_1920x1080_m0"])
