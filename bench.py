@@ -106,29 +106,23 @@ def parse():
     ap.add_argument("--solo-when", default="before", choices=["before", "after"],
                     help="solo frames (the roofline's kernel time) run just before the warm-up-to-timed handover, "
                          "or after the timed frames")
-    ap.add_argument("--frame-group", type=int, default=0,
-                    help="multi-frame launches: frames per interleaved group (RT_OPT_FRAME_GROUP; 0 = library default)")
     ap.add_argument("--settle-ms", type=float, default=40.0,
                     help="untimed frames of the timed loop itself for about this much time right before the timed "
                          "region (a moving object: one pass over the timed poses, native loop only; 0: none)")
     ap.add_argument("--pipeline", type=int, default=2,
                     help="rccl: buffer sets in flight (frame i+1 renders while frame i is gathered)")
     ap.add_argument("--kernel", type=int, default=3,
-                    help="KD kernel: 1 per-lane DFS (own-box records), 2 per-lane DFS (child-box records), "
-                         "3 wave-cooperative item pool")
+                    help="KD kernel: 2 per-lane DFS in the reference's order, 3 wave-cooperative item pool")
     ap.add_argument("--tile-order", type=int, default=3,
                     help="0 XCD-contiguous, 1 natural, 2 centre-out, 3 by the cost an earlier frame measured")
     ap.add_argument("--rays", type=int, default=0,
-                    help="kernel 3: pixels per wave (64, 32, 16, 8; 0 = the library's automatic choice)")
+                    help="kernel 3: pixels per wave (32, 16, 8; 0 = the library's automatic choice)")
     ap.add_argument("--items", type=int, default=2, help="kernel 3: items each lane pops per iteration (1, 2)")
     ap.add_argument("--order", type=int, default=-1,
                     help="interior record order: 0 BFS, 1 DFS preorder, 2 treelets (-1: the library default)")
     ap.add_argument("--treelet", type=int, default=0, help="treelet height for --order 2 (0: library default)")
     ap.add_argument("--flat", type=int, default=-1,
-                    help="flat-list kernel form: 0 one triangle per iteration, 1 pairs, 2 packed float2 pairs, "
-                         "3 pipelined 2, 4 signed pairs + min3 screen, 5 4 unrolled x2, 6 5 behind one branch, "
-                         "7 5 with V first, 8 7 one pair per iteration, 9 7 pipelined, 10-13 9 over 8/4/16/32 chunks "
-                         "(-1: the library default, 12)")
+                    help="flat-list kernel form: 9 one pass, 12 the list in 16 chunks (-1: the library default, 12)")
     ap.add_argument("--coarse", type=int, default=8,
                     help="kernel 3: 8x8 groups per wave outside the root box's screen rectangle (0 = off)")
     ap.add_argument("--event-every", type=int, default=0,
@@ -603,7 +597,6 @@ def main():
     cam.set_option(_lib.RT_OPT_RAYS, a.rays)
     cam.set_option(_lib.RT_OPT_ITEMS, a.items)
     cam.set_option(_lib.RT_OPT_COARSE, a.coarse)
-    cam.set_option(_lib.RT_OPT_FRAME_GROUP, a.frame_group)
     cam.set_option(_lib.RT_OPT_SHADOW_ORDER, a.shadow_order)
     if a.flat >= 0:
         cam.set_option(_lib.RT_OPT_FLAT, a.flat)
@@ -1107,7 +1100,7 @@ def main():
                 **({"demand_frac_excl_root_misses": round((bytes_per_launch - B_INT * (my_pix - root_passes)) / kern_s
                                                           / 1e9 / HBM_PEAK_GBS, 4),
                     "root_pass_pixels": root_passes} if root_passes is not None and not multi else {}),
-                "kernel": {1: "k_trace_kd", 2: "k_trace_kd2", 3: "k_trace_kd3"}[a.kernel] if a.mode == 0
+                "kernel": {2: "k_trace_kd2", 3: "k_trace_kd3"}[a.kernel] if a.mode == 0
                           else "k_trace_flat",
                 "kernel_options": {"kernel": a.kernel, "tile_order": a.tile_order,
                                    "rays_per_wave": cam.get_option(_lib.RT_OPT_RAYS_USED),
@@ -1138,7 +1131,7 @@ def main():
             **({"ranks": ranks_info} if ranks_info is not None else {}),
             "host": {"us_per_frame": round(host_us_per_frame, 2), "pre_timed_idle_us": round(pre_timed_idle_us, 1),
                      "settle_frames": settle,
-                     **({"frame_group": cam.get_option(_lib.RT_OPT_FRAME_GROUP)} if persistent else {}), "loop": "native (rt_run_frames)"
+                     "loop": "native (rt_run_frames)"
                      if not isinstance(loop, PyLoop) else "python",
                      "frames_in_flight": ("multi-frame launches" if persistent else inflight)
                      if not isinstance(loop, PyLoop) else 1,

@@ -75,7 +75,6 @@ struct rt_camera {
     float4* d_tpair = nullptr;       // flat variant 2: camera-relative triangle pairs
     uint32_t trec_cap = 0;
     int64_t inode_cap = 0;           // in float4
-    int prepared_layout = 0;         // interior record layout of d_inode (1 or 2)
     int kernel_version = 3;          // kOptKernel
     int tile_order = 3;              // kOptTileOrder
     // kOptDebug (diagnostics): 1 skip traversal, 2 per-wave stamps, 4 every
@@ -86,7 +85,6 @@ struct rt_camera {
     int pool_cap = kPoolCapMax;      // kOptPoolCap
     unsigned long long* d_dbg = nullptr;
     int64_t dbg_cap = 0;             // in u64
-    int64_t istamp_off = 0;          // debug bit 128 (RT_ITER_STAMPS builds): stamps' offset in d_dbg, u64
     Hold hold;                       // the fine region renders keep (set_fine_region)
     int32_t* d_order = nullptr;      // the current tile permutation (a slot's buffer)
     int64_t order_key[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
@@ -113,7 +111,6 @@ struct rt_camera {
     int noused = 0;
     bool oused_overflow = false;
     int coarse = 8;                  // kOptCoarse: coarse groups per wave (0 = off)
-    int frame_group = 0;             // kOptFrameGroup: multi-frame launches' group (0 = RT_PF_GROUP)
     bool multiframe = false;         // inside rt_run_frames' multi-frame launches (auto_rays)
     std::vector<int32_t> centre;     // centre-out permutation of the current fine grid (host copy)
     // 8x8 groups (x / 8, y / 8) holding a pixel whose primary ray has a zero
@@ -142,18 +139,15 @@ struct rt_camera {
     int frames_since = 0;
     uint64_t layout_gen = 0, cost_gen = 0;   // fine-grid generation, and the one h_cost was read for
     // The order ranks tiles by the cost of one wave per unit (pool
-    // iterations).  Coop tiles write no cost (their walk is no measure of
-    // it) and split halves report an estimate, so each tile's cost as last
-    // measured unsplit and not coop is remembered (per grid) and used while
-    // it renders split or coop: sample_mode holds, per tile, how the sampled
-    // frame rendered it (0 whole, 1 coop, 2 split; taken when the sample is
-    // queued).
-    std::vector<uint8_t> sample_coop;
+    // iterations).  Split halves report an estimate, so each tile's cost as
+    // last measured unsplit is remembered (per grid) and used while it
+    // renders split: sample_split holds, per tile, whether the sampled frame
+    // rendered it split (taken when the sample is queued).
+    std::vector<uint8_t> sample_split;
     std::vector<uint32_t> cost_mem;
     uint64_t mem_gen = ~0ull;
     uint64_t order_gen = ~0ull;              // generation whose cost order d_order holds
-    int32_t order_split = 0;                 // split tiles after the coop tiles of that cost order
-    int32_t order_coop = 0;                  // coop tiles at the head of that cost order
+    int32_t order_split = 0;                 // split tiles at the head of that cost order
     int rays = 0;                    // kOptRays: pixels per wave of kernel 3 (0: auto_rays)
     int last_rays = 0;               // the pixels per wave the last kernel-3 render used
     int items = 2;                   // kOptItems: items per lane per pool iteration
@@ -200,12 +194,6 @@ struct rt_camera {
     // rt_run_frames: events kept across calls (the timed call reuses the
     // warm-up call's), pairs bracketing sampled frames' renders
     std::vector<hipEvent_t> loop_ev;
-    // rt_run_frames' dispatch gate: per lane, the count of started blocks
-    // of its kernel-3 frames (device, zeroed once) and how many it will reach
-    // once every frame launched so far has dispatched (host)
-    unsigned long long* d_started = nullptr;
-    unsigned long long started_cum[RT_LOOP_MAX_LANES] = {};
-    unsigned long long started_last[RT_LOOP_MAX_LANES] = {};  // blocks of each lane's last gated frame
     struct RectCache {
         bool valid = false;
         uint64_t gen = 0, tree = 0;
@@ -253,13 +241,11 @@ void dev_free(T*& p) {
 // 3's marked path codes take height + 1 <= 25 bits.
 int effective_kernel(const rt_camera* c) { return c->kernel_version; }
 
-int record_layout(int kernel) { return kernel == 1 ? 1 : 2; }
 
 int prepare_camera_object(rt_camera* c) {
     rt_scene* s = c->obj;
     if (!s) return fail(RT_ERR_STATE, "camera has no object (rt_camera_add_object)");
-    const int layout = record_layout(effective_kernel(c));
-    if (c->prepared_version == s->tree_version + 1 && c->prepared_layout == layout) return RT_OK;
+    if (c->prepared_version == s->tree_version + 1) return RT_OK;
     int rc;
     if (c->trec_cap < s->ntri) {
         dev_free(c->d_trec);
@@ -275,7 +261,7 @@ int prepare_camera_object(rt_camera* c) {
         (rc = launch_pair_tri(c->d_trec, s->ntri, c->d_tpair, nullptr)))
         return rc;
     if (s->d_nodes) {
-        const int64_t need = std::max<int64_t>(s->ninterior, 1) * (layout == 1 ? 3 : 4);
+        const int64_t need = std::max<int64_t>(s->ninterior, 1) * 4;
         if (c->inode_cap < need) {
             dev_free(c->d_inode);
             if ((rc = dev_alloc(&c->d_inode, (size_t)need, "hipMalloc(inode)"))) return rc;
@@ -283,12 +269,11 @@ int prepare_camera_object(rt_camera* c) {
         }
         // init_camera_voxel_device_memory (TD/Camera.cu:163-187)
         if ((rc = launch_cam_nodes(s->d_nodes, s->d_interior_ids, s->d_node_ref, s->ninterior, c->pos,
-                                   c->d_inode, layout, nullptr)))
+                                   c->d_inode, nullptr)))
             return rc;
     }
     if ((rc = hip_check(hipDeviceSynchronize(), "camera object prep"))) return rc;
     c->prepared_version = s->tree_version + 1;
-    c->prepared_layout = layout;
     return RT_OK;
 }
 
@@ -404,7 +389,6 @@ int ensure_order(rt_camera* c, const TraceParams& p, hipStream_t st) {
     c->d_order = o.d;
     c->order_gen = ~0ull;  // no cost order for this grid yet
     c->order_split = 0;    // nor split tiles
-    c->order_coop = 0;     // nor coop tiles
     std::copy(key, key + 8, c->order_key);
     c->centre.swap(order);
     c->layout_gen++;
@@ -563,57 +547,6 @@ constexpr int64_t kSplitMaxTiles = RT_SPLIT_MAX_TILES;
 #ifndef RT_SPLIT8
 #define RT_SPLIT8 1
 #endif
-// coop tiles: cost > RT_COOP_PCT % of the top (grids of fewer than
-// kSplitMaxTiles tiles; RT_COOP_PCT_LARGE % for larger ones), at most
-// n / RT_COOP_CAP_DIV and RT_COOP_MAX tiles (each takes 4 blocks)
-// Measured (round 4, r04d-r04h): coop tiles shorten the heaviest units'
-// chains (dragon 960x540: 25-27 -> 17-18 iterations) but their extra waves
-// slow the other heavy units' iterations (1.10 -> 1.25 us), and the frame
-// lost: C3 47.8k -> 43.2k FPS, knot 960x540 31.0k -> 30.2k, dragon 1080p
-// 16.48k -> 16.36k.  Off by default (0); debug bit 8192 selects them at
-// 60 % / 70 % (tests), 4096 makes every tile a coop tile.
-#ifndef RT_COOP_PCT
-#define RT_COOP_PCT 0
-#endif
-#ifndef RT_COOP_PCT_LARGE
-#define RT_COOP_PCT_LARGE 0
-#endif
-#ifndef RT_COOP_CAP_DIV
-#define RT_COOP_CAP_DIV 8
-#endif
-#ifndef RT_COOP_MAX
-#define RT_COOP_MAX 256
-#endif
-// rt_run_frames' dispatch gate: a lane's frame starts once the previous
-// frame (other lane) has started RT_GATE_PCT % of its blocks
-// Measured (r04g, r04h: knot 1080p, the driver's 20 frames / 1000 frames):
-// gate off 8.90k / 10.32k FPS, at 70 % 8.83k, 50 % 8.29-8.58k / 9.82k, 30 %
-// 8.22k / 9.36k, 15 % 8.02-8.21k / 9.37k, at 100 % (every block started)
-// 7.63-7.75k / 8.44k: the free-running lanes overlap more than any gate
-// lets them.  Off by default (0).
-#ifndef RT_GATE_PCT
-#define RT_GATE_PCT 0
-#endif
-// multi-frame launches: frames per interleaved group (1: frame-major)
-#ifndef RT_PF_GROUP
-#define RT_PF_GROUP 1
-#endif
-
-
-// Experiments: a tuning constant from the environment (read once), else
-// the compiled default.  RT_TUNE_COOP_PCT, RT_TUNE_COOP_PCT_LARGE,
-// RT_TUNE_COOP_CAP_DIV, RT_TUNE_SPLIT_PCT, RT_TUNE_SPLIT_PCT_LARGE.
-int tune(const char* name, int dflt) {
-    static std::mutex m;
-    static std::vector<std::pair<std::string, int>> cache;
-    std::lock_guard<std::mutex> lk(m);
-    for (const auto& kv : cache)
-        if (kv.first == name) return kv.second;
-    const char* v = getenv(name);
-    const int x = v && *v ? atoi(v) : dflt;
-    cache.emplace_back(name, x);
-    return x;
-}
 
 // Whether the frame about to launch on `st` is a cost sample: its kernel then
 // writes its units' costs into c->h_cost (zeroed here) instead of nothing.
@@ -636,18 +569,18 @@ int cost_feedback(rt_camera* c, const TraceParams& p, void* stream, bool sampled
         c->frames_since = 0;
         if (c->cost_gen != c->layout_gen || (int64_t)c->centre.size() != n) return RT_OK;  // stale sample
         // the sampled costs, with the remembered unsplit cost of each tile the
-        // sampled frame rendered split or coop (coop units write no cost)
+        // sampled frame rendered split (a half reports an estimate)
         if (c->mem_gen != c->layout_gen || (int64_t)c->cost_mem.size() != n) {
             c->cost_mem.assign((size_t)n, 0u);
             c->mem_gen = c->layout_gen;
         }
         std::vector<uint32_t> eff(c->h_cost, c->h_cost + kCostSlots * (size_t)n);
-        const bool have_flags = (int64_t)c->sample_coop.size() == n;
+        const bool have_flags = (int64_t)c->sample_split.size() == n;
         for (int64_t t = 0; t < n; t++) {
             uint32_t* e = eff.data() + kCostSlots * (size_t)t;
             uint32_t m = 0;
             for (int k = 0; k < kCostSlots; k++) m = std::max(m, e[k]);
-            const uint8_t mode = have_flags ? c->sample_coop[(size_t)t] : 0;
+            const uint8_t mode = have_flags ? c->sample_split[(size_t)t] : 0;
             if (mode && c->cost_mem[(size_t)t] > 0) {
                 for (int k = 0; k < kCostSlots; k++) e[k] = 0u;
                 e[0] = c->cost_mem[(size_t)t];
@@ -666,38 +599,20 @@ int cost_feedback(rt_camera* c, const TraceParams& p, void* stream, bool sampled
         // end near the unsplit ones' (a unit's chain is mostly its items:
         // half the rays, about half the pool iterations); at most a quarter
         // of the tiles.  Debug bit 512: none.
-        // Coop tiles (kernel 3, 16- and 8-ray units): the tiles costlier than
-        // RT_COOP_PCT % of the heaviest (at most n / RT_COOP_CAP_DIV and
-        // RT_COOP_MAX) head the order and render each unit with a whole
-        // block on one pool (k_trace_kd3's trace_unit_coop); debug bit 2048:
-        // none.
-        int32_t split = 0, coop = 0;
+        int32_t split = 0;
         auto cost_of = [&](int64_t t) {
             uint32_t m = 0;
             for (int k = 0; k < kCostSlots; k++) m = std::max(m, eff[kCostSlots * (size_t)t + k]);
             return m;
         };
         const uint32_t top = n > 0 ? cost_of(ord[0]) : 0;
-        const bool sel8192 = (c->debug & 8192) != 0;
-        const int64_t cpct = n < kSplitMaxTiles ? (sel8192 ? 60 : tune("RT_TUNE_COOP_PCT", RT_COOP_PCT))
-                                                : (sel8192 ? 70 : tune("RT_TUNE_COOP_PCT_LARGE", RT_COOP_PCT_LARGE));
-        if (c->tile_order == 3 && (p.rays == 16 || p.rays == 8) && kd3_waves(p.rays) == 4 && !(c->debug & 2048) &&
-            n > 0 && (cpct > 0 || (c->debug & 4096))) {
-            const int64_t pct = cpct;
-            while (coop < std::min<int64_t>(n / tune("RT_TUNE_COOP_CAP_DIV", RT_COOP_CAP_DIV), RT_COOP_MAX) &&
-                   100ull * cost_of(ord[(size_t)coop]) > (uint64_t)pct * top && top >= 24)
-                coop++;
-            if (c->debug & 4096) coop = (int32_t)n;  // tests: every tile a coop tile
-        }
         if (c->tile_order == 3 && (p.rays == 16 || (p.rays == 8 && RT_SPLIT8)) && kd3_waves(p.rays) == 4 &&
             !(c->debug & 512) && n > 0 && (n < kSplitMaxTiles || RT_SPLIT_PCT_LARGE > 0)) {
-            const uint64_t pct = n < kSplitMaxTiles ? tune("RT_TUNE_SPLIT_PCT", RT_SPLIT_PCT)
-                                                    : tune("RT_TUNE_SPLIT_PCT_LARGE", RT_SPLIT_PCT_LARGE);
-            while (coop + split < n / RT_SPLIT_CAP_DIV && 100ull * cost_of(ord[(size_t)(coop + split)]) > pct * top &&
-                   top >= 24)
+            const uint64_t pct = n < kSplitMaxTiles ? RT_SPLIT_PCT : RT_SPLIT_PCT_LARGE;
+            while (split < n / RT_SPLIT_CAP_DIV && 100ull * cost_of(ord[(size_t)split]) > pct * top && top >= 24)
                 split++;
         }
-        same = same && split == c->order_split && coop == c->order_coop;
+        same = same && split == c->order_split;
         if (same && c->order_gen == c->layout_gen) return RT_OK;  // d_order already holds it
         int rc;
         // frames on other streams (frames in flight on the library's lanes,
@@ -722,7 +637,6 @@ int cost_feedback(rt_camera* c, const TraceParams& p, void* stream, bool sampled
         c->cost_up_valid = true;
         c->order_pending = true;
         c->order_split = split;  // launches after this upload (stream order) use it
-        c->order_coop = coop;
         c->order_gen = c->layout_gen;
         return RT_OK;
     }
@@ -734,13 +648,13 @@ int cost_feedback(rt_camera* c, const TraceParams& p, void* stream, bool sampled
     if ((rc = hip_check(hipEventRecord(c->cost_ev, st), "cost event"))) return rc;
     c->cost_pending = true;
     c->cost_gen = c->layout_gen;
-    // how the order this frame launched with rendered each tile (render_common:
-    // coop tiles order[0..coop), split tiles order[coop..coop + split))
-    c->sample_coop.assign((size_t)n, 0);
+    // which tiles the order this frame launched with rendered split
+    // (render_common: order[0..split))
+    c->sample_split.assign((size_t)n, 0);
     if (c->order_gen == c->layout_gen)
-        for (int32_t k = 0; k < p.coop + p.split && k < n; k++) {
+        for (int32_t k = 0; k < p.split && k < n; k++) {
             const int32_t t = c->h_order[k];
-            if (t >= 0 && t < n) c->sample_coop[(size_t)t] = k < p.coop ? 1 : 2;
+            if (t >= 0 && t < n) c->sample_split[(size_t)t] = 1;
         }
     return RT_OK;
 }
@@ -1054,9 +968,9 @@ bool frame_geometry(const FrameGeom& g, const float* xform, const rt_tile* tile,
     const int32_t nbands = (g.h + kTileH - 1) / kTileH;
     const int kernel = mode == RT_MODE_KD ? g.kernel : 0;
     p.rays = kernel == 3 ? (g.rays > 0 ? g.rays : auto_rays(g, p)) : 64;
-    if (kernel == 0 || kernel == 1) {        // flat / v1: 32x8 tiles, four 8x8 waves
+    if (kernel == 0) {                       // flat: 32x8 tiles, four 8x8 waves
         p.tile_w = kTileWFlat; p.tile_h = kTileH;
-    } else if (p.rays == 64) {               // v2 / v3: 16x8 tiles, two 8x8 waves
+    } else if (p.rays == 64) {               // v2: 16x8 tiles, two 8x8 waves
         p.tile_w = kTileWKd; p.tile_h = kTileH;
     } else {                                 // v3, two stacked 8 x (rays/8) waves
         p.tile_w = 8; p.tile_h = kd3_waves(p.rays) * (p.rays / 8);
@@ -1122,23 +1036,13 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
     p.tile_order = c->tile_order;
     p.order = nullptr;
     p.split = 0;
-    p.coop = 0;
     p.debug = c->debug;
     p.pool_cap = c->pool_cap;
     p.items = c->items;
     p.dbg = nullptr;
-    p.started = nullptr;
-#if RT_ITER_STAMPS
-    p.istamp = nullptr;
-#endif
     if (c->debug & 2) {
-        // (fine tiles four times: a split tile adds a block, a coop tile three)
-        int64_t need = (4 * (int64_t)p.tiles_x * p.block_rows + p.coarse_blocks + p.fill_blocks) * 4 * 3;
-        c->istamp_off = need;
-#if RT_ITER_STAMPS
-        // debug bit 128: per-iteration stamps of every wave slot after the per-wave records
-        if (c->debug & 128) need += (need / 3) * 4 * kIterStamps;
-#endif
+        // (fine tiles twice: a split tile adds a block)
+        const int64_t need = (2 * (int64_t)p.tiles_x * p.block_rows + p.coarse_blocks + p.fill_blocks) * 4 * 3;
         if (c->dbg_cap < need) {
             dev_free(c->d_dbg);
             int rc = dev_alloc(&c->d_dbg, (size_t)need, "hipMalloc(dbg)");
@@ -1146,9 +1050,6 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
             c->dbg_cap = need;
         }
         p.dbg = c->d_dbg;
-#if RT_ITER_STAMPS
-        if (c->debug & 128) p.istamp = c->d_dbg + c->istamp_off;
-#endif
         int rc = hip_check(hipMemset(c->d_dbg, 0, sizeof(uint64_t) * (size_t)need), "memset dbg");
         if (rc) return rc;
     }
@@ -1617,7 +1518,6 @@ struct PersistArgs {
 
 static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32_t flags, const rt_tile* tile,
                          uint32_t* argb, int64_t* hit, void* stream, uint32_t* display = nullptr,
-                         unsigned long long* started = nullptr, int64_t* blocks = nullptr,
                          const PersistArgs* pf = nullptr, int32_t* rendered = nullptr) {
     if (rendered) *rendered = 1;
     if (!c) return fail(RT_ERR_INVALID, "rt_render: null camera");
@@ -1700,14 +1600,6 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
     // behind its upload; other streams wait for it above)
     p.split = (p.order && p.order == c->d_order && p.cost && (p.rays == 16 || (p.rays == 8 && RT_SPLIT8)) &&
                !(c->debug & 512)) ? c->order_split : 0;
-    p.coop = (p.order && p.order == c->d_order && p.cost && (p.rays == 16 || p.rays == 8) && !(c->debug & 2048))
-                 ? c->order_coop : 0;
-    if (p.coop && (flags & RT_FLAG_SHADOW)) {
-        // shadow walks have no coop form: the coop tiles render as split
-        // tiles (halves) there, ahead of the order's split tiles
-        if (!(c->debug & 512)) p.split += p.coop;
-        p.coop = 0;
-    }
     const bool order3 = p.cost != nullptr;
     // a multi-frame launch (KD kernel 3, fused far fill, no per-frame
     // outputs beyond the frame): one launch for pf->frames frames, no cost
@@ -1725,7 +1617,6 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
         p.pf_frames = (int32_t)std::max<int64_t>(1, std::min<int64_t>(pf->frames, max_blocks / std::max(1, p.pf_blocks)));
         p.pf_nbuf = pf->nbuf;
         p.pf_seq0 = pf->seq0 % pf->nbuf;
-        p.pf_group = std::max(1, std::min(p.pf_frames, c->frame_group > 0 ? c->frame_group : RT_PF_GROUP));
         for (int k = 0; k < RT_LOOP_MAX_BUF; k++) p.pf_argb[k] = k < pf->nbuf ? pf->argb[k] : nullptr;
         if (rendered) *rendered = p.pf_frames;
     }
@@ -1733,15 +1624,11 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
     if (sampled) {
         p.cost = c->d_cost_host;
         // the kernel writes this frame's costs into the pinned host buffer;
-        // slots a tile does not write (coop tiles, missing waves) read 0
+        // slots a tile does not write (missing waves) read 0
         memset(c->h_cost, 0, sizeof(uint32_t) * kCostSlots * (size_t)p.tiles_x * p.block_rows);
     } else {
         p.cost = nullptr;
     }
-    // kernel 3 counts its started blocks for rt_run_frames' dispatch gate
-    const bool kd3 = mode == RT_MODE_KD && effective_kernel(c) == 3;
-    p.started = kd3 ? started : nullptr;
-    if (blocks) *blocks = kd3 && started ? (int64_t)fine_grid_blocks(p) : 0;
     if ((rc = launch_split(c, p, mode, flags, stream))) return rc;
     if (p.order) {  // the streams that read the current order slot
         note_order_stream(c, st);
@@ -2082,7 +1969,6 @@ extern "C" void rt_camera_destroy(rt_camera* c) {
     }
     c->d_order = nullptr;
     dev_free(c->d_dbg);
-    dev_free(c->d_started);
     for (auto& k : c->flat_keys) dev_free(k.d);
     for (hipEvent_t e : c->slot_join_ev)
         if (e) (void)hipEventDestroy(e);
@@ -2109,12 +1995,15 @@ extern "C" int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value) {
     c->geom_gen++;  // cached launch geometry is stale
     switch (key) {
     case kOptKernel:
-        if (value < 1 || value > 3) return fail(RT_ERR_INVALID, "kernel version %d", value);
+        // kernel 1 (round 1's per-lane DFS over own-box records, 1.8 ms per
+        // 1080p frame) is gone; 2 is the reference-order per-lane DFS
+        if (value < 2 || value > 3) return fail(RT_ERR_INVALID, "kernel version %d (2, 3)", value);
         c->kernel_version = value;
         return RT_OK;
     case kOptRays:
-        if (value != 0 && value != 8 && value != 16 && value != 32 && value != 64)
-            return fail(RT_ERR_INVALID, "rays per wave %d (0 auto, 8, 16, 32, 64)", value);
+        // (64 rays per wave measured slower everywhere, r04u-w, and is gone)
+        if (value != 0 && value != 8 && value != 16 && value != 32)
+            return fail(RT_ERR_INVALID, "rays per wave %d (0 auto, 8, 16, 32)", value);
         c->rays = value;
         return RT_OK;
     case kOptItems:
@@ -2142,16 +2031,13 @@ extern "C" int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value) {
         c->tune_pending = false;
         return RT_OK;
     case kOptFlat:
-        if (value < 0 || value > 13) return fail(RT_ERR_INVALID, "flat kernel form %d (0..13)", value);
+        // forms 0-8, 10, 11, 13 of rounds 1-2 measured slower and are gone
+        if (value != 9 && value != 12) return fail(RT_ERR_INVALID, "flat kernel form %d (9 or 12)", value);
         c->flat_variant = value;
         return RT_OK;
     case kOptTileOrder:
         if (value < 0 || value > 4) return fail(RT_ERR_INVALID, "tile order %d (0..4)", value);
         c->tile_order = value;
-        return RT_OK;
-    case kOptFrameGroup:
-        if (value < 0 || value > 8) return fail(RT_ERR_INVALID, "frames per group %d (0 default, 1..8)", value);
-        c->frame_group = value;
         return RT_OK;
     default:
         return fail(RT_ERR_INVALID, "rt_camera_set_option: unknown key %d", key);
@@ -2169,10 +2055,7 @@ extern "C" int rt_camera_get_option(const rt_camera* c, int32_t key, int32_t* va
     case kOptFlat: *value = c->flat_variant; return RT_OK;
     case kOptRaysUsed: *value = c->last_rays; return RT_OK;
     case kOptDebug: *value = c->debug; return RT_OK;
-    case kOptStampOffset: *value = (int32_t)c->istamp_off; return RT_OK;
     case kOptSplitUsed: *value = c->order_split; return RT_OK;
-    case kOptCoopUsed: *value = c->order_coop; return RT_OK;
-    case kOptFrameGroup: *value = c->frame_group > 0 ? c->frame_group : RT_PF_GROUP; return RT_OK;
     case kOptShadowOrder: *value = c->shadow_order >= 0 ? c->shadow_order : c->any_best; return RT_OK;
     default: return fail(RT_ERR_INVALID, "rt_camera_get_option: unknown key %d", key);
     }
@@ -2216,14 +2099,6 @@ static int ensure_lanes(rt_camera* c, int L, bool comm) {
             return rc;
         if (!c->lane_ev[k] && (rc = hip_check(hipEventCreateWithFlags(&c->lane_ev[k], hipEventDisableTiming), "lane event")))
             return rc;
-    }
-    if (!c->d_started) {  // the dispatch gate's counters (rt_run_frames)
-        if ((rc = dev_alloc(&c->d_started, RT_LOOP_MAX_LANES, "hipMalloc(started)")) ||
-            (rc = hip_check(hipMemset(c->d_started, 0, sizeof(unsigned long long) * RT_LOOP_MAX_LANES), "memset started")) ||
-            (rc = hip_check(hipDeviceSynchronize(), "started init")))
-            return rc;
-        for (auto& v : c->started_cum) v = 0;
-        for (auto& v : c->started_last) v = 0;
     }
     return RT_OK;
 }
@@ -2269,7 +2144,7 @@ static int run_frames_multiframe(rt_camera* c, const rt_frame_loop* a, int32_t n
         const PersistArgs pf{chunk, (int32_t)((*seq) % a->nbuf), a->nbuf, a->d_local};
         const int k = (int)((*seq) % a->nbuf);
         int32_t done = 1;
-        rc = render_common(c, a->xform, a->mode, a->flags, tile, a->d_local[k], nullptr, rs, nullptr, nullptr, nullptr,
+        rc = render_common(c, a->xform, a->mode, a->flags, tile, a->d_local[k], nullptr, rs, nullptr,
                            chunk > 1 ? &pf : nullptr, &done);
         if (rc) break;
         if (time_it) {
@@ -2388,13 +2263,9 @@ extern "C" int rt_run_frames(rt_camera* c, rt_comm* comm, const rt_frame_loop* a
         c->nactive = L;
         for (int l = 0; l < L; l++) c->active[l] = lane[l];
     }
-    // The dispatch gate (k_gate): frame j > 0 of the call starts on its lane
-    // once every block of frame j - 1 (on the previous lane) has started, so
-    // the lanes never run in lockstep; KD frames of kernel 3 only (its blocks
-    // count themselves).  RT_TUNE_GATE=0 turns it off (A/B).
-    const int gate_pct = tune("RT_TUNE_GATE_PCT", RT_GATE_PCT);
-    const bool gated = L > 1 && a->mode == RT_MODE_KD && effective_kernel(c) == 3 && c->d_started &&
-                       tune("RT_TUNE_GATE", 1) != 0 && gate_pct > 0;
+    // (a dispatch gate holding a lane's frame until the other lane's had
+    // started a share of its blocks, and a sleep staggering the lanes,
+    // measured slower at every setting: round 4, r04e-r04h)
     const rt_tile* tile = a->tile.nranks > 0 ? &a->tile : nullptr;
     // rank 0 renders its bands straight into the frame it assembles (its
     // part of the frame is never copied); the gather places the peers' parts
@@ -2426,27 +2297,12 @@ extern "C" int rt_run_frames(rt_camera* c, rt_comm* comm, const rt_frame_loop* a
         if (linked && used[k] && hipEventQuery(sent[k]) != hipSuccess &&
             (rc = hip_check(hipStreamWaitEvent(ls, sent[k], 0), "render wait")))
             break;
-        const int ln = j % L;
-        if (gated && j > 0) {
-            // frame j - 1 (lane pl) has started gate_pct % of its blocks
-            const int pl = (j - 1) % L;
-            const unsigned long long prev = c->started_last[pl];
-            const unsigned long long target = c->started_cum[pl] - prev + (prev * (unsigned)gate_pct + 99) / 100;
-            rc = launch_gate(c->d_started + pl, target, 2000.0, ls);
-            if (rc) break;
-        }
         const bool timed = every > 0 && j % every == 0;
         const int64_t t = every > 0 ? j / every : 0;
         rc = timed ? hip_check(hipEventRecord(c->loop_ev[(size_t)(2 * t)], ls), "loop timing") : RT_OK;
         uint32_t* target = direct ? a->d_frame[k] : a->d_local[k];
-        int64_t blocks = 0;
         if (!rc)
-            rc = render_common(c, xf, a->mode, a->flags | (direct ? RT_FLAG_FRAME_OUT : 0u), tile, target, nullptr, ls,
-                               nullptr, gated ? c->d_started + ln : nullptr, &blocks);
-        if (!rc && gated) {
-            c->started_cum[ln] += (unsigned long long)blocks;
-            c->started_last[ln] = (unsigned long long)blocks;
-        }
+            rc = render_common(c, xf, a->mode, a->flags | (direct ? RT_FLAG_FRAME_OUT : 0u), tile, target, nullptr, ls);
         if (!rc && timed) rc = hip_check(hipEventRecord(c->loop_ev[(size_t)(2 * t + 1)], ls), "loop timing");
         if (!rc && comm) {
             if (linked) {

@@ -32,7 +32,7 @@ constexpr int kTileWFlat = 32;
 constexpr int kTileWKd = 16;
 constexpr int kBlockMax = 256;
 
-// Interior record (64 B) of the v2 KD layout: the two children's
+// Interior record (64 B) of the KD layout: the two children's
 // camera-relative boxes plus this node's split planes and child references.
 //   r0 = (L.t0x, L.t1x, L.t0y, L.t1y)   r1 = (L.t0z, L.t1z, R.t0x, R.t1x)
 //   r2 = (R.t0y, R.t1y, R.t0z, R.t1z)   r3 = (s1, s2, Lref | axis << 29, Rref)
@@ -41,27 +41,22 @@ constexpr uint32_t kAxisShift = 29;
 
 // rt_camera_set_option keys.
 enum Option : int32_t {
-    kOptKernel = 1,     // KD kernel version: 1 (node-own box, 48 B) or 2 (child boxes, 64 B)
+    kOptKernel = 1,     // KD kernel: 2 (per-lane DFS in the reference's order) or 3 (item pool, default)
     kOptTileOrder = 2,  // 0 XCD-contiguous, 1 natural, 2 centre-out, 3 by measured cost (kernel 3)
-    kOptRays = 3,       // kernel 3 pixels per wave: 64, 32, 16 or 8
+    kOptRays = 3,       // kernel 3 pixels per wave: 32, 16 or 8 (0 = auto)
     kOptItems = 4,      // kernel 3 items popped per lane per iteration: 1 or 2
     kOptCoarse = 5,     // kernel 3 coarse groups per wave outside the root box's rectangle (0 = off)
     kOptShadowOrder = 6,  // kernel 3 any-hit push order 0..3, -1 = timed choice (default)
-    kOptFlat = 7,       // flat-list kernel: 0 one triangle per iteration, 1 pairs, 2 packed pairs, 3 pipelined
+    kOptFlat = 7,       // flat-list kernel: 9 one pass, 12 the list in 16 chunks (default)
     kOptRaysUsed = 8,   // get only: pixels per wave of the last kernel-3 render
-    kOptSplitUsed = 9,  // get only: split tiles after the coop tiles of the current cost order (kernel 3)
-    kOptCoopUsed = 10,  // get only: coop tiles at the head of the current cost order (kernel 3)
-    kOptFrameGroup = 11,  // multi-frame launches: frames per interleaved group (0 = default)
+    kOptSplitUsed = 9,  // get only: split tiles at the head of the current cost order (kernel 3)
     kOptDebug = 100,    // diagnostics: 1 = skip traversal, 2 = per-wave timestamps, 4 = every group
                         // coarse, 8 = coarse kernel on a side stream beside the fine one,
                         // 16 = counted shadow walks stop at occluders (the timed walk's work),
-                        // 32 = counting renders stop after the root test, 128 = per-iteration
-                        // stamps (RT_ITER_STAMPS builds, with 2), 512 = no split tiles,
-                        // 1024 = no two-level iterations, 2048 = no coop tiles, 4096 = every
-                        // tile of a cost order a coop tile (tests), 8192 = coop tiles above
-                        // 60 % / 70 % of the heaviest tile (tests; off by default)
+                        // 32 = counting renders stop after the root test, 64 = order / cost
+                        // buffers sized for the current grid only, 256 = no held fine region,
+                        // 512 = no split tiles, 1024 = no two-level iterations
     kOptPoolCap = 101,  // tests: shrink kernel 3's item pool (66..kPoolCap) to force its fallback
-    kOptStampOffset = 102,  // get only: offset (u64) of the per-iteration stamps in the debug buffer
 };
 constexpr int kPoolCapMax = 640;
 
@@ -82,13 +77,8 @@ constexpr int kCostSlots = 8;
 // ---------------------------------------------------------------------------
 // Device layouts (all 16-byte aligned, read with dwordx4 loads).
 //
-// InteriorNode (48 B), camera-relative, one per interior node of the tree in
-// BFS order (init_cam_voxel_mem_cuda, TD/Camera.cu:137-162):
-//   a = (t0x, t1x, t0y, t1y)   d_Bo = h_bound - camera position
-//   b = (t0z, t1z, s1, s2)     split planes minus camera[axis]
-//   c = (left_ref, right_ref, axis, s1_eps_bits)
-//        s1_eps = (float)((double)s1 + 1e-16), used when the object
-//        translation is zero (TD/Trixel.cu:150 with ds == 0).
+// Interior records: above (kRefMask, kAxisShift), camera-relative, one per
+// interior node (init_cam_voxel_mem_cuda, TD/Camera.cu:137-162).
 //
 // TriRecord (64 B), camera-relative, one per triangle, indexed by
 // tri_list_index (init_tri_mem_cuda + init_cam_tri_mem_cuda,
@@ -136,13 +126,11 @@ struct TraceParams {
     int32_t far_rect[4];           // root box's screen rectangle + 2 px (x0, x1, y0, y1; frame pixels)
     int32_t far_all;               // every group background: the box lies behind the eye (box_behind)
     int32_t tile_w, tile_h;        // pixels per block (tile_h divides the 8-row band)
-    int32_t rays;                  // pixels (rays) per wave: 64, 32 or 16
+    int32_t rays;                  // pixels (rays) per wave: 32, 16 or 8
     int32_t tile_order;            // Option kOptTileOrder
     const int32_t* order;          // tile permutation (tile_order 2: centre-out, 3: by cost)
-    // kernel 3, tile order 3 (16- and 8-ray units): order[0..coop) render each
-    // unit with a whole block on one pool (4 blocks per tile), then
-    // order[coop..coop + split) as two halves (2 blocks per tile)
-    int32_t coop;
+    // kernel 3, tile order 3 (16- and 8-ray units): order[0..split) render as
+    // two halves (2 blocks per tile)
     int32_t split;
     uint32_t* cost;                // tile_order 3: pool iterations per fine unit [tile][kCostSlots], or null
     float root_box[6];             // camera-relative root AABB (t0x,t1x,t0y,t1y,t0z,t1z)
@@ -150,11 +138,10 @@ struct TraceParams {
     int32_t items;                 // kernel 3 items per lane per iteration (1 or 2)
     int32_t debug;                 // diagnostic builds only: 1 = skip traversal
     unsigned long long* dbg;       // per-wave (t_start, t_end, visits) when non-null
-    unsigned long long* started;   // kernel 3: count of started blocks (rt_run_frames' dispatch gate), or null
     // A multi-frame launch (kernel 3; pf_frames > 0): pf_frames frames of
-    // pf_blocks blocks each in one grid, in groups of pf_group frames whose
-    // blocks interleave; frame f writes pf_argb[(pf_seq0 + f) % pf_nbuf].
-    int32_t pf_frames, pf_blocks, pf_seq0, pf_nbuf, pf_group;
+    // pf_blocks blocks each in one grid, frame-major; frame f writes
+    // pf_argb[(pf_seq0 + f) % pf_nbuf].
+    int32_t pf_frames, pf_blocks, pf_seq0, pf_nbuf;
     uint32_t* pf_argb[RT_LOOP_MAX_BUF];
     uint32_t root_ref;
     uint32_t ntri;
@@ -163,25 +150,16 @@ struct TraceParams {
     // kernel 3's two-level iterations: the deepest node depth whose children
     // are interior records at positions 2i + 1, 2i + 2 (-1: off)
     int32_t two_depth;
-    int32_t flat_variant;          // Option kOptFlat: flat-list kernel form (0..12)
-    // chunked flat forms (10-12, non-counting renders): per-pixel (w bits, triangle)
-    // minima of the chunks, all ones between frames; and the chunk count
+    int32_t flat_variant;          // Option kOptFlat: flat-list kernel form (9 or 12)
+    // the chunked flat form (12, non-counting renders): per-pixel (w bits,
+    // triangle) minima of the chunks, all ones between frames; and the chunk count
     unsigned long long* flat_key;
     int32_t flat_chunks;
-#if RT_ITER_STAMPS
-    // diagnostic builds (-DRT_ITER_STAMPS=1, debug bit 128): per-iteration
-    // shader-clock stamps of kernel 3's pool walk, kIterStamps iterations per
-    // unit, 4 u64 each (tools/diag_iters.py)
-    unsigned long long* istamp;
-#endif
 };
-#if RT_ITER_STAMPS
-constexpr int kIterStamps = 96;
-#endif
 
-// Blocks of k_trace_kd3's grid (fine tiles, coop and split extras, far fill).
+// Blocks of k_trace_kd3's grid (fine tiles, split extras, far fill).
 inline unsigned fine_grid_blocks(const TraceParams& p) {
-    return (unsigned)(p.tiles_x * p.block_rows) + 3u * (unsigned)p.coop + (unsigned)p.split + (unsigned)p.fill_blocks;
+    return (unsigned)(p.tiles_x * p.block_rows) + (unsigned)p.split + (unsigned)p.fill_blocks;
 }
 
 }  // namespace rt
@@ -195,7 +173,7 @@ int launch_cam_tri(const float4* tri_world, uint32_t ntri, const float pos[3],
 int launch_pair_tri(const float4* trec, uint32_t ntri, float4* tpair, void* stream);
 int launch_cam_nodes(const rt_kd_node* nodes, const int32_t* interior_ids,
                      const uint32_t* node_ref, int64_t ninterior, const float pos[3],
-                     float4* inode, int version, void* stream);
+                     float4* inode, void* stream);
 // part: the coarse groups then the fine tiles (kPartAll), or one of them.
 enum LaunchPart : int { kPartAll = 0, kPartFine = 1, kPartCoarse = 2 };
 int launch_trace(const TraceParams& p, uint32_t mode, uint32_t flags, int kernel_version,
@@ -219,9 +197,6 @@ int launch_node_ref(const rt_kd_node* d_nodes, int64_t nnode, const int32_t* d_i
                     uint32_t* d_ref, void* stream);
 // rt_kd_build's input checks: tri indices a permutation of [0, n), no NaN bound.
 int validate_leafs(const rt_leaf_aabb* leafs, uint32_t n, const char* what);
-// rt_run_frames' dispatch gate: one wave on `stream` until *started >= target
-// (blocks of another lane's frames that have started) or timeout_us passed.
-int launch_gate(const unsigned long long* started, unsigned long long target, double timeout_us, void* stream);
 int launch_unpack(int32_t w, int32_t h, int32_t nranks, const uint32_t* gathered,
                   uint32_t* frame, void* stream);
 // Slots s of `rank` whose band rank + s*nranks lies in [b0, b1): [s0, s1).

@@ -26,32 +26,13 @@ int launch_cam_tri(const float4* tri_world, uint32_t ntri, const float pos[3], f
 }
 
 int launch_cam_nodes(const rt_kd_node* nodes, const int32_t* ids, const uint32_t* node_ref,
-                     int64_t ninterior, const float pos[3], float4* inode, int version, void* stream) {
+                     int64_t ninterior, const float pos[3], float4* inode, void* stream) {
     if (ninterior == 0) return RT_OK;
     k_cam_nodes<<<(unsigned)((ninterior + 255) / 256), 256, 0, (hipStream_t)stream>>>(
-        nodes, ids, node_ref, ninterior, pos[0], pos[1], pos[2], inode, version);
+        nodes, ids, node_ref, ninterior, pos[0], pos[1], pos[2], inode);
     return check_launch<void>("k_cam_nodes");
 }
 
-
-template <int V>
-TraceFn flat_kernel_v(bool wh, bool cnt) {
-    return wh ? (cnt ? k_trace_flat<true, true, V> : k_trace_flat<true, false, V>)
-              : (cnt ? k_trace_flat<false, true, V> : k_trace_flat<false, false, V>);
-}
-
-TraceFn flat_kernel(bool wh, bool cnt, int variant) {
-    if (variant == 0) return flat_kernel_v<0>(wh, cnt);
-    if (variant == 1) return flat_kernel_v<1>(wh, cnt);
-    if (variant == 2) return flat_kernel_v<2>(wh, cnt);
-    if (variant == 3) return flat_kernel_v<3>(wh, cnt);
-    if (variant == 4) return flat_kernel_v<4>(wh, cnt);
-    if (variant == 5) return flat_kernel_v<5>(wh, cnt);
-    if (variant == 6) return flat_kernel_v<6>(wh, cnt);
-    if (variant == 7) return flat_kernel_v<7>(wh, cnt);
-    if (variant == 8) return flat_kernel_v<8>(wh, cnt);
-    return flat_kernel_v<9>(wh, cnt);
-}
 
 int launch_pair_tri(const float4* trec, uint32_t ntri, float4* tpair, void* stream) {
     if (ntri == 0) return RT_OK;
@@ -68,16 +49,17 @@ int launch_trace(const TraceParams& p, uint32_t mode, uint32_t flags, int kernel
     const unsigned threads = (unsigned)((p.tile_w / 8) * (p.tile_h / (p.rays / 8)) * 64);
     if (mode == RT_MODE_FLAT) {
         if (fine == 0) return RT_OK;
-        if (p.flat_key && !cnt) {  // chunked forms: the chunks, then the shading
+        if (p.flat_key && !cnt) {  // the chunked form: the chunks, then the shading
             k_flat_chunk<<<fine * (unsigned)p.flat_chunks, threads, 0, s>>>(p);
             int rc = check_launch<void>("k_flat_chunk");
             if (rc) return rc;
             (wh ? k_flat_shade<true> : k_flat_shade<false>)<<<fine, threads, 0, s>>>(p);
             return check_launch<void>("k_flat_shade");
         }
-        // counting renders of the chunked forms take form 9 (the accept
-        // counter counts updates of the running minimum in index order)
-        TraceFn fn = flat_kernel(wh, cnt, p.flat_variant >= 10 ? 9 : p.flat_variant);
+        // one pass (form 9, and counting renders: the accept counter counts
+        // updates of the running minimum in index order)
+        TraceFn fn = wh ? (cnt ? k_trace_flat<true, true> : k_trace_flat<true, false>)
+                        : (cnt ? k_trace_flat<false, true> : k_trace_flat<false, false>);
         fn<<<fine, threads, 0, s>>>(p);
         return check_launch<void>("k_trace_flat");
     }
@@ -101,11 +83,6 @@ int launch_trace(const TraceParams& p, uint32_t mode, uint32_t flags, int kernel
         if (rc) return rc;
     }
     return RT_OK;
-}
-
-int launch_gate(const unsigned long long* started, unsigned long long target, double timeout_us, void* stream) {
-    k_gate<<<1, 64, 0, (hipStream_t)stream>>>(started, target, (uint64_t)(timeout_us * 100.0));  // 100 MHz counter
-    return check_launch<void>("k_gate");
 }
 
 int launch_unpack(int32_t w, int32_t h, int32_t nranks, const uint32_t* gathered, uint32_t* frame,

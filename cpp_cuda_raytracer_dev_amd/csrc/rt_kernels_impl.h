@@ -3,13 +3,15 @@
 // combination, by rt_kd_dispatch.hip, so the KD kernels' many template
 // instances compile in parallel translation units).
 //
-// One fused kernel per frame: primary ray -> object transform -> KD-tree DFS
-// (or the flat triangle list) -> Moller-Trumbore -> Phong -> u32 0x00RRGGBB.
-// One ray per lane; a block is a 32x8 pixel tile (four 8x8 wave64 tiles), so
-// a wave's rays are spatially coherent and walk the same upper tree.  The DFS
-// stack lives in LDS (per-lane columns of a [depth][256] array) with its top
-// entry in a register.  Blocks are remapped so each XCD's L2 serves a
-// contiguous band of screen tiles.
+// One fused kernel per frame: primary ray -> object transform -> KD-tree
+// traversal (or the flat triangle list) -> Moller-Trumbore -> Phong -> u32
+// 0x00RRGGBB.  The KD path's kernel is k_trace_kd3: a wave pools the (ray,
+// node) items of its 8/16/32 rays in an LDS stack and every lane visits any
+// ray's item, with ballot / mbcnt compaction of the pushed children and a
+// 64-bit LDS minimum of (w, DFS path code) for the reference's tie rule.
+// k_trace_kd2 is the per-lane DFS in the reference's visiting order (its
+// counters are the reference's, bench.py's counting frame).  Blocks take
+// screen tiles in a cost-ordered permutation the host keeps.
 //
 // Arithmetic follows the reference expression by expression (SURVEY.md §5
 // H1-H16): single precision with contraction off (-ffp-contract=off), the
@@ -98,13 +100,6 @@ __device__ __forceinline__ uint32_t phong(const float pnt[3], const float nrm[3]
     return (to_u8((pr / mx) * 255) << 16) | (to_u8((pg / mx) * 255) << 8) | to_u8((pb / mx) * 255);
 }
 
-// Block -> (tile_x, slot).  Order 0: blocks b and b+8 share an XCD, so give
-// each XCD a contiguous run of tiles (bijective for any grid size); order 1:
-// natural (neighbouring tiles on different XCDs); order 2: the host's
-// centre-out permutation, so the heavy centre tiles are dispatched first;
-// order 3: the host's permutation by the tiles' measured cost in an earlier
-// frame, heaviest first (centre-out until costs arrive); order 4: the same
-// per XCD over 8 screen regions of equal cost.
 // A pixel's frame write.  With P.display (rt_render_display) it also writes
 // the reference's displayed frame: the clean buffer argb still holds the
 // previous frame, which a miss keeps on screen (ghosting under motion: the
@@ -121,6 +116,13 @@ __device__ __forceinline__ void put_pixel(const TraceParams& P, int64_t out, uin
     base[out] = argb;
 }
 
+// Block -> tile.  Order 0: blocks b and b+8 share an XCD, so give each XCD a
+// contiguous run of tiles (bijective for any grid size); order 1: natural
+// (neighbouring tiles on different XCDs); order 2: the host's centre-out
+// permutation, so the heavy centre tiles are dispatched first; order 3: the
+// host's permutation by the tiles' measured cost in an earlier frame,
+// heaviest first (centre-out until costs arrive); order 4: the same per XCD
+// over 8 screen regions of equal cost.
 __device__ __forceinline__ int32_t tile_index(const TraceParams& P, int32_t b) {
     const int32_t nblocks = P.tiles_x * P.block_rows;
     if (P.tile_order == 0) {
@@ -246,152 +248,6 @@ __device__ __forceinline__ void wave_count_add(unsigned long long* dst, uint32_t
     if (v) atomicAdd(dst, (unsigned long long)v);
 }
 
-// ---------------------------------------------------------------- KD trace
-
-// intersect_voxel_cuda (TD/Trixel.cu:41-172) fused with set_cam_cuda +
-// color_cam_cuda (TD/Camera.cu:12-69).
-template <bool kTranslated, bool kWriteHit, bool kCount>
-__global__ __launch_bounds__(kTileWFlat * kTileH) void k_trace_kd(TraceParams P) {
-    constexpr int kBlock = kTileWFlat * kTileH;
-    __shared__ uint32_t stack[kMaxDepth * kBlock];
-    Pixel px;
-    const bool live = pixel_of_thread(P, px);
-    if (!live) return;  // no barriers in this kernel
-
-    float cam[3];
-    primary_ray(P, px.x, px.y, cam);
-    const float* X = P.xf;
-    // object transform of the ray, TD/Trixel.cu:60-66 (identity in every config)
-    const float odx = X[3], ody = X[7], odz = X[11];
-    const float rx = -1 * (X[0] * -cam[0] + X[1] * -cam[1] + X[2] * -cam[2]);
-    const float ry = -1 * (X[4] * -cam[0] + X[5] * -cam[1] + X[6] * -cam[2]);
-    const float rz = -1 * (X[8] * -cam[0] + X[9] * -cam[1] + X[10] * -cam[2]);
-    // per-ray invariants of the slab test (TD/Trixel.cu:76-95)
-    const float ix = 1 / rx, iy = 1 / ry, iz = 1 / rz;
-    const float ox = odx / rx, oy = ody / ry, oz = odz / rz;
-    const bool sx = rx > 0, sy = ry > 0, sz = rz > 0;
-    // dir and ds for each one-hot cut axis (TD/Trixel.cu:88-90)
-    const float dir_a[3] = {(rx * 1.0f) + (ry * 0.0f) + (rz * 0.0f),
-                            (rx * 0.0f) + (ry * 1.0f) + (rz * 0.0f),
-                            (rx * 0.0f) + (ry * 0.0f) + (rz * 1.0f)};
-    const float ds_a[3] = {(odx * 1.0f) + (ody * 0.0f) + (odz * 0.0f),
-                           (odx * 0.0f) + (ody * 1.0f) + (odz * 0.0f),
-                           (odx * 0.0f) + (ody * 0.0f) + (odz * 1.0f)};
-
-    float d = kDrawDistance;
-    uint32_t best = kMiss;
-    uint32_t n_int = 0, n_leaf = 0, n_acc = 0, n_desc = 0;
-    uint32_t* stk = stack + threadIdx.x;   // column of this lane: stk[k * kBlock]
-    int sp = 0;
-    uint32_t ref = P.root_ref;
-    for (;;) {
-        if (ref & kLeafBit) {
-            // Moller-Trumbore at a leaf, TD/Trixel.cu:98-145
-            const uint32_t t = ref & ~kLeafBit;
-            if (kCount) n_leaf++;
-            const float4 A = P.trec[4 * (size_t)t];
-            const float4 B = P.trec[4 * (size_t)t + 1];
-            const float4 Cq = P.trec[4 * (size_t)t + 2];
-            const float e1x = A.x, e1y = A.y, e1z = A.z;
-            const float e2x = A.w, e2y = B.x, e2z = B.y;
-            const float dtx = B.z, dty = B.w, dtz = Cq.x;
-            float qpx, qpy, qpz;
-            cross3(qpx, qpy, qpz, rx, ry, rz, e2x, e2y, e2z);
-            const float f = dot3(qpx, qpy, qpz, e1x, e1y, e1z);
-            if (!(f < kEpsF && f > -kEpsF)) {
-                const float pe1 = 1.0f / f;   // == (float)(1.0 / (double)f)
-                const float tx = dtx - odx, ty = dty - ody, tz = dtz - odz;
-                const float u = pe1 * dot3(qpx, qpy, qpz, tx, ty, tz);
-                float qx, qy, qz;
-                cross3(qx, qy, qz, tx, ty, tz, e1x, e1y, e1z);
-                const float v = pe1 * dot3(rx, ry, rz, qx, qy, qz);
-                const float w = pe1 * dot3(e2x, e2y, e2z, qx, qy, qz);
-                // (u+v) > 1 + 1e-16 is (u+v) > 1.0 in double
-                if ((w < d) && !((u < kEpsF) || (v < kEpsF) || ((u + v) > 1.0f) || (w < kEpsF))) {
-                    d = w;
-                    best = t;
-                    if (kCount) n_acc++;
-                }
-            }
-            if (sp == 0) break;
-            ref = stk[(--sp) * kBlock];
-            continue;
-        }
-        // interior node: slab test and split-plane child order, TD/Trixel.cu:76-95,146-168
-        if (kCount) n_int++;
-        const float4 a = P.inode[3 * (size_t)ref];
-        const float4 b = P.inode[3 * (size_t)ref + 1];
-        const uint4 c = reinterpret_cast<const uint4*>(P.inode)[3 * (size_t)ref + 2];
-        const float t0x = sx ? a.x * ix : a.y * ix;
-        const float t1x = sx ? a.y * ix : a.x * ix;
-        const float t0y = sy ? a.z * iy : a.w * iy;
-        const float t1y = sy ? a.w * iy : a.z * iy;
-        const float t0z = sz ? b.x * iz : b.y * iz;
-        const float t1z = sz ? b.y * iz : b.x * iz;
-        float maxt0 = fmaxf(t0z + oz, fmaxf(t0x + ox, t0y + oy));
-        float mint1 = fminf(t1z + oz, fminf(t1x + ox, t1y + oy));
-        if (pred::enter(maxt0, mint1)) {
-            if (kCount) n_desc++;
-            const uint32_t axis = c.z;
-            const float dir = axis == 0 ? dir_a[0] : axis == 1 ? dir_a[1] : dir_a[2];
-            maxt0 *= dir;
-            mint1 *= dir;
-            float s1, s2;
-            if (kTranslated) {
-                const float ds = axis == 0 ? ds_a[0] : axis == 1 ? ds_a[1] : ds_a[2];
-                s1 = (float)((double)b.z + kEps + (double)ds);
-                s2 = b.w + ds;
-            } else {
-                s1 = __uint_as_float(c.w);   // (float)((double)s1 + 1e-16), ds == 0
-                s2 = b.w;
-            }
-            const uint32_t L = c.x, R = c.y;
-            if (pred::lt_eps(maxt0, s2)) {
-                // pushes right (if) then left: left is popped first
-                if (pred::gt_eps(mint1, s2)) {
-                    if (sp >= P.max_depth) { atomicOr(P.err, 1); break; }
-                    stk[(sp++) * kBlock] = R;
-                }
-                ref = L;
-            } else {
-                // pushes left (if) then right: right is popped first
-                if (mint1 < s1 || maxt0 < s1) {
-                    if (sp >= P.max_depth) { atomicOr(P.err, 1); break; }
-                    stk[(sp++) * kBlock] = L;
-                }
-                ref = R;
-            }
-            continue;
-        }
-        if (sp == 0) break;
-        ref = stk[(--sp) * kBlock];
-    }
-
-    uint32_t argb = kBackground;
-    if (best != kMiss) {
-        // nearest-hit writes of TD/Trixel.cu:128-140, done once for the final hit
-        const float4 N = P.shade[2 * (size_t)best];
-        const float4 M = P.shade[2 * (size_t)best + 1];
-        const float pnt[3] = {d * rx + odx, d * ry + ody, d * rz + odz};
-        // norm.device_rotate(rot_m, i, -1), TD/vector.cuh:23-33
-        const float ax = -1 * N.x, ay = -1 * N.y, az = -1 * N.z;
-        const float nrm[3] = {(ax * X[0] + ay * X[1] + az * X[2]) * -1,
-                              (ax * X[4] + ay * X[5] + az * X[6]) * -1,
-                              (ax * X[8] + ay * X[9] + az * X[10]) * -1};
-        const float rad[3] = {M.x, M.y, M.z};
-        argb = phong(pnt, nrm, cam, rad);
-    }
-    put_pixel(P, px.out, argb, best != kMiss);
-    if (kWriteHit) P.hit[px.out] = best == kMiss ? (int64_t)-1 : (int64_t)best;
-    if (kCount) {
-        wave_count_add(&P.counters[0], n_int);
-        wave_count_add(&P.counters[1], n_leaf);
-        wave_count_add(&P.counters[2], n_acc);
-        wave_count_add(&P.counters[3], best != kMiss ? 1u : 0u);
-        wave_count_add(&P.counters[4], n_desc);
-    }
-}
-
 // ------------------------------------------------------------- KD trace v2
 
 // Issues the four dwordx4 loads of a 64-B record together and consumes them
@@ -416,34 +272,7 @@ struct Ray {
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 
-// Measured slower: knot 1080p 9.98k -> 9.32k FPS, fill 1080p 765 -> 834 us
-// (r03f); the packed operands cost more register moves than the six
-// multiplies and adds per box they save.
-#ifndef RT_PK_SLAB
-#define RT_PK_SLAB 0
-#endif
-// The leaf test and the child ordering without exec-mask branches: the
-// pool loop's SALU exec bookkeeping is a third of its instructions (knot
-// 1080p 9.98k -> 10.12k FPS, fill 765 -> 759 us, r03f; 78 VGPRs).
-#ifndef RT_BRANCHLESS
-#define RT_BRANCHLESS 1
-#endif
-// Walks whose rays have no object offset and no zero component skip the
-// slab tests' od/r additions (slab_vals<true>); 0: never.
-#ifndef RT_NO_OFF
-#define RT_NO_OFF 1
-#endif
-// RT_PK_NOOFF 1: the offset-free slab's products as v_pk_mul_f32 pairs:
-// solo frames 1-2 % shorter, but two frames in flight 1.5-2 % slower (knot
-// 1080p 10.56k -> 10.40k FPS, fill 1,373 -> 1,343, r03y); off.
-#ifndef RT_PK_NOOFF
-#define RT_PK_NOOFF 0
-#endif
-
 // Slab parameters of one node, TD/Trixel.cu:76-95: entry maxt0, exit mint1.
-// RT_PK_SLAB: each axis's (lo, hi) pair as packed float2 (v_pk_mul_f32 /
-// v_pk_add_f32 round each half as the scalar operation does), the near/far
-// swap by the ray's sign between the multiply and the add.
 // kNoOff: the walk's rays have no object offset and no zero component, so
 // every od/r term is a signed zero (0/r, r != 0): adding it changes at most
 // the sign of a zero t, which no comparison downstream tells apart (entry
@@ -453,33 +282,12 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 template <bool kNoOff = false>
 __device__ __forceinline__ void slab_vals(const Ray& R, float lx, float hx, float ly, float hy, float lz,
                                           float hz, float& maxt0, float& mint1) {
-    if (RT_PK_SLAB) {
-        const f2v px = f2v{lx, hx} * f2v{R.ix, R.ix};
-        const f2v py = f2v{ly, hy} * f2v{R.iy, R.iy};
-        const f2v pz = f2v{lz, hz} * f2v{R.iz, R.iz};
-        const f2v ax = (R.sx ? px : px.yx) + f2v{R.ox, R.ox};   // (t0x + ox, t1x + ox)
-        const f2v ay = (R.sy ? py : py.yx) + f2v{R.oy, R.oy};
-        const f2v az = (R.sz ? pz : pz.yx) + f2v{R.oz, R.oz};
-        maxt0 = fmaxf(az.x, fmaxf(ax.x, ay.x));
-        mint1 = fminf(az.y, fminf(ax.y, ay.y));
-        return;
-    }
     const float t0x = R.sx ? lx * R.ix : hx * R.ix;
     const float t1x = R.sx ? hx * R.ix : lx * R.ix;
     const float t0y = R.sy ? ly * R.iy : hy * R.iy;
     const float t1y = R.sy ? hy * R.iy : ly * R.iy;
     const float t0z = R.sz ? lz * R.iz : hz * R.iz;
     const float t1z = R.sz ? hz * R.iz : lz * R.iz;
-    if (kNoOff && RT_PK_NOOFF) {
-        // each axis's (lo, hi) products as one v_pk_mul_f32 (each half
-        // rounds as the scalar multiply does), then the sign's selection
-        const f2v px = f2v{lx, hx} * f2v{R.ix, R.ix};
-        const f2v py = f2v{ly, hy} * f2v{R.iy, R.iy};
-        const f2v pz = f2v{lz, hz} * f2v{R.iz, R.iz};
-        maxt0 = fmaxf(R.sz ? pz.x : pz.y, fmaxf(R.sx ? px.x : px.y, R.sy ? py.x : py.y));
-        mint1 = fminf(R.sz ? pz.y : pz.x, fminf(R.sx ? px.y : px.x, R.sy ? py.y : py.x));
-        return;
-    }
     if (kNoOff) {
         maxt0 = fmaxf(t0z, fmaxf(t0x, t0y));
         mint1 = fminf(t1z, fminf(t1x, t1y));
@@ -529,6 +337,8 @@ __device__ __forceinline__ bool leaf_test_rec(const Ray& R, const float4 A, cons
 // so cross(t, e1) is the record's d_q and dot(e2, cross(t, e1)) its d_w,
 // both computed by k_cam_tri with the same float operations (products
 // commute exactly): 14 fewer VALU operations per leaf visit, the same bits.
+// Every lane evaluates the whole test and selects (no exec-mask branches;
+// the 1/f of a rejected f is never used).
 __device__ __forceinline__ bool leaf_test_cam(const Ray& R, const float4 A, const float4 B, const float4 Cq,
                                               const float4 Dq, uint32_t t, float& d, uint32_t& best) {
     const float e1x = A.x, e1y = A.y, e1z = A.z;
@@ -537,31 +347,15 @@ __device__ __forceinline__ bool leaf_test_cam(const Ray& R, const float4 A, cons
     float qpx, qpy, qpz;
     cross3(qpx, qpy, qpz, R.rx, R.ry, R.rz, e2x, e2y, e2z);
     const float f = dot3(qpx, qpy, qpz, e1x, e1y, e1z);
-    if (RT_BRANCHLESS) {
-        // every lane evaluates the whole test (no exec-mask branches; 1/f of
-        // a rejected f is never used), then selects
-        const float pe1 = 1.0f / f;
-        const float u = pe1 * dot3(qpx, qpy, qpz, tx, ty, tz);
-        const float v = pe1 * dot3(R.rx, R.ry, R.rz, Cq.y, Cq.z, Cq.w);
-        const float w = pe1 * Dq.x;
-        const bool acc = !(f < kEpsF && f > -kEpsF) & (w < d) &
-                         !((u < kEpsF) | (v < kEpsF) | ((u + v) > 1.0f) | (w < kEpsF));
-        d = acc ? w : d;
-        best = acc ? t : best;
-        return acc;
-    }
-    if (!(f < kEpsF && f > -kEpsF)) {
-        const float pe1 = 1.0f / f;   // == (float)(1.0 / (double)f)
-        const float u = pe1 * dot3(qpx, qpy, qpz, tx, ty, tz);
-        const float v = pe1 * dot3(R.rx, R.ry, R.rz, Cq.y, Cq.z, Cq.w);
-        const float w = pe1 * Dq.x;
-        if ((w < d) && !((u < kEpsF) || (v < kEpsF) || ((u + v) > 1.0f) || (w < kEpsF))) {
-            d = w;
-            best = t;
-            return true;
-        }
-    }
-    return false;
+    const float pe1 = 1.0f / f;   // == (float)(1.0 / (double)f)
+    const float u = pe1 * dot3(qpx, qpy, qpz, tx, ty, tz);
+    const float v = pe1 * dot3(R.rx, R.ry, R.rz, Cq.y, Cq.z, Cq.w);
+    const float w = pe1 * Dq.x;
+    const bool acc = !(f < kEpsF && f > -kEpsF) & (w < d) &
+                     !((u < kEpsF) | (v < kEpsF) | ((u + v) > 1.0f) | (w < kEpsF));
+    d = acc ? w : d;
+    best = acc ? t : best;
+    return acc;
 }
 
 __device__ __forceinline__ bool leaf_test(const Ray& R, const float4* __restrict__ trec, uint32_t t,
@@ -746,28 +540,12 @@ constexpr int kPoolCap = kPoolCapMax;
 constexpr int kCodeBits = kMaxDepth;       // left-aligned code width in the key
 constexpr uint32_t kCodeMarkMask = (1u << 26) - 1;
 
-// Both records of an iteration are issued before either is consumed.  1
-// (default): a scheduling barrier after the loads, so item 0 waits only for
-// its own record (vmcnt counts loads in order) while item 1's is still in
-// flight; 0 (rounds 1-2): an empty asm reading all 32 registers, which also
-// made the wave wait for both records before visiting item 0.  Measured, two
-// frames in flight: dragon 1080p 14.6k -> 15.3k FPS (solo 86.7 -> 82.2 us),
-// 960x540 30.4k -> 32.7k, the 1080p fill view 868 -> 829 us, happy 4K with
-// shadow rays 464 -> 436 us.
-#ifndef RT_FENCE_MODE
-#define RT_FENCE_MODE 1
-#endif
-#if RT_FENCE_MODE == 0
-#define RT_RECORD_FENCE(a0, a1, a2, a3, b0, b1, b2, b3)                                                              \
-    do {                                                                                                            \
-        asm volatile("" ::"v"(a0.x), "v"(a0.y), "v"(a0.z), "v"(a0.w), "v"(a1.x), "v"(a1.y), "v"(a1.z), "v"(a1.w),  \
-                     "v"(a2.x), "v"(a2.y), "v"(a2.z), "v"(a2.w), "v"(a3.x), "v"(a3.y), "v"(a3.z), "v"(a3.w));      \
-        asm volatile("" ::"v"(b0.x), "v"(b0.y), "v"(b0.z), "v"(b0.w), "v"(b1.x), "v"(b1.y), "v"(b1.z), "v"(b1.w),  \
-                     "v"(b2.x), "v"(b2.y), "v"(b2.z), "v"(b2.w), "v"(b3.x), "v"(b3.y), "v"(b3.z), "v"(b3.w));      \
-    } while (0)
-#else
-#define RT_RECORD_FENCE(a0, a1, a2, a3, b0, b1, b2, b3) __builtin_amdgcn_sched_barrier(0)
-#endif
+// Both records of an iteration are issued before either is consumed, and a
+// scheduling barrier after the loads lets item 0 wait only for its own record
+// (vmcnt counts loads in order) while item 1's is still in flight (round 2:
+// an empty asm reading all 32 registers made the wave wait for both; dragon
+// 1080p 14.6k -> 15.3k FPS, solo 86.7 -> 82.2 us).
+#define RT_RECORD_FENCE() __builtin_amdgcn_sched_barrier(0)
 
 struct Item {
     uint32_t ref;      // node ref (kLeafBit | tri, or interior index)
@@ -798,7 +576,7 @@ __device__ __forceinline__ uint32_t code_key(uint32_t marked) {
 #endif
 template <int kRays>
 constexpr int pool_cap_for() {
-    return kRays == 64 ? kPoolCap : kRays == 32 ? RT_POOL_CAP_R32 : kRays == 16 ? RT_POOL_CAP_R16 : RT_POOL_CAP_R8;
+    return kRays == 32 ? RT_POOL_CAP_R32 : kRays == 16 ? RT_POOL_CAP_R16 : RT_POOL_CAP_R8;
 }
 
 // Per-ray data of the pool walk in LDS: rd[0] = (rx, ry, rz, 1/rx),
@@ -821,12 +599,6 @@ constexpr int pool_cap_for() {
 //   f4 (odz/rz, dir axis 0)  f5 (dir axis 1, dir axis 2)
 //   translated / shadow walks add f6 (odx, ody)  f7 (odz, ds axis 0)
 //   f8 (ds axis 1, ds axis 2)  f9 (Lmax, hit triangle)
-// RT_RAY_HOIST 1: an item's ray fields are read once before the leaf /
-// interior branch (no faster on gfx950, and it spilled 3 VGPRs of the 16-ray
-// instance); 0 (default): each path reads its own.
-#ifndef RT_RAY_HOIST
-#define RT_RAY_HOIST 0
-#endif
 // The 32-ray instance (multi-frame launches of small frames, auto_rays)
 // spaces its fields 48 float2s apart, so that two fields of one ray read
 // together do not share banks: C3 65.6-65.7k -> 66.9-67.0k FPS, knot
@@ -964,20 +736,11 @@ __device__ __forceinline__ void visit_leaf(const Ray& Q, float4 q4, uint4 it, fl
     uint32_t best = kMiss;
     const bool acc = kTranslated ? leaf_test_rec(Q, r0, r1, r2, it.x & ~kLeafBit, d, best)
                                  : leaf_test_cam(Q, r0, r1, r2, r3, it.x & ~kLeafBit, d, best);
-    if (RT_BRANCHLESS) {
-        const bool c = acc && (!kAny || best != __float_as_uint(q4.w));
-        o.cand = c;
-        o.ctri = best;
-        o.key = kAny ? 0ull : ((unsigned long long)__float_as_uint(d) << 32) | code_key(it.w & kCodeMarkMask);
-        if (kCount) n_acc += c ? 1u : 0u;
-        return;
-    }
-    if (acc && (!kAny || best != __float_as_uint(q4.w))) {
-        o.cand = true;
-        o.ctri = best;
-        o.key = kAny ? 0ull : ((unsigned long long)__float_as_uint(d) << 32) | code_key(it.w & kCodeMarkMask);
-        if (kCount) n_acc++;
-    }
+    const bool c = acc && (!kAny || best != __float_as_uint(q4.w));
+    o.cand = c;
+    o.ctri = best;
+    o.key = kAny ? 0ull : ((unsigned long long)__float_as_uint(d) << 32) | code_key(it.w & kCodeMarkMask);
+    if (kCount) n_acc += c ? 1u : 0u;
 }
 
 // The outcome of an interior node's child ordering (TD/Trixel.cu:146-170):
@@ -1010,9 +773,7 @@ __device__ __forceinline__ void order_node(float4 q2, float4 q3, float4 q4, floa
     const uint32_t L = lw & ~(3u << kAxisShift), Rr = __float_as_uint(r3.w);
     const float dir = axis == 0 ? q2.y : axis == 1 ? q2.z : q2.w;
     const float mx = t0 * dir, mn = t1 * dir;
-    // The reference's double-promoted epsilon tests (TD/Trixel.cu:146-157);
-    // with -DRT_GUARDED_PRED single float compares when every guard of the
-    // visit holds (rt_predicates.h, checked on edge sets), else these.
+    // The reference's double-promoted epsilon tests (TD/Trixel.cu:146-157).
     float s1, s2;
     bool left_first, push_second, lpass, rpass;
     if (kTranslated) {
@@ -1022,33 +783,15 @@ __device__ __forceinline__ void order_node(float4 q2, float4 q3, float4 q4, floa
     } else {
         s2 = r3.y;
     }
-#ifndef RT_GUARDED_PRED
-    // The guarded float forms (-DRT_GUARDED_PRED) measured slower on gfx950:
-    // 94 vs 86.5 us per 1080p dragon frame, the guards and the branch cost
-    // more than the double arithmetic they skip.  The double forms stand.
-    const bool guarded = false;
-#else
-    const bool guarded = !kTranslated && pred::split_safe(r3.x) && pred::split_safe(s2) && mx != s2 && mn != s2 &&
-                         pred::entry_safe(lt0) && pred::entry_safe(rt0);
-#endif
-    if (guarded) {
-        s1 = r3.x;
-        left_first = pred::lt_eps_f(mx, s2);
-        push_second = left_first ? pred::gt_eps_f(mn, s2) : (mn < s1 || mx < s1);
-        lpass = pred::enter_f(lt0, lt1);
-        rpass = pred::enter_f(rt0, rt1);
-    } else {
-        if (!kTranslated) s1 = pred::add_eps_ref(r3.x);
-        left_first = pred::lt_eps_ref(mx, s2);
-        if (RT_BRANCHLESS) {
-            const bool pa = pred::gt_eps_ref(mn, s2), pb = (mn < s1) | (mx < s1);
-            push_second = (left_first & pa) | (!left_first & pb);
-        } else {
-            push_second = left_first ? pred::gt_eps_ref(mn, s2) : (mn < s1 || mx < s1);
-        }
-        lpass = pred::enter_ref(lt0, lt1);
-        rpass = pred::enter_ref(rt0, rt1);
-    }
+    // (guarded single-float forms of these, rt_predicates.h, measured slower
+    // in round 2: 94 vs 86.5 us per 1080p dragon frame)
+    if (!kTranslated) s1 = pred::add_eps_ref(r3.x);
+    left_first = pred::lt_eps_ref(mx, s2);
+    // every term computed, then selected (no exec-mask branches)
+    const bool pa = pred::gt_eps_ref(mn, s2), pb = (mn < s1) | (mx < s1);
+    push_second = (left_first & pa) | (!left_first & pb);
+    lpass = pred::enter_ref(lt0, lt1);
+    rpass = pred::enter_ref(rt0, rt1);
     const uint32_t first = left_first ? L : Rr;
     const uint32_t second = left_first ? Rr : L;
     const bool first_leaf = (first & kLeafBit) != 0, second_leaf = (second & kLeafBit) != 0;
@@ -1096,11 +839,9 @@ __device__ __forceinline__ void visit_item(const float2* rd, uint4 it, float4 r0
                                            uint32_t& n_desc) {
     Ray Q;
     float4 q2, q3, q4;
-    if (RT_RAY_HOIST) {
-        ray_of<kTranslated, kStride>(rd, Q, q2, q3, q4);
-        if (it.x & kLeafBit) visit_leaf<kTranslated, kCount, kAny>(Q, q4, it, r0, r1, r2, r3, o, n_leaf, n_acc);
-        else visit_interior<kTranslated, kCount, kNoOff>(Q, q2, q3, q4, it, r0, r1, r2, r3, o, n_int, n_desc);
-    } else if (it.x & kLeafBit) {
+    // each path reads its own ray fields (read once before the branch, they
+    // spilled 3 VGPRs of the 16-ray instance, no faster)
+    if (it.x & kLeafBit) {
         ray_of<kTranslated, kStride>(rd, Q, q2, q3, q4);
         visit_leaf<kTranslated, kCount, kAny>(Q, q4, it, r0, r1, r2, r3, o, n_leaf, n_acc);
     } else {
@@ -1112,47 +853,6 @@ __device__ __forceinline__ void visit_item(const float2* rd, uint4 it, float4 r0
 __device__ __forceinline__ uint32_t lanes_below(unsigned long long b) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
 }
-
-// Nearest-candidate / any-hit bookkeeping of two visited items.
-template <bool kAny>
-__device__ __forceinline__ void record_candidates(unsigned long long* s_key, uint32_t* s_tri, const uint4& it0,
-                                                  const uint4& it1, const Visit& v0, const Visit& v1) {
-    const uint32_t ray0 = it0.w >> 26, ray1 = it1.w >> 26;
-    if (kAny) {
-        if (v0.cand) s_key[ray0] = 0ull;
-        if (v1.cand) s_key[ray1] = 0ull;
-    } else {
-        // nearest candidate per ray: 64-bit min of (w, path code), then the
-        // unique item holding the minimum records its triangle
-        if (v0.cand) atomicMin(&s_key[ray0], v0.key);
-        if (v1.cand) atomicMin(&s_key[ray1], v1.key);
-        __builtin_amdgcn_wave_barrier();
-        if (v0.cand && s_key[ray0] == v0.key) s_tri[ray0] = v0.ctri;
-        if (v1.cand && s_key[ray1] == v1.key) s_tri[ray1] = v1.ctri;
-    }
-}
-
-#ifndef RT_SEQ_PUSH
-#define RT_SEQ_PUSH 1
-#endif
-#ifndef RT_MAX_ITEMS
-#define RT_MAX_ITEMS 2
-#endif
-#ifndef RT_NEAREST_ORDER
-#define RT_NEAREST_ORDER 0
-#endif
-#ifndef RT_SKIP_SLOT1
-#define RT_SKIP_SLOT1 1
-#endif
-#ifndef RT_PRIO_HEAVY
-#define RT_PRIO_HEAVY 0
-#endif
-// RT_LEAF_FIRST 1 pushes leaf children below interior ones (fewer mixed
-// slots): measured slower for primary rays (dragon 1080p 15.3k -> 14.0k FPS,
-// fill 825 -> 927 us), faster only for happy 4K shadows (436 -> 420 us).
-#ifndef RT_LEAF_FIRST
-#define RT_LEAF_FIRST 0
-#endif
 
 // One visited item's candidate: any-hit marks the ray; nearest-hit takes the
 // 64-bit min of (w, path code) and the unique holder of the minimum records
@@ -1185,7 +885,7 @@ template <bool kAny, int any_order>
 __device__ __forceinline__ int push_children(uint4* items, int at, const Visit& v) {
     const unsigned long long m1 = __ballot(v.ka), m2 = __ballot(v.kb);
     const int n1 = __builtin_popcountll(m1), n2 = __builtin_popcountll(m2);
-    constexpr int ord = kAny ? any_order : RT_NEAREST_ORDER;
+    constexpr int ord = kAny ? any_order : 0;
     if (ord & 1) {   // per-lane pairs
         const int off = (int)(lanes_below(m1) + lanes_below(m2));
         if (ord == 1) {
@@ -1198,18 +898,6 @@ __device__ __forceinline__ int push_children(uint4* items, int at, const Visit& 
     } else if (ord == 2) {
         if (v.kb) items[at + (int)lanes_below(m2)] = v.cb;
         if (v.ka) items[at + n2 + (int)lanes_below(m1)] = v.ca;
-    } else if (RT_LEAF_FIRST) {
-        // leaf children below interior ones: the next pops take interior
-        // items from the top, so a 64-item slot rarely holds both kinds
-        // (a mixed slot runs the leaf and the interior code under divergence)
-        const bool la = v.ka && (v.ca.x & kLeafBit) != 0, lb = v.kb && (v.cb.x & kLeafBit) != 0;
-        const bool ia = v.ka && !la, ib = v.kb && !lb;
-        const unsigned long long l1 = __ballot(la), l2 = __ballot(lb), i1 = __ballot(ia), i2 = __ballot(ib);
-        const int nl1 = __builtin_popcountll(l1), nl2 = __builtin_popcountll(l2), ni1 = __builtin_popcountll(i1);
-        if (la) items[at + (int)lanes_below(l1)] = v.ca;
-        if (lb) items[at + nl1 + (int)lanes_below(l2)] = v.cb;
-        if (ia) items[at + nl1 + nl2 + (int)lanes_below(i1)] = v.ca;
-        if (ib) items[at + nl1 + nl2 + ni1 + (int)lanes_below(i2)] = v.cb;
     } else {
         if (v.ka) items[at + (int)lanes_below(m1)] = v.ca;
         if (v.kb) items[at + n1 + (int)lanes_below(m2)] = v.cb;
@@ -1217,7 +905,7 @@ __device__ __forceinline__ int push_children(uint4* items, int at, const Visit& 
     return n1 + n2;
 }
 
-// Two-level pool iterations (RT_TWO_LEVEL, default on; debug bit 1024 or a
+// Two-level pool iterations (default on; debug bit 1024 or a
 // non-BFS record order turns them off).  A wave's chain of pool iterations is
 // at least the tree's depth, and most iterations pop small pools (24 items on
 // average, r03 stamps), so most lanes idle.  When the pool holds at most 16
@@ -1232,9 +920,6 @@ __device__ __forceinline__ int push_children(uint4* items, int at, const Visit& 
 // push the grandchildren.  So two tree levels of a small pool take one
 // iteration of about one level's instructions.  The visited (ray, node) items
 // are the reference's, as with any pop order, and so are the counters.
-#ifndef RT_TWO_LEVEL
-#define RT_TWO_LEVEL 1
-#endif
 #ifndef RT_TWO_MAX
 #define RT_TWO_MAX 16
 #endif
@@ -1326,20 +1011,11 @@ template <int kCap, int kStride, bool kTranslated, bool kCount, bool kAny, int k
 __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, const float2* s_ray,
                                           unsigned long long* s_key, uint32_t* s_tri, int n, int lane,
                                           uint32_t& iters, uint32_t& popped, uint32_t& n_int, uint32_t& n_leaf,
-                                          uint32_t& n_acc,
-                                          uint32_t& n_desc, unsigned long long* st = nullptr) {
+                                          uint32_t& n_acc, uint32_t& n_desc) {
     const int cap = min(P.pool_cap, kCap);
-#if RT_ITER_STAMPS
-    // diagnostics: the stamps read a value of each phase (readfirstlane), so
-    // they wait for it; the walk is slower with them, the split is the point
-#define RT_STAMP(v) (__builtin_amdgcn_sched_barrier(0), (void)__builtin_amdgcn_readfirstlane(v), \
-                     __builtin_amdgcn_s_memtime())
-#endif
     const int slack = P.tree_height + 1;
-    constexpr bool kTwo = RT_MAX_ITEMS > 1;  // compile-time: one-item builds drop item 1's registers
-    const int per = kTwo && P.items > 1 ? 128 : 64;
+    const int per = P.items > 1 ? 128 : 64;
     while (n > 0) {
-#if RT_TWO_LEVEL
         // a pool of at most RT_TWO_MAX items (and room for 4 children each
         // plus the DFS slack): one two-level iteration over all of it.
         // Nearest-hit walks only: an any-hit (shadow) walk stops a ray at its
@@ -1353,7 +1029,6 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
             __builtin_amdgcn_wave_barrier();
             continue;
         }
-#endif
         // Pop as many items as the pool has room for the children of plus
         // the DFS slack below; a single (DFS-like) pop when there is none.
         // Popping k items pushes at most 2k, so a parallel pop leaves
@@ -1362,10 +1037,6 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
         // (slack = height + 1, height <= 24), so the pool never overflows.
         int take = min(min(n, per), cap - slack - n);
         if (take < 1) take = 1;
-#if RT_ITER_STAMPS
-        const unsigned long long s0 = st ? __builtin_amdgcn_s_memtime() : 0ull;
-        const uint32_t it_no = iters;
-#endif
         iters++;
         popped += (uint32_t)take;
         const int base = n - take;
@@ -1373,9 +1044,9 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
         // re-read item `base`, a live item, whose record is a valid address):
         // with guarded loads hipcc zero-fills the registers of the idle path
         // and waits for the first record before issuing the second.
-        bool act0 = lane < take, act1 = kTwo && lane + 64 < take;
+        bool act0 = lane < take, act1 = lane + 64 < take;
         const uint4 it0 = items[base + (act0 ? lane : 0)];
-        const uint4 it1 = kTwo ? items[base + (act1 ? lane + 64 : 0)] : it0;
+        const uint4 it1 = items[base + (act1 ? lane + 64 : 0)];
         __builtin_amdgcn_wave_barrier();
         // any-hit: a ray already shadowed needs no more visits (kept when
         // counting, so the counters match the oracle's full walk, unless
@@ -1385,19 +1056,11 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
             if (act1 && s_key[it1.w >> 26] == 0ull) act1 = false;
         }
         // both records in flight before either is consumed
-#if RT_ITER_STAMPS
-        const unsigned long long s1 = st ? RT_STAMP(it0.x ^ it1.x) : 0ull;
-#endif
         const float4* p0 = record_of(P, it0.x);
         const float4* p1 = record_of(P, it1.x);
         const float4 a0 = p0[0], a1 = p0[1], a2 = p0[2], a3 = p0[3];
-        const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        const float4 b0 = kTwo ? p1[0] : z, b1 = kTwo ? p1[1] : z, b2 = kTwo ? p1[2] : z, b3 = kTwo ? p1[3] : z;
-        RT_RECORD_FENCE(a0, a1, a2, a3, b0, b1, b2, b3);
-#if RT_ITER_STAMPS
-        const unsigned long long s2 = st ? RT_STAMP(__float_as_uint(a3.w) ^ __float_as_uint(b3.w)) : 0ull;
-#endif
-#if RT_SEQ_PUSH
+        const float4 b0 = p1[0], b1 = p1[1], b2 = p1[2], b3 = p1[3];
+        RT_RECORD_FENCE();
         // item 0 is visited, recorded and pushed before item 1 is visited, so
         // its results die before item 1's are made (fewer live VGPRs)
         int total = 0;
@@ -1410,13 +1073,10 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
             record_candidate<kAny>(s_key, s_tri, it0, v0);
             total += push_children<kAny, (kOrder & 3)>(items, base + total, v0);
         }
-#if RT_ITER_STAMPS
-        const unsigned long long s3 = st ? RT_STAMP(total) : 0ull;
-#endif
         // take is wave-uniform: a pop of at most 64 items leaves slot 1 empty
         // on every lane, and skipping its bookkeeping (candidate, ballots,
         // push) outright saves ~300 cycles of such an iteration
-        if (!RT_SKIP_SLOT1 || take > 64) {
+        if (take > 64) {
             Visit v1;
             v1.ka = v1.kb = false; v1.cand = false;
             if (act1)
@@ -1429,170 +1089,7 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
             if (lane == 0) atomicOr(P.err, 2);
             break;
         }
-#if RT_ITER_STAMPS
-        if (st && lane == 0 && it_no < (uint32_t)kIterStamps) {
-            const unsigned long long s4 = RT_STAMP(total);
-            unsigned long long* q = st + 4 * (size_t)it_no;
-            q[0] = s0;
-            q[1] = (s1 - s0) | ((s2 - s1) << 32);
-            q[2] = (s3 - s2) | ((s4 - s3) << 32);
-            q[3] = (unsigned long long)(uint32_t)take | ((unsigned long long)(uint32_t)n << 32);
-        }
-#endif
-#else
-        Visit v0, v1;  // children / key fields are read only where nk / cand say so
-        v0.ka = v0.kb = false; v0.cand = false;
-        v1.ka = v1.kb = false; v1.cand = false;
-        if (act0)
-            visit_item<kStride, kTranslated, kCount, kAny, kNoOff>(s_ray + (size_t)(it0.w >> 26), it0, a0, a1, a2, a3, v0,
-                                                        n_int, n_leaf, n_acc, n_desc);
-        if (act1)
-            visit_item<kStride, kTranslated, kCount, kAny, kNoOff>(s_ray + (size_t)(it1.w >> 26), it1, b0, b1, b2, b3, v1,
-                                                        n_int, n_leaf, n_acc, n_desc);
-        record_candidates<kAny>(s_key, s_tri, it0, it1, v0, v1);
-        // push the children (all first children of item 0, all second ones, then item 1's): ballot compaction
-        const unsigned long long m1 = __ballot(v0.ka), m2 = __ballot(v0.kb);
-        const unsigned long long m3 = __ballot(v1.ka), m4 = __ballot(v1.kb);
-        const int n1 = __builtin_popcountll(m1), n2 = __builtin_popcountll(m2), n3 = __builtin_popcountll(m3);
-        const int total = n1 + n2 + n3 + __builtin_popcountll(m4);
-        if (base + total > cap) {  // unreachable by the pop rule above; guard anyway
-            if (lane == 0) atomicOr(P.err, 2);
-            break;
-        }
-        if (v0.ka) items[base + (int)lanes_below(m1)] = v0.ca;
-        if (v0.kb) items[base + n1 + (int)lanes_below(m2)] = v0.cb;
-        if (v1.ka) items[base + n1 + n2 + (int)lanes_below(m3)] = v1.ca;
-        if (v1.kb) items[base + n1 + n2 + n3 + (int)lanes_below(m4)] = v1.cb;
-#endif
         n = base + total;
-        __builtin_amdgcn_wave_barrier();
-    }
-}
-
-// Measured slower for primary rays on gfx950 (dragon 1080p 13.7k -> 12.6k
-// FPS, 960x540 27.4k -> 24.5k, two frames in flight; leaf batches of 16-64
-// the same): slot 1 given to a few leaves caps the interior pops at 64 per
-// iteration, which costs more than the divergence it removes.  Off by
-// default; -DRT_SPLIT_LEAF=1 builds it (with RT_LEAF_BATCH 1, leaves tested
-// every iteration, it passed the GPU parity suite; dragon 1080p with shadow
-// rays was the one config it sped up, 4.8k -> 5.5k FPS).
-#ifndef RT_SPLIT_LEAF
-#define RT_SPLIT_LEAF 0
-#endif
-#ifndef RT_LEAF_BATCH
-#define RT_LEAF_BATCH 1
-#endif
-
-// Pushes an interior visit's children into the split pool: interior children
-// on the interior stack (items[0, ni), growing up; all first children, then
-// all second ones, or the any-hit order), leaf children on the leaf stack
-// (items[cap - nl, cap), growing down).
-template <bool kAny, int any_order>
-__device__ __forceinline__ void push_split(uint4* items, int cap, int& ni, int& nl, const Visit& v) {
-    const bool la = (v.ca.x & kLeafBit) != 0, lb = (v.cb.x & kLeafBit) != 0;
-    const bool ia = v.ka && !la, ib = v.kb && !lb;
-    const bool fa = v.ka && la, fb = v.kb && lb;
-    Visit w = v;
-    w.ka = ia;
-    w.kb = ib;
-    ni += push_children<kAny, any_order>(items, ni, w);
-    const unsigned long long m1 = __ballot(fa), m2 = __ballot(fb);
-    const int n1 = __builtin_popcountll(m1);
-    if (fa) items[cap - nl - 1 - (int)lanes_below(m1)] = v.ca;
-    if (fb) items[cap - nl - 1 - n1 - (int)lanes_below(m2)] = v.cb;
-    nl += n1 + __builtin_popcountll(m2);
-}
-
-// The pool walk with leaves apart (RT_SPLIT_LEAF, two items per lane): the
-// pool holds an interior stack and a leaf stack, and each iteration's two
-// slots are wave-uniform in kind -- slot 0 up to 64 interior items, slot 1
-// up to 64 leaf items when any are pooled, else up to 64 more interior
-// items.  A slot of mixed items runs both the interior and the leaf code
-// under divergence, so every iteration of the mixed pool paid both paths
-// twice; here it pays each at most once.  The nearest hit does not depend on
-// the visiting order (every intersected node is visited; the minimum of
-// (w, path code) is order-free), and a pooled leaf waits at most until the
-// next iteration.  Capacity: popping k interior and j leaf items pushes at
-// most 2k, so k <= cap - slack - (ni + nl - j) keeps the pool within
-// cap - slack; when that leaves no room a single interior pop runs (a DFS
-// step, growing the interior stack by at most the height over a run) while
-// slot 1 drains up to 64 leaves.
-template <int kCap, int kStride, bool kTranslated, bool kCount, bool kAny, int kOrder = 0>
-__device__ __forceinline__ void pool_walk_split(const TraceParams& P, uint4* items, const float2* s_ray,
-                                                unsigned long long* s_key, uint32_t* s_tri, int n, int lane,
-                                                uint32_t& iters, uint32_t& popped, uint32_t& n_int, uint32_t& n_leaf,
-                                                uint32_t& n_acc, uint32_t& n_desc) {
-    const int cap = min(P.pool_cap, kCap);
-    const int slack = P.tree_height + 1;
-    int ni = n, nl = 0;
-    if (P.root_ref & kLeafBit) {  // a leaf root: the seeded items are leaf items
-        const uint4 v = items[lane < n ? lane : 0];
-        __builtin_amdgcn_wave_barrier();
-        if (lane < n) items[cap - n + lane] = v;
-        __builtin_amdgcn_wave_barrier();
-        ni = 0;
-        nl = n;
-    }
-    while (ni + nl > 0) {
-        // slot 1 tests pooled leaves when slot 1 has no interior items to
-        // take anyway, or once RT_LEAF_BATCH leaves wait (wave-uniform)
-        // or when the pool has no room for a parallel pop: single interior
-        // pops then run with the leaves drained, so the pool cannot grow
-        // past the DFS bound
-        const bool leafslot = nl > 0 && (ni <= 64 || nl >= RT_LEAF_BATCH || cap - slack - (ni + nl) < 1);
-        const int j = leafslot ? min(nl, 64) : 0;
-        int k = min(min(ni, leafslot ? 64 : 128), cap - slack - (ni + nl - j));
-        if (k < 1) k = ni > 0 ? 1 : 0;
-        iters++;
-        popped += (uint32_t)(k + j);
-        const int bi = ni - k;
-        bool act0 = lane < k;
-        bool act1 = leafslot ? lane < j : lane + 64 < k;
-        // idle lanes re-read a live item (its record address is valid)
-        const int i0 = k > 0 ? bi + (act0 ? lane : 0) : cap - nl;
-        const int i1 = leafslot ? cap - nl + (act1 ? lane : 0) : bi + (act1 ? lane + 64 : 0);
-        const uint4 it0 = items[i0];
-        const uint4 it1 = items[i1];
-        __builtin_amdgcn_wave_barrier();
-        if (kAny && (!kCount || kOrder >= 4)) {
-            if (act0 && s_key[it0.w >> 26] == 0ull) act0 = false;
-            if (act1 && s_key[it1.w >> 26] == 0ull) act1 = false;
-        }
-        const float4* p0 = record_of(P, it0.x);
-        const float4* p1 = record_of(P, it1.x);
-        const float4 a0 = p0[0], a1 = p0[1], a2 = p0[2], a3 = p0[3];
-        const float4 b0 = p1[0], b1 = p1[1], b2 = p1[2], b3 = p1[3];
-        RT_RECORD_FENCE(a0, a1, a2, a3, b0, b1, b2, b3);
-        int ti = bi, tl = nl - j;
-        {
-            Visit v0;
-            v0.ka = v0.kb = false; v0.cand = false;
-            if (act0)
-                visit_item<kStride, kTranslated, kCount, kAny>(s_ray + (size_t)(it0.w >> 26), it0, a0, a1, a2,
-                                                               a3, v0, n_int, n_leaf, n_acc, n_desc);
-            push_split<kAny, (kOrder & 3)>(items, cap, ti, tl, v0);
-        }
-        {
-            Visit v1;
-            v1.ka = v1.kb = false; v1.cand = false;
-            if (leafslot) {
-                if (act1)
-                    visit_item<kStride, kTranslated, kCount, kAny>(s_ray + (size_t)(it1.w >> 26), it1, b0, b1,
-                                                                   b2, b3, v1, n_int, n_leaf, n_acc, n_desc);
-                record_candidate<kAny>(s_key, s_tri, it1, v1);
-            } else {
-                if (act1)
-                    visit_item<kStride, kTranslated, kCount, kAny>(s_ray + (size_t)(it1.w >> 26), it1, b0, b1,
-                                                                   b2, b3, v1, n_int, n_leaf, n_acc, n_desc);
-                push_split<kAny, (kOrder & 3)>(items, cap, ti, tl, v1);
-            }
-        }
-        if (ti + tl > cap) {  // unreachable by the pop rule above; guard anyway
-            if (lane == 0) atomicOr(P.err, 2);
-            break;
-        }
-        ni = ti;
-        nl = tl;
         __builtin_amdgcn_wave_barrier();
     }
 }
@@ -1673,27 +1170,13 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
         // (bench.py's roofline without the root-miss visits)
         if (kCount && (P.debug & 32)) n = 0;
     }
-    if (RT_SPLIT_LEAF && P.items > 1)
-        pool_walk_split<kCap, RL::kStride, kTranslated, kCount, false>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters,
-                                                                  popped, C.n_int, C.n_leaf, C.n_acc, C.n_desc);
-    else if (RT_NO_OFF && !kTranslated && no_off)
+    if (!kTranslated && no_off)
         pool_walk<kCap, RL::kStride, kTranslated, kCount, false, 0, true>(P, items, S_.ray, S_.key, S_.tri, n, lane,
                                                                      iters, popped, C.n_int, C.n_leaf, C.n_acc,
-                                                                     C.n_desc
-#if RT_ITER_STAMPS
-                                                                     , (P.istamp && dbg_slot != kNoDbg)
-                                                                           ? P.istamp + 4 * (size_t)kIterStamps * dbg_slot
-                                                                           : nullptr
-#endif
-        );
+                                                                     C.n_desc);
     else
         pool_walk<kCap, RL::kStride, kTranslated, kCount, false>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters, popped,
-                                                            C.n_int, C.n_leaf, C.n_acc, C.n_desc
-#if RT_ITER_STAMPS
-                                                            , (P.istamp && dbg_slot != kNoDbg)
-                                                                  ? P.istamp + 4 * (size_t)kIterStamps * dbg_slot : nullptr
-#endif
-        );
+                                                            C.n_int, C.n_leaf, C.n_acc, C.n_desc);
     float cam[3];
     Ray R;
     {
@@ -1735,12 +1218,7 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
         }
         __builtin_amdgcn_wave_barrier();
         n = seed_root<kCount>(P, items, Sh, sh_live, lane, C.n_int, C.n_desc);
-        if (RT_SPLIT_LEAF && P.items > 1)
-            pool_walk_split<kCap, RL::kStride, true, kCount, true, kShadow - 1>(P, items, S_.ray, S_.key, S_.tri, n, lane,
-                                                                           iters, popped, C.n_int, C.n_leaf, C.n_acc,
-                                                                           C.n_desc);
-        else
-            pool_walk<kCap, RL::kStride, true, kCount, true, kShadow - 1>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters,
+        pool_walk<kCap, RL::kStride, true, kCount, true, kShadow - 1>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters,
                                                                      popped, C.n_int, C.n_leaf, C.n_acc, C.n_desc);
         if (lane < kRays) shadowed = S_.key[lane] == 0ull;
     }
@@ -1982,7 +1460,7 @@ __device__ __forceinline__ unsigned long long coarse_root(const TraceParams& P, 
     uint32_t ni = 0, nd = 0;
     const bool has = root_pass<kCount>(P, R, live, t0, t1, ni, nd);
     const unsigned long long b = __ballot(has);
-    constexpr unsigned long long kSub = kRays == 64 ? ~0ull : ((1ull << (kRays & 63)) - 1);
+    constexpr unsigned long long kSub = (1ull << kRays) - 1;
     const bool traced = ((b >> ((lane / kRays) * kRays)) & kSub) != 0;
     if (live && !traced) {
         put_pixel(P, px.out, kBackground, false);
@@ -1992,273 +1470,6 @@ __device__ __forceinline__ unsigned long long coarse_root(const TraceParams& P, 
     return b;
 }
 
-// ---------------------------------------------------------------------------
-// Block-cooperative units.  A frame ends with the pool
-// chains of its heaviest units: 3,000-6,000 items popped at most 128 per
-// iteration by one wave (knot 1080p: 75 iterations for the heaviest 16-ray
-// unit, tools/sched_sim.c).  The host names the heaviest P.coop tiles of its
-// cost order (order[0..coop)); each of their units is rendered by a whole
-// 4-wave block popping ONE LDS pool: up to 4 x 128 items per iteration, and
-// two-level iterations while the pool holds at most 4 x 16 items -- the
-// simulated chain of the heaviest unit drops from 75 to 23 iterations (knot
-// 1080p), 24 to 18 (dragon 960x540, against the split 8-ray halves).
-//
-// One iteration: every wave takes its share of the top `take` items (wave w:
-// items base + 64w + lane, slot 1 base + 256 + 64w + lane), issues their
-// records, and meets the others at barrier A (every popped item is in
-// registers, and the shared push counter holds `base`); each wave then visits
-// its items and appends their children at offsets it reserves with one LDS
-// atomic add on the counter; barrier B, and every wave reads the new pool
-// size.  The visited (ray, node) items are the reference's whatever the pop
-// order, as in the per-wave pool.  Nearest-candidate bookkeeping stays per
-// wave (each wave its own (w, path code) minimum per ray, race-free as in the
-// per-wave pool); the unit's result is the minimum over the four rows, the
-// reference's winner (keys are unique per ray and leaf).
-// ---------------------------------------------------------------------------
-#ifndef RT_COOP
-#define RT_COOP 1
-#endif
-
-constexpr int kCoopWaves = 4;
-
-template <int kRays, int kRayVec>
-struct CoopHead {
-    float2 ray[RayLayout<kRays>::kStride * kRayVec * 2];
-    unsigned long long key[kCoopWaves][kRays];
-    uint32_t tri[kCoopWaves][kRays];
-    // pool size / push counter, double-buffered: iteration i pushes through
-    // top[i & 1] while a slow wave may still read top[(i - 1) & 1]
-    int32_t top[2];
-    int32_t pad[2];
-};
-
-// The coop pool takes the LDS of the block's four wave pools.
-template <int kRays, int kCap, int kRayVec>
-constexpr int coop_cap() {
-    return (int)((sizeof(WaveLds<kRays, kCap, kRayVec>) * kCoopWaves - sizeof(CoopHead<kRays, kRayVec>)) /
-                 sizeof(uint4));
-}
-
-template <int kRays, int kCap, int kRayVec>
-struct CoopLds {
-    uint4 items[coop_cap<kRays, kCap, kRayVec>()];
-    CoopHead<kRays, kRayVec> h;
-};
-
-// Workgroup barrier for the coop pool: this wave's LDS operations complete,
-// then s_barrier; the memory clobber keeps the compiler from moving LDS
-// accesses across it (outstanding global loads stay in flight).
-__device__ __forceinline__ void coop_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-// `count` pool slots for this wave's pushes (wave-uniform count, all lanes
-// active): the offset of the first.
-__device__ __forceinline__ int coop_reserve(int32_t* top, int count, int lane) {
-    int at = 0;
-    if (count > 0 && lane == 0) at = atomicAdd(top, count);
-    return __builtin_amdgcn_readfirstlane(at);
-}
-
-// A two-level iteration (see two_level_iter) over the coop pool: wave w takes
-// items [16w, 16w + 16) of the n <= 64 pooled items, one quad per item;
-// pushes are reserved on the shared counter (reset to 0 by wave 0 before the
-// barrier, since the whole pool is popped).
-template <int kStride, bool kTranslated, bool kCount, bool kNoOff>
-__device__ __forceinline__ void two_level_coop(const TraceParams& P, uint4* items, int32_t* top, const float2* s_ray,
-                                               unsigned long long* s_key, uint32_t* s_tri, int n, int wv, int lane,
-                                               uint32_t& n_int, uint32_t& n_leaf, uint32_t& n_acc, uint32_t& n_desc) {
-    int l = lane;
-    asm volatile("" : "+v"(l));
-    const int k = wv * 16 + (l >> 2), role = l & 3;
-    bool act = k < n;
-    const uint4 it = items[act ? k : 0];
-    if (wv == 0 && lane == 0) *top = 0;
-    const uint32_t marked = it.w & kCodeMarkMask;
-    const bool interior = (it.x & kLeafBit) == 0;
-    const int depth = 31 - __builtin_clz(marked);
-    const bool el = act && interior && depth <= P.two_depth;
-    const bool child = (role == 1 || role == 2) && el;
-    const float4* pa = child ? P.inode + 4 * (2 * (size_t)it.x + (size_t)role) : record_of(P, it.x);
-    const float4 a0 = pa[0], a1 = pa[1], a2 = pa[2], a3 = pa[3];
-    coop_barrier();  // A: every wave holds its items; the pool may be overwritten
-    Ray Q;
-    float4 q2, q3, q4;
-    ray_of<kTranslated, kStride>(s_ray + (size_t)(it.w >> 26), Q, q2, q3, q4);
-    float at0, at1, bt0, bt1;
-    slab_vals<kNoOff>(Q, a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, at0, at1);
-    slab_vals<kNoOff>(Q, a1.z, a1.w, a2.x, a2.y, a2.z, a2.w, bt0, bt1);
-    const float xl0 = quad_bcast0(at0), xl1 = quad_bcast0(at1), xr0 = quad_bcast0(bt0), xr1 = quad_bcast0(bt1);
-    const float t0 = role == 0 ? __uint_as_float(it.y) : role == 1 ? xl0 : xr0;
-    const float t1 = role == 0 ? __uint_as_float(it.z) : role == 1 ? xl1 : xr1;
-    Order o;
-    order_node<kTranslated, kCount>(q2, q3, q4, t0, t1, a3, at0, at1, bt0, bt1, false, o, n_int, n_desc);
-    const uint32_t fl = quad_bcast0((o.left_first ? 1u : 0u) | (o.ka ? 2u : 0u) | (o.kb ? 4u : 0u));
-    const bool lfirst = (fl & 1u) != 0;
-    const bool is_first = (role == 1) == lfirst;
-    const bool kept = child && ((fl & (is_first ? 2u : 4u)) != 0);
-    const bool real = role == 0 ? (act && interior) : kept;
-    if (kCount && real) count_order(o, n_int, n_desc);
-    const bool push = role == 0 ? (act && interior && !el) : kept;
-    const uint32_t code = role == 0 ? marked : ((marked << 1) | (is_first ? 0u : 1u));
-    const uint32_t meta = ((it.w >> 26) << 26) | (code << 1);
-    const bool p1 = push && o.ka, p2 = push && o.kb;
-    const unsigned long long m1 = __ballot(p1), m2 = __ballot(p2);
-    const int n1 = __builtin_popcountll(m1);
-    const int at = coop_reserve(top, n1 + __builtin_popcountll(m2), lane);
-    if (p1) items[at + (int)lanes_below(m1)] = make_uint4(o.first, __float_as_uint(o.f0), __float_as_uint(o.f1), meta);
-    if (p2)
-        items[at + n1 + (int)lanes_below(m2)] =
-            make_uint4(o.second, __float_as_uint(o.g0), __float_as_uint(o.g1), meta | 1u);
-    {
-        Visit v;
-        v.ka = v.kb = false; v.cand = false;
-        if (role == 0 && act && !interior) visit_leaf<kTranslated, kCount, false>(Q, q4, it, a0, a1, a2, a3, v, n_leaf, n_acc);
-        record_candidate<false>(s_key, s_tri, it, v);
-    }
-}
-
-// The coop pool walk of one unit (nearest hit; every wave of the block runs
-// it, the loop is uniform across them since n is read from LDS after each
-// barrier B).  Returns the iterations and items popped.
-template <int kCap, int kStride, bool kTranslated, bool kCount, bool kNoOff>
-__device__ __forceinline__ void pool_walk_coop(const TraceParams& P, uint4* items, int32_t* tops, const float2* s_ray,
-                                               unsigned long long* s_key, uint32_t* s_tri, int n, int wv, int lane,
-                                               uint32_t& iters, uint32_t& popped, uint32_t& n_int, uint32_t& n_leaf,
-                                               uint32_t& n_acc, uint32_t& n_desc) {
-    const int cap = min(kCoopWaves * P.pool_cap, kCap);
-    const int slack = P.tree_height + 1;
-    constexpr int per = kCoopWaves * 128;
-    int par = 0;  // tops[0] holds the seeded size
-    while (n > 0) {
-        iters++;
-        par ^= 1;
-        int32_t* top = tops + par;
-        if (RT_TWO_LEVEL && n <= kCoopWaves * RT_TWO_MAX && P.two_depth >= 0 && 4 * n <= cap - slack) {
-            popped += (uint32_t)n;
-            two_level_coop<kStride, kTranslated, kCount, kNoOff>(P, items, top, s_ray, s_key, s_tri, n, wv, lane, n_int,
-                                                                n_leaf, n_acc, n_desc);
-        } else {
-            int take = min(min(n, per), cap - slack - n);
-            if (take < 1) take = 1;
-            popped += (uint32_t)take;
-            const int base = n - take;
-            const int i0 = wv * 64 + lane, i1 = kCoopWaves * 64 + wv * 64 + lane;
-            const bool act0 = i0 < take, act1 = i1 < take;
-            const uint4 it0 = items[base + (act0 ? i0 : 0)];
-            const uint4 it1 = items[base + (act1 ? i1 : 0)];
-            if (wv == 0 && lane == 0) *top = base;
-            const float4* p0 = record_of(P, it0.x);
-            const float4* p1 = record_of(P, it1.x);
-            const float4 a0 = p0[0], a1 = p0[1], a2 = p0[2], a3 = p0[3];
-            const bool two = kCoopWaves * 64 + wv * 64 < take;  // wave-uniform: this wave's slot 1 holds items
-            const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            float4 b0 = z, b1 = z, b2 = z, b3 = z;
-            if (two) { b0 = p1[0]; b1 = p1[1]; b2 = p1[2]; b3 = p1[3]; }
-            coop_barrier();  // A: every wave holds its items; the counter holds base
-            {
-                Visit v0;
-                v0.ka = v0.kb = false; v0.cand = false;
-                if (act0)
-                    visit_item<kStride, kTranslated, kCount, false, kNoOff>(s_ray + (size_t)(it0.w >> 26), it0, a0, a1,
-                                                                           a2, a3, v0, n_int, n_leaf, n_acc, n_desc);
-                record_candidate<false>(s_key, s_tri, it0, v0);
-                const int c0 = __builtin_popcountll(__ballot(v0.ka)) + __builtin_popcountll(__ballot(v0.kb));
-                push_children<false, 0>(items, coop_reserve(top, c0, lane), v0);
-            }
-            if (two) {
-                Visit v1;
-                v1.ka = v1.kb = false; v1.cand = false;
-                if (act1)
-                    visit_item<kStride, kTranslated, kCount, false, kNoOff>(s_ray + (size_t)(it1.w >> 26), it1, b0, b1,
-                                                                           b2, b3, v1, n_int, n_leaf, n_acc, n_desc);
-                record_candidate<false>(s_key, s_tri, it1, v1);
-                const int c1 = __builtin_popcountll(__ballot(v1.ka)) + __builtin_popcountll(__ballot(v1.kb));
-                push_children<false, 0>(items, coop_reserve(top, c1, lane), v1);
-            }
-        }
-        coop_barrier();  // B: every push has landed
-        n = __builtin_amdgcn_readfirstlane(*(volatile int32_t*)top);
-        if (n > cap) {  // unreachable by the pop rule; guard anyway (uniform)
-            if (lane == 0 && wv == 0) atomicOr(P.err, 2);
-            break;
-        }
-    }
-}
-
-// One unit rendered by the whole block (all kCoopWaves waves call it).
-template <int kRays, int kCap, int kRayVec, bool kTranslated, bool kWriteHit, bool kCount>
-__device__ __forceinline__ void trace_unit_coop(const TraceParams& P, CoopLds<kRays, kCap, kRayVec>& S,
-                                                const Unit& U, int wv, int lane, size_t dbg_slot, uint32_t* cost,
-                                                Counts& C) {
-    using RL = RayLayout<kRays>;
-    constexpr int kCoopCap = coop_cap<kRays, kCap, kRayVec>();
-    Pixel px;
-    bool live = unit_pixel(P, U, kRays / 8, lane, px);
-    const unsigned long long t_start = P.dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    uint32_t iters = 0, popped = 0;
-    int n = 0;
-    bool no_off;
-    {
-        float cam0[3];
-        Ray R0;
-        camera_ray(P, px, live, cam0, R0);
-        no_off = !kTranslated && __ballot(live && !(fabsf(R0.rx) > 0.0f && fabsf(R0.ry) > 0.0f &&
-                                                    fabsf(R0.rz) > 0.0f)) == 0ull;
-        if (lane < kRays) {
-            S.h.key[wv][lane] = ~0ull;
-            S.h.tri[wv][lane] = kMiss;
-        }
-        if (wv == 0) {
-            if (lane < kRays) store_ray(&S.h.ray[lane], RL::kStride, R0, kTranslated, 0.0f, 0u);
-            n = seed_root<kCount>(P, S.items, R0, live, lane, C.n_int, C.n_desc);
-            if (kCount && (P.debug & 32)) n = 0;
-            if (lane == 0) S.h.top[0] = n;
-        }
-    }
-    coop_barrier();
-    n = __builtin_amdgcn_readfirstlane(*(volatile int32_t*)&S.h.top[0]);
-    if (RT_NO_OFF && !kTranslated && no_off)
-        pool_walk_coop<kCoopCap, RL::kStride, kTranslated, kCount, true>(P, S.items, S.h.top, S.h.ray, S.h.key[wv],
-                                                                        S.h.tri[wv], n, wv, lane, iters, popped,
-                                                                        C.n_int, C.n_leaf, C.n_acc, C.n_desc);
-    else
-        pool_walk_coop<kCoopCap, RL::kStride, kTranslated, kCount, false>(P, S.items, S.h.top, S.h.ray, S.h.key[wv],
-                                                                         S.h.tri[wv], n, wv, lane, iters, popped,
-                                                                         C.n_int, C.n_leaf, C.n_acc, C.n_desc);
-    // every candidate of every wave has landed (the walk ends after a barrier
-    // B); wave 0 shades the unit
-    if (wv != 0) return;
-    if (P.dbg && lane == 0 && dbg_slot != kNoDbg) {
-        P.dbg[3 * dbg_slot] = t_start;
-        P.dbg[3 * dbg_slot + 1] = __builtin_amdgcn_s_memrealtime();
-        P.dbg[3 * dbg_slot + 2] = iters | ((unsigned long long)popped << 32);
-    }
-    if (cost && lane == 0) *cost = iters;  // (the kernel passes none: see k_trace_kd3)
-    float cam[3];
-    Ray R;
-    {
-        int32_t l2 = lane;
-        asm volatile("" : "+v"(l2));
-        live = unit_pixel(P, U, kRays / 8, l2, px);
-        camera_ray(P, px, live, cam, R);
-    }
-    unsigned long long kbest = ~0ull;
-    uint32_t best = kMiss;
-    if (lane < kRays) {
-#pragma unroll
-        for (int w = 0; w < kCoopWaves; w++) {
-            const unsigned long long k = S.h.key[w][lane];
-            if (k < kbest) {
-                kbest = k;
-                best = S.h.tri[w][lane];
-            }
-        }
-    }
-    if (!live) return;
-    shade_out<kWriteHit, kCount>(P, px, R, cam, kbest, best, false, C);
-}
-
-// kRays pixels per wave (64: 8x8; 32: 8x4; 16: 8x2; 8: 8x1): fewer rays per wave
-// spread a heavy tile's items over more SIMDs, the other lanes only help.
 // kShadow: a second pool walk traces one shadow ray per hit (SURVEY.md §8a
 // a12; definition in oracle/oracle.c trace_shadow): the segment from the light
 // (2,2,2) to the hit, walked from the light with the reference's rules.
@@ -2269,15 +1480,8 @@ __device__ __forceinline__ void trace_unit_coop(const TraceParams& P, CoopLds<kR
 // (4 VGPRs spill to scratch in the timed variant).  Measured with two frames
 // in flight: dragon 1080p 13.7k -> 14.7k FPS, the 93 % fill view 940 ->
 // 873 us per frame; one frame at a time unchanged (86.7 -> 88.8 us).  The
-// 8-ray blocks are LDS-bound at 4 and keep their registers.  0: no bound.
-#ifndef RT_KD3_WAVES_PER_SIMD
-#define RT_KD3_WAVES_PER_SIMD 6
-#endif
-#if RT_KD3_WAVES_PER_SIMD > 0
-#define RT_KD3_BOUNDS(threads) __launch_bounds__(threads, RT_KD3_WAVES_PER_SIMD)
-#else
-#define RT_KD3_BOUNDS(threads) __launch_bounds__(threads)
-#endif
+// 8-ray blocks are LDS-bound at 4 and keep their registers.
+#define RT_KD3_BOUNDS(threads) __launch_bounds__(threads, 6)
 // One block of k_trace_kd3's grid: block index b (blockIdx.x, or the virtual
 // index within a multi-frame launch, below).
 template <int kRays, bool kTranslated, bool kWriteHit, bool kCount, int kShadow, int kCap, int kRayVec>
@@ -2287,13 +1491,11 @@ __device__ __forceinline__ void kd3_block(const TraceParams& P, WaveLds<kRays, k
     Counts C;
     const int32_t ntiles = P.tiles_x * P.block_rows;
     const int32_t bslot = b;  // diagnostics slot of this block
-    // blocks: 4 per coop tile, 2 per split tile, 1 per other fine tile, then
-    // the far fill
-    const int32_t head = 3 * P.coop + P.split;
-    if (b >= ntiles + head) {
+    // blocks: 2 per split tile, 1 per other fine tile, then the far fill
+    if (b >= ntiles + P.split) {
         // fused far fill: blocks after the fine tiles write the coarse groups,
         // all far by construction (set_fine_region); unrolled as in k_coarse_kd3
-        const int32_t j0 = ((b - ntiles - head) * kWaves + wv) * P.coarse_per_wave;
+        const int32_t j0 = ((b - ntiles - P.split) * kWaves + wv) * P.coarse_per_wave;
         const int32_t j1 = min(j0 + P.coarse_per_wave, (int32_t)P.coarse_groups);
         bool ok = true;
 #pragma unroll 8
@@ -2311,44 +1513,16 @@ __device__ __forceinline__ void kd3_block(const TraceParams& P, WaveLds<kRays, k
     // 8-ray units a 4-pixel half row per wave -- which halves the heaviest
     // units' pool chains; the other tiles follow.  (Quarters of the heaviest
     // tiles, four 4-ray units of a 16-ray unit, measured slower: dragon
-    // 960x540 43.0-45.8k -> 38.0-39.4k FPS, r03s.)
-    // Coop tiles (the host's heaviest P.coop of its cost order, order[0..coop)):
-    // block 4k + u renders unit u of tile order[k] with all four waves.
-    if constexpr (RT_COOP && kWaves == kCoopWaves && kRays <= 16 && kShadow == 0) {
-        if (b < 4 * P.coop) {
-            const int32_t ti = P.order[b >> 2];
-            if ((uint32_t)ti >= (uint32_t)ntiles) {  // a stale order: never index past the grid
-                if (lane == 0 && wv == 0) atomicOr(P.err, 8);
-                return;
-            }
-            const int u = b & 3;
-            // a coop unit leaves its tile's cost slots as the tile's last
-            // per-wave render wrote them (the coop chain is no measure of the
-            // single-wave cost the order and the thresholds compare)
-            uint32_t* cost = nullptr;
-            static_assert(sizeof(CoopLds<kRays, kCap, kRayVec>) <= kWaves * sizeof(WaveLds<kRays, kCap, kRayVec>),
-                          "coop pool exceeds the block's LDS");
-            trace_unit_coop<kRays, kCap, kRayVec, kTranslated, kWriteHit, kCount>(
-                P, *reinterpret_cast<CoopLds<kRays, kCap, kRayVec>*>(s_lds), unit_of_tile(P, ti, u), wv, lane,
-                (size_t)bslot * kWaves + wv, cost, C);
-            if (kCount) count_flush(P, C);
-            return;
-        }
-    }
-    b -= 4 * P.coop;  // the split tiles order[coop..coop + split), then the rest
+    // 960x540 43.0-45.8k -> 38.0-39.4k FPS, r03s; block-cooperative units, a
+    // whole block on one pool, slower at every threshold, r04.)
     const bool split = b < 2 * P.split;
-    const int32_t ti = split ? P.order[P.coop + (b >> 1)] : tile_index(P, b - P.split + P.coop);
+    const int32_t ti = split ? P.order[b >> 1] : tile_index(P, b - P.split);
     if ((uint32_t)ti >= (uint32_t)ntiles) {  // a stale order: never index past the grid
         if (lane == 0) atomicOr(P.err, 8);
         return;
     }
     uint32_t* cost = P.cost ? P.cost + kCostSlots * (size_t)ti + wv + (split ? (b & 1) * 4 : 0) : nullptr;
     if (cost && !split && lane == 0) cost[4] = 0u;  // no second half
-    // RT_PRIO_HEAVY (experiment): the heaviest tiles of the cost order (the
-    // split halves, or the first RT_PRIO_HEAVY blocks) issue ahead of the
-    // other waves of their SIMD
-    if (RT_PRIO_HEAVY > 0 && P.cost && P.order && b < max(2 * P.split, (int32_t)RT_PRIO_HEAVY))
-        __builtin_amdgcn_s_setprio(2);
     Unit U = unit_of_tile(P, ti, wv);
     if (split && kRays == 16) U.yin = (U.yin - wv * (kRays / 8)) + (b & 1) * kWaves + wv;
     if (split && kRays == 8) U.x0 += (b & 1) * 4;
@@ -2364,26 +1538,18 @@ __device__ __forceinline__ void kd3_block(const TraceParams& P, WaveLds<kRays, k
 // i / pf_blocks into P.pf_argb[(P.pf_seq0 + frame) % P.pf_nbuf].  Blocks are
 // dispatched in index order, so frame f + 1's heaviest tiles start on the CUs
 // frame f's tail frees, with no launch between frames (static scenes: every
-// frame is the same frame).  With pf_group G > 1 the frames go in groups of
-// G whose blocks interleave (block i of a group renders block i / G of its
-// frame i % G): G frames dispatch side by side, as G lanes' frames do.
+// frame is the same frame).  (Interleaving the blocks of groups of 2-3
+// frames measured the same, r04m-n.)
 template <int kRays, bool kTranslated, bool kWriteHit, bool kCount, int kShadow>
 __global__ RT_KD3_BOUNDS(64 * kd3_waves(kRays)) void k_trace_kd3(TraceParams P) {
     constexpr int kCap = pool_cap_for<kRays>();
     constexpr int kRayVec = (kTranslated || kShadow) ? 5 : 3;  // float4s of per-ray data in LDS
     __shared__ WaveLds<kRays, kCap, kRayVec> s_lds[kd3_waves(kRays)];
     const int wv = wave_id(), lane = (int)threadIdx.x & 63;
-    if (P.started && threadIdx.x == 0) atomicAdd(P.started, 1ull);  // the dispatch gate's count (k_gate)
     int32_t b = (int32_t)blockIdx.x;
     if (P.pf_frames > 0) {
-        // frames in groups of pf_group, frame-major across groups and
-        // interleaved block by block inside one (the last group may be short)
-        const int32_t gsz = P.pf_group * P.pf_blocks;
-        const int32_t grp = b / gsz;
-        const int32_t r = b - grp * gsz;
-        const int32_t gc = min(P.pf_group, P.pf_frames - grp * P.pf_group);
-        const int32_t f = grp * P.pf_group + r % gc;
-        b = r / gc;
+        const int32_t f = b / P.pf_blocks;
+        b -= f * P.pf_blocks;
         // every wave's lane 0 stores the same pointer, then its own lanes read it
         if (lane == 0) s_pf_argb = P.pf_argb[(P.pf_seq0 + f) % P.pf_nbuf];
         __builtin_amdgcn_wave_barrier();
@@ -2399,7 +1565,7 @@ __global__ __launch_bounds__(128) void k_coarse_kd3(TraceParams P) {
     constexpr int kWaves = 2;
     constexpr int kCap = pool_cap_for<kRays>();
     constexpr int kRayVec = (kTranslated || kShadow) ? 5 : 3;
-    constexpr unsigned long long kSub = kRays == 64 ? ~0ull : ((1ull << (kRays & 63)) - 1);
+    constexpr unsigned long long kSub = (1ull << kRays) - 1;
     __shared__ WaveLds<kRays, kCap, kRayVec> s_lds[kWaves];
     const int wv = wave_id(), lane = (int)threadIdx.x & 63;
     Counts C;
@@ -2458,24 +1624,11 @@ __global__ __launch_bounds__(128) void k_coarse_kd3(TraceParams P) {
 // -------------------------------------------------------------- flat trace
 
 // intersect_trixel_cuda (TD/Trixel.cu:173-209) fused with the shading.  The
-// triangle loop index is wave-uniform, so its records arrive through the
-// scalar data cache into SGPRs; an exact sign screen skips the division for
-// the (common) rays that cannot pass u >= eps, v >= eps or w >= eps.
+// triangle loop index is wave-uniform, so the pair layout's records arrive
+// through the scalar data cache into SGPRs; a screen on the signed layout
+// (k_pair_tri) skips the correctly rounded division for the (common) rays
+// that cannot pass u >= eps, v >= eps or w >= eps.
 //
-// The screen.  u = pe1*U, v = pe1*V, w = pe1*W with sign(pe1) = sign(f), so
-// with U, V, W sign-flipped when f is negative (an XOR of f's sign bit), a
-// flipped value <= 0 makes u, v or w <= 0 < eps: rejected.  min3 ignores NaN
-// (IEEE minNum), so a NaN U, V or W never rejects by itself (the full test
-// decides); f = +-0 or NaN makes the full test reject anyway (|f| < eps, or
-// NaN w fails w < d).  A ray passes the screen iff !(min3 <= 0).
-__device__ __forceinline__ float flip_by(float x, float f) {
-    return __uint_as_float(__float_as_uint(x) ^ (__float_as_uint(f) & 0x80000000u));
-}
-__device__ __forceinline__ bool flat_screen(float f, float U, float V, float W) {
-    const float m = fminf(fminf(flip_by(U, f), flip_by(V, f)), flip_by(W, f));
-    return !(m <= 0.0f);
-}
-
 // The rest of one flat test (TD/Trixel.cu:185-205) for a ray that passed
 // the screen: strict w < d, so among equal w the lowest index wins.
 __device__ __forceinline__ void flat_accept(float f, float U, float V, float W, uint32_t t, float& d,
@@ -2510,43 +1663,14 @@ struct FlatPair {
         pair ^= __float_as_uint(prev.dw.y) & zero;
         load(Q + 16 * (size_t)pair);
     }
-    // device_cross(rmd, e2) then the dots (TD/Trixel.cu:180-186) per half;
-    // triangle t then t + 1, so equal w keeps the lower index.
-    __device__ __forceinline__ void test(const f2v X, const f2v Y, const f2v Z, uint32_t t, float& d, uint32_t& best,
-                                         uint32_t& n_acc) const {
-        const f2v qx = Y * e2z - Z * e2y;
-        const f2v qy = Z * e2x - X * e2z;
-        const f2v qz = X * e2y - Y * e2x;
-        const f2v f = (qx * e1x + qy * e1y) + qz * e1z;
-        const f2v U = (qx * tx + qy * ty) + qz * tz;
-        const f2v V = (X * dqx + Y * dqy) + Z * dqz;
-        const bool c0 = flat_screen(f.x, U.x, V.x, dw.x), c1 = flat_screen(f.y, U.y, V.y, dw.y);
-        if (c0 || c1) {
-            if (c0) flat_accept(f.x, U.x, V.x, dw.x, t, d, best, n_acc);
-            if (c1) flat_accept(f.y, U.y, V.y, dw.y, t + 1, d, best, n_acc);
-        }
-    }
-    // Form 4: the same products over the signed layout (k_pair_tri: d_w >= 0,
-    // so a ray can pass only where f > 0, u >= 0 and v >= 0 in the primed
-    // values), screened by one min3 per triangle: a pair is skipped unless
-    // max(min3(U, V, f) of each half) is > 0 (or NaN).  min3 ignores NaN, so
-    // a NaN U or V never rejects by itself; a triangle whose min3 is NaN has
-    // f NaN, which the full test rejects.
-    __device__ __forceinline__ void products(const f2v X, const f2v Y, const f2v Z, f2v& f, f2v& U, f2v& V) const {
-        const f2v qx = Y * e2z - Z * e2y;
-        const f2v qy = Z * e2x - X * e2z;
-        const f2v qz = X * e2y - Y * e2x;
-        f = (qx * e1x + qy * e1y) + qz * e1z;
-        U = (qx * tx + qy * ty) + qz * tz;
-        V = (X * dqx + Y * dqy) + Z * dqz;
-    }
-    // Form 7: V first.  v's numerator V = r . d_q depends on the ray only
-    // through one dot product, and the signed layout needs V > 0 (or NaN)
-    // for an accept; V <= 0 in every lane of the wave for both triangles --
+    // The test, V first.  On the signed layout a triangle can be accepted
+    // only where f > 0, U > 0 and V > 0 (or NaN): min3 ignores NaN, so a NaN
+    // U or V never rejects by itself, and a NaN f fails the full test.  v's
+    // numerator V = r . d_q depends on the ray only through one dot product; V <= 0 in every lane of the wave for both triangles --
     // an 8x8 pixel tile wholly on the outer side of the two edge planes,
     // about half the (tile, pair) combinations -- skips the cross product,
-    // f and U (19 of the pair's 24 packed operations).  The lanes that go on
-    // compute exactly form 4's values.
+    // f and U (19 of the pair's 24 packed operations); triangle t then t + 1,
+    // so equal w keeps the lower index.
     __device__ __forceinline__ void test_signed_v(const f2v X, const f2v Y, const f2v Z, uint32_t t, float& d,
                                                   uint32_t& best, uint32_t& n_acc) const {
         const f2v V = (X * dqx + Y * dqy) + Z * dqz;
@@ -2561,16 +1685,6 @@ struct FlatPair {
                 if (!(m0 <= 0.0f)) flat_accept(f.x, U.x, V.x, dw.x, t, d, best, n_acc);
                 if (!(m1 <= 0.0f)) flat_accept(f.y, U.y, V.y, dw.y, t + 1, d, best, n_acc);
             }
-        }
-    }
-    __device__ __forceinline__ void test_signed(const f2v X, const f2v Y, const f2v Z, uint32_t t, float& d,
-                                                uint32_t& best, uint32_t& n_acc) const {
-        f2v f, U, V;
-        products(X, Y, Z, f, U, V);
-        const float m0 = fminf(fminf(U.x, V.x), f.x), m1 = fminf(fminf(U.y, V.y), f.y);
-        if (!(fmaxf(m0, m1) <= 0.0f)) {
-            if (!(m0 <= 0.0f)) flat_accept(f.x, U.x, V.x, dw.x, t, d, best, n_acc);
-            if (!(m1 <= 0.0f)) flat_accept(f.y, U.y, V.y, dw.y, t + 1, d, best, n_acc);
         }
     }
 };
@@ -2593,180 +1707,38 @@ __device__ __forceinline__ void flat_shade_out(const TraceParams& P, const Pixel
     if (kWriteHit) P.hit[px.out] = best == kMiss ? (int64_t)-1 : (int64_t)best;
 }
 
-// kVariant 0: one triangle per iteration, the 64-B camera-relative record
-// (the first form).  1: two triangles per iteration, both records loaded
-// before either is tested, branch-free screen.  2: the same pair as packed
-// float2 arithmetic (v_pk_mul_f32 / v_pk_add_f32, one IEEE rounding per half,
-// so every value is the unpacked one) over the pair layout P.tpair.  3: 2,
-// software pipelined (the next pair's loads in flight during a pair's tests).
-template <bool kWriteHit, bool kCount, int kVariant>
+// The flat list in one pass (RT_OPT_FLAT 9; counting renders): pair p + 1's
+// scalar loads are issued once pair p's have arrived (scalar loads return
+// out of order, so a wait is always for all of them) and overlap pair p's
+// tests.  Forms 0-8 of rounds 1-2 (one triangle per iteration, unpacked
+// pairs, packed pairs without the signed layout or the V-first skip)
+// measured 19.8-35.0 ms per C2 frame against this form's 18.3.
+template <bool kWriteHit, bool kCount>
 __global__ __launch_bounds__(kTileWFlat * kTileH) void k_trace_flat(TraceParams P) {
     Pixel px;
     if (!pixel_of_thread(P, px)) return;
     float rmd[3];
     primary_ray(P, px.x, px.y, rmd);
-    const float rx = rmd[0], ry = rmd[1], rz = rmd[2];
     float d = kDrawDistance;
     uint32_t best = kMiss;
     uint32_t n_acc = 0;
-    const float4* __restrict__ T = P.trec;
     const uint32_t ntri = P.ntri;
-    if (kVariant == 0) {
-        for (uint32_t t = 0; t < ntri; t++) {
-            const float4 A = T[4 * (size_t)t];
-            const float4 B = T[4 * (size_t)t + 1];
-            const float4 Cq = T[4 * (size_t)t + 2];
-            const float4 D = T[4 * (size_t)t + 3];
-            float qpx, qpy, qpz;
-            cross3(qpx, qpy, qpz, rx, ry, rz, A.w, B.x, B.y);
-            const float f = dot3(qpx, qpy, qpz, A.x, A.y, A.z);
-            const float U = dot3(qpx, qpy, qpz, B.z, B.w, Cq.x);
-            const float V = dot3(rx, ry, rz, Cq.y, Cq.z, Cq.w);
-            const float W = D.x;
-            const bool pos = f > 0;
-            const bool reject = (pos ? (U <= 0 || V <= 0 || W <= 0) : (U >= 0 || V >= 0 || W >= 0));
-            if (reject) continue;
-            flat_accept(f, U, V, W, t, d, best, n_acc);
-        }
-    } else if (kVariant == 1) {
-        uint32_t t = 0;
-        for (; t + 1 < ntri; t += 2) {
-            const float4 A0 = T[4 * (size_t)t], B0 = T[4 * (size_t)t + 1], C0 = T[4 * (size_t)t + 2],
-                         D0 = T[4 * (size_t)t + 3];
-            const float4 A1 = T[4 * (size_t)t + 4], B1 = T[4 * (size_t)t + 5], C1 = T[4 * (size_t)t + 6],
-                         D1 = T[4 * (size_t)t + 7];
-            float q0x, q0y, q0z, q1x, q1y, q1z;
-            cross3(q0x, q0y, q0z, rx, ry, rz, A0.w, B0.x, B0.y);
-            cross3(q1x, q1y, q1z, rx, ry, rz, A1.w, B1.x, B1.y);
-            const float f0 = dot3(q0x, q0y, q0z, A0.x, A0.y, A0.z);
-            const float f1 = dot3(q1x, q1y, q1z, A1.x, A1.y, A1.z);
-            const float U0 = dot3(q0x, q0y, q0z, B0.z, B0.w, C0.x);
-            const float U1 = dot3(q1x, q1y, q1z, B1.z, B1.w, C1.x);
-            const float V0 = dot3(rx, ry, rz, C0.y, C0.z, C0.w);
-            const float V1 = dot3(rx, ry, rz, C1.y, C1.z, C1.w);
-            const bool c0 = flat_screen(f0, U0, V0, D0.x), c1 = flat_screen(f1, U1, V1, D1.x);
-            if (c0 || c1) {
-                if (c0) flat_accept(f0, U0, V0, D0.x, t, d, best, n_acc);
-                if (c1) flat_accept(f1, U1, V1, D1.x, t + 1, d, best, n_acc);
-            }
-        }
-        if (t < ntri) {
-            const float4 A = T[4 * (size_t)t], B = T[4 * (size_t)t + 1], Cq = T[4 * (size_t)t + 2],
-                         D = T[4 * (size_t)t + 3];
-            float qpx, qpy, qpz;
-            cross3(qpx, qpy, qpz, rx, ry, rz, A.w, B.x, B.y);
-            const float f = dot3(qpx, qpy, qpz, A.x, A.y, A.z);
-            const float U = dot3(qpx, qpy, qpz, B.z, B.w, Cq.x);
-            const float V = dot3(rx, ry, rz, Cq.y, Cq.z, Cq.w);
-            if (flat_screen(f, U, V, D.x)) flat_accept(f, U, V, D.x, t, d, best, n_acc);
-        }
-    } else {
-        // pair p = triangles (2p, 2p+1): 13 float2 (e1, e2, d_t, d_q, d_w), 128 B;
-        // an odd count's last pair holds a dead twin (d_w = 0: never accepted)
-        const f2v* __restrict__ Q = reinterpret_cast<const f2v*>(P.tpair);
-        const f2v X = {rx, rx}, Y = {ry, ry}, Z = {rz, rz};
-        const uint32_t npair = (ntri + 1) >> 1;
-        if (kVariant == 2) {
-            for (uint32_t p = 0; p < npair; p++) {
-                FlatPair c;
-                c.load(Q + 16 * (size_t)p);
-                c.test(X, Y, Z, 2 * p, d, best, n_acc);
-            }
-        } else if (kVariant == 4) {
-            for (uint32_t p = 0; p < npair; p++) {
-                FlatPair c;
-                c.load(Q + 16 * (size_t)p);
-                c.test_signed(X, Y, Z, 2 * p, d, best, n_acc);
-            }
-        } else if (kVariant == 6) {
-            // form 4, two pairs per iteration behind one screen branch (the
-            // four triangles' accepts in index order inside it)
-            uint32_t p = 0;
-            for (; p + 1 < npair; p += 2) {
-                FlatPair a, b;
-                a.load(Q + 16 * (size_t)p);
-                b.load(Q + 16 * (size_t)p + 16);
-                f2v fa, Ua, Va, fb, Ub, Vb;
-                a.products(X, Y, Z, fa, Ua, Va);
-                b.products(X, Y, Z, fb, Ub, Vb);
-                const float m0 = fminf(fminf(Ua.x, Va.x), fa.x), m1 = fminf(fminf(Ua.y, Va.y), fa.y);
-                const float m2 = fminf(fminf(Ub.x, Vb.x), fb.x), m3 = fminf(fminf(Ub.y, Vb.y), fb.y);
-                if (!(fmaxf(fmaxf(m0, m1), fmaxf(m2, m3)) <= 0.0f)) {
-                    const uint32_t t = 2 * p;
-                    if (!(m0 <= 0.0f)) flat_accept(fa.x, Ua.x, Va.x, a.dw.x, t, d, best, n_acc);
-                    if (!(m1 <= 0.0f)) flat_accept(fa.y, Ua.y, Va.y, a.dw.y, t + 1, d, best, n_acc);
-                    if (!(m2 <= 0.0f)) flat_accept(fb.x, Ub.x, Vb.x, b.dw.x, t + 2, d, best, n_acc);
-                    if (!(m3 <= 0.0f)) flat_accept(fb.y, Ub.y, Vb.y, b.dw.y, t + 3, d, best, n_acc);
-                }
-            }
-            if (p < npair) {
-                FlatPair a;
-                a.load(Q + 16 * (size_t)p);
-                a.test_signed(X, Y, Z, 2 * p, d, best, n_acc);
-            }
-        } else if (kVariant == 9) {
-            // form 7 software pipelined as form 3: pair p + 1's scalar loads
-            // issued once pair p's have arrived, in flight during its tests
-            const uint32_t zero = ntri >> 31;  // 0: scenes hold < 2^29 triangles
-            FlatPair a, b;
-            a.load(Q);
-            uint32_t p = 0;
-            for (; p + 1 < npair; p += 2) {
-                b.load_after(Q, p + 1, a, zero);
-                a.test_signed_v(X, Y, Z, 2 * p, d, best, n_acc);
-                a.load_after(Q, min(p + 2, npair - 1), b, zero);
-                b.test_signed_v(X, Y, Z, 2 * p + 2, d, best, n_acc);
-            }
-            if (p < npair) a.test_signed_v(X, Y, Z, 2 * p, d, best, n_acc);
-        } else if (kVariant == 7 || kVariant == 8) {
-            // form 7: form 5 with V first (test_signed_v); 8: one pair per iteration
-            uint32_t p = 0;
-            if (kVariant == 7) {
-                for (; p + 1 < npair; p += 2) {
-                    FlatPair a, b;
-                    a.load(Q + 16 * (size_t)p);
-                    b.load(Q + 16 * (size_t)p + 16);
-                    a.test_signed_v(X, Y, Z, 2 * p, d, best, n_acc);
-                    b.test_signed_v(X, Y, Z, 2 * p + 2, d, best, n_acc);
-                }
-            }
-            for (; p < npair; p++) {
-                FlatPair a;
-                a.load(Q + 16 * (size_t)p);
-                a.test_signed_v(X, Y, Z, 2 * p, d, best, n_acc);
-            }
-        } else if (kVariant == 5) {
-            // form 4, two pairs per iteration
-            uint32_t p = 0;
-            for (; p + 1 < npair; p += 2) {
-                FlatPair a, b;
-                a.load(Q + 16 * (size_t)p);
-                b.load(Q + 16 * (size_t)p + 16);
-                a.test_signed(X, Y, Z, 2 * p, d, best, n_acc);
-                b.test_signed(X, Y, Z, 2 * p + 2, d, best, n_acc);
-            }
-            if (p < npair) {
-                FlatPair a;
-                a.load(Q + 16 * (size_t)p);
-                a.test_signed(X, Y, Z, 2 * p, d, best, n_acc);
-            }
-        } else {
-            // software pipelined: pair p + 1's scalar loads are issued once
-            // pair p's have arrived (scalar loads return out of order, so a
-            // wait is always for all of them) and overlap pair p's tests
-            const uint32_t zero = ntri >> 31;  // 0: scenes hold < 2^29 triangles
-            FlatPair a, b;
-            a.load(Q);
-            uint32_t p = 0;
-            for (; p + 1 < npair; p += 2) {
-                b.load_after(Q, p + 1, a, zero);
-                a.test(X, Y, Z, 2 * p, d, best, n_acc);
-                a.load_after(Q, min(p + 2, npair - 1), b, zero);
-                b.test(X, Y, Z, 2 * p + 2, d, best, n_acc);
-            }
-            if (p < npair) a.test(X, Y, Z, 2 * p, d, best, n_acc);
-        }
+    // pair p = triangles (2p, 2p+1): 13 float2 (e1, e2, d_t, d_q, d_w), 128 B;
+    // an odd count's last pair holds a dead twin (d_w = 0: never accepted)
+    const f2v* __restrict__ Q = reinterpret_cast<const f2v*>(P.tpair);
+    const f2v X = {rmd[0], rmd[0]}, Y = {rmd[1], rmd[1]}, Z = {rmd[2], rmd[2]};
+    const uint32_t npair = (ntri + 1) >> 1;
+    const uint32_t zero = ntri >> 31;  // 0: scenes hold < 2^29 triangles
+    FlatPair a, b;
+    a.load(Q);
+    uint32_t p = 0;
+    for (; p + 1 < npair; p += 2) {
+        b.load_after(Q, p + 1, a, zero);
+        a.test_signed_v(X, Y, Z, 2 * p, d, best, n_acc);
+        a.load_after(Q, min(p + 2, npair - 1), b, zero);
+        b.test_signed_v(X, Y, Z, 2 * p + 2, d, best, n_acc);
     }
+    if (p < npair) a.test_signed_v(X, Y, Z, 2 * p, d, best, n_acc);
     flat_shade_out<kWriteHit>(P, px, rmd, d, best);
     if (kCount) {
         wave_count_add(&P.counters[1], ntri);
@@ -2775,9 +1747,9 @@ __global__ __launch_bounds__(kTileWFlat * kTileH) void k_trace_flat(TraceParams 
     }
 }
 
-// Chunked flat list (forms 10-12, renders without counters): block b of a
+// Chunked flat list (RT_OPT_FLAT 12, the default; renders without counters): block b of a
 // grid of fine blocks x P.flat_chunks tests its tile's rays against chunk
-// b / fine of the pair list (form 9's loop: V first, pipelined loads) and
+// b / fine of the pair list (k_trace_flat's loop: V first, pipelined loads) and
 // folds each ray's nearest hit into P.flat_key[pixel] as the 64-bit minimum
 // of (w bits, triangle); k_flat_shade then shades every pixel from its key
 // and resets it.  w >= eps > 0, so the float bits order as the values, and
@@ -2941,26 +1913,16 @@ __device__ __forceinline__ void rel_split(const rt_kd_node& nd, float cx, float 
 }
 
 // init_cam_voxel_mem_cuda (TD/Camera.cu:137-162) into the dense interior
-// record layouts of rt_internal.h (v1: own box, 48 B; v2: children's boxes, 64 B).
+// record layout of rt_internal.h (the children's boxes, 64 B).
 __global__ void k_cam_nodes(const rt_kd_node* __restrict__ nodes, const int32_t* __restrict__ ids,
                             const uint32_t* __restrict__ node_ref, int64_t ninterior, float cx,
-                            float cy, float cz, float4* __restrict__ out, int version) {
+                            float cy, float cz, float4* __restrict__ out) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= ninterior) return;
     const rt_kd_node nd = nodes[ids[k]];
     float s1, s2;
     uint32_t axis;
     rel_split(nd, cx, cy, cz, s1, s2, axis);
-    if (version == 1) {
-        float b[6];
-        rel_box(nd, cx, cy, cz, b);
-        const float s1e = (float)((double)s1 + kEps);
-        out[3 * k] = make_float4(b[0], b[1], b[2], b[3]);
-        out[3 * k + 1] = make_float4(b[4], b[5], s1, s2);
-        out[3 * k + 2] = make_float4(__uint_as_float(node_ref[nd.left]), __uint_as_float(node_ref[nd.right]),
-                                     __uint_as_float(axis), s1e);
-        return;
-    }
     float lb[6], rb[6];
     rel_box(nodes[nd.left], cx, cy, cz, lb);
     rel_box(nodes[nd.right], cx, cy, cz, rb);
@@ -3057,26 +2019,6 @@ __global__ void k_unpack_rect(int32_t w, int32_t nranks, int32_t x0, int32_t x1,
     }
 }
 
-// The dispatch gate of frames in flight (rt_run_frames): one lane waits
-// until every block of the other lane's previous frame has started, so the
-// next frame's blocks fill the CUs the previous frame's tail frees, and two
-// frames never run in lockstep (their tails would coincide: r04c/r04e traces
-// of the driver's 20-frame run, both lanes' kernels 210-230 us, start to
-// start within 12 us).  k_trace_kd3 counts its started blocks (P.started);
-// the gate polls that count with vector loads (a VGPR address) and gives up
-// after `timeout` ticks of the 100 MHz counter, so it always ends.
-__global__ __launch_bounds__(64) void k_gate(const unsigned long long* started, unsigned long long target,
-                                           uint64_t timeout) {
-    if (threadIdx.x != 0) return;
-    int z;
-    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-    const unsigned long long* q = started + z;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target &&
-           __builtin_amdgcn_s_memrealtime() - t0 < timeout)
-        __builtin_amdgcn_s_sleep(2);
-}
-
 template <class K>
 int check_launch(const char* what) {
     hipError_t e = hipGetLastError();
@@ -3091,13 +2033,11 @@ TraceFn kd3_kernel(int rays, bool coarse) {
     if (coarse) {
         if (rays == 8) return k_coarse_kd3<8, T, H, C, S>;
         if (rays == 16) return k_coarse_kd3<16, T, H, C, S>;
-        if (rays == 32) return k_coarse_kd3<32, T, H, C, S>;
-        return k_coarse_kd3<64, T, H, C, S>;
+        return k_coarse_kd3<32, T, H, C, S>;
     }
     if (rays == 8) return k_trace_kd3<8, T, H, C, S>;
     if (rays == 16) return k_trace_kd3<16, T, H, C, S>;
-    if (rays == 32) return k_trace_kd3<32, T, H, C, S>;
-    return k_trace_kd3<64, T, H, C, S>;
+    return k_trace_kd3<32, T, H, C, S>;
 }
 
 // shadow: -1 none, else the any-hit push order (0..3), + 4 for counting
@@ -3106,7 +2046,6 @@ TraceFn kd3_kernel(int rays, bool coarse) {
 // work: one instance serves them.
 template <bool T, bool H, bool C>
 TraceFn kd_kernel(int version, int rays, int shadow, bool coarse) {
-    if (version == 1) return k_trace_kd<T, H, C>;
     if (version == 2) return k_trace_kd2<T, H, C>;
     if (shadow < 0) return kd3_kernel<T, H, C, 0>(rays, coarse);
     if constexpr (C) {

@@ -381,9 +381,9 @@ int rt_camera_error(rt_camera* c, int32_t* err, int reset);
 /* Kernel launch geometry and the traversal stack depth in use. */
 int rt_camera_info(const rt_camera* c, int32_t* w, int32_t* h, int32_t* max_depth);
 
-/* Tuning knobs (not in the reference): key 1 = KD kernel (1: per-lane DFS,
- * node-own box records; 2: per-lane DFS, child-box records; 3: wave-
- * cooperative item pool, default), key 2 = tile dispatch order (0: XCD-
+/* Tuning knobs (not in the reference): key 1 = KD kernel (2: per-lane DFS
+ * in the reference's visiting order, child-box records, its counters are the
+ * reference's; 3: wave-cooperative item pool, default), key 2 = tile dispatch order (0: XCD-
  * contiguous, 1: natural, 2: centre-out, 3: heaviest first by the cost an
  * earlier frame measured, default; every 16th frame of kernel 3 writes
  * its units' costs into page-locked host memory, read once that frame's
@@ -391,7 +391,7 @@ int rt_camera_info(const rt_camera* c, int32_t* w, int32_t* h, int32_t* max_dept
  * Every setting renders the identical frame. */
 #define RT_OPT_KERNEL 1
 #define RT_OPT_TILE_ORDER 2
-#define RT_OPT_RAYS 3 /* kernel 3: pixels per wave (64, 32, 16, 8; 0 = auto, default: 8 when this rank's
+#define RT_OPT_RAYS 3 /* kernel 3: pixels per wave (32, 16, 8; 0 = auto, default: 8 when this rank's
                          share of the object's screen rectangle is too small to fill the GPU with 16,
                          else 16; inside rt_run_frames' multi-frame launches (RT_LOOP_MULTIFRAME) 32
                          when that rectangle holds fewer than 8,192 16-pixel units, else 16) */
@@ -402,39 +402,22 @@ int rt_camera_info(const rt_camera* c, int32_t* w, int32_t* h, int32_t* max_dept
  * bracketed by events and the fastest is kept; never blocks, skipped under
  * stream capture).  Get returns the order in use. */
 #define RT_OPT_SHADOW_ORDER 6
-/* Flat-list kernel form (same frame): 0 one triangle per iteration, 1 two
- * per iteration, 2 two per iteration as packed float2 arithmetic,
- * 3 = 2 software pipelined, 4 = 2 over the signed pair layout with one min3
- * screen per triangle, 5 = 4 unrolled to two pairs, 6 = 5 behind one screen
- * branch per two pairs, 7 = 5 with v's numerator first (a wave whose rays
- * all have V <= 0 skips the rest of the pair), 8 = 7 one pair per
- * iteration, 9 = 7 software pipelined as 3; 10, 11, 12 (default), 13 = 9
- * over 8, 4, 16, 32 chunks of the list (a grid of short waves; the chunks'
- * nearest hits meet in a per-pixel 64-bit minimum, then a shading pass;
- * counting renders take 9). */
+/* Flat-list kernel form (same frame): 9 = one pass over the signed pair
+ * layout, packed float2 arithmetic, v's numerator first (a wave whose rays
+ * all have V <= 0 skips the rest of the pair), the next pair's scalar loads
+ * in flight during a pair's tests; 12 (default) = 9 over 16 chunks of the
+ * list (a grid of short waves; the chunks' nearest hits meet in a per-pixel
+ * 64-bit minimum, then a shading pass; counting renders take 9). */
 #define RT_OPT_FLAT 7
 #define RT_OPT_RAYS_USED 8 /* get only: the pixels per wave the last kernel-3 render used */
 /* get only: tiles of the current cost order (tile order 3, 16- and 8-ray
  * units) rendered as two halves (a 16-ray unit as two 8-ray rows, an 8-ray
- * unit as two 4-pixel halves): after the coop tiles, those costlier than 50 %
- * of the heaviest tile in grids of fewer than 2,048 tiles and 75 % in larger
- * ones, at most a quarter of the tiles counting the coop ones.  Costs are
- * pool iterations per unit (8 slots per tile: the 4 units and the second
- * halves).  The frame is the same either way. */
+ * unit as two 4-pixel halves): those costlier than 50 % of the heaviest tile
+ * in grids of fewer than 2,048 tiles and 75 % in larger ones, at most a
+ * quarter of the tiles.  Costs are pool iterations per unit (8 slots per
+ * tile: the 4 units and the second halves).  The frame is the same either
+ * way. */
 #define RT_OPT_SPLIT_USED 9
-/* get only: tiles at the head of the current cost order whose units each
- * render with a whole 4-wave block on one item pool (block-cooperative
- * units).  Off by default (measured slower with frames in flight, DESIGN.md
- * §4 round 4); diagnostics bit 8192 selects the tiles costlier than 60 % of
- * the heaviest (70 % in grids of 2,048 tiles or more, at most an eighth of
- * the tiles), bit 4096 every tile.  The frame is the same. */
-#define RT_OPT_COOP_USED 10
-/* multi-frame launches (RT_LOOP_MULTIFRAME): frames per group, 0 = the
- * default, 1..8.  A launch renders its frames in groups of this many whose
- * blocks interleave (the group's frames dispatch side by side, as frames on
- * separate lanes do); 1 renders them one after another (frame-major).  The
- * frames are the same either way. */
-#define RT_OPT_FRAME_GROUP 11
 int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value);
 int rt_camera_get_option(const rt_camera* c, int32_t key, int32_t* value);
 
