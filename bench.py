@@ -32,7 +32,11 @@ After the timed frames every line carries `device_err` (the camera's device
 error word; the run exits non-zero when it is set) and, at N = 1, a
 `frame_check`: the last timed frame against the oracle's committed full-frame
 hash (tests/golden/frame_hashes.json), or against an oracle render on this
-host when no hash matches.
+host when no hash matches.  With multi-frame launches as the headline (the
+default at N = 1 for a static KD frame), the line also carries
+`per_frame_loop`: --second-frames frames of the per-frame loop (two frames in
+flight on the library's render lanes), timed after the headline with their own
+settle and frame check -- the rate a loop with new input every frame sees.
 """
 from __future__ import annotations
 
@@ -106,6 +110,10 @@ def parse():
     ap.add_argument("--solo-when", default="before", choices=["before", "after"],
                     help="solo frames (the roofline's kernel time) run just before the warm-up-to-timed handover, "
                          "or after the timed frames")
+    ap.add_argument("--second-frames", type=int, default=1000,
+                    help="with multi-frame launches as the headline: also time this many frames of the per-frame "
+                         "loop (two frames in flight on the library's render lanes) after it and report them as "
+                         "the line's per_frame_loop object (0 = off)")
     ap.add_argument("--settle-ms", type=float, default=40.0,
                     help="untimed frames of the timed loop itself for about this much time right before the timed "
                          "region (a moving object: one pass over the timed poses, native loop only; 0: none)")
@@ -895,6 +903,37 @@ def main():
         last = outs[loop.last_set()] if not isinstance(loop, PyLoop) else out
         frame_check = frame_check_n1(last.cpu().numpy().view(np.uint32), pts, nodes, cam_kw, a,
                                      xform=xf if masks else None)
+    per_frame_loop = None
+    if persistent and a.second_frames > 0:
+        # VERDICT r04 item 7 / ADVICE r04: the headline batches copies of one
+        # static frame per launch; the per-frame loop a moving scene would run
+        # (rt_run_frames with two frames in flight on the render lanes, no
+        # multi-frame launches) is timed here over its own frames, after the
+        # same kind of settle, and reported beside it with its own frame check
+        pl = R.FrameLoop(cam, outs, xform=xf, mode=a.mode, flags=sflag, render_stream=sptr, event_every=0,
+                         inflight=inflight)
+        ts = time.perf_counter()
+        pl.run(50)
+        torch.cuda.synchronize(dev)
+        per = (time.perf_counter() - ts) / 50
+        n2 = int(math.ceil(a.settle_ms * 1e-3 / max(per, 1e-6)))
+        pl.run(n2)
+        torch.cuda.synchronize(dev)
+        t2 = time.perf_counter()
+        _, _, host2 = pl.run(a.second_frames)
+        torch.cuda.synchronize(dev)
+        el2 = time.perf_counter() - t2
+        err2 = cam.device_error(reset=True)
+        check2 = frame_check_n1(outs[pl.last_set()].cpu().numpy().view(np.uint32), pts, nodes, cam_kw, a)
+        per_frame_loop = {"loop": f"per-frame loop (rt_run_frames), {inflight} frames in flight on the library's "
+                                  f"render lanes, no multi-frame launches",
+                          "value": round(a.second_frames / el2, 2), "unit": "frames/s",
+                          "mray_per_s": round(a.second_frames * w * h / el2 / 1e6, 2),
+                          "frames": a.second_frames, "ms_per_frame": round(1e3 * el2 / a.second_frames, 5),
+                          "settle_frames": 50 + n2, "host_us_per_frame": round(1e3 * host2 / a.second_frames, 2),
+                          "device_err": err2, "frame_check": check2}
+        if err2:
+            dev_err = dev_err or err2
     ranks_info = None
     if multi:
         ok = gathered_frame_ok(loop)
@@ -1104,6 +1143,7 @@ def main():
                           else "k_trace_flat",
                 "kernel_options": {"kernel": a.kernel, "tile_order": a.tile_order,
                                    "rays_per_wave": cam.get_option(_lib.RT_OPT_RAYS_USED),
+                                   "fast_walks": cam.get_option(_lib.RT_OPT_FAST_USED),
                                    "rays_per_wave_option": a.rays,
                                    "record_order": trixel.get_option(_lib.RT_SCENE_ORDER),
                                    "treelet_height": trixel.get_option(_lib.RT_SCENE_TREELET_HEIGHT),
@@ -1143,6 +1183,10 @@ def main():
         }
         if frame_check is not None:
             res["frame_check"] = frame_check
+        if per_frame_loop is not None:
+            res["per_frame_loop"] = per_frame_loop
+            if per_frame_loop["frame_check"].get("matches_oracle") is False:
+                frame_check = per_frame_loop["frame_check"]
         if a.deliver and world == 1:
             res["delivery"] = delivery(cam, R, torch, dev, w, h, xf, a.mode, sflag, a.steps, a.warmup)
         if not a.no_cpu_baseline and world == 1:

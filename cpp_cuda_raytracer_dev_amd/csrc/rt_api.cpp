@@ -72,6 +72,8 @@ struct rt_camera {
     uint64_t prepared_version = 0;
     float4* d_trec = nullptr;        // camera-relative triangle records
     float4* d_inode = nullptr;       // camera-relative interior nodes
+    int32_t* d_cam_flags = nullptr;  // k_cam_nodes' flags (kCamTinyS1, kCamUnordered) ...
+    int32_t cam_flags = kCamUnordered;  // ... read back once the records are built
     float4* d_tpair = nullptr;       // flat variant 2: camera-relative triangle pairs
     uint32_t trec_cap = 0;
     int64_t inode_cap = 0;           // in float4
@@ -148,8 +150,21 @@ struct rt_camera {
     uint64_t mem_gen = ~0ull;
     uint64_t order_gen = ~0ull;              // generation whose cost order d_order holds
     int32_t order_split = 0;                 // split tiles at the head of that cost order
+    // the last cost orders of two grids (order_key): a camera that
+    // alternates between two tilings -- rt_run_frames' multi-frame rays rule
+    // against the per-frame one on a small frame -- starts each
+    // switch with the order it last measured there, not the centre order
+    struct KeptOrder {
+        int64_t key[8] = {};
+        std::vector<int32_t> ord;
+        std::vector<uint32_t> mem;  // cost_mem with it
+        int32_t split = 0;
+    };
+    KeptOrder kept[2];
+    int kept_next = 0;
     int rays = 0;                    // kOptRays: pixels per wave of kernel 3 (0: auto_rays)
     int last_rays = 0;               // the pixels per wave the last kernel-3 render used
+    int last_fast = 0;               // whether it took the kFast walks (fast_proof)
     int items = 2;                   // kOptItems: items per lane per pool iteration
     int flat_variant = 12;           // kOptFlat: flat-list kernel form
     // chunked flat forms: one per-pixel key buffer per stream that renders
@@ -267,12 +282,19 @@ int prepare_camera_object(rt_camera* c) {
             if ((rc = dev_alloc(&c->d_inode, (size_t)need, "hipMalloc(inode)"))) return rc;
             c->inode_cap = need;
         }
+        if (!c->d_cam_flags && (rc = dev_alloc(&c->d_cam_flags, 1, "hipMalloc(cam flags)"))) return rc;
         // init_camera_voxel_device_memory (TD/Camera.cu:163-187)
-        if ((rc = launch_cam_nodes(s->d_nodes, s->d_interior_ids, s->d_node_ref, s->ninterior, c->pos,
-                                   c->d_inode, nullptr)))
+        if ((rc = hip_check(hipMemset(c->d_cam_flags, 0, sizeof(int32_t)), "memset cam flags")) ||
+            (rc = launch_cam_nodes(s->d_nodes, s->d_interior_ids, s->d_node_ref, s->ninterior, c->pos,
+                                   c->d_inode, c->d_cam_flags, nullptr)))
             return rc;
     }
     if ((rc = hip_check(hipDeviceSynchronize(), "camera object prep"))) return rc;
+    c->cam_flags = 0;
+    if (s->d_nodes && s->ninterior > 0 &&
+        (rc = hip_check(hipMemcpy(&c->cam_flags, c->d_cam_flags, sizeof(int32_t), hipMemcpyDeviceToHost), "D2H cam flags")))
+        return rc;
+    c->geom_gen++;  // cached launch parameters carry the flags
     c->prepared_version = s->tree_version + 1;
     return RT_OK;
 }
@@ -557,6 +579,50 @@ bool cost_sample_now(rt_camera* c, hipStream_t st) {
     return true;
 }
 
+void keep_order(rt_camera* c, const std::vector<int32_t>& ord, int32_t split) {
+    rt_camera::KeptOrder* k = nullptr;
+    for (auto& e : c->kept)
+        if (std::equal(e.key, e.key + 8, c->order_key)) k = &e;
+    if (!k) {
+        k = &c->kept[c->kept_next];
+        c->kept_next ^= 1;
+    }
+    std::copy(c->order_key, c->order_key + 8, k->key);
+    k->ord = ord;
+    k->mem = c->cost_mem;
+    k->split = split;
+}
+
+// A fresh grid (no cost order yet) that held a cost order before: upload it
+// (on st, behind ensure_order's centre order; frames on other streams wait
+// for it as for cost_feedback's uploads).
+int restore_order(rt_camera* c, const TraceParams& p, hipStream_t st) {
+    const int64_t n = (int64_t)p.tiles_x * p.block_rows;
+    if (c->order_gen == c->layout_gen || c->order_pending || n > c->host_cap) return RT_OK;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return RT_OK;
+    const rt_camera::KeptOrder* k = nullptr;
+    for (const auto& e : c->kept)
+        if ((int64_t)e.ord.size() == n && std::equal(e.key, e.key + 8, c->order_key)) k = &e;
+    if (!k || c->noused > 0) return RT_OK;  // (only before the grid's first launch)
+    std::copy(k->ord.begin(), k->ord.end(), c->h_order);
+    int rc;
+    if ((rc = hip_check(hipMemcpyAsync(c->d_order, c->h_order, sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice, st),
+                        "H2D kept cost order")) ||
+        (rc = hip_check(hipEventRecord(c->order_ev, st), "order event")))
+        return rc;
+    c->cost_up_stream = st;
+    c->cost_up_valid = true;
+    c->order_pending = true;
+    c->order_split = k->split;
+    c->order_gen = c->layout_gen;
+    if ((int64_t)k->mem.size() == n) {
+        c->cost_mem = k->mem;
+        c->mem_gen = c->layout_gen;
+    }
+    return RT_OK;
+}
+
 int cost_feedback(rt_camera* c, const TraceParams& p, void* stream, bool sampled) {
     hipStream_t st = (hipStream_t)stream;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -638,6 +704,7 @@ int cost_feedback(rt_camera* c, const TraceParams& p, void* stream, bool sampled
         c->order_pending = true;
         c->order_split = split;  // launches after this upload (stream order) use it
         c->order_gen = c->layout_gen;
+        keep_order(c, ord, split);
         return RT_OK;
     }
     if (!sampled) {
@@ -686,7 +753,36 @@ struct FrameGeom {
     // renders only (fill_params): the fine region the camera holds for this
     // tiling (set_fine_region), or null for the exact region
     Hold* hold = nullptr;
+    int32_t cam_flags = kCamUnordered;  // k_cam_nodes' flags of the camera's records (renders only)
 };
+
+// kFast walks of kernel 3 (rt_kernels_impl.h order_node, slab_fast): the
+// identity transform, ordered child boxes inside their parents' (k_cam_nodes),
+// and a proof that every box's entry parameter maxt0 is at least 2^-20 for
+// every ray of the frame, so that the reference's double entry test
+// (TD/Trixel.cu:146) is the float mint1 >= maxt0.  The proof: an axis k along
+// which every pixel's direction has one sign -- its numerator n + u x + v y
+// is affine in the pixel, so its sign is fixed when it has that sign at the
+// frame's four corners by a margin of 1e-5 of its terms' magnitudes (which
+// covers the float evaluation; the positive normalisation keeps the sign) --
+// and the root box, which holds every box of the tree, lies at least 2^-19
+// beyond the eye on that side.  Then every box's t_k = bound * (1/r_k) >=
+// 2^-19 / (1 + 2^-22) >= 2^-20 (|r_k| <= 1 + 2^-22 after the 21-step
+// normalisation), and maxt0 >= t_k.  The default view (the eye at z = -1
+// looking +z, the object at z > -0.1) proves it along z.
+bool fast_proof(const FrameGeom& g, const TraceParams& p) {
+    if (!p.plain_xf || (g.cam_flags & kCamUnordered) || g.root_leaf) return false;
+    const double fx = g.w - 1, fy = g.h - 1;
+    for (int k = 0; k < 3; k++) {
+        const double n = g.n_mod[k], u = g.u_mod[k], v = g.v_mod[k];
+        const double c0 = n, c1 = n + u * fx, c2 = n + v * fy, c3 = n + u * fx + v * fy;
+        const double e = 1e-5 * (std::fabs(n) + std::fabs(u) * fx + std::fabs(v) * fy);
+        const double lo = std::min(std::min(c0, c1), std::min(c2, c3)), hi = std::max(std::max(c0, c1), std::max(c2, c3));
+        if (lo > e && g.root_box[2 * k] >= 0x1p-19f) return true;
+        if (hi < -e && g.root_box[2 * k + 1] <= -0x1p-19f) return true;
+    }
+    return false;
+}
 
 bool root_rect(const FrameGeom& g, const TraceParams& p, double r[4]) {
     const float* X = p.xf;
@@ -979,6 +1075,8 @@ bool frame_geometry(const FrameGeom& g, const float* xform, const rt_tile* tile,
     p.block_rows = ((nbands + p.nranks - 1) / p.nranks) * (kTileH / p.tile_h);
     p.plain_xf = 1;
     for (int k = 0; k < 12; k++) p.plain_xf &= (p.xf[k] == ident[k]) ? 1 : 0;
+    p.fast = kernel == 3 && !(g.debug & 2048) && fast_proof(g, p) ? 1 : 0;  // debug bit 2048: never
+    p.tiny_s1 = (g.cam_flags & kCamTinyS1) ? 1 : 0;
     // Far groups go to the fine kernel's extra blocks when every coarse group
     // can be far (identity transform, interior root, no diagnostics);
     // otherwise to k_coarse_kd3.
@@ -1004,6 +1102,7 @@ FrameGeom camera_geom(rt_camera* c) {
     g.debug = c->debug;
     find_tiny_groups(c);
     g.tiny = &c->tiny_groups;
+    g.cam_flags = c->cam_flags;
     return g;
 }
 
@@ -1059,7 +1158,9 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
         if (rc) return rc;
         p.order = c->d_order;
         if (c->tile_order >= 3 && kernel == 3) {
-            if ((rc = ensure_cost(c, std::max<int64_t>(all_tiles(c, p), (int64_t)p.tiles_x * p.block_rows)))) return rc;
+            if ((rc = ensure_cost(c, std::max<int64_t>(all_tiles(c, p), (int64_t)p.tiles_x * p.block_rows))) ||
+                (rc = restore_order(c, p, st)))
+                return rc;
             p.cost = c->d_cost_host;  // (marks tile order 3; render_common passes it to sampled frames only)
         }
     }
@@ -1570,7 +1671,10 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
         const int64_t npair = (c->obj->ntri + 1) / 2;
         if (p.flat_chunks > npair) p.flat_chunks = (int32_t)npair;
     }
-    if (mode == RT_MODE_KD && effective_kernel(c) == 3) c->last_rays = p.rays;
+    if (mode == RT_MODE_KD && effective_kernel(c) == 3) {
+        c->last_rays = p.rays;
+        c->last_fast = p.fast;
+    }
     int trial;
     p.any_order = any_order_for(c, flags, stream, trial) | ((c->debug & 16) ? 4 : 0);
     hipStream_t st = (hipStream_t)stream;
@@ -1957,6 +2061,7 @@ extern "C" void rt_camera_destroy(rt_camera* c) {
     dev_free(c->d_hit);
     dev_free(c->d_counters);
     dev_free(c->d_err);
+    dev_free(c->d_cam_flags);
     dev_free(c->d_trec);
     dev_free(c->d_inode);
     dev_free(c->d_tpair);
@@ -2056,6 +2161,7 @@ extern "C" int rt_camera_get_option(const rt_camera* c, int32_t key, int32_t* va
     case kOptRaysUsed: *value = c->last_rays; return RT_OK;
     case kOptDebug: *value = c->debug; return RT_OK;
     case kOptSplitUsed: *value = c->order_split; return RT_OK;
+    case kOptFastUsed: *value = c->last_fast; return RT_OK;
     case kOptShadowOrder: *value = c->shadow_order >= 0 ? c->shadow_order : c->any_best; return RT_OK;
     default: return fail(RT_ERR_INVALID, "rt_camera_get_option: unknown key %d", key);
     }
@@ -2123,7 +2229,22 @@ static int run_frames_multiframe(rt_camera* c, const rt_frame_loop* a, int32_t n
     } mf_scope(c);
     hipStream_t rs = (hipStream_t)a->render_stream;
     const rt_tile* tile = a->tile.nranks > 0 ? &a->tile : nullptr;
-    std::vector<std::pair<int, int32_t>> timed;  // (event pair, frames) of bracketed launches
+    // bracketed launches reuse a ring of kRing event pairs (single-frame
+    // launches before a cost order exists would otherwise take a pair per
+    // frame): a pair is read back before it is recorded again
+    constexpr int kRing = 32;
+    int32_t ring_frames[kRing] = {};
+    int64_t nbracket = 0;
+    double sum = 0.0;
+    int32_t cnt = 0;
+    auto harvest = [&](int slot) {
+        float ms = 0.0f;
+        if (hipEventSynchronize(c->loop_ev[(size_t)(2 * slot + 1)]) == hipSuccess &&
+            hipEventElapsedTime(&ms, c->loop_ev[(size_t)(2 * slot)], c->loop_ev[(size_t)(2 * slot + 1)]) == hipSuccess) {
+            sum += ms;
+            cnt += ring_frames[slot];
+        }
+    };
     int rc = RT_OK;
     const int every = a->event_every;
     const auto h0 = std::chrono::steady_clock::now();
@@ -2131,7 +2252,7 @@ static int run_frames_multiframe(rt_camera* c, const rt_frame_loop* a, int32_t n
         const bool have_order = c->tile_order != 3 || c->order_gen == c->layout_gen;
         const int32_t chunk = have_order ? std::min(nframes - j, kPersistChunk) : 1;
         const bool time_it = every > 0;
-        const int pair = (int)timed.size();
+        const int pair = (int)(nbracket % kRing);
         if (time_it && (int64_t)c->loop_ev.size() < 2 * (pair + 1)) {
             hipEvent_t e0 = nullptr, e1 = nullptr;
             if ((rc = hip_check(hipEventCreate(&e0), "loop timing event")) ||
@@ -2140,6 +2261,7 @@ static int run_frames_multiframe(rt_camera* c, const rt_frame_loop* a, int32_t n
             c->loop_ev.push_back(e0);
             c->loop_ev.push_back(e1);
         }
+        if (time_it && nbracket >= kRing) harvest(pair);
         if (time_it && (rc = hip_check(hipEventRecord(c->loop_ev[(size_t)(2 * pair)], rs), "loop timing"))) break;
         const PersistArgs pf{chunk, (int32_t)((*seq) % a->nbuf), a->nbuf, a->d_local};
         const int k = (int)((*seq) % a->nbuf);
@@ -2149,7 +2271,8 @@ static int run_frames_multiframe(rt_camera* c, const rt_frame_loop* a, int32_t n
         if (rc) break;
         if (time_it) {
             if ((rc = hip_check(hipEventRecord(c->loop_ev[(size_t)(2 * pair + 1)], rs), "loop timing"))) break;
-            timed.emplace_back(pair, done);
+            ring_frames[pair] = done;
+            nbracket++;
         }
         j += done;
         *seq += done;
@@ -2161,16 +2284,7 @@ static int run_frames_multiframe(rt_camera* c, const rt_frame_loop* a, int32_t n
         (void)hipDeviceSynchronize();
         return rc;
     }
-    double sum = 0.0;
-    int32_t cnt = 0;
-    for (const auto& tp : timed) {
-        float ms = 0.0f;
-        if (hipEventElapsedTime(&ms, c->loop_ev[(size_t)(2 * tp.first)], c->loop_ev[(size_t)(2 * tp.first + 1)]) ==
-            hipSuccess) {
-            sum += ms;
-            cnt += tp.second;
-        }
-    }
+    for (int64_t b = std::max<int64_t>(0, nbracket - kRing); b < nbracket; b++) harvest((int)(b % kRing));
     // per frame: the launches' bracketed time over the frames they rendered
     if (kernel_ms_avg) *kernel_ms_avg = cnt ? sum / cnt : 0.0;
     if (kernel_ms_frames) *kernel_ms_frames = cnt;

@@ -33,11 +33,16 @@ constexpr int kTileWKd = 16;
 constexpr int kBlockMax = 256;
 
 // Interior record (64 B) of the KD layout: the two children's
-// camera-relative boxes plus this node's split planes and child references.
+// camera-relative boxes plus this node's split thresholds and child references.
 //   r0 = (L.t0x, L.t1x, L.t0y, L.t1y)   r1 = (L.t0z, L.t1z, R.t0x, R.t1x)
-//   r2 = (R.t0y, R.t1y, R.t0z, R.t1z)   r3 = (s1, s2, Lref | axis << 29, Rref)
+//   r2 = (R.t0y, R.t1y, R.t0z, R.t1z)   r3 = (S_gt, S_lt, Lref | axis << 29, Rref | tiny_s1 << 29)
+// (k_cam_nodes: S_gt / S_lt are the exact float forms of the reference's
+// double tests against s2; s1 = L's high and s2 = R's low bound on the axis.)
 constexpr uint32_t kRefMask = 0x1FFFFFFFu;
 constexpr uint32_t kAxisShift = 29;
+constexpr uint32_t kTinyS1Bit = 1u << 29;
+// k_cam_nodes' flags of a camera's records
+constexpr int32_t kCamTinyS1 = 1, kCamUnordered = 2;
 
 // rt_camera_set_option keys.
 enum Option : int32_t {
@@ -50,12 +55,13 @@ enum Option : int32_t {
     kOptFlat = 7,       // flat-list kernel: 9 one pass, 12 the list in 16 chunks (default)
     kOptRaysUsed = 8,   // get only: pixels per wave of the last kernel-3 render
     kOptSplitUsed = 9,  // get only: split tiles at the head of the current cost order (kernel 3)
+    kOptFastUsed = 10,  // get only: whether the last kernel-3 render took the kFast walks
     kOptDebug = 100,    // diagnostics: 1 = skip traversal, 2 = per-wave timestamps, 4 = every group
                         // coarse, 8 = coarse kernel on a side stream beside the fine one,
                         // 16 = counted shadow walks stop at occluders (the timed walk's work),
                         // 32 = counting renders stop after the root test, 64 = order / cost
                         // buffers sized for the current grid only, 256 = no held fine region,
-                        // 512 = no split tiles, 1024 = no two-level iterations
+                        // 512 = no split tiles, 1024 = no two-level iterations, 2048 = no kFast walks
     kOptPoolCap = 101,  // tests: shrink kernel 3's item pool (66..kPoolCap) to force its fallback
 };
 constexpr int kPoolCapMax = 640;
@@ -123,6 +129,11 @@ struct TraceParams {
     int32_t fill_blocks;           // blocks after the fine grid filling far groups (fused mode)
     int64_t coarse_groups;         // total coarse groups
     int32_t plain_xf;              // object transform is the identity (rotation 1, offset 0)
+    // kernel 3's kFast walks apply (rt_api.cpp fast_proof): identity
+    // transform, ordered boxes, and every box's entry parameter >= 2^-20
+    // for every ray of the frame
+    int32_t fast;
+    int32_t tiny_s1;               // some interior record of the camera has the tiny-s1 flag
     int32_t far_rect[4];           // root box's screen rectangle + 2 px (x0, x1, y0, y1; frame pixels)
     int32_t far_all;               // every group background: the box lies behind the eye (box_behind)
     int32_t tile_w, tile_h;        // pixels per block (tile_h divides the 8-row band)
@@ -173,7 +184,7 @@ int launch_cam_tri(const float4* tri_world, uint32_t ntri, const float pos[3],
 int launch_pair_tri(const float4* trec, uint32_t ntri, float4* tpair, void* stream);
 int launch_cam_nodes(const rt_kd_node* nodes, const int32_t* interior_ids,
                      const uint32_t* node_ref, int64_t ninterior, const float pos[3],
-                     float4* inode, void* stream);
+                     float4* inode, int32_t* flags, void* stream);
 // part: the coarse groups then the fine tiles (kPartAll), or one of them.
 enum LaunchPart : int { kPartAll = 0, kPartFine = 1, kPartCoarse = 2 };
 int launch_trace(const TraceParams& p, uint32_t mode, uint32_t flags, int kernel_version,

@@ -26,10 +26,10 @@ int launch_cam_tri(const float4* tri_world, uint32_t ntri, const float pos[3], f
 }
 
 int launch_cam_nodes(const rt_kd_node* nodes, const int32_t* ids, const uint32_t* node_ref,
-                     int64_t ninterior, const float pos[3], float4* inode, void* stream) {
+                     int64_t ninterior, const float pos[3], float4* inode, int32_t* flags, void* stream) {
     if (ninterior == 0) return RT_OK;
     k_cam_nodes<<<(unsigned)((ninterior + 255) / 256), 256, 0, (hipStream_t)stream>>>(
-        nodes, ids, node_ref, ninterior, pos[0], pos[1], pos[2], inode);
+        nodes, ids, node_ref, ninterior, pos[0], pos[1], pos[2], inode, flags);
     return check_launch<void>("k_cam_nodes");
 }
 

@@ -262,6 +262,15 @@ __device__ __forceinline__ void load_record(const float4* __restrict__ p, float4
                  "v"(r3.w));
 }
 
+// s1 (the left child's high bound) and s2 (the right child's low bound) on
+// the cut axis, from an interior record's boxes (k_cam_nodes).
+__device__ __forceinline__ float rec_s1(float4 r0, float4 r1, uint32_t axis) {
+    return axis == 0 ? r0.y : axis == 1 ? r0.w : r1.y;
+}
+__device__ __forceinline__ float rec_s2(float4 r1, float4 r2, uint32_t axis) {
+    return axis == 0 ? r1.z : axis == 1 ? r2.x : r2.z;
+}
+
 struct Ray {
     float rx, ry, rz;          // object-space direction, TD/Trixel.cu:64-66
     float odx, ody, odz;       // object translation, TD/Trixel.cu:60-62
@@ -273,13 +282,6 @@ struct Ray {
 typedef float f2v __attribute__((ext_vector_type(2)));
 
 // Slab parameters of one node, TD/Trixel.cu:76-95: entry maxt0, exit mint1.
-// kNoOff: the walk's rays have no object offset and no zero component, so
-// every od/r term is a signed zero (0/r, r != 0): adding it changes at most
-// the sign of a zero t, which no comparison downstream tells apart (entry
-// and exit tests, the split-plane order, the products t * dir); the six adds
-// per box are skipped.  A ray with a zero component keeps them (0/0 = NaN
-// drops that axis from the reference's test, TD/Trixel.cu:94-95).
-template <bool kNoOff = false>
 __device__ __forceinline__ void slab_vals(const Ray& R, float lx, float hx, float ly, float hy, float lz,
                                           float hz, float& maxt0, float& mint1) {
     const float t0x = R.sx ? lx * R.ix : hx * R.ix;
@@ -288,13 +290,24 @@ __device__ __forceinline__ void slab_vals(const Ray& R, float lx, float hx, floa
     const float t1y = R.sy ? hy * R.iy : ly * R.iy;
     const float t0z = R.sz ? lz * R.iz : hz * R.iz;
     const float t1z = R.sz ? hz * R.iz : lz * R.iz;
-    if (kNoOff) {
-        maxt0 = fmaxf(t0z, fmaxf(t0x, t0y));
-        mint1 = fminf(t1z, fminf(t1x, t1y));
-        return;
-    }
     maxt0 = fmaxf(t0z + R.oz, fmaxf(t0x + R.ox, t0y + R.oy));
     mint1 = fminf(t1z + R.oz, fminf(t1x + R.ox, t1y + R.oy));
+}
+
+// The same for a kFast walk (untranslated, every ray component normal and
+// nonzero, ordered boxes): each od/r term is a signed zero (0/r), and adding
+// it changes at most the sign of a zero t, which no comparison downstream
+// tells apart (the entry test, the split-plane order, the products t * dir),
+// so it is skipped; with 1/r finite and nonzero and lo <= hi, the product of
+// lo is the smaller one exactly when r > 0, so min / max of an axis's two
+// products are the reference's sign-selected t0 / t1.  Each axis's two
+// products are one v_pk_mul_f32 (each half rounds as the scalar multiply
+// does) of the record's (lo, hi) pair by the broadcast 1/r.
+__device__ __forceinline__ void slab_fast(f2v bx, f2v by, f2v bz, float ix, float iy, float iz, float& maxt0,
+                                          float& mint1) {
+    const f2v px = bx * ix, py = by * iy, pz = bz * iz;
+    maxt0 = fmaxf(fminf(pz.x, pz.y), fmaxf(fminf(px.x, px.y), fminf(py.x, py.y)));
+    mint1 = fminf(fmaxf(pz.x, pz.y), fminf(fmaxf(px.x, px.y), fmaxf(py.x, py.y)));
 }
 
 // Slab test of one node, TD/Trixel.cu:76-95,146: entry/exit parameters and
@@ -425,24 +438,28 @@ __global__ __launch_bounds__(kTileWKd * kTileH) void k_trace_kd2(TraceParams P) 
             load_record(P.inode + 4 * (size_t)ref, r0, r1, r2, r3);
             const uint32_t lw = __float_as_uint(r3.z);
             const uint32_t axis = (lw >> kAxisShift) & 3u;
-            const uint32_t L = lw & ~(3u << kAxisShift), Rr = __float_as_uint(r3.w);
+            const uint32_t L = lw & ~(3u << kAxisShift), Rr = __float_as_uint(r3.w) & ~kTinyS1Bit;
             const float dir = axis == 0 ? dir_a[0] : axis == 1 ? dir_a[1] : dir_a[2];
             const float mx = cmax * dir, mn = cmin * dir;
-            float s1, s2;
+            float s1;
+            bool lt, gt;  // the reference's double tests against s2 (TD/Trixel.cu:155-157)
             if (kTranslated) {
                 const float ds = axis == 0 ? ds_a[0] : axis == 1 ? ds_a[1] : ds_a[2];
-                s1 = (float)((double)r3.x + kEps + (double)ds);
-                s2 = r3.y + ds;
-            } else {  // ds == 0: the same values without the +0
-                s1 = pred::add_eps(r3.x);
-                s2 = r3.y;
+                s1 = (float)((double)rec_s1(r0, r1, axis) + kEps + (double)ds);
+                const float s2 = rec_s2(r1, r2, axis) + ds;
+                lt = pred::lt_eps(mx, s2);
+                gt = pred::gt_eps(mn, s2);
+            } else {  // ds == 0: the record's exact float thresholds
+                s1 = pred::add_eps(rec_s1(r0, r1, axis));
+                lt = mx < r3.y;
+                gt = mn > r3.x;
             }
             // Push order of TD/Trixel.cu:155-168.  `first` is popped next,
             // `second` (if pushed) after first's subtree.
             bool left_first, push_second;
-            if (pred::lt_eps(mx, s2)) {
+            if (lt) {
                 left_first = true;
-                push_second = pred::gt_eps(mn, s2);
+                push_second = gt;
             } else {
                 left_first = false;
                 push_second = (mn < s1 || mx < s1);
@@ -707,11 +724,13 @@ __device__ __forceinline__ const float4* record_of(const TraceParams& P, uint32_
 // The per-ray data of an item's ray from LDS (see store_ray), as the float4s
 // (q2 = (odz/rz, dir per axis), q3 = (od, ds axis 0), q4 = (ds axes 1-2,
 // Lmax, hit triangle)) the visits read.
-template <bool kTranslated, int kStride>
+// kFast walks read the first three fields only (direction and 1/r: no
+// offsets, and the direction per cut axis is the component itself).
+template <bool kTranslated, int kStride, bool kFast = false>
 __device__ __forceinline__ void ray_of(const float2* rd, Ray& Q, float4& q2, float4& q3, float4& q4) {
-    const float2 f0 = rd[0], f1 = rd[kStride], f2 = rd[2 * kStride], f3 = rd[3 * kStride], f4 = rd[4 * kStride],
-                 f5 = rd[5 * kStride];
     const float2 z = make_float2(0.0f, 0.0f);
+    const float2 f0 = rd[0], f1 = rd[kStride], f2 = rd[2 * kStride];
+    const float2 f3 = kFast ? z : rd[3 * kStride], f4 = kFast ? z : rd[4 * kStride], f5 = kFast ? z : rd[5 * kStride];
     const float2 f6 = kTranslated ? rd[6 * kStride] : z, f7 = kTranslated ? rd[7 * kStride] : z,
                  f8 = kTranslated ? rd[8 * kStride] : z, f9 = kTranslated ? rd[9 * kStride] : z;
     q2 = make_float4(f4.x, f4.y, f5.x, f5.y);
@@ -764,34 +783,57 @@ __device__ __forceinline__ void count_order(const Order& o, uint32_t& n_int, uin
 // from its child-box record's split word r3 and its children's slab values
 // (lt0, lt1) and (rt0, rt1).  kCount: the reference's visit counters of the
 // node's children (when `real`).
-template <bool kTranslated, bool kCount>
-__device__ __forceinline__ void order_node(float4 q2, float4 q3, float4 q4, float t0, float t1, float4 r3, float lt0,
+//
+// kFast (untranslated walks of rays with normal, nonzero components, under
+// the frame proof P.fast): the direction per cut axis is the ray component
+// itself (r_a * 1 + r_b * 0 + r_c * 0 == r_a for finite nonzero r), and the
+// entry test mint1 >= maxt0 - 1e-16 && maxt0 > -1e-16 (TD/Trixel.cu:146) is
+// mint1 >= maxt0: P.fast holds only when every box's maxt0 is >= 2^-20 for
+// every ray of the frame (rt_api.cpp fast_proof), where maxt0 - 1e-16 rounds
+// to a double above the float below maxt0.
+template <bool kTranslated, bool kCount, bool kFast = false>
+__device__ __forceinline__ void order_node(const TraceParams& P, const Ray& Q, float4 q2, float4 q3, float4 q4,
+                                           float t0, float t1, float4 r0, float4 r1, float4 r2, float4 r3, float lt0,
                                            float lt1, float rt0, float rt1, bool real, Order& o, uint32_t& n_int,
                                            uint32_t& n_desc) {
-    const uint32_t lw = __float_as_uint(r3.z);
+    const uint32_t lw = __float_as_uint(r3.z), rw = __float_as_uint(r3.w);
     const uint32_t axis = (lw >> kAxisShift) & 3u;
-    const uint32_t L = lw & ~(3u << kAxisShift), Rr = __float_as_uint(r3.w);
-    const float dir = axis == 0 ? q2.y : axis == 1 ? q2.z : q2.w;
+    const uint32_t L = lw & ~(3u << kAxisShift), Rr = rw & ~kTinyS1Bit;
+    const float dir = kFast ? (axis == 0 ? Q.rx : axis == 1 ? Q.ry : Q.rz) : (axis == 0 ? q2.y : axis == 1 ? q2.z : q2.w);
     const float mx = t0 * dir, mn = t1 * dir;
-    // The reference's double-promoted epsilon tests (TD/Trixel.cu:146-157).
-    float s1, s2;
-    bool left_first, push_second, lpass, rpass;
+    // The reference's double-promoted epsilon tests (TD/Trixel.cu:146-157):
+    // against s2 through the record's exact float thresholds (k_cam_nodes)
+    // unless the object is translated
+    const float s1r = rec_s1(r0, r1, axis);
+    float s1;
+    bool left_first, pa;
     if (kTranslated) {
         const float ds = axis == 0 ? q3.w : axis == 1 ? q4.x : q4.y;
-        s1 = (float)((double)r3.x + kEps + (double)ds);
-        s2 = r3.y + ds;
+        s1 = (float)((double)s1r + kEps + (double)ds);
+        const float s2 = rec_s2(r1, r2, axis) + ds;
+        left_first = pred::lt_eps_ref(mx, s2);
+        pa = pred::gt_eps_ref(mn, s2);
     } else {
-        s2 = r3.y;
+        left_first = mx < r3.y;
+        pa = mn > r3.x;
+        if (kFast) {
+            // (float)((double)s1 + 1e-16) == s1 unless s1 is tiny (the
+            // record's flag; the camera's P.tiny_s1 says whether any is):
+            // the double form for those, behind a wave-uniform branch
+            s1 = s1r;
+            if (P.tiny_s1) {
+                const bool tiny = (rw & kTinyS1Bit) != 0;
+                if (__ballot(tiny) != 0ull) s1 = tiny ? pred::add_eps_ref(s1r) : s1r;
+            }
+        } else {
+            s1 = pred::add_eps_ref(s1r);
+        }
     }
-    // (guarded single-float forms of these, rt_predicates.h, measured slower
-    // in round 2: 94 vs 86.5 us per 1080p dragon frame)
-    if (!kTranslated) s1 = pred::add_eps_ref(r3.x);
-    left_first = pred::lt_eps_ref(mx, s2);
     // every term computed, then selected (no exec-mask branches)
-    const bool pa = pred::gt_eps_ref(mn, s2), pb = (mn < s1) | (mx < s1);
-    push_second = (left_first & pa) | (!left_first & pb);
-    lpass = pred::enter_ref(lt0, lt1);
-    rpass = pred::enter_ref(rt0, rt1);
+    const bool pb = (mn < s1) | (mx < s1);
+    const bool push_second = (left_first & pa) | (!left_first & pb);
+    const bool lpass = kFast ? lt1 >= lt0 : pred::enter_ref(lt0, lt1);
+    const bool rpass = kFast ? rt1 >= rt0 : pred::enter_ref(rt0, rt1);
     const uint32_t first = left_first ? L : Rr;
     const uint32_t second = left_first ? Rr : L;
     const bool first_leaf = (first & kLeafBit) != 0, second_leaf = (second & kLeafBit) != 0;
@@ -808,21 +850,33 @@ __device__ __forceinline__ void order_node(float4 q2, float4 q3, float4 q4, floa
     if (kCount && real) count_order(o, n_int, n_desc);
 }
 
+// The slab parameters of an interior record's two child boxes (r0..r2).
+template <bool kFast>
+__device__ __forceinline__ void child_slabs(const Ray& Q, float4 r0, float4 r1, float4 r2, float& lt0, float& lt1,
+                                            float& rt0, float& rt1) {
+    if (kFast) {
+        slab_fast(f2v{r0.x, r0.y}, f2v{r0.z, r0.w}, f2v{r1.x, r1.y}, Q.ix, Q.iy, Q.iz, lt0, lt1);
+        slab_fast(f2v{r1.z, r1.w}, f2v{r2.x, r2.y}, f2v{r2.z, r2.w}, Q.ix, Q.iy, Q.iz, rt0, rt1);
+    } else {
+        slab_vals(Q, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, lt0, lt1);
+        slab_vals(Q, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w, rt0, rt1);
+    }
+}
+
 // An interior item whose child-box record (r0..r3) has arrived: the node's
 // child ordering (TD/Trixel.cu:146-170) and the children's slab tests.
-template <bool kTranslated, bool kCount, bool kNoOff = false>
-__device__ __forceinline__ void visit_interior(const Ray& Q, float4 q2, float4 q3, float4 q4, uint4 it, float4 r0,
-                                               float4 r1, float4 r2, float4 r3, Visit& o, uint32_t& n_int,
-                                               uint32_t& n_desc) {
+template <bool kTranslated, bool kCount, bool kFast = false>
+__device__ __forceinline__ void visit_interior(const TraceParams& P, const Ray& Q, float4 q2, float4 q3, float4 q4,
+                                               uint4 it, float4 r0, float4 r1, float4 r2, float4 r3, Visit& o,
+                                               uint32_t& n_int, uint32_t& n_desc) {
     const uint32_t ray = it.w >> 26;
     const uint32_t marked = it.w & kCodeMarkMask;
     // children's slab parameters from the boxes in this record
     float lt0, lt1, rt0, rt1;
-    slab_vals<kNoOff>(Q, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, lt0, lt1);
-    slab_vals<kNoOff>(Q, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w, rt0, rt1);
+    child_slabs<kFast>(Q, r0, r1, r2, lt0, lt1, rt0, rt1);
     Order od;
-    order_node<kTranslated, kCount>(q2, q3, q4, __uint_as_float(it.y), __uint_as_float(it.z), r3, lt0, lt1, rt0, rt1,
-                                    true, od, n_int, n_desc);
+    order_node<kTranslated, kCount, kFast>(P, Q, q2, q3, q4, __uint_as_float(it.y), __uint_as_float(it.z), r0, r1, r2,
+                                           r3, lt0, lt1, rt0, rt1, true, od, n_int, n_desc);
     const uint32_t meta_first = (ray << 26) | (marked << 1);
     const uint32_t meta_second = meta_first | 1u;
     o.ca = make_uint4(od.first, __float_as_uint(od.f0), __float_as_uint(od.f1), meta_first);
@@ -833,20 +887,20 @@ __device__ __forceinline__ void visit_interior(const Ray& Q, float4 q2, float4 q
 
 // Visits one item whose record has arrived: a leaf's MT test or an interior
 // node's child ordering and slab tests.
-template <int kStride, bool kTranslated, bool kCount, bool kAny, bool kNoOff = false>
-__device__ __forceinline__ void visit_item(const float2* rd, uint4 it, float4 r0, float4 r1, float4 r2, float4 r3,
-                                           Visit& o, uint32_t& n_int, uint32_t& n_leaf, uint32_t& n_acc,
-                                           uint32_t& n_desc) {
+template <int kStride, bool kTranslated, bool kCount, bool kAny, bool kFast = false>
+__device__ __forceinline__ void visit_item(const TraceParams& P, const float2* rd, uint4 it, float4 r0, float4 r1,
+                                           float4 r2, float4 r3, Visit& o, uint32_t& n_int, uint32_t& n_leaf,
+                                           uint32_t& n_acc, uint32_t& n_desc) {
     Ray Q;
     float4 q2, q3, q4;
     // each path reads its own ray fields (read once before the branch, they
     // spilled 3 VGPRs of the 16-ray instance, no faster)
     if (it.x & kLeafBit) {
-        ray_of<kTranslated, kStride>(rd, Q, q2, q3, q4);
+        ray_of<kTranslated, kStride, kFast>(rd, Q, q2, q3, q4);
         visit_leaf<kTranslated, kCount, kAny>(Q, q4, it, r0, r1, r2, r3, o, n_leaf, n_acc);
     } else {
-        ray_of<kTranslated, kStride>(rd, Q, q2, q3, q4);
-        visit_interior<kTranslated, kCount, kNoOff>(Q, q2, q3, q4, it, r0, r1, r2, r3, o, n_int, n_desc);
+        ray_of<kTranslated, kStride, kFast>(rd, Q, q2, q3, q4);
+        visit_interior<kTranslated, kCount, kFast>(P, Q, q2, q3, q4, it, r0, r1, r2, r3, o, n_int, n_desc);
     }
 }
 
@@ -905,6 +959,87 @@ __device__ __forceinline__ int push_children(uint4* items, int at, const Visit& 
     return n1 + n2;
 }
 
+// One slot of a kFast one-level pool iteration (nearest-hit walks): the
+// item `it` of each lane (act: the lane holds one) whose record r0..r3 has
+// arrived, its visit, its candidate, and the pushes of the children, at
+// items[at...]; returns how many the wave pushed.  The child ordering's
+// booleans are wave lane masks (ballots of the compares, combined by scalar
+// ops), and the pushes store under those masks: all left children, then all
+// right ones, each carrying its DFS path bit (0 for the child the reference
+// pops first).  Which children are visited, and each item's path code, are
+// the reference's (TD/Trixel.cu:146-170); only the pool order differs, and
+// the nearest hit does not depend on it.
+template <int kStride, bool kCount>
+__device__ __forceinline__ int fast_slot(const TraceParams& P, uint4* items, int at, const float2* s_ray,
+                                         unsigned long long* s_key, uint32_t* s_tri, uint4 it, bool act, float4 r0,
+                                         float4 r1, float4 r2, float4 r3, uint32_t& n_int, uint32_t& n_leaf,
+                                         uint32_t& n_acc, uint32_t& n_desc) {
+    // The leaf and the interior code each run behind a wave-uniform branch
+    // (taken when some lane holds that kind) with every lane computing, and
+    // their results are masked by the kind: no exec-mask bookkeeping, and the
+    // ballots of the ordering stay scalar.  A lane of the other kind reads
+    // its own record as this kind's (plain floats; its results are dropped).
+    const float2* rd = s_ray + (size_t)(it.w >> 26);
+    const unsigned long long A = __ballot(act), LEAF = __ballot((it.x & kLeafBit) != 0) & A, INT = A & ~LEAF;
+    const float2 f0 = rd[0], f1 = rd[kStride], f2 = rd[2 * kStride];
+    const float rx = f0.x, ry = f0.y, rz = f1.x, ix = f1.y, iy = f2.x, iz = f2.y;
+    Visit v;
+    v.cand = false;
+    if (LEAF) {
+        Ray Q;
+        Q.rx = rx; Q.ry = ry; Q.rz = rz;
+        uint32_t nl = 0, na = 0;
+        visit_leaf<false, kCount, false>(Q, make_float4(0.0f, 0.0f, 0.0f, 0.0f), it, r0, r1, r2, r3, v, nl, na);
+        const bool mine = __builtin_amdgcn_inverse_ballot_w64(LEAF);
+        v.cand = v.cand && mine;
+        if (kCount) {
+            n_leaf += mine ? nl : 0u;
+            n_acc += mine ? na : 0u;
+        }
+    }
+    record_candidate<false>(s_key, s_tri, it, v);
+    if (!INT) return 0;
+    float lt0, lt1, rt0, rt1;
+    slab_fast(f2v{r0.x, r0.y}, f2v{r0.z, r0.w}, f2v{r1.x, r1.y}, ix, iy, iz, lt0, lt1);
+    slab_fast(f2v{r1.z, r1.w}, f2v{r2.x, r2.y}, f2v{r2.z, r2.w}, ix, iy, iz, rt0, rt1);
+    const uint32_t lw = __float_as_uint(r3.z), rw = __float_as_uint(r3.w);
+    const uint32_t axis = (lw >> kAxisShift) & 3u;
+    const uint32_t L = lw & ~(3u << kAxisShift), R = rw & ~kTinyS1Bit;
+    // the direction on the cut axis is the component itself (order_node)
+    const float dir = axis == 2 ? rz : axis == 1 ? ry : rx;
+    const float t0 = __uint_as_float(it.y), t1 = __uint_as_float(it.z);
+    const float mx = t0 * dir, mn = t1 * dir;
+    float s1 = rec_s1(r0, r1, axis);
+    if (P.tiny_s1) {
+        const bool tiny = (rw & kTinyS1Bit) != 0;
+        if (__ballot(tiny) & INT) s1 = tiny ? pred::add_eps_ref(s1) : s1;
+    }
+    // TD/Trixel.cu:146-168 as lane masks: left first (maxt0 < s2 + eps),
+    // the second child pushed (mint1 > s2 - eps, or below s1), each child
+    // kept when a leaf or entered (the kFast entry test)
+    const bool lf = mx < r3.y;
+    const unsigned long long LF = __ballot(lf);
+    const unsigned long long PS = (LF & __ballot(mn > r3.x)) | (~LF & __ballot(fminf(mn, mx) < s1));
+    const unsigned long long mL = INT & __ballot(lt1 >= lt0 || (L & kLeafBit) != 0) & (LF | PS);
+    const unsigned long long mR = INT & __ballot(rt1 >= rt0 || (R & kLeafBit) != 0) & (~LF | PS);
+    const uint32_t meta = (it.w & ~kCodeMarkMask) | ((it.w & kCodeMarkMask) << 1);
+    if (kCount && __builtin_amdgcn_inverse_ballot_w64(INT)) {  // the reference's counters (count_order)
+        const bool ps = __builtin_amdgcn_inverse_ballot_w64(PS);
+        const bool li = (L & kLeafBit) == 0, ri = (R & kLeafBit) == 0, lp = lt1 >= lt0, rp = rt1 >= rt0;
+        const bool fi = lf ? li : ri, si = lf ? ri : li, fp = lf ? lp : rp, sp = lf ? rp : lp;
+        n_int += (fi ? 1u : 0u) + ((ps && si) ? 1u : 0u);
+        n_desc += ((fi && fp) ? 1u : 0u) + ((ps && si && sp) ? 1u : 0u);
+    }
+    // all left children, then all right ones, each with its path bit
+    const int nL = __builtin_popcountll(mL);
+    if (__builtin_amdgcn_inverse_ballot_w64(mL))
+        items[at + (int)lanes_below(mL)] = make_uint4(L, __float_as_uint(lt0), __float_as_uint(lt1), meta | (lf ? 0u : 1u));
+    if (__builtin_amdgcn_inverse_ballot_w64(mR))
+        items[at + nL + (int)lanes_below(mR)] =
+            make_uint4(R, __float_as_uint(rt0), __float_as_uint(rt1), meta | (lf ? 1u : 0u));
+    return nL + __builtin_popcountll(mR);
+}
+
 // Two-level pool iterations (default on; debug bit 1024 or a
 // non-BFS record order turns them off).  A wave's chain of pool iterations is
 // at least the tree's depth, and most iterations pop small pools (24 items on
@@ -934,7 +1069,7 @@ __device__ __forceinline__ float quad_bcast0(float x) { return __uint_as_float(q
 // One two-level iteration over the whole pool (n <= 16 items); returns the
 // new pool size (<= 4n: an item pushes its two children or its four
 // grandchildren).
-template <int kStride, bool kTranslated, bool kCount, bool kAny, int kOrder, bool kNoOff>
+template <int kStride, bool kTranslated, bool kCount, bool kAny, int kOrder, bool kFast>
 __device__ __forceinline__ int two_level_iter(const TraceParams& P, uint4* items, const float2* s_ray,
                                               unsigned long long* s_key, uint32_t* s_tri, int n, int lane,
                                               uint32_t& n_int, uint32_t& n_leaf, uint32_t& n_acc, uint32_t& n_desc) {
@@ -959,18 +1094,18 @@ __device__ __forceinline__ int two_level_iter(const TraceParams& P, uint4* items
     const float4 a0 = pa[0], a1 = pa[1], a2 = pa[2], a3 = pa[3];
     Ray Q;
     float4 q2, q3, q4;
-    ray_of<kTranslated, kStride>(s_ray + (size_t)(it.w >> 26), Q, q2, q3, q4);
+    ray_of<kTranslated, kStride, kFast>(s_ray + (size_t)(it.w >> 26), Q, q2, q3, q4);
     // the slab values of the record's two child boxes (role 0: the node's
     // children; roles 1, 2: the child's children), then each lane's node's
     // own values: role 0 the item's, roles 1, 2 what role 0 computed for them
     float at0, at1, bt0, bt1;
-    slab_vals<kNoOff>(Q, a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, at0, at1);
-    slab_vals<kNoOff>(Q, a1.z, a1.w, a2.x, a2.y, a2.z, a2.w, bt0, bt1);
+    child_slabs<kFast>(Q, a0, a1, a2, at0, at1, bt0, bt1);
     const float xl0 = quad_bcast0(at0), xl1 = quad_bcast0(at1), xr0 = quad_bcast0(bt0), xr1 = quad_bcast0(bt1);
     const float t0 = role == 0 ? __uint_as_float(it.y) : role == 1 ? xl0 : xr0;
     const float t1 = role == 0 ? __uint_as_float(it.z) : role == 1 ? xl1 : xr1;
     Order o;
-    order_node<kTranslated, kCount>(q2, q3, q4, t0, t1, a3, at0, at1, bt0, bt1, false, o, n_int, n_desc);
+    order_node<kTranslated, kCount, kFast>(P, Q, q2, q3, q4, t0, t1, a0, a1, a2, a3, at0, at1, bt0, bt1, false, o, n_int,
+                                           n_desc);
     // role 0's verdict on its node's children, to roles 1 and 2
     const uint32_t fl = quad_bcast0((o.left_first ? 1u : 0u) | (o.ka ? 2u : 0u) | (o.kb ? 4u : 0u));
     const bool lfirst = (fl & 1u) != 0;
@@ -1007,7 +1142,7 @@ __device__ __forceinline__ int two_level_iter(const TraceParams& P, uint4* items
 // key[ray] = 0; without counters the items of such rays are dropped.
 // Each lane pops up to P.items (1 or 2) items per iteration and fetches their
 // records together, so a lane keeps two memory round trips in flight.
-template <int kCap, int kStride, bool kTranslated, bool kCount, bool kAny, int kOrder = 0, bool kNoOff = false>
+template <int kCap, int kStride, bool kTranslated, bool kCount, bool kAny, int kOrder = 0, bool kFast = false>
 __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, const float2* s_ray,
                                           unsigned long long* s_key, uint32_t* s_tri, int n, int lane,
                                           uint32_t& iters, uint32_t& popped, uint32_t& n_int, uint32_t& n_leaf,
@@ -1024,7 +1159,7 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
         if (!kAny && n <= RT_TWO_MAX && P.two_depth >= 0 && 4 * n <= cap - slack) {
             iters++;
             popped += (uint32_t)n;
-            n = two_level_iter<kStride, kTranslated, kCount, kAny, kOrder, kNoOff>(P, items, s_ray, s_key, s_tri, n, lane,
+            n = two_level_iter<kStride, kTranslated, kCount, kAny, kOrder, kFast>(P, items, s_ray, s_key, s_tri, n, lane,
                                                                           n_int, n_leaf, n_acc, n_desc);
             __builtin_amdgcn_wave_barrier();
             continue;
@@ -1064,12 +1199,19 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
         // item 0 is visited, recorded and pushed before item 1 is visited, so
         // its results die before item 1's are made (fewer live VGPRs)
         int total = 0;
+        if (kFast && !kAny) {
+            total = fast_slot<kStride, kCount>(P, items, base, s_ray, s_key, s_tri, it0, act0, a0, a1, a2, a3, n_int,
+                                               n_leaf, n_acc, n_desc);
+            if (take > 64)
+                total += fast_slot<kStride, kCount>(P, items, base + total, s_ray, s_key, s_tri, it1, act1, b0, b1, b2,
+                                                    b3, n_int, n_leaf, n_acc, n_desc);
+        } else {
         {
             Visit v0;
             v0.ka = v0.kb = false; v0.cand = false;
             if (act0)
-                visit_item<kStride, kTranslated, kCount, kAny, kNoOff>(s_ray + (size_t)(it0.w >> 26), it0, a0, a1, a2, a3,
-                                                            v0, n_int, n_leaf, n_acc, n_desc);
+                visit_item<kStride, kTranslated, kCount, kAny, kFast>(P, s_ray + (size_t)(it0.w >> 26), it0, a0, a1, a2,
+                                                                      a3, v0, n_int, n_leaf, n_acc, n_desc);
             record_candidate<kAny>(s_key, s_tri, it0, v0);
             total += push_children<kAny, (kOrder & 3)>(items, base + total, v0);
         }
@@ -1080,10 +1222,11 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
             Visit v1;
             v1.ka = v1.kb = false; v1.cand = false;
             if (act1)
-                visit_item<kStride, kTranslated, kCount, kAny, kNoOff>(s_ray + (size_t)(it1.w >> 26), it1, b0, b1, b2, b3,
-                                                            v1, n_int, n_leaf, n_acc, n_desc);
+                visit_item<kStride, kTranslated, kCount, kAny, kFast>(P, s_ray + (size_t)(it1.w >> 26), it1, b0, b1, b2,
+                                                                      b3, v1, n_int, n_leaf, n_acc, n_desc);
             record_candidate<kAny>(s_key, s_tri, it1, v1);
             total += push_children<kAny, (kOrder & 3)>(items, base + total, v1);
+        }
         }
         if (base + total > cap) {  // unreachable by the pop rule above; guard anyway
             if (lane == 0) atomicOr(P.err, 2);
@@ -1150,15 +1293,18 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
     uint32_t iters = 0, popped = 0;
 
     int n;
-    bool no_off;  // the walk may skip the slab tests' od/r terms (slab_vals, kNoOff)
+    bool fast;  // the walk takes the kFast forms (slab_fast, order_node)
     {
         // the ray goes to LDS for the walk; shading recomputes it afterwards
         // (the same float expressions), so it is not live across the walk
         float cam0[3];
         Ray R0;
         camera_ray(P, px, live, cam0, R0);
-        no_off = !kTranslated && __ballot(live && !(fabsf(R0.rx) > 0.0f && fabsf(R0.ry) > 0.0f &&
-                                                    fabsf(R0.rz) > 0.0f)) == 0ull;
+        // every live ray's components normal and nonzero (1/r finite), under
+        // the frame proof P.fast (rt_api.cpp)
+        fast = !kTranslated && P.fast &&
+               __ballot(live && !(fabsf(R0.rx) >= 0x1p-126f && fabsf(R0.ry) >= 0x1p-126f &&
+                                  fabsf(R0.rz) >= 0x1p-126f)) == 0ull;
         if (lane < kRays) {
             store_ray(&S_.ray[lane], RL::kStride, R0, kTranslated, 0.0f, 0u);
             S_.key[lane] = ~0ull;
@@ -1170,7 +1316,7 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
         // (bench.py's roofline without the root-miss visits)
         if (kCount && (P.debug & 32)) n = 0;
     }
-    if (!kTranslated && no_off)
+    if (!kTranslated && fast)
         pool_walk<kCap, RL::kStride, kTranslated, kCount, false, 0, true>(P, items, S_.ray, S_.key, S_.tri, n, lane,
                                                                      iters, popped, C.n_int, C.n_leaf, C.n_acc,
                                                                      C.n_desc);
@@ -1912,11 +2058,37 @@ __device__ __forceinline__ void rel_split(const rt_kd_node& nd, float cx, float 
     axis = fx != 0.0f ? 0u : fy != 0.0f ? 1u : 2u;
 }
 
+// The smallest float >= d and the largest float <= d (d a double; NaN stays
+// NaN): for a float x, (double)x < d <=> x < ceil_f(d) and (double)x > d <=>
+// x > floor_f(d) -- a float between d and its float ceiling would be a
+// smaller float >= d.
+__device__ __forceinline__ float ceil_f(double d) {
+    const float f = (float)d;
+    return (double)f < d ? nextafterf(f, INFINITY) : f;
+}
+__device__ __forceinline__ float floor_f(double d) {
+    const float f = (float)d;
+    return (double)f > d ? nextafterf(f, -INFINITY) : f;
+}
+
 // init_cam_voxel_mem_cuda (TD/Camera.cu:137-162) into the dense interior
-// record layout of rt_internal.h (the children's boxes, 64 B).
+// record layout of rt_internal.h (the children's boxes, 64 B).  The split
+// word holds the reference's double-promoted split-plane tests as exact float
+// thresholds of the camera-relative s2 (TD/Trixel.cu:155-157):
+//   (double)mx < (double)s2 + 1e-16  <=>  mx < S_lt = ceil_f(fl64(s2 + 1e-16))
+//   (double)mn > (double)s2 - 1e-16  <=>  mn > S_gt = floor_f(fl64(s2 - 1e-16))
+// s1 and s2 themselves are the left child's high and the right child's low
+// bound on the cut axis (TD/Trixel.h:353-376: the same floats, minus the
+// same camera coordinate), read from the boxes where a walk needs them.
+// Bit 29 of the right reference marks a node whose s1 is tiny (|s1| < 2^-20
+// or NaN), where (float)((double)s1 + 1e-16) differs from s1.
+// flags |= kCamTinyS1 when some node's s1 is tiny, kCamUnordered when some
+// child box has a low bound not <= its high bound or is not inside its
+// parent's box (the kFast walk needs ordered boxes, and its frame proof
+// boxes inside the root's: rt_api.cpp fast_proof).
 __global__ void k_cam_nodes(const rt_kd_node* __restrict__ nodes, const int32_t* __restrict__ ids,
                             const uint32_t* __restrict__ node_ref, int64_t ninterior, float cx,
-                            float cy, float cz, float4* __restrict__ out) {
+                            float cy, float cz, float4* __restrict__ out, int32_t* __restrict__ flags) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= ninterior) return;
     const rt_kd_node nd = nodes[ids[k]];
@@ -1929,8 +2101,18 @@ __global__ void k_cam_nodes(const rt_kd_node* __restrict__ nodes, const int32_t*
     out[4 * k] = make_float4(lb[0], lb[1], lb[2], lb[3]);
     out[4 * k + 1] = make_float4(lb[4], lb[5], rb[0], rb[1]);
     out[4 * k + 2] = make_float4(rb[2], rb[3], rb[4], rb[5]);
-    out[4 * k + 3] = make_float4(s1, s2, __uint_as_float(node_ref[nd.left] | (axis << kAxisShift)),
-                                 __uint_as_float(node_ref[nd.right]));
+    const float s_gt = floor_f((double)s2 - kEps), s_lt = ceil_f((double)s2 + kEps);
+    const uint32_t tiny = fabsf(s1) >= 0x1p-20f ? 0u : kTinyS1Bit;
+    float pb[6];
+    rel_box(nd, cx, cy, cz, pb);
+    bool ordered = true;
+    for (int a = 0; a < 3; a++)
+        ordered = ordered && lb[2 * a] <= lb[2 * a + 1] && rb[2 * a] <= rb[2 * a + 1] && lb[2 * a] >= pb[2 * a] &&
+                  rb[2 * a] >= pb[2 * a] && lb[2 * a + 1] <= pb[2 * a + 1] && rb[2 * a + 1] <= pb[2 * a + 1];
+    const int32_t f = (tiny ? kCamTinyS1 : 0) | (ordered ? 0 : kCamUnordered);
+    if (f) atomicOr(flags, f);
+    out[4 * k + 3] = make_float4(s_gt, s_lt, __uint_as_float(node_ref[nd.left] | (axis << kAxisShift)),
+                                 __uint_as_float(node_ref[nd.right] | tiny));
 }
 
 // Rank 0's frame assembly after the gather: [rank][slot][8 rows][w] -> frame.

@@ -418,6 +418,10 @@ int rt_camera_info(const rt_camera* c, int32_t* w, int32_t* h, int32_t* max_dept
  * tile: the 4 units and the second halves).  The frame is the same either
  * way. */
 #define RT_OPT_SPLIT_USED 9
+/* get only: 1 when the last kernel-3 render's frame proved the float entry
+ * test (its walks took the single-precision slab and ordering forms; the
+ * frame is the same either way), else 0 */
+#define RT_OPT_FAST_USED 10
 int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value);
 int rt_camera_get_option(const rt_camera* c, int32_t key, int32_t* value);
 

@@ -45,7 +45,7 @@ def test_small_frames_vs_golden(name, w, h, mode):
     _assert_same((argb, hit), (oargb, ohit), key + " vs oracle")
 
 
-KERNELS = [(2, 0, 64), (2, 2, 64), (2, 1, 64), (3, 2, 32), (3, 1, 32), (3, 0, 32), (3, 2, 16), (3, 2, 8), (3, 3, 16),
+KERNELS = [(2, 0, 0), (2, 2, 0), (2, 1, 0), (3, 2, 32), (3, 1, 32), (3, 0, 32), (3, 2, 16), (3, 2, 8), (3, 3, 16),
            (3, 3, 8), (3, 4, 16), (3, 3, 0), (3, 3, 32)]  # (KD kernel, tile order, rays/wave; 0 = automatic)
 
 
@@ -1474,3 +1474,94 @@ def test_multiframe_launch_loop(key):
     with pytest.raises(_lib.RtError):
         R.FrameLoop(s.cam, bufs, mode=0, render_stream=st.cuda_stream, inflight=_lib.RT_LOOP_MULTIFRAME,
                     xforms=np.stack([np.eye(3, 4, dtype=np.float32).reshape(12)] * 2)).run(4)
+
+
+def test_multiframe_alternating_loops_kept_order():
+    """a small frame whose rays-per-wave rule differs between
+    multi-frame launches (32) and the per-frame loop (16) switches tilings on
+    every rt_run_frames call; each switch starts from the cost order last
+    measured for that tiling (rt_api.cpp restore_order).  Every frame of
+    every call is still the oracle's (committed hash)."""
+    import hashlib
+    import torch
+    from cpp_cuda_raytracer_dev_amd import _lib
+    ent = H.frame_hashes()["dragon_960x540_m0"]
+    if not H.mesh_matches(ent):
+        pytest.skip("stand-in mesh bits differ on this host")
+    w, h = ent["w"], ent["h"]
+    s = H.GpuScene(ent["scene"], w, h)
+    dev = torch.device("cuda:0")
+    st = torch.cuda.Stream(device=dev)
+    bufs = [torch.full((w * h,), 0x7BADBEEF, dtype=torch.int32, device=dev) for _ in range(2)]
+    mf = R.FrameLoop(s.cam, bufs, mode=0, render_stream=st.cuda_stream, event_every=1,
+                     inflight=_lib.RT_LOOP_MULTIFRAME)
+    lanes = R.FrameLoop(s.cam, bufs, mode=0, render_stream=st.cuda_stream, event_every=8, inflight=2)
+    used = set()
+    for i in range(6):
+        loop = mf if i % 2 == 0 else lanes
+        for b in bufs:
+            b.fill_(0x7BADBEEF)
+        torch.cuda.synchronize()
+        loop.run(60)
+        torch.cuda.synchronize()
+        used.add(s.cam.get_option(_lib.RT_OPT_RAYS_USED))
+        shas = {hashlib.sha256(b.cpu().numpy().view(np.uint32).tobytes()).hexdigest() for b in bufs}
+        assert shas == {ent["argb_sha"]}, (i, s.cam.get_option(_lib.RT_OPT_RAYS_USED))
+    assert used == {16, 32}
+    assert s.cam.device_error(reset=True) == 0
+    s.close()
+
+
+# kFast walks (rt_kernels_impl.h fast_slot / order_node<kFast>): the float
+# entry test and the float ordering thresholds must give the reference's
+# frame, its visit counts included, wherever rt_api.cpp fast_proof admits
+# the frame.  Each pose renders with the proof's walks and with debug bit
+# 2048 (the double-promoted forms) and the two must agree bit for bit; the
+# default view is also checked against the oracle.
+FAST_POSES = [None,  # the default view (eye at z = -1, looking +z)
+              dict(pos=(0.9, 0.35, 0.2), look_at=(0.0, 0.1, 0.0)),     # from the side (proof along x)
+              dict(pos=(0.05, 1.2, 0.01), look_at=(0.0, 0.1, 0.0)),    # from above (along y)
+              dict(pos=(-0.3, 0.0, 0.6), look_at=(0.0, 0.12, 0.0)),    # from behind, below
+              dict(pos=(0.0, 0.1, -0.25), look_at=(0.0, 0.1, 0.0))]    # close in front (large field)
+
+
+@pytest.mark.parametrize("pose", range(len(FAST_POSES)))
+@pytest.mark.parametrize("scene,w,h", [("tester", 320, 180), ("rabbit_70k", 480, 270), ("dragon", 480, 270)])
+def test_fast_walk_same_frame(scene, w, h, pose):
+    from cpp_cuda_raytracer_dev_amd import _lib
+    kw = FAST_POSES[pose]
+    outs = []
+    for debug in (0, 2048):
+        s = H.GpuScene(scene, w, h, cam_kw=kw, kernel=3, debug=debug)
+        try:
+            argb, hit, cnt = s.render(0, count=True)
+            used = s.cam.get_option(_lib.RT_OPT_FAST_USED)
+            argb2, hit2, _ = s.render(0)  # the timed (uncounted) instance
+        finally:
+            s.close()
+        _assert_same((argb2, hit2), (argb, hit), f"{scene} pose {pose} debug {debug} counted vs timed")
+        outs.append((argb, hit, [int(x) for x in cnt], used))
+    assert outs[1][3] == 0
+    if kw is None:
+        assert outs[0][3] == 1, "the default view proves the float entry test"
+    _assert_same(outs[0][:2], outs[1][:2], f"{scene} pose {pose} fast vs double forms")
+    assert outs[0][2] == outs[1][2]
+    if kw is None:
+        oargb, ohit, ocnt = H.oracle_render(scene, w, h, 0)
+        _assert_same(outs[0][:2], (oargb, ohit), f"{scene} fast vs oracle")
+        _counters_match(outs[0][2], ocnt, 3)
+
+
+def test_fast_walk_refused_inside_box():
+    """An eye inside the root box on every axis: no axis proves the entry
+    test, so the walks keep the double-promoted forms."""
+    from cpp_cuda_raytracer_dev_amd import _lib
+    s = H.GpuScene("dragon", 320, 180, cam_kw=dict(pos=(0.0, 0.12, 0.0), look_at=(0.0, 0.12, 1.0)), kernel=3)
+    try:
+        argb, hit, _ = s.render(0)
+        assert s.cam.get_option(_lib.RT_OPT_FAST_USED) == 0
+    finally:
+        s.close()
+    oargb, ohit, _ = H.oracle_render("dragon", 320, 180, 0,
+                                     cam_kw=dict(pos=(0.0, 0.12, 0.0), look_at=(0.0, 0.12, 1.0)))
+    _assert_same((argb, hit), (oargb, ohit), "dragon inside the root box vs oracle")
