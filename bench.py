@@ -125,7 +125,7 @@ def parse():
                     help="0 XCD-contiguous, 1 natural, 2 centre-out, 3 by the cost an earlier frame measured")
     ap.add_argument("--rays", type=int, default=0,
                     help="kernel 3: pixels per wave (32, 16, 8; 0 = the library's automatic choice)")
-    ap.add_argument("--items", type=int, default=2, help="kernel 3: items each lane pops per iteration (1, 2)")
+    ap.add_argument("--items", type=int, default=2, help="kernel 3: items each lane pops per iteration (1, 2; 65..128: two only when the pool holds that many)")
     ap.add_argument("--order", type=int, default=-1,
                     help="interior record order: 0 BFS, 1 DFS preorder, 2 treelets (-1: the library default)")
     ap.add_argument("--treelet", type=int, default=0, help="treelet height for --order 2 (0: library default)")

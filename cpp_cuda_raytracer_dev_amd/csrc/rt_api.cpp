@@ -76,7 +76,13 @@ struct rt_camera {
     int32_t cam_flags = kCamUnordered;  // ... read back once the records are built
     float4* d_tpair = nullptr;       // flat variant 2: camera-relative triangle pairs
     uint32_t trec_cap = 0;
-    int64_t inode_cap = 0;           // in float4
+    // d_inode and d_trec are one allocation, the interior records first, so
+    // kernel 3's kFast walks address both from d_inode with a 32-bit byte
+    // offset (leaf_off: the byte offset of d_trec; 0 when the records exceed
+    // 4 GiB, and then no kFast walk runs)
+    float4* d_rec = nullptr;
+    int64_t rec_cap = 0;             // in float4
+    uint32_t leaf_off = 0;
     int kernel_version = 3;          // kOptKernel
     int tile_order = 3;              // kOptTileOrder
     // kOptDebug (diagnostics): 1 skip traversal, 2 per-wave stamps, 4 every
@@ -262,12 +268,20 @@ int prepare_camera_object(rt_camera* c) {
     if (!s) return fail(RT_ERR_STATE, "camera has no object (rt_camera_add_object)");
     if (c->prepared_version == s->tree_version + 1) return RT_OK;
     int rc;
+    const int64_t nint4 = std::max<int64_t>(s->d_nodes ? s->ninterior : 0, 1) * 4, ntri4 = (int64_t)s->ntri * 4;
+    if (c->rec_cap < nint4 + ntri4) {
+        dev_free(c->d_rec);
+        c->d_rec = c->d_inode = c->d_trec = nullptr;
+        c->rec_cap = 0;
+        if ((rc = dev_alloc(&c->d_rec, (size_t)(nint4 + ntri4), "hipMalloc(records)"))) return rc;
+        c->rec_cap = nint4 + ntri4;
+    }
+    c->d_inode = c->d_rec;
+    c->d_trec = c->d_rec + nint4;
+    c->leaf_off = (nint4 + ntri4) * 16 < (int64_t)UINT32_MAX ? (uint32_t)(nint4 * 16) : 0u;
     if (c->trec_cap < s->ntri) {
-        dev_free(c->d_trec);
         dev_free(c->d_tpair);
-        if ((rc = dev_alloc(&c->d_trec, (size_t)s->ntri * 4, "hipMalloc(trec)")) ||
-            (rc = dev_alloc(&c->d_tpair, (size_t)((s->ntri + 1) / 2) * 8, "hipMalloc(tpair)")))
-            return rc;
+        if ((rc = dev_alloc(&c->d_tpair, (size_t)((s->ntri + 1) / 2) * 8, "hipMalloc(tpair)"))) return rc;
         c->trec_cap = s->ntri;
     }
     // init_camera_trixel_device_memory (TD/Trixel.cu:244-264), plus its pair
@@ -276,12 +290,6 @@ int prepare_camera_object(rt_camera* c) {
         (rc = launch_pair_tri(c->d_trec, s->ntri, c->d_tpair, nullptr)))
         return rc;
     if (s->d_nodes) {
-        const int64_t need = std::max<int64_t>(s->ninterior, 1) * 4;
-        if (c->inode_cap < need) {
-            dev_free(c->d_inode);
-            if ((rc = dev_alloc(&c->d_inode, (size_t)need, "hipMalloc(inode)"))) return rc;
-            c->inode_cap = need;
-        }
         if (!c->d_cam_flags && (rc = dev_alloc(&c->d_cam_flags, 1, "hipMalloc(cam flags)"))) return rc;
         // init_camera_voxel_device_memory (TD/Camera.cu:163-187)
         if ((rc = hip_check(hipMemset(c->d_cam_flags, 0, sizeof(int32_t)), "memset cam flags")) ||
@@ -771,7 +779,7 @@ struct FrameGeom {
 // normalisation), and maxt0 >= t_k.  The default view (the eye at z = -1
 // looking +z, the object at z > -0.1) proves it along z.
 bool fast_proof(const FrameGeom& g, const TraceParams& p) {
-    if (!p.plain_xf || (g.cam_flags & kCamUnordered) || g.root_leaf) return false;
+    if (!p.plain_xf || (g.cam_flags & kCamUnordered) || g.root_leaf || !p.leaf_off) return false;
     const double fx = g.w - 1, fy = g.h - 1;
     for (int k = 0; k < 3; k++) {
         const double n = g.n_mod[k], u = g.u_mod[k], v = g.v_mod[k];
@@ -1117,6 +1125,7 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
     const rt_scene* s = c->obj;
     p.inode = c->d_inode;
     p.trec = c->d_trec;
+    p.leaf_off = c->leaf_off;
     p.tpair = c->d_tpair;
     p.flat_variant = c->flat_variant;
     p.shade = s->d_shade;
@@ -2062,8 +2071,7 @@ extern "C" void rt_camera_destroy(rt_camera* c) {
     dev_free(c->d_counters);
     dev_free(c->d_err);
     dev_free(c->d_cam_flags);
-    dev_free(c->d_trec);
-    dev_free(c->d_inode);
+    dev_free(c->d_rec);
     dev_free(c->d_tpair);
     for (auto& o : c->oslot) {
         dev_free(o.d);
@@ -2112,7 +2120,8 @@ extern "C" int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value) {
         c->rays = value;
         return RT_OK;
     case kOptItems:
-        if (value != 1 && value != 2) return fail(RT_ERR_INVALID, "items per lane %d (1, 2)", value);
+        if (value != 1 && value != 2 && !(value >= 65 && value <= 128))
+            return fail(RT_ERR_INVALID, "items per lane %d (1, 2, or 65..128: two when the pool holds that many)", value);
         c->items = value;
         return RT_OK;
     case kOptCoarse:

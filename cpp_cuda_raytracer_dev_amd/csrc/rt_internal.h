@@ -133,6 +133,7 @@ struct TraceParams {
     // transform, ordered boxes, and every box's entry parameter >= 2^-20
     // for every ray of the frame
     int32_t fast;
+    uint32_t leaf_off;             // byte offset of trec from inode (one allocation; rt_api.cpp prepare_camera_object)
     int32_t tiny_s1;               // some interior record of the camera has the tiny-s1 flag
     int32_t far_rect[4];           // root box's screen rectangle + 2 px (x0, x1, y0, y1; frame pixels)
     int32_t far_all;               // every group background: the box lies behind the eye (box_behind)

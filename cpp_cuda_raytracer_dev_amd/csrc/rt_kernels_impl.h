@@ -721,6 +721,14 @@ __device__ __forceinline__ const float4* record_of(const TraceParams& P, uint32_
     return (ref & kLeafBit) ? P.trec + 4 * (size_t)(ref & ~kLeafBit) : P.inode + 4 * (size_t)ref;
 }
 
+// record_of for kFast walks: the records are one allocation (inode, then
+// trec at byte offset P.leaf_off < 4 GiB), so the address is P.inode plus a
+// 32-bit offset: ref << 6 drops the leaf bit, and a leaf adds leaf_off.
+__device__ __forceinline__ const float4* record_fast(const TraceParams& P, uint32_t ref) {
+    const uint32_t off = (ref << 6) + ((int32_t)ref < 0 ? P.leaf_off : 0u);
+    return (const float4*)((const char*)P.inode + off);
+}
+
 // The per-ray data of an item's ray from LDS (see store_ray), as the float4s
 // (q2 = (odz/rz, dir per axis), q3 = (od, ds axis 0), q4 = (ds axes 1-2,
 // Lmax, hit triangle)) the visits read.
@@ -784,6 +792,14 @@ __device__ __forceinline__ void count_order(const Order& o, uint32_t& n_int, uin
 // (lt0, lt1) and (rt0, rt1).  kCount: the reference's visit counters of the
 // node's children (when `real`).
 //
+// A value the compiler cannot see through: the double-precision fix-ups of
+// tiny s1 values take it, so they stay behind their (rarely taken) uniform
+// branches instead of being computed for every record and selected.
+__device__ __forceinline__ float opaque(float x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
 // kFast (untranslated walks of rays with normal, nonzero components, under
 // the frame proof P.fast): the direction per cut axis is the ray component
 // itself (r_a * 1 + r_b * 0 + r_c * 0 == r_a for finite nonzero r), and the
@@ -823,7 +839,7 @@ __device__ __forceinline__ void order_node(const TraceParams& P, const Ray& Q, f
             s1 = s1r;
             if (P.tiny_s1) {
                 const bool tiny = (rw & kTinyS1Bit) != 0;
-                if (__ballot(tiny) != 0ull) s1 = tiny ? pred::add_eps_ref(s1r) : s1r;
+                if (__ballot(tiny) != 0ull) s1 = tiny ? pred::add_eps_ref(opaque(s1r)) : s1r;
             }
         } else {
             s1 = pred::add_eps_ref(s1r);
@@ -1012,7 +1028,7 @@ __device__ __forceinline__ int fast_slot(const TraceParams& P, uint4* items, int
     float s1 = rec_s1(r0, r1, axis);
     if (P.tiny_s1) {
         const bool tiny = (rw & kTinyS1Bit) != 0;
-        if (__ballot(tiny) & INT) s1 = tiny ? pred::add_eps_ref(s1) : s1;
+        if (__ballot(tiny) & INT) s1 = tiny ? pred::add_eps_ref(opaque(s1)) : s1;
     }
     // TD/Trixel.cu:146-168 as lane masks: left first (maxt0 < s2 + eps),
     // the second child pushed (mint1 > s2 - eps, or below s1), each child
@@ -1136,6 +1152,104 @@ __device__ __forceinline__ int two_level_iter(const TraceParams& P, uint4* items
     return n1 + __builtin_popcountll(m2);
 }
 
+// The two-level iteration of a kFast walk, as lane masks (fast_slot's forms):
+// lane 4k + r holds item k; role 0 its node, roles 1 and 2 the node's left
+// and right child when the item expands two levels, role 3 the item's node
+// again.  Role 3's slab values of the node's right box reach role 2 and role
+// 0's of its left box reach role 1 in one quad_perm [0, 0, 3, 3] exchange per
+// value.  Which nodes are visited and pushed, and every path code, are
+// two_level_iter's.
+template <int kStride, bool kCount>
+__device__ __forceinline__ int two_level_fast(const TraceParams& P, uint4* items, const float2* s_ray,
+                                              unsigned long long* s_key, uint32_t* s_tri, int n, int lane,
+                                              uint32_t& n_int, uint32_t& n_leaf, uint32_t& n_acc, uint32_t& n_desc) {
+    int l = lane;
+    asm volatile("" : "+v"(l));
+    const int k = l >> 2, role = l & 3;
+    const bool act = k < n;
+    const uint4 it = items[act ? k : 0];
+    __builtin_amdgcn_wave_barrier();
+    constexpr unsigned long long R0 = 0x1111111111111111ull;  // the role-0 lanes
+    const uint32_t marked = it.w & kCodeMarkMask;
+    const bool interior = (it.x & kLeafBit) == 0;
+    const int depth = 31 - __builtin_clz(marked);
+    const unsigned long long INT0 = __ballot(act && interior) & R0;
+    const unsigned long long EL0 = __ballot(act && interior && depth <= P.two_depth) & R0;
+    const bool child = __builtin_amdgcn_inverse_ballot_w64((EL0 << 1) | (EL0 << 2));
+    const float4* pa = child ? (const float4*)((const char*)P.inode + ((2 * it.x + (uint32_t)role) << 6))
+                             : record_fast(P, it.x);
+    const float4 a0 = pa[0], a1 = pa[1], a2 = pa[2], a3 = pa[3];
+    const float2* rd = s_ray + (size_t)(it.w >> 26);
+    const float2 f0 = rd[0], f1 = rd[kStride], f2 = rd[2 * kStride];
+    const float rx = f0.x, ry = f0.y, rz = f1.x, ix = f1.y, iy = f2.x, iz = f2.y;
+    // the record's child boxes; each lane's own node's (t0, t1)
+    float lt0, lt1, rt0, rt1;
+    slab_fast(f2v{a0.x, a0.y}, f2v{a0.z, a0.w}, f2v{a1.x, a1.y}, ix, iy, iz, lt0, lt1);
+    slab_fast(f2v{a1.z, a1.w}, f2v{a2.x, a2.y}, f2v{a2.z, a2.w}, ix, iy, iz, rt0, rt1);
+    const float u0 = role == 3 ? rt0 : lt0, u1 = role == 3 ? rt1 : lt1;
+    const float x0 = __uint_as_float((uint32_t)__builtin_amdgcn_mov_dpp((int)__float_as_uint(u0), 0xF0, 0xF, 0xF, true));
+    const float x1 = __uint_as_float((uint32_t)__builtin_amdgcn_mov_dpp((int)__float_as_uint(u1), 0xF0, 0xF, 0xF, true));
+    const float t0 = role == 0 ? __uint_as_float(it.y) : x0, t1 = role == 0 ? __uint_as_float(it.z) : x1;
+    // the order of each lane's node (fast_slot)
+    const uint32_t lw = __float_as_uint(a3.z), rw = __float_as_uint(a3.w);
+    const uint32_t axis = (lw >> kAxisShift) & 3u;
+    const uint32_t L = lw & ~(3u << kAxisShift), R = rw & ~kTinyS1Bit;
+    const float dir = axis == 2 ? rz : axis == 1 ? ry : rx;
+    const float mx = t0 * dir, mn = t1 * dir;
+    float s1 = rec_s1(a0, a1, axis);
+    if (P.tiny_s1) {
+        const bool tiny = (rw & kTinyS1Bit) != 0;
+        if (__ballot(tiny)) s1 = tiny ? pred::add_eps_ref(opaque(s1)) : s1;
+    }
+    const bool lf = mx < a3.y;
+    const unsigned long long LF = __ballot(lf);
+    const unsigned long long PS = (LF & __ballot(mn > a3.x)) | (~LF & __ballot(fminf(mn, mx) < s1));
+    const unsigned long long KL = __ballot(lt1 >= lt0 || (L & kLeafBit) != 0) & (LF | PS);
+    const unsigned long long KR = __ballot(rt1 >= rt0 || (R & kLeafBit) != 0) & (~LF | PS);
+    // the children role 0 keeps are visited by roles 1 and 2
+    const unsigned long long KEPT = ((EL0 & KL) << 1) | ((EL0 & KR) << 2);
+    const unsigned long long VIS = INT0 | KEPT;
+    if (kCount && __builtin_amdgcn_inverse_ballot_w64(VIS)) {  // the reference's counters (count_order)
+        const bool ps = __builtin_amdgcn_inverse_ballot_w64(PS);
+        const bool li = (L & kLeafBit) == 0, ri = (R & kLeafBit) == 0, lp = lt1 >= lt0, rp = rt1 >= rt0;
+        const bool fi = lf ? li : ri, si = lf ? ri : li, fp = lf ? lp : rp, sp = lf ? rp : lp;
+        n_int += (fi ? 1u : 0u) + ((ps && si) ? 1u : 0u);
+        n_desc += ((fi && fp) ? 1u : 0u) + ((ps && si && sp) ? 1u : 0u);
+    }
+    // role 0 pushes its node's children unless roles 1 and 2 expand them;
+    // a kept child pushes its own.  A child's path bit: 0 for the child the
+    // parent pops first (role 1 when the parent's left comes first)
+    const unsigned long long PUSH = (INT0 & ~EL0) | KEPT;
+    const unsigned long long mL = PUSH & KL, mR = PUSH & KR;
+    const unsigned long long LF0 = LF & R0;
+    const uint32_t second = __builtin_amdgcn_inverse_ballot_w64(((~LF0 & R0) << 1) | (LF0 << 2)) ? 1u : 0u;
+    const uint32_t code = role == 0 ? marked : ((marked << 1) | second);
+    const uint32_t meta = (it.w & ~kCodeMarkMask) | (code << 1);
+    const int nL = __builtin_popcountll(mL);
+    if (__builtin_amdgcn_inverse_ballot_w64(mL))
+        items[(int)lanes_below(mL)] = make_uint4(L, __float_as_uint(lt0), __float_as_uint(lt1), meta | (lf ? 0u : 1u));
+    if (__builtin_amdgcn_inverse_ballot_w64(mR))
+        items[nL + (int)lanes_below(mR)] = make_uint4(R, __float_as_uint(rt0), __float_as_uint(rt1), meta | (lf ? 1u : 0u));
+    // role 0, a leaf item: the MT test (last)
+    const unsigned long long LEAF0 = __ballot(act && !interior) & R0;
+    Visit v;
+    v.cand = false;
+    if (LEAF0) {
+        Ray Q;
+        Q.rx = rx; Q.ry = ry; Q.rz = rz;
+        uint32_t nlf = 0, na = 0;
+        visit_leaf<false, kCount, false>(Q, make_float4(0.0f, 0.0f, 0.0f, 0.0f), it, a0, a1, a2, a3, v, nlf, na);
+        const bool mine = __builtin_amdgcn_inverse_ballot_w64(LEAF0);
+        v.cand = v.cand && mine;
+        if (kCount) {
+            n_leaf += mine ? nlf : 0u;
+            n_acc += mine ? na : 0u;
+        }
+    }
+    record_candidate<false>(s_key, s_tri, it, v);
+    return nL + __builtin_popcountll(mR);
+}
+
 // The pool walk of one wave.  kAny = false: nearest hit per ray, key[ray] =
 // min (w, path code), tri[ray] = its triangle.  kAny = true (shadow rays): any
 // accepted leaf with w < Lmax other than the ray's own hit triangle sets
@@ -1149,7 +1263,10 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
                                           uint32_t& n_acc, uint32_t& n_desc) {
     const int cap = min(P.pool_cap, kCap);
     const int slack = P.tree_height + 1;
-    const int per = P.items > 1 ? 128 : 64;
+    // P.items: 1 = one item per lane, 2 = two; 65..128 = two only when the
+    // pool holds at least that many (a second slot of few items costs a
+    // whole slot's instructions)
+    const int two_min = P.items == 1 ? 1 << 30 : P.items == 2 ? 65 : P.items;
     while (n > 0) {
         // a pool of at most RT_TWO_MAX items (and room for 4 children each
         // plus the DFS slack): one two-level iteration over all of it.
@@ -1159,8 +1276,11 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
         if (!kAny && n <= RT_TWO_MAX && P.two_depth >= 0 && 4 * n <= cap - slack) {
             iters++;
             popped += (uint32_t)n;
-            n = two_level_iter<kStride, kTranslated, kCount, kAny, kOrder, kFast>(P, items, s_ray, s_key, s_tri, n, lane,
-                                                                          n_int, n_leaf, n_acc, n_desc);
+            if (kFast && !kAny)
+                n = two_level_fast<kStride, kCount>(P, items, s_ray, s_key, s_tri, n, lane, n_int, n_leaf, n_acc, n_desc);
+            else
+                n = two_level_iter<kStride, kTranslated, kCount, kAny, kOrder, kFast>(P, items, s_ray, s_key, s_tri, n,
+                                                                              lane, n_int, n_leaf, n_acc, n_desc);
             __builtin_amdgcn_wave_barrier();
             continue;
         }
@@ -1170,7 +1290,7 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
         // n <= cap - slack; a run of single pops starting at n0 is a DFS of
         // the top item's subtree and never holds more than n0 + height items
         // (slack = height + 1, height <= 24), so the pool never overflows.
-        int take = min(min(n, per), cap - slack - n);
+        int take = min(min(n, n >= two_min ? 128 : 64), cap - slack - n);
         if (take < 1) take = 1;
         iters++;
         popped += (uint32_t)take;
@@ -1191,8 +1311,8 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
             if (act1 && s_key[it1.w >> 26] == 0ull) act1 = false;
         }
         // both records in flight before either is consumed
-        const float4* p0 = record_of(P, it0.x);
-        const float4* p1 = record_of(P, it1.x);
+        const float4* p0 = kFast && !kAny ? record_fast(P, it0.x) : record_of(P, it0.x);
+        const float4* p1 = kFast && !kAny ? record_fast(P, it1.x) : record_of(P, it1.x);
         const float4 a0 = p0[0], a1 = p0[1], a2 = p0[2], a3 = p0[3];
         const float4 b0 = p1[0], b1 = p1[1], b2 = p1[2], b3 = p1[3];
         RT_RECORD_FENCE();

@@ -395,7 +395,7 @@ int rt_camera_info(const rt_camera* c, int32_t* w, int32_t* h, int32_t* max_dept
                          share of the object's screen rectangle is too small to fill the GPU with 16,
                          else 16; inside rt_run_frames' multi-frame launches (RT_LOOP_MULTIFRAME) 32
                          when that rectangle holds fewer than 8,192 16-pixel units, else 16) */
-#define RT_OPT_ITEMS 4 /* kernel 3: items each lane pops per iteration (1, 2 default) */
+#define RT_OPT_ITEMS 4 /* kernel 3: items each lane pops per iteration (1, 2 default; 65..128: two only when the pool holds at least that many) */
 #define RT_OPT_COARSE 5 /* kernel 3: 8x8 groups per wave outside the root box's screen rectangle (0..32, 8 default, 0 = off) */
 /* kernel 3, shadow rays: the order the any-hit walk pushes children in (0..3;
  * -1 = timed, default: every 2048 shadow frames each order runs 3 frames

@@ -464,11 +464,12 @@ def test_camera_pose_fuzz(name):
         assert s.cam.device_error(reset=True) == 0
 
 
-@pytest.mark.parametrize("items", [1, 2])
+@pytest.mark.parametrize("items", [1, 2, 96])
 @pytest.mark.parametrize("rays", [32, 16, 8])
 @pytest.mark.parametrize("shadow", [False, True])
 def test_items_per_lane(items, rays, shadow):
-    """Kernel 3 pops one or two items per lane per iteration; same frame and counters."""
+    """Kernel 3 pops one or two items per lane per iteration (96: two only from
+    96 pooled items on); same frame and counters."""
     s = H.GpuScene("dragon", 960, 540, kernel=3, rays=rays, items=items)
     argb, hit, cnt = s.render(0, count=True, shadow=shadow)
     oargb, ohit, ocnt = H.oracle_render("dragon", 960, 540, 0, shadow=shadow)
