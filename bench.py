@@ -898,6 +898,8 @@ def main():
     # the device error word of this rank's timed frames (stack / pool
     # overflow, a far-group proof that failed): reported, and fatal below
     dev_err = cam.device_error(reset=True)
+    # the timed frames' launch shape (before the per-frame loop below renders with its own)
+    rays_used, fast_used = cam.get_option(_lib.RT_OPT_RAYS_USED), cam.get_option(_lib.RT_OPT_FAST_USED)
     frame_check = None
     if not multi and rank == 0:
         last = outs[loop.last_set()] if not isinstance(loop, PyLoop) else out
@@ -927,6 +929,7 @@ def main():
         check2 = frame_check_n1(outs[pl.last_set()].cpu().numpy().view(np.uint32), pts, nodes, cam_kw, a)
         per_frame_loop = {"loop": f"per-frame loop (rt_run_frames), {inflight} frames in flight on the library's "
                                   f"render lanes, no multi-frame launches",
+                          "rays_per_wave": cam.get_option(_lib.RT_OPT_RAYS_USED),
                           "value": round(a.second_frames / el2, 2), "unit": "frames/s",
                           "mray_per_s": round(a.second_frames * w * h / el2 / 1e6, 2),
                           "frames": a.second_frames, "ms_per_frame": round(1e3 * el2 / a.second_frames, 5),
@@ -1142,8 +1145,8 @@ def main():
                 "kernel": {2: "k_trace_kd2", 3: "k_trace_kd3"}[a.kernel] if a.mode == 0
                           else "k_trace_flat",
                 "kernel_options": {"kernel": a.kernel, "tile_order": a.tile_order,
-                                   "rays_per_wave": cam.get_option(_lib.RT_OPT_RAYS_USED),
-                                   "fast_walks": cam.get_option(_lib.RT_OPT_FAST_USED),
+                                   "rays_per_wave": rays_used,
+                                   "fast_walks": fast_used,
                                    "rays_per_wave_option": a.rays,
                                    "record_order": trixel.get_option(_lib.RT_SCENE_ORDER),
                                    "treelet_height": trixel.get_option(_lib.RT_SCENE_TREELET_HEIGHT),

@@ -1747,7 +1747,10 @@ __device__ __forceinline__ unsigned long long coarse_root(const TraceParams& P, 
 // in flight: dragon 1080p 13.7k -> 14.7k FPS, the 93 % fill view 940 ->
 // 873 us per frame; one frame at a time unchanged (86.7 -> 88.8 us).  The
 // 8-ray blocks are LDS-bound at 4 and keep their registers.
-#define RT_KD3_BOUNDS(threads) __launch_bounds__(threads, 6)
+#ifndef RT_KD3_OCC
+#define RT_KD3_OCC 6
+#endif
+#define RT_KD3_BOUNDS(threads) __launch_bounds__(threads, RT_KD3_OCC)
 // One block of k_trace_kd3's grid: block index b (blockIdx.x, or the virtual
 // index within a multi-frame launch, below).
 template <int kRays, bool kTranslated, bool kWriteHit, bool kCount, int kShadow, int kCap, int kRayVec>
