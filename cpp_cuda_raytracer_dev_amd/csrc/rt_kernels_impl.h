@@ -985,6 +985,29 @@ __device__ __forceinline__ int push_children(uint4* items, int at, const Visit& 
 // pops first).  Which children are visited, and each item's path code, are
 // the reference's (TD/Trixel.cu:146-170); only the pool order differs, and
 // the nearest hit does not depend on it.
+// The first three fields of the items' rays (kFast walks).  A 32-ray wave's
+// lanes read up to 32 distinct rays: one 8-byte field of each is 256 bytes,
+// one pass over the 64 banks, so each field is its own ds_read_b64 (merged
+// into a ds_read2_b64 the two fields take two passes, counted as bank
+// conflicts: 0.47-0.75 conflict cycles per LDS instruction at C3).
+#ifndef RT_RAY_READ_SPLIT
+#define RT_RAY_READ_SPLIT 1
+#endif
+template <int kStride>
+__device__ __forceinline__ void ray_fields3(const float2* rd, float2& f0, float2& f1, float2& f2) {
+    if (RT_RAY_READ_SPLIT && kStride == RT_RAY_STRIDE32) {
+        f0 = rd[0];
+        asm volatile("" ::: "memory");
+        f1 = rd[kStride];
+        asm volatile("" ::: "memory");
+        f2 = rd[2 * kStride];
+    } else {
+        f0 = rd[0];
+        f1 = rd[kStride];
+        f2 = rd[2 * kStride];
+    }
+}
+
 template <int kStride, bool kCount>
 __device__ __forceinline__ int fast_slot(const TraceParams& P, uint4* items, int at, const float2* s_ray,
                                          unsigned long long* s_key, uint32_t* s_tri, uint4 it, bool act, float4 r0,
@@ -997,7 +1020,8 @@ __device__ __forceinline__ int fast_slot(const TraceParams& P, uint4* items, int
     // its own record as this kind's (plain floats; its results are dropped).
     const float2* rd = s_ray + (size_t)(it.w >> 26);
     const unsigned long long A = __ballot(act), LEAF = __ballot((it.x & kLeafBit) != 0) & A, INT = A & ~LEAF;
-    const float2 f0 = rd[0], f1 = rd[kStride], f2 = rd[2 * kStride];
+    float2 f0, f1, f2;
+    ray_fields3<kStride>(rd, f0, f1, f2);
     const float rx = f0.x, ry = f0.y, rz = f1.x, ix = f1.y, iy = f2.x, iz = f2.y;
     Visit v;
     v.cand = false;
