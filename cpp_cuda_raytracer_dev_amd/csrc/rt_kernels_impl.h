@@ -1036,8 +1036,8 @@ __device__ __forceinline__ int fast_slot(const TraceParams& P, uint4* items, int
             n_leaf += mine ? nl : 0u;
             n_acc += mine ? na : 0u;
         }
+        record_candidate<false>(s_key, s_tri, it, v);
     }
-    record_candidate<false>(s_key, s_tri, it, v);
     if (!INT) return 0;
     float lt0, lt1, rt0, rt1;
     slab_fast(f2v{r0.x, r0.y}, f2v{r0.z, r0.w}, f2v{r1.x, r1.y}, ix, iy, iz, lt0, lt1);
@@ -1050,9 +1050,9 @@ __device__ __forceinline__ int fast_slot(const TraceParams& P, uint4* items, int
     const float t0 = __uint_as_float(it.y), t1 = __uint_as_float(it.z);
     const float mx = t0 * dir, mn = t1 * dir;
     float s1 = rec_s1(r0, r1, axis);
-    if (P.tiny_s1) {
-        const bool tiny = (rw & kTinyS1Bit) != 0;
-        if (__ballot(tiny) & INT) s1 = tiny ? pred::add_eps_ref(opaque(s1)) : s1;
+    if (P.tiny_s1) {  // (a scalar branch; inside, the double form for every lane and a select)
+        const float s1t = pred::add_eps_ref(opaque(s1));
+        s1 = (rw & kTinyS1Bit) != 0 ? s1t : s1;
     }
     // TD/Trixel.cu:146-168 as lane masks: left first (maxt0 < s2 + eps),
     // the second child pushed (mint1 > s2 - eps, or below s1), each child
@@ -1060,9 +1060,13 @@ __device__ __forceinline__ int fast_slot(const TraceParams& P, uint4* items, int
     const bool lf = mx < r3.y;
     const unsigned long long LF = __ballot(lf);
     const unsigned long long PS = (LF & __ballot(mn > r3.x)) | (~LF & __ballot(fminf(mn, mx) < s1));
-    const unsigned long long mL = INT & __ballot(lt1 >= lt0 || (L & kLeafBit) != 0) & (LF | PS);
-    const unsigned long long mR = INT & __ballot(rt1 >= rt0 || (R & kLeafBit) != 0) & (~LF | PS);
-    const uint32_t meta = (it.w & ~kCodeMarkMask) | ((it.w & kCodeMarkMask) << 1);
+    // (each ballot of one compare: a ballot of an or-ed lane mask makes the
+    // compiler rebuild it from a 0/1 VGPR)
+    const unsigned long long mL = INT & (__ballot(lt1 >= lt0) | __ballot((int32_t)L < 0)) & (LF | PS);
+    const unsigned long long mR = INT & (__ballot(rt1 >= rt0) | __ballot((int32_t)R < 0)) & (~LF | PS);
+    // the children's marked code: the item's shifted up a level (marked <
+    // 2^25, so adding it to the word is the shift)
+    const uint32_t meta = it.w + (it.w & kCodeMarkMask);
     if (kCount && __builtin_amdgcn_inverse_ballot_w64(INT)) {  // the reference's counters (count_order)
         const bool ps = __builtin_amdgcn_inverse_ballot_w64(PS);
         const bool li = (L & kLeafBit) == 0, ri = (R & kLeafBit) == 0, lp = lt1 >= lt0, rp = rt1 >= rt0;
@@ -1222,14 +1226,14 @@ __device__ __forceinline__ int two_level_fast(const TraceParams& P, uint4* items
     const float mx = t0 * dir, mn = t1 * dir;
     float s1 = rec_s1(a0, a1, axis);
     if (P.tiny_s1) {
-        const bool tiny = (rw & kTinyS1Bit) != 0;
-        if (__ballot(tiny)) s1 = tiny ? pred::add_eps_ref(opaque(s1)) : s1;
+        const float s1t = pred::add_eps_ref(opaque(s1));
+        s1 = (rw & kTinyS1Bit) != 0 ? s1t : s1;
     }
     const bool lf = mx < a3.y;
     const unsigned long long LF = __ballot(lf);
     const unsigned long long PS = (LF & __ballot(mn > a3.x)) | (~LF & __ballot(fminf(mn, mx) < s1));
-    const unsigned long long KL = __ballot(lt1 >= lt0 || (L & kLeafBit) != 0) & (LF | PS);
-    const unsigned long long KR = __ballot(rt1 >= rt0 || (R & kLeafBit) != 0) & (~LF | PS);
+    const unsigned long long KL = (__ballot(lt1 >= lt0) | __ballot((int32_t)L < 0)) & (LF | PS);
+    const unsigned long long KR = (__ballot(rt1 >= rt0) | __ballot((int32_t)R < 0)) & (~LF | PS);
     // the children role 0 keeps are visited by roles 1 and 2
     const unsigned long long KEPT = ((EL0 & KL) << 1) | ((EL0 & KR) << 2);
     const unsigned long long VIS = INT0 | KEPT;
@@ -1269,8 +1273,8 @@ __device__ __forceinline__ int two_level_fast(const TraceParams& P, uint4* items
             n_leaf += mine ? nlf : 0u;
             n_acc += mine ? na : 0u;
         }
+        record_candidate<false>(s_key, s_tri, it, v);
     }
-    record_candidate<false>(s_key, s_tri, it, v);
     return nL + __builtin_popcountll(mR);
 }
 
@@ -2227,8 +2231,8 @@ __device__ __forceinline__ float floor_f(double d) {
 // s1 and s2 themselves are the left child's high and the right child's low
 // bound on the cut axis (TD/Trixel.h:353-376: the same floats, minus the
 // same camera coordinate), read from the boxes where a walk needs them.
-// Bit 29 of the right reference marks a node whose s1 is tiny (|s1| < 2^-20
-// or NaN), where (float)((double)s1 + 1e-16) differs from s1.
+// Bit 29 of the right reference marks a node whose s1 is tiny: where
+// (float)((double)s1 + 1e-16) differs from s1.
 // flags |= kCamTinyS1 when some node's s1 is tiny, kCamUnordered when some
 // child box has a low bound not <= its high bound or is not inside its
 // parent's box (the kFast walk needs ordered boxes, and its frame proof
@@ -2249,7 +2253,9 @@ __global__ void k_cam_nodes(const rt_kd_node* __restrict__ nodes, const int32_t*
     out[4 * k + 1] = make_float4(lb[4], lb[5], rb[0], rb[1]);
     out[4 * k + 2] = make_float4(rb[2], rb[3], rb[4], rb[5]);
     const float s_gt = floor_f((double)s2 - kEps), s_lt = ceil_f((double)s2 + kEps);
-    const uint32_t tiny = fabsf(s1) >= 0x1p-20f ? 0u : kTinyS1Bit;
+    // exactly the records where (float)((double)s1 + 1e-16) is not s1 (bit
+    // for bit: zeros, and values within ~2^-29 of zero; NaN)
+    const uint32_t tiny = __float_as_uint(pred::add_eps_ref(s1)) == __float_as_uint(s1) ? 0u : kTinyS1Bit;
     float pb[6];
     rel_box(nd, cx, cy, cz, pb);
     bool ordered = true;
