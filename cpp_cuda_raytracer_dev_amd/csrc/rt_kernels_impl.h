@@ -310,6 +310,35 @@ __device__ __forceinline__ void slab_fast(f2v bx, f2v by, f2v bz, float ix, floa
     mint1 = fminf(fmaxf(pz.x, pz.y), fminf(fmaxf(px.x, px.y), fmaxf(py.x, py.y)));
 }
 
+// slab_fast for both child boxes of a record (r0..r2: the left box's (lo,
+// hi) pairs on x, y, z, then the right box's), for a walk whose live rays all
+// lie in one octant (kOct bit k: component k positive; 8: any).  Then the
+// reference's sign-selected t0 of an axis (TD/Trixel.cu:76-83) is the product
+// of lo (r > 0) or of hi (r < 0), known at compile time, and each box takes
+// one max3 and one min3 after its products instead of a min and a max per
+// axis (the same values: with lo <= hi and 1/r of the component's sign, the
+// selected product is the smaller one).  pool_walk_oct instantiates the walk
+// per octant, so no per-slot switch is paid.
+#ifndef RT_OCT_WALKS
+#define RT_OCT_WALKS 1
+#endif
+template <int kOct>
+__device__ __forceinline__ void slab_pair_oct(float4 r0, float4 r1, float4 r2, float ix, float iy, float iz,
+                                              float& lt0, float& lt1, float& rt0, float& rt1) {
+    if constexpr (kOct >= 8) {
+        slab_fast(f2v{r0.x, r0.y}, f2v{r0.z, r0.w}, f2v{r1.x, r1.y}, ix, iy, iz, lt0, lt1);
+        slab_fast(f2v{r1.z, r1.w}, f2v{r2.x, r2.y}, f2v{r2.z, r2.w}, ix, iy, iz, rt0, rt1);
+    } else {
+        const f2v ax = f2v{r0.x, r0.y} * ix, ay = f2v{r0.z, r0.w} * iy, az = f2v{r1.x, r1.y} * iz;
+        const f2v bx = f2v{r1.z, r1.w} * ix, by = f2v{r2.x, r2.y} * iy, bz = f2v{r2.z, r2.w} * iz;
+        constexpr bool sx = (kOct & 1) != 0, sy = (kOct & 2) != 0, sz = (kOct & 4) != 0;
+        lt0 = fmaxf(sz ? az.x : az.y, fmaxf(sx ? ax.x : ax.y, sy ? ay.x : ay.y));
+        lt1 = fminf(sz ? az.y : az.x, fminf(sx ? ax.y : ax.x, sy ? ay.y : ay.x));
+        rt0 = fmaxf(sz ? bz.x : bz.y, fmaxf(sx ? bx.x : bx.y, sy ? by.x : by.y));
+        rt1 = fminf(sz ? bz.y : bz.x, fminf(sx ? bx.y : bx.x, sy ? by.y : by.x));
+    }
+}
+
 // Slab test of one node, TD/Trixel.cu:76-95,146: entry/exit parameters and
 // whether the reference descends into the node.
 __device__ __forceinline__ bool slab(const Ray& R, float lx, float hx, float ly, float hy, float lz,
@@ -1008,7 +1037,7 @@ __device__ __forceinline__ void ray_fields3(const float2* rd, float2& f0, float2
     }
 }
 
-template <int kStride, bool kCount>
+template <int kStride, bool kCount, int kOct = 8>
 __device__ __forceinline__ int fast_slot(const TraceParams& P, uint4* items, int at, const float2* s_ray,
                                          unsigned long long* s_key, uint32_t* s_tri, uint4 it, bool act, float4 r0,
                                          float4 r1, float4 r2, float4 r3, uint32_t& n_int, uint32_t& n_leaf,
@@ -1040,8 +1069,7 @@ __device__ __forceinline__ int fast_slot(const TraceParams& P, uint4* items, int
     }
     if (!INT) return 0;
     float lt0, lt1, rt0, rt1;
-    slab_fast(f2v{r0.x, r0.y}, f2v{r0.z, r0.w}, f2v{r1.x, r1.y}, ix, iy, iz, lt0, lt1);
-    slab_fast(f2v{r1.z, r1.w}, f2v{r2.x, r2.y}, f2v{r2.z, r2.w}, ix, iy, iz, rt0, rt1);
+    slab_pair_oct<kOct>(r0, r1, r2, ix, iy, iz, lt0, lt1, rt0, rt1);
     const uint32_t lw = __float_as_uint(r3.z), rw = __float_as_uint(r3.w);
     const uint32_t axis = (lw >> kAxisShift) & 3u;
     const uint32_t L = lw & ~(3u << kAxisShift), R = rw & ~kTinyS1Bit;
@@ -1187,7 +1215,7 @@ __device__ __forceinline__ int two_level_iter(const TraceParams& P, uint4* items
 // 0's of its left box reach role 1 in one quad_perm [0, 0, 3, 3] exchange per
 // value.  Which nodes are visited and pushed, and every path code, are
 // two_level_iter's.
-template <int kStride, bool kCount>
+template <int kStride, bool kCount, int kOct = 8>
 __device__ __forceinline__ int two_level_fast(const TraceParams& P, uint4* items, const float2* s_ray,
                                               unsigned long long* s_key, uint32_t* s_tri, int n, int lane,
                                               uint32_t& n_int, uint32_t& n_leaf, uint32_t& n_acc, uint32_t& n_desc) {
@@ -1212,8 +1240,7 @@ __device__ __forceinline__ int two_level_fast(const TraceParams& P, uint4* items
     const float rx = f0.x, ry = f0.y, rz = f1.x, ix = f1.y, iy = f2.x, iz = f2.y;
     // the record's child boxes; each lane's own node's (t0, t1)
     float lt0, lt1, rt0, rt1;
-    slab_fast(f2v{a0.x, a0.y}, f2v{a0.z, a0.w}, f2v{a1.x, a1.y}, ix, iy, iz, lt0, lt1);
-    slab_fast(f2v{a1.z, a1.w}, f2v{a2.x, a2.y}, f2v{a2.z, a2.w}, ix, iy, iz, rt0, rt1);
+    slab_pair_oct<kOct>(a0, a1, a2, ix, iy, iz, lt0, lt1, rt0, rt1);
     const float u0 = role == 3 ? rt0 : lt0, u1 = role == 3 ? rt1 : lt1;
     const float x0 = __uint_as_float((uint32_t)__builtin_amdgcn_mov_dpp((int)__float_as_uint(u0), 0xF0, 0xF, 0xF, true));
     const float x1 = __uint_as_float((uint32_t)__builtin_amdgcn_mov_dpp((int)__float_as_uint(u1), 0xF0, 0xF, 0xF, true));
@@ -1284,7 +1311,8 @@ __device__ __forceinline__ int two_level_fast(const TraceParams& P, uint4* items
 // key[ray] = 0; without counters the items of such rays are dropped.
 // Each lane pops up to P.items (1 or 2) items per iteration and fetches their
 // records together, so a lane keeps two memory round trips in flight.
-template <int kCap, int kStride, bool kTranslated, bool kCount, bool kAny, int kOrder = 0, bool kFast = false>
+template <int kCap, int kStride, bool kTranslated, bool kCount, bool kAny, int kOrder = 0, bool kFast = false,
+          int kOct = 8>
 __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, const float2* s_ray,
                                           unsigned long long* s_key, uint32_t* s_tri, int n, int lane,
                                           uint32_t& iters, uint32_t& popped, uint32_t& n_int, uint32_t& n_leaf,
@@ -1305,7 +1333,7 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
             iters++;
             popped += (uint32_t)n;
             if (kFast && !kAny)
-                n = two_level_fast<kStride, kCount>(P, items, s_ray, s_key, s_tri, n, lane, n_int, n_leaf, n_acc, n_desc);
+                n = two_level_fast<kStride, kCount, kOct>(P, items, s_ray, s_key, s_tri, n, lane, n_int, n_leaf, n_acc, n_desc);
             else
                 n = two_level_iter<kStride, kTranslated, kCount, kAny, kOrder, kFast>(P, items, s_ray, s_key, s_tri, n,
                                                                               lane, n_int, n_leaf, n_acc, n_desc);
@@ -1348,10 +1376,10 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
         // its results die before item 1's are made (fewer live VGPRs)
         int total = 0;
         if (kFast && !kAny) {
-            total = fast_slot<kStride, kCount>(P, items, base, s_ray, s_key, s_tri, it0, act0, a0, a1, a2, a3, n_int,
+            total = fast_slot<kStride, kCount, kOct>(P, items, base, s_ray, s_key, s_tri, it0, act0, a0, a1, a2, a3, n_int,
                                                n_leaf, n_acc, n_desc);
             if (take > 64)
-                total += fast_slot<kStride, kCount>(P, items, base + total, s_ray, s_key, s_tri, it1, act1, b0, b1, b2,
+                total += fast_slot<kStride, kCount, kOct>(P, items, base + total, s_ray, s_key, s_tri, it1, act1, b0, b1, b2,
                                                     b3, n_int, n_leaf, n_acc, n_desc);
         } else {
         {
@@ -1442,6 +1470,7 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
 
     int n;
     bool fast;  // the walk takes the kFast forms (slab_fast, order_node)
+    int oct = 8;  // the octant every live ray of the unit lies in (slab_pair_oct), 8 = mixed
     {
         // the ray goes to LDS for the walk; shading recomputes it afterwards
         // (the same float expressions), so it is not live across the walk
@@ -1453,6 +1482,12 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
         fast = !kTranslated && P.fast &&
                __ballot(live && !(fabsf(R0.rx) >= 0x1p-126f && fabsf(R0.ry) >= 0x1p-126f &&
                                   fabsf(R0.rz) >= 0x1p-126f)) == 0ull;
+        if (RT_OCT_WALKS && fast) {
+            const unsigned long long LV = __ballot(live), PX = __ballot(live && R0.rx > 0.0f),
+                                     PY = __ballot(live && R0.ry > 0.0f), PZ = __ballot(live && R0.rz > 0.0f);
+            if ((PX == 0ull || PX == LV) && (PY == 0ull || PY == LV) && (PZ == 0ull || PZ == LV))
+                oct = (PX == LV ? 1 : 0) | (PY == LV ? 2 : 0) | (PZ == LV ? 4 : 0);
+        }
         if (lane < kRays) {
             store_ray(&S_.ray[lane], RL::kStride, R0, kTranslated, 0.0f, 0u);
             S_.key[lane] = ~0ull;
@@ -1464,10 +1499,26 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
         // (bench.py's roofline without the root-miss visits)
         if (kCount && (P.debug & 32)) n = 0;
     }
-    if (!kTranslated && fast)
-        pool_walk<kCap, RL::kStride, kTranslated, kCount, false, 0, true>(P, items, S_.ray, S_.key, S_.tri, n, lane,
-                                                                     iters, popped, C.n_int, C.n_leaf, C.n_acc,
-                                                                     C.n_desc);
+    if (!kTranslated && fast) {
+        // one instance of the walk per octant (the views' rays look along +z
+        // or -z; x and y change sign across the frame), the mixed one else
+#define RT_OCT_WALK(o)                                                                                          \
+    pool_walk<kCap, RL::kStride, kTranslated, kCount, false, 0, true, o>(P, items, S_.ray, S_.key, S_.tri, n, lane, \
+                                                                          iters, popped, C.n_int, C.n_leaf,         \
+                                                                          C.n_acc, C.n_desc)
+        switch (oct) {
+        case 0: RT_OCT_WALK(0); break;
+        case 1: RT_OCT_WALK(1); break;
+        case 2: RT_OCT_WALK(2); break;
+        case 3: RT_OCT_WALK(3); break;
+        case 4: RT_OCT_WALK(4); break;
+        case 5: RT_OCT_WALK(5); break;
+        case 6: RT_OCT_WALK(6); break;
+        case 7: RT_OCT_WALK(7); break;
+        default: RT_OCT_WALK(8); break;
+        }
+#undef RT_OCT_WALK
+    }
     else
         pool_walk<kCap, RL::kStride, kTranslated, kCount, false>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters, popped,
                                                             C.n_int, C.n_leaf, C.n_acc, C.n_desc);
