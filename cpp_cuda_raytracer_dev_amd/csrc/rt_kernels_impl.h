@@ -1229,8 +1229,10 @@ __device__ __forceinline__ int two_level_fast(const TraceParams& P, uint4* items
     const uint32_t marked = it.w & kCodeMarkMask;
     const bool interior = (it.x & kLeafBit) == 0;
     const int depth = 31 - __builtin_clz(marked);
-    const unsigned long long INT0 = __ballot(act && interior) & R0;
-    const unsigned long long EL0 = __ballot(act && interior && depth <= P.two_depth) & R0;
+    // (ballots of single compares, combined by scalar ops)
+    const unsigned long long ACT0 = __ballot(act) & R0, INTB = __ballot(interior);
+    const unsigned long long INT0 = ACT0 & INTB;
+    const unsigned long long EL0 = INT0 & __ballot(depth <= P.two_depth);
     const bool child = __builtin_amdgcn_inverse_ballot_w64((EL0 << 1) | (EL0 << 2));
     const float4* pa = child ? (const float4*)((const char*)P.inode + ((2 * it.x + (uint32_t)role) << 6))
                              : record_fast(P, it.x);
@@ -1286,7 +1288,7 @@ __device__ __forceinline__ int two_level_fast(const TraceParams& P, uint4* items
     if (__builtin_amdgcn_inverse_ballot_w64(mR))
         items[nL + (int)lanes_below(mR)] = make_uint4(R, __float_as_uint(rt0), __float_as_uint(rt1), meta | (lf ? 1u : 0u));
     // role 0, a leaf item: the MT test (last)
-    const unsigned long long LEAF0 = __ballot(act && !interior) & R0;
+    const unsigned long long LEAF0 = ACT0 & ~INTB;
     Visit v;
     v.cand = false;
     if (LEAF0) {
