@@ -54,6 +54,19 @@ __device__ __forceinline__ float rsqrt21(float x, float y, float z) {
     return r;
 }
 
+// The correctly rounded 1.0f / x (the reference's 1 / r and (float)(1.0 /
+// (double)f)) for |x| in [2^-126, 2^126): the hardware reciprocal and one
+// Newton step with fused multiply-adds.  tools/check_rcp.hip compares it
+// with the division bit for bit over every float of that range (both signs,
+// 4.23e9 values, no difference on the MI355X: profiles/r05/check_rcp.json);
+// callers take it only for waves whose operands all lie in the range.
+__device__ __forceinline__ float rcp_nr(float x) {
+    const float r = __builtin_amdgcn_rcpf(x);
+    const float e = fmaf(-x, r, 1.0f);
+    return fmaf(e, r, r);
+}
+__device__ __forceinline__ bool rcp_nr_ok(float x) { return fabsf(x) >= 0x1p-126f && fabsf(x) < 0x1p126f; }
+
 // device_cross / device_dot, TD/vector.cuh:72-77,121-124
 __device__ __forceinline__ void cross3(float& cx, float& cy, float& cz, float ax, float ay,
                                        float az, float bx, float by, float bz) {
@@ -231,15 +244,23 @@ __device__ __forceinline__ bool pixel_of_thread(const TraceParams& P, Pixel& px)
 }
 
 // init_cam_mem_cuda, TD/Camera.cu:103-104: rmd = n + u*ix + v*iy, normalised.
+// kR: the normalisation factor is given (rn, computed by an earlier call for
+// the same pixel) instead of computed; else it is returned in rn.
+template <bool kR = false>
 __device__ __forceinline__ void primary_ray(const TraceParams& P, int32_t ix, int32_t iy,
-                                            float rmd[3]) {
+                                            float rmd[3], float& rn) {
     // (float)ix of the reference's unsigned pixel index: exact and equal for any ix < 2^32
     const float fx = (float)(uint32_t)ix, fy = (float)(uint32_t)iy;
     float x = P.n_mod[0] + P.u_mod[0] * fx + P.v_mod[0] * fy;
     float y = P.n_mod[1] + P.u_mod[1] * fx + P.v_mod[1] * fy;
     float z = P.n_mod[2] + P.u_mod[2] * fx + P.v_mod[2] * fy;
-    const float r = rsqrt21(x, y, z);
+    const float r = kR ? rn : rsqrt21(x, y, z);
+    rn = r;
     rmd[0] = x * r; rmd[1] = y * r; rmd[2] = z * r;
+}
+__device__ __forceinline__ void primary_ray(const TraceParams& P, int32_t ix, int32_t iy, float rmd[3]) {
+    float rn;
+    primary_ray<false>(P, ix, iy, rmd, rn);
 }
 
 __device__ __forceinline__ void wave_count_add(unsigned long long* dst, uint32_t v) {
@@ -389,7 +410,9 @@ __device__ __forceinline__ bool leaf_test_cam(const Ray& R, const float4 A, cons
     float qpx, qpy, qpz;
     cross3(qpx, qpy, qpz, R.rx, R.ry, R.rz, e2x, e2y, e2z);
     const float f = dot3(qpx, qpy, qpz, e1x, e1y, e1z);
-    const float pe1 = 1.0f / f;   // == (float)(1.0 / (double)f)
+    // pe1 == (float)(1.0 / (double)f): rcp_nr unless a lane's |f| is 2^126 or
+    // more (|f| below 2^-126 is below 1e-16, rejected whatever pe1 is)
+    const float pe1 = __ballot(fabsf(f) >= 0x1p126f) == 0ull ? rcp_nr(f) : 1.0f / f;
     const float u = pe1 * dot3(qpx, qpy, qpz, tx, ty, tz);
     const float v = pe1 * dot3(R.rx, R.ry, R.rz, Cq.y, Cq.z, Cq.w);
     const float w = pe1 * Dq.x;
@@ -681,23 +704,47 @@ __device__ __forceinline__ void store_ray(float2* rd, int stride, const Ray& R, 
 }
 
 // Derived fields of a ray whose direction and translation are set.
+// kPlain: an untranslated instance, whose od components are signed zeros:
+// od / r is then a signed zero of sign(od) ^ sign(r), or NaN when r is 0 or
+// NaN (0 / 0), computed without a division; 1 / r takes rcp_nr when every
+// lane's components are in its range.
+__device__ __forceinline__ float zero_over(float od, float r) {
+    return (r == 0.0f || r != r) ? __builtin_nanf("")
+                                 : __uint_as_float((__float_as_uint(od) ^ __float_as_uint(r)) & 0x80000000u);
+}
+template <bool kPlain = false>
 __device__ __forceinline__ void finish_ray(Ray& R) {
-    R.ix = 1 / R.rx; R.iy = 1 / R.ry; R.iz = 1 / R.rz;
-    R.ox = R.odx / R.rx; R.oy = R.ody / R.ry; R.oz = R.odz / R.rz;
+    if (kPlain && __ballot(!(rcp_nr_ok(R.rx) && rcp_nr_ok(R.ry) && rcp_nr_ok(R.rz))) == 0ull) {
+        R.ix = rcp_nr(R.rx); R.iy = rcp_nr(R.ry); R.iz = rcp_nr(R.rz);
+    } else {
+        R.ix = 1 / R.rx; R.iy = 1 / R.ry; R.iz = 1 / R.rz;
+    }
+    if (kPlain) {
+        R.ox = zero_over(R.odx, R.rx); R.oy = zero_over(R.ody, R.ry); R.oz = zero_over(R.odz, R.rz);
+    } else {
+        R.ox = R.odx / R.rx; R.oy = R.ody / R.ry; R.oz = R.odz / R.rz;
+    }
     R.sx = R.rx > 0; R.sy = R.ry > 0; R.sz = R.rz > 0;
 }
 
 // The primary ray of a pixel (TD/Camera.cu:103-104) and its object-space form
 // (TD/Trixel.cu:60-66); dead lanes get a harmless +z ray.
-__device__ __forceinline__ void camera_ray(const TraceParams& P, const Pixel& px, bool live, float cam[3], Ray& R) {
+// kR / rn: as primary_ray's (a live lane's normalisation factor, given or returned).
+template <bool kR = false, bool kPlain = false>
+__device__ __forceinline__ void camera_ray(const TraceParams& P, const Pixel& px, bool live, float cam[3], Ray& R,
+                                           float& rn) {
     cam[0] = 0.0f; cam[1] = 0.0f; cam[2] = 1.0f;
-    if (live) primary_ray(P, px.x, px.y, cam);
+    if (live) primary_ray<kR>(P, px.x, px.y, cam, rn);
     const float* X = P.xf;
     R.odx = X[3]; R.ody = X[7]; R.odz = X[11];
     R.rx = -1 * (X[0] * -cam[0] + X[1] * -cam[1] + X[2] * -cam[2]);
     R.ry = -1 * (X[4] * -cam[0] + X[5] * -cam[1] + X[6] * -cam[2]);
     R.rz = -1 * (X[8] * -cam[0] + X[9] * -cam[1] + X[10] * -cam[2]);
-    finish_ray(R);
+    finish_ray<kPlain>(R);
+}
+__device__ __forceinline__ void camera_ray(const TraceParams& P, const Pixel& px, bool live, float cam[3], Ray& R) {
+    float rn = 1.0f;
+    camera_ray<false>(P, px, live, cam, R, rn);
 }
 
 // The reference's root visit (TD/Trixel.cu:53,71-95): a leaf root is always
@@ -1422,6 +1469,7 @@ struct WaveLds {
     float2 ray[RayLayout<kRays>::kStride * kRayVec * 2];
     unsigned long long key[kRays];
     uint32_t tri[kRays];
+    float rn[kRays];  // each ray's rsqrt21 factor, for the shading's second camera_ray
 };
 
 struct Counts {
@@ -1478,7 +1526,8 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
         // (the same float expressions), so it is not live across the walk
         float cam0[3];
         Ray R0;
-        camera_ray(P, px, live, cam0, R0);
+        float rn0 = 1.0f;
+        camera_ray<false, !kTranslated>(P, px, live, cam0, R0, rn0);
         // every live ray's components normal and nonzero (1/r finite), under
         // the frame proof P.fast (rt_api.cpp)
         fast = !kTranslated && P.fast &&
@@ -1494,6 +1543,7 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
             store_ray(&S_.ray[lane], RL::kStride, R0, kTranslated, 0.0f, 0u);
             S_.key[lane] = ~0ull;
             S_.tri[lane] = kMiss;
+            S_.rn[lane] = rn0;
         }
         n = seed_root<kCount>(P, items, R0, live, lane, C.n_int, C.n_desc);
         // diagnostics (debug bit 32, counting renders): stop after the root
@@ -1530,10 +1580,13 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
         // the pixel is recomputed from the lane index behind an empty asm, so
         // neither the first ray's partial products nor the pixel's output
         // index stay live (and spilled) across the walk
+        // (the rsqrt21 factor comes back from LDS: the same float, 21
+        // Newton steps fewer)
         int32_t l2 = lane;
         asm volatile("" : "+v"(l2));
         live = unit_pixel(P, U, nrows, l2, px, ncols);
-        camera_ray(P, px, live, cam, R);
+        float rn = lane < kRays ? S_.rn[lane] : 1.0f;
+        camera_ray<true, !kTranslated>(P, px, live, cam, R, rn);
     }
     unsigned long long kbest = ~0ull;
     uint32_t best = kMiss;

@@ -1566,3 +1566,19 @@ def test_fast_walk_refused_inside_box():
     oargb, ohit, _ = H.oracle_render("dragon", 320, 180, 0,
                                      cam_kw=dict(pos=(0.0, 0.12, 0.0), look_at=(0.0, 0.12, 1.0)))
     _assert_same((argb, hit), (oargb, ohit), "dragon inside the root box vs oracle")
+
+
+def test_rcp_newton_exhaustive():
+    """rcp_nr (rt_kernels_impl.h: v_rcp_f32 and one fused Newton step), which
+    kFast walks use for 1/r and the leaf test's 1/f, equals the correctly
+    rounded 1.0f / x for every float of magnitude in [2^-126, 2^126), both
+    signs (4.23e9 values; tools/check_rcp.hip, built by build.py)."""
+    import json
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "check_rcp")
+    if not os.path.exists(exe):
+        pytest.fail("tools/check_rcp is not built (python -m cpp_cuda_raytracer_dev_amd.build)")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=100)
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert r.returncode == 0 and out["bad"] == 0 and out["checked"] == 2 * 252 * (1 << 23), out
