@@ -1544,7 +1544,7 @@ def test_fast_walk_same_frame(scene, w, h, pose):
         outs.append((argb, hit, [int(x) for x in cnt], used))
     assert outs[1][3] == 0
     if kw is None:
-        assert outs[0][3] == 1, "the default view proves the float entry test"
+        assert outs[0][3] & 1, "the default view proves the float entry test"
     _assert_same(outs[0][:2], outs[1][:2], f"{scene} pose {pose} fast vs double forms")
     assert outs[0][2] == outs[1][2]
     if kw is None:
@@ -1582,3 +1582,43 @@ def test_rcp_newton_exhaustive():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=100)
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert r.returncode == 0 and out["bad"] == 0 and out["checked"] == 2 * 252 * (1 << 23), out
+
+
+@pytest.mark.parametrize("scene", ["dragon", "rabbit_70k"])
+def test_fast_walk_tiny_s1_fixup(scene):
+    """kFast walks take s1 itself as the reference's (float)((double)s1 +
+    1e-16) except on records where that sum rounds off s1 (k_cam_nodes'
+    tiny-s1 flag), which take the double form.  A camera whose x (or y) lies
+    exactly on an interior node's s1 makes that node's camera-relative s1 a
+    zero (0 + 1e-16 rounds to 1e-16, not 0), so the camera's records carry
+    the flag and the fix-up runs; the frame, hit buffer and counters equal
+    the double-form walk's (debug bit 2048) and the oracle's."""
+    from cpp_cuda_raytracer_dev_amd import _lib
+    nodes = H.product_tree(scene)
+    interior = np.flatnonzero((nodes["is_leaf"] == 0) & (nodes["cut_flag"] % 3 != 2))
+    k = int(interior[min(3, len(interior) - 1)])
+    axis = int(nodes["cut_flag"][k]) % 3
+    pos = [0.0, 0.1, -1.0]
+    pos[axis] = float(nodes["s1"][k])
+    look = [pos[0], pos[1], 0.0]
+    kw = dict(pos=tuple(pos), look_at=tuple(look))
+    w, h = 320, 180
+    outs = []
+    for debug in (0, 2048):
+        s = H.GpuScene(scene, w, h, cam_kw=kw, kernel=3, debug=debug)
+        try:
+            argb, hit, cnt = s.render(0, count=True)
+            used = s.cam.get_option(_lib.RT_OPT_FAST_USED)
+            argb2, hit2, _ = s.render(0)
+        finally:
+            s.close()
+        _assert_same((argb2, hit2), (argb, hit), f"{scene} tiny-s1 debug {debug} counted vs timed")
+        outs.append((argb, hit, [int(x) for x in cnt], used))
+    assert outs[0][3] == 1, outs[0][3]  # kFast walks (with the fix-up: the relative s1 of node k is 0)
+    assert np.float32(nodes["s1"][k]) - np.float32(pos[axis]) == 0.0
+    assert outs[1][3] == 0
+    _assert_same(outs[0][:2], outs[1][:2], f"{scene} tiny-s1 fast vs double forms")
+    assert outs[0][2] == outs[1][2]
+    oargb, ohit, ocnt = H.oracle_render(scene, w, h, 0, cam_kw=kw)
+    _assert_same(outs[0][:2], (oargb, ohit), f"{scene} tiny-s1 fast vs oracle")
+    _counters_match(outs[0][2], ocnt, 3)
