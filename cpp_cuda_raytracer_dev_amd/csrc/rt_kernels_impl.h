@@ -1159,6 +1159,26 @@ __device__ __forceinline__ int fast_slot(const TraceParams& P, uint4* items, int
     return nL + __builtin_popcountll(mR);
 }
 
+// Record loads by the lanes that use them only (kFast walks of 8- and 16-ray
+// units; RT_MASKED_LOADS32 for 32-ray units).  The walk's busiest unit is the
+// vector memory path (r05w: TA busy 0.85, TD busy 0.96 of the knot's cycles),
+// whose cost follows the lanes a load instruction carries, not the distinct
+// addresses: an idle lane that re-reads a live item's record costs as much
+// as a real one, and so does a lane whose buffer load the range check drops
+// (r05y).  Exec-masked loads: knot 1080p +3.9 %, dragon 1080p +11 %; 32-ray
+// units (C3, knot 960x540), whose walks are HBM-bound, lose 3-4 % (r05z).
+// 0: every lane loads (idle lanes a live item's record).
+#ifndef RT_MASKED_LOADS
+#define RT_MASKED_LOADS 1
+#endif
+#ifndef RT_MASKED_LOADS32
+#define RT_MASKED_LOADS32 0
+#endif
+template <int kStride>
+constexpr bool masked_loads() {
+    return kStride == RT_RAY_STRIDE32 ? RT_MASKED_LOADS32 != 0 : RT_MASKED_LOADS != 0;
+}
+
 // Two-level pool iterations (default on; debug bit 1024 or a
 // non-BFS record order turns them off).  A wave's chain of pool iterations is
 // at least the tree's depth, and most iterations pop small pools (24 items on
@@ -1260,8 +1280,9 @@ __device__ __forceinline__ int two_level_iter(const TraceParams& P, uint4* items
 // and right child when the item expands two levels, role 3 the item's node
 // again.  Role 3's slab values of the node's right box reach role 2 and role
 // 0's of its left box reach role 1 in one quad_perm [0, 0, 3, 3] exchange per
-// value.  Which nodes are visited and pushed, and every path code, are
-// two_level_iter's.
+// value; with masked loads (masked_loads) role 3 loads no record and roles 1
+// and 2 take both boxes' values from role 0, two exchanges per value.  Which
+// nodes are visited and pushed, and every path code, are two_level_iter's.
 template <int kStride, bool kCount, int kOct = 8>
 __device__ __forceinline__ int two_level_fast(const TraceParams& P, uint4* items, const float2* s_ray,
                                               unsigned long long* s_key, uint32_t* s_tri, int n, int lane,
@@ -1283,16 +1304,33 @@ __device__ __forceinline__ int two_level_fast(const TraceParams& P, uint4* items
     const bool child = __builtin_amdgcn_inverse_ballot_w64((EL0 << 1) | (EL0 << 2));
     const float4* pa = child ? (const float4*)((const char*)P.inode + ((2 * it.x + (uint32_t)role) << 6))
                              : record_fast(P, it.x);
-    const float4 a0 = pa[0], a1 = pa[1], a2 = pa[2], a3 = pa[3];
+    float4 a0, a1, a2, a3;
+    if (masked_loads<kStride>()) {
+        // only the lanes whose record is used load one: role 0 of a live
+        // item, roles 1 and 2 of an expanded one
+        if (role == 0 ? act : child) {
+            a0 = pa[0]; a1 = pa[1]; a2 = pa[2]; a3 = pa[3];
+        }
+    } else {
+        a0 = pa[0]; a1 = pa[1]; a2 = pa[2]; a3 = pa[3];
+    }
     const float2* rd = s_ray + (size_t)(it.w >> 26);
     const float2 f0 = rd[0], f1 = rd[kStride], f2 = rd[2 * kStride];
     const float rx = f0.x, ry = f0.y, rz = f1.x, ix = f1.y, iy = f2.x, iz = f2.y;
     // the record's child boxes; each lane's own node's (t0, t1)
     float lt0, lt1, rt0, rt1;
     slab_pair_oct<kOct>(a0, a1, a2, ix, iy, iz, lt0, lt1, rt0, rt1);
-    const float u0 = role == 3 ? rt0 : lt0, u1 = role == 3 ? rt1 : lt1;
-    const float x0 = __uint_as_float((uint32_t)__builtin_amdgcn_mov_dpp((int)__float_as_uint(u0), 0xF0, 0xF, 0xF, true));
-    const float x1 = __uint_as_float((uint32_t)__builtin_amdgcn_mov_dpp((int)__float_as_uint(u1), 0xF0, 0xF, 0xF, true));
+    float x0, x1;
+    if (masked_loads<kStride>()) {
+        // role 0's values of both boxes, to roles 1 (left) and 2 (right)
+        const float bl0 = quad_bcast0(lt0), bl1 = quad_bcast0(lt1), br0 = quad_bcast0(rt0), br1 = quad_bcast0(rt1);
+        x0 = role == 1 ? bl0 : br0;
+        x1 = role == 1 ? bl1 : br1;
+    } else {
+        const float u0 = role == 3 ? rt0 : lt0, u1 = role == 3 ? rt1 : lt1;
+        x0 = __uint_as_float((uint32_t)__builtin_amdgcn_mov_dpp((int)__float_as_uint(u0), 0xF0, 0xF, 0xF, true));
+        x1 = __uint_as_float((uint32_t)__builtin_amdgcn_mov_dpp((int)__float_as_uint(u1), 0xF0, 0xF, 0xF, true));
+    }
     const float t0 = role == 0 ? __uint_as_float(it.y) : x0, t1 = role == 0 ? __uint_as_float(it.z) : x1;
     // the order of each lane's node (fast_slot)
     const uint32_t lw = __float_as_uint(a3.z), rw = __float_as_uint(a3.w);
@@ -1418,8 +1456,22 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
         // both records in flight before either is consumed
         const float4* p0 = kFast && !kAny ? record_fast(P, it0.x) : record_of(P, it0.x);
         const float4* p1 = kFast && !kAny ? record_fast(P, it1.x) : record_of(P, it1.x);
-        const float4 a0 = p0[0], a1 = p0[1], a2 = p0[2], a3 = p0[3];
-        const float4 b0 = p1[0], b1 = p1[1], b2 = p1[2], b3 = p1[3];
+        float4 a0, a1, a2, a3, b0, b1, b2, b3;
+        if (kFast && !kAny && masked_loads<kStride>()) {
+            // a pop of more than 64 items fills slot 0: both slots load on
+            // every lane, issued together; a smaller pop loads slot 0's live
+            // lanes only (an exec-masked second group waits for the first
+            // group's loads before it issues: 32-ray C3 -9 %, r05x)
+            if (take > 64) {
+                a0 = p0[0]; a1 = p0[1]; a2 = p0[2]; a3 = p0[3];
+                b0 = p1[0]; b1 = p1[1]; b2 = p1[2]; b3 = p1[3];
+            } else if (act0) {
+                a0 = p0[0]; a1 = p0[1]; a2 = p0[2]; a3 = p0[3];
+            }
+        } else {
+            a0 = p0[0]; a1 = p0[1]; a2 = p0[2]; a3 = p0[3];
+            b0 = p1[0]; b1 = p1[1]; b2 = p1[2]; b3 = p1[3];
+        }
         RT_RECORD_FENCE();
         // item 0 is visited, recorded and pushed before item 1 is visited, so
         // its results die before item 1's are made (fewer live VGPRs)
