@@ -12,6 +12,8 @@ for path in sys.argv[1:]:
             r = json.loads(line)
         except ValueError:
             continue
+        if not isinstance(r, dict) or "value" not in r:  # another tool's JSON (pmc_traffic.py)
+            continue
         rf = r.get("roofline") or {}
         cb = r.get("cpu_baseline") or {}
         fc = r.get("frame_check") or {}
