@@ -67,6 +67,7 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--out", default="")
     ap.add_argument("--session", default="r04o", help="the bench session whose lines are checked")
+    ap.add_argument("--trace-session", default="*", help="the session of the kernel traces and solo profiles (default: the latest by name)")
     a = ap.parse_args()
     pmc = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
     rows = []
@@ -87,13 +88,13 @@ def main():
         # repeats and variants of a configuration share its solo profile
         name = {"drv": "knot", "drv2": "knot", "drv_lanes": "knot", "knot_lanes": "knot", "trace_drv": "knot",
                 "rehearse": "knot", "anim2": "anim", "anim3": "anim"}.get(name, name)
-        st = sorted(glob.glob(os.path.join(a.dir, "rocprof", f"*_{name}_solo_kernel_stats.csv")))[-1:]
+        st = sorted(glob.glob(os.path.join(a.dir, "rocprof", f"{a.trace_session}_{name}_solo_kernel_stats.csv")))[-1:]
         kern = "k_trace_flat" if rf.get("unit") == "TFLOP/s" else "k_trace_kd3"
         avg = stats_avg_us(st[0], "k_flat_chunk" if kern == "k_trace_flat" else kern) if st else None
         if key and key.endswith("_mf"):
             # multi-frame launches: the per-frame time of the launches in a
             # kernel trace of the bench's own command (no solo profile)
-            tr = sorted(glob.glob(os.path.join(a.dir, "rocprof", f"*_trace_{name}_mf_kernel_trace.csv*")))[-1:]
+            tr = sorted(glob.glob(os.path.join(a.dir, "rocprof", f"{a.trace_session}_trace_{name}_mf_kernel_trace.csv*")))[-1:]
             pf = trace_per_frame_us(tr[0]) if tr else None
             avg = (pf[0], "multi-frame launches", pf[1]) if pf else None
         rec = None
