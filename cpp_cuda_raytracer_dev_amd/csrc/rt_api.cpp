@@ -2224,6 +2224,14 @@ static int ensure_lanes(rt_camera* c, int L, bool comm) {
 // Until a cost order exists (tile order 3) frames launch one at a time, so
 // that cost samples are taken; multi-frame launches take none.
 constexpr int32_t kPersistChunk = 128;
+// Each chunk of 4 or more frames as two concurrent launches of half the
+// frames, on the render stream and a second lane, when the launches take
+// 16-ray units (large fine regions): the driver's knot 1080p window 11.95-12.02k
+// -> 12.31-12.38k FPS, 1,000 frames 12.20k -> 12.82k, dragon 1080p 20.21k ->
+// 20.76k; 32-ray launches (960x540) lose 5 % and stay one launch (r05al).
+#ifndef RT_MF_SPLIT
+#define RT_MF_SPLIT 1
+#endif
 
 static int run_frames_multiframe(rt_camera* c, const rt_frame_loop* a, int32_t nframes, int64_t* seq,
                                  double* kernel_ms_avg, int32_t* kernel_ms_frames, double* host_ms) {
@@ -2272,11 +2280,37 @@ static int run_frames_multiframe(rt_camera* c, const rt_frame_loop* a, int32_t n
         }
         if (time_it && nbracket >= kRing) harvest(pair);
         if (time_it && (rc = hip_check(hipEventRecord(c->loop_ev[(size_t)(2 * pair)], rs), "loop timing"))) break;
-        const PersistArgs pf{chunk, (int32_t)((*seq) % a->nbuf), a->nbuf, a->d_local};
         const int k = (int)((*seq) % a->nbuf);
         int32_t done = 1;
-        rc = render_common(c, a->xform, a->mode, a->flags, tile, a->d_local[k], nullptr, rs, nullptr,
-                           chunk > 1 ? &pf : nullptr, &done);
+        if (RT_MF_SPLIT && chunk >= 4 && c->last_rays != 32 && (rc = ensure_lanes(c, 2, false)) == RT_OK) {
+            // two launches of half the frames each, on the render stream and
+            // a second lane at the same time (the two-lane loop's overlap of
+            // one grid's tail with another's head, with multi-frame launches)
+            const int32_t h1 = chunk / 2;
+            hipStream_t s2 = c->lanes[1];
+            if ((rc = hip_check(hipEventRecord(c->lane_ev[1], rs), "split fork")) ||
+                (rc = hip_check(hipStreamWaitEvent(s2, c->lane_ev[1], 0), "split fork wait")))
+                break;
+            const PersistArgs p1{h1, (int32_t)((*seq) % a->nbuf), a->nbuf, a->d_local};
+            rc = render_common(c, a->xform, a->mode, a->flags, tile, a->d_local[k], nullptr, rs, nullptr, &p1, &done);
+            if (rc) break;
+            if (done == h1) {
+                const PersistArgs p2{chunk - h1, (int32_t)((*seq + h1) % a->nbuf), a->nbuf, a->d_local};
+                int32_t done2 = 1;
+                rc = render_common(c, a->xform, a->mode, a->flags, tile, a->d_local[(*seq + h1) % a->nbuf], nullptr, s2,
+                                   nullptr, &p2, &done2);
+                if (rc) break;
+                done += done2;
+            }
+            if ((rc = hip_check(hipEventRecord(c->lane_ev[1], s2), "split join")) ||
+                (rc = hip_check(hipStreamWaitEvent(rs, c->lane_ev[1], 0), "split join wait")))
+                break;
+        } else {
+            if (rc) break;
+            const PersistArgs pf{chunk, (int32_t)((*seq) % a->nbuf), a->nbuf, a->d_local};
+            rc = render_common(c, a->xform, a->mode, a->flags, tile, a->d_local[k], nullptr, rs, nullptr,
+                               chunk > 1 ? &pf : nullptr, &done);
+        }
         if (rc) break;
         if (time_it) {
             if ((rc = hip_check(hipEventRecord(c->loop_ev[(size_t)(2 * pair + 1)], rs), "loop timing"))) break;

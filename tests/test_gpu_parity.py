@@ -1444,7 +1444,9 @@ def test_multiframe_launch_loop(key):
     each one k_trace_kd3 grid holding every frame's blocks, frame-major.
     Every buffer set holds the oracle's frame (committed hash) after 1, 3, 20
     and 200 frames, with 2 and 3 sets; the first frames before a cost order
-    exists launch one at a time.  A moving object or a gather is rejected."""
+    exists launch one at a time, and at 1920x1080 (16-ray units) a chunk of
+    4 or more frames runs as two concurrent launches of half the frames each
+    (RT_MF_SPLIT).  A moving object or a gather is rejected."""
     import hashlib
     import torch
     from cpp_cuda_raytracer_dev_amd import _lib

@@ -53,12 +53,23 @@ def trace_per_frame_us(path, kernel="k_trace_kd3"):
     g0 = min(grids)
     small = [g for g in grids if g < 1.5 * g0]
     one = max(set(small), key=small.count)
-    dur = frames = 0
+    # the union of the multi-frame launches' intervals (a chunk may run as
+    # two concurrent launches on two streams, RT_MF_SPLIT) over their frames
+    iv = []
+    frames = 0
     for r, g in zip(rows, grids):
         f = int(round(g / one))
         if f > 1:
-            dur += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            iv.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
             frames += f
+    dur, end = 0, None
+    for a, b in sorted(iv):
+        if end is None or a > end:
+            dur += b - a
+            end = b
+        elif b > end:
+            dur += b - end
+            end = b
     return (dur / frames / 1e3, frames) if frames else None
 
 
