@@ -2264,6 +2264,14 @@ static int run_frames_multiframe(rt_camera* c, const rt_frame_loop* a, int32_t n
     };
     int rc = RT_OK;
     const int every = a->event_every;
+    // the split (RT_MF_SPLIT) for launches of 16-ray units: the rays per
+    // wave this call's launches take (the multi-frame rule of auto_rays, or
+    // RT_OPT_RAYS), from the frame's geometry (static within the call)
+    bool split_ok = false;
+    if (RT_MF_SPLIT && a->mode == RT_MODE_KD && effective_kernel(c) == 3 && c->obj) {
+        TraceParams tp{};
+        split_ok = frame_geometry(camera_geom(c), a->xform, tile, a->mode, tp) && tp.rays != 32;
+    }
     const auto h0 = std::chrono::steady_clock::now();
     for (int32_t j = 0; j < nframes && !rc;) {
         const bool have_order = c->tile_order != 3 || c->order_gen == c->layout_gen;
@@ -2282,7 +2290,7 @@ static int run_frames_multiframe(rt_camera* c, const rt_frame_loop* a, int32_t n
         if (time_it && (rc = hip_check(hipEventRecord(c->loop_ev[(size_t)(2 * pair)], rs), "loop timing"))) break;
         const int k = (int)((*seq) % a->nbuf);
         int32_t done = 1;
-        if (RT_MF_SPLIT && chunk >= 4 && c->last_rays != 32 && (rc = ensure_lanes(c, 2, false)) == RT_OK) {
+        if (split_ok && chunk >= 4 && (rc = ensure_lanes(c, 2, false)) == RT_OK) {
             // two launches of half the frames each, on the render stream and
             // a second lane at the same time (the two-lane loop's overlap of
             // one grid's tail with another's head, with multi-frame launches)
