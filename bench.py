@@ -431,24 +431,74 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
+def visible_gpu_count():
+    """The GPUs a rank process could use, counted without torch, amdsmi or
+    HIP (torch.cuda.device_count() falls back to
+    hipGetDeviceCount, which initialises HIP, whenever amdsmi fails): the
+    KFD topology's nodes with SIMDs (a CPU node has simd_count 0), in node
+    order, then narrowed by ROCR_VISIBLE_DEVICES and HIP_VISIBLE_DEVICES
+    (CUDA_VISIBLE_DEVICES when HIP's is unset), each a comma list of indices
+    into the devices the previous filter left.  UUID entries count as one
+    device each.  None when the topology cannot be read (the ROCm runtime
+    enumerates GPUs from the same files, so a host whose runtime works has
+    it).  RT_KFD_TOPOLOGY names another topology directory (tests)."""
+    root = os.environ.get("RT_KFD_TOPOLOGY", "/sys/class/kfd/kfd/topology/nodes")
+    try:
+        names = sorted((d for d in os.listdir(root) if d.isdigit()), key=int)
+    except OSError:
+        return None
+    n = 0
+    for d in names:
+        try:
+            with open(os.path.join(root, d, "properties")) as fp:
+                props = dict(line.split(None, 1) for line in fp if len(line.split(None, 1)) == 2)
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0").strip() or 0) > 0:
+            n += 1
+
+    def narrow(count: int, spec) -> int:
+        if spec is None:
+            return count
+        keep = 0
+        for tok in (t.strip() for t in spec.split(",")):
+            if not tok:
+                break
+            if tok.isdigit():
+                if int(tok) >= count:
+                    break  # the runtimes stop at the first invalid index
+                keep += 1
+            else:
+                keep += 1  # a UUID names one device
+        return min(keep, count)
+
+    n = narrow(n, os.environ.get("ROCR_VISIBLE_DEVICES"))
+    hip = os.environ.get("HIP_VISIBLE_DEVICES")
+    return narrow(n, hip if hip is not None else os.environ.get("CUDA_VISIBLE_DEVICES"))
+
+
 def launch_ranks(a) -> int:
     """`--gpus N` (N > 1) without torch.distributed.run (WORLD_SIZE unset):
     start N fresh rank processes of this script with RANK / LOCAL_RANK /
     WORLD_SIZE / MASTER_ADDR (127.0.0.1) / MASTER_PORT set, one per GPU, and
-    wait for them.  This process never touches a GPU:
-    it only counts the visible devices (torch.cuda.device_count() does not
-    initialise HIP on this image) and fails fast when there are fewer than N.
-    Rank 0 prints the JSON line.  When a rank fails the others get 60 s to
-    finish, then are killed (by PID); the first failing rank's exit code is
-    returned."""
+    wait for them.  This process never touches a GPU,
+    nor loads torch or the HIP runtime: it counts the visible devices from
+    the KFD topology (visible_gpu_count) and fails fast when there are fewer
+    than N.  Rank 0 prints the JSON line.  When a rank fails the others get
+    60 s to finish, then are killed (by PID); the first failing rank's exit
+    code is returned.  RT_BENCH_LAUNCH_MAPS (tests) names a file the parent
+    copies its /proc/self/maps into just before it starts the ranks."""
     import subprocess
     n = a.gpus
-    if not a.launch_dry_run:
-        import torch
-        have = torch.cuda.device_count()
-        if have < n:
-            print(f"bench.py: --gpus {n} but only {have} GPU(s) visible", file=sys.stderr, flush=True)
-            return 2
+    have = visible_gpu_count()
+    if have is None:
+        print("bench.py: no KFD topology to count GPUs from; starting the ranks unchecked", file=sys.stderr, flush=True)
+    elif have < n:
+        print(f"bench.py: --gpus {n} but only {have} GPU(s) visible", file=sys.stderr, flush=True)
+        return 2
+    if os.environ.get("RT_BENCH_LAUNCH_MAPS"):
+        with open("/proc/self/maps") as src, open(os.environ["RT_BENCH_LAUNCH_MAPS"], "w") as dst:
+            dst.write(src.read())
     port = free_port()
     procs = []
     for r in range(n):

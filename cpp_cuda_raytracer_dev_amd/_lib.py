@@ -32,7 +32,8 @@ RT_OPT_SHADOW_ORDER = 6
 RT_OPT_FLAT = 7
 RT_OPT_RAYS_USED = 8
 RT_OPT_SPLIT_USED = 9
-RT_OPT_FAST_USED = 10
+RT_OPT_FAST_USED = 12
+RT_OPT_ORDER_RESTORES = 13
 RT_SCENE_ORDER = 1
 RT_SCENE_TREELET_HEIGHT = 2
 RT_SCENE_TWO_LEVEL_DEPTH = 3

@@ -18,6 +18,10 @@
 
 using namespace rt;
 
+// A tile grid's cost-order key (ensure_order): tile shape, grid size, ranks,
+// fine-region origin, rays per wave.
+constexpr int kOrderKey = 9;
+
 // A moving object's screen rectangle changes every frame, so its fine grid
 // did too: every frame got a new tile order slot, and the cost order (tile
 // order 3) never applied (its samples were always of a stale grid).  Renders
@@ -95,7 +99,7 @@ struct rt_camera {
     int64_t dbg_cap = 0;             // in u64
     Hold hold;                       // the fine region renders keep (set_fine_region)
     int32_t* d_order = nullptr;      // the current tile permutation (a slot's buffer)
-    int64_t order_key[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+    int64_t order_key[kOrderKey] = {-1, -1, -1, -1, -1, -1, -1, -1, -1};
     // Tile permutations live in a ring of slots: a new fine grid (a moving
     // object changes it every frame) writes the next slot behind the
     // caller's stream instead of rewriting the buffer earlier frames still
@@ -161,13 +165,14 @@ struct rt_camera {
     // against the per-frame one on a small frame -- starts each
     // switch with the order it last measured there, not the centre order
     struct KeptOrder {
-        int64_t key[8] = {};
+        int64_t key[kOrderKey] = {};
         std::vector<int32_t> ord;
         std::vector<uint32_t> mem;  // cost_mem with it
         int32_t split = 0;
     };
     KeptOrder kept[2];
     int kept_next = 0;
+    uint64_t restores = 0;           // kOptOrderRestores: kept orders restored
     int rays = 0;                    // kOptRays: pixels per wave of kernel 3 (0: auto_rays)
     int last_rays = 0;               // the pixels per wave the last kernel-3 render used
     int last_fast = 0;               // whether it took the kFast walks (fast_proof)
@@ -303,6 +308,11 @@ int prepare_camera_object(rt_camera* c) {
         (rc = hip_check(hipMemcpy(&c->cam_flags, c->d_cam_flags, sizeof(int32_t), hipMemcpyDeviceToHost), "D2H cam flags")))
         return rc;
     c->geom_gen++;  // cached launch parameters carry the flags
+    // kept cost orders measured another object or tree: a grid
+    // of the same key must not restart from them (the camera's position is
+    // fixed at rt_camera_create, so this covers every input of a cost order)
+    for (auto& e : c->kept) e = rt_camera::KeptOrder();
+    c->kept_next = 0;
     c->prepared_version = s->tree_version + 1;
     return RT_OK;
 }
@@ -332,8 +342,11 @@ int64_t all_tiles(const rt_camera* c, const TraceParams& p) {
 }
 
 int ensure_order(rt_camera* c, const TraceParams& p, hipStream_t st) {
-    const int64_t key[8] = {p.tile_w, p.tile_h, p.tiles_x, p.block_rows, p.nranks, p.rank, p.fine_tx0, p.fine_s0};
-    if (std::equal(key, key + 8, c->order_key)) return RT_OK;
+    // (the rays per wave too: 16- and 32-ray units both tile 8 x 8, and a cost
+    // order measured with one is kept for it, keep_order / restore_order)
+    const int64_t key[kOrderKey] = {p.tile_w, p.tile_h, p.tiles_x, p.block_rows, p.nranks,
+                                    p.rank, p.fine_tx0, p.fine_s0, p.rays};
+    if (std::equal(key, key + kOrderKey, c->order_key)) return RT_OK;
     const int64_t n = (int64_t)p.tiles_x * p.block_rows;
     const int64_t per_band = kTileH / p.tile_h;
     // centre-out: a counting sort of the tiles by their distance from the
@@ -419,7 +432,7 @@ int ensure_order(rt_camera* c, const TraceParams& p, hipStream_t st) {
     c->d_order = o.d;
     c->order_gen = ~0ull;  // no cost order for this grid yet
     c->order_split = 0;    // nor split tiles
-    std::copy(key, key + 8, c->order_key);
+    std::copy(key, key + kOrderKey, c->order_key);
     c->centre.swap(order);
     c->layout_gen++;
     // tile order 3: sample the new grid's costs once it has held for two
@@ -590,12 +603,12 @@ bool cost_sample_now(rt_camera* c, hipStream_t st) {
 void keep_order(rt_camera* c, const std::vector<int32_t>& ord, int32_t split) {
     rt_camera::KeptOrder* k = nullptr;
     for (auto& e : c->kept)
-        if (std::equal(e.key, e.key + 8, c->order_key)) k = &e;
+        if (std::equal(e.key, e.key + kOrderKey, c->order_key)) k = &e;
     if (!k) {
         k = &c->kept[c->kept_next];
         c->kept_next ^= 1;
     }
-    std::copy(c->order_key, c->order_key + 8, k->key);
+    std::copy(c->order_key, c->order_key + kOrderKey, k->key);
     k->ord = ord;
     k->mem = c->cost_mem;
     k->split = split;
@@ -606,12 +619,18 @@ void keep_order(rt_camera* c, const std::vector<int32_t>& ord, int32_t split) {
 // for it as for cost_feedback's uploads).
 int restore_order(rt_camera* c, const TraceParams& p, hipStream_t st) {
     const int64_t n = (int64_t)p.tiles_x * p.block_rows;
-    if (c->order_gen == c->layout_gen || c->order_pending || n > c->host_cap) return RT_OK;
+    if (c->order_gen == c->layout_gen || n > c->host_cap) return RT_OK;
+    // the previous grid's last cost-order upload reads h_order: wait for it
+    // by query only (cost_feedback clears the flag at its next sample)
+    if (c->order_pending) {
+        if (hipEventQuery(c->order_ev) != hipSuccess) return RT_OK;
+        c->order_pending = false;
+    }
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return RT_OK;
     const rt_camera::KeptOrder* k = nullptr;
     for (const auto& e : c->kept)
-        if ((int64_t)e.ord.size() == n && std::equal(e.key, e.key + 8, c->order_key)) k = &e;
+        if ((int64_t)e.ord.size() == n && std::equal(e.key, e.key + kOrderKey, c->order_key)) k = &e;
     if (!k || c->noused > 0) return RT_OK;  // (only before the grid's first launch)
     std::copy(k->ord.begin(), k->ord.end(), c->h_order);
     int rc;
@@ -624,6 +643,7 @@ int restore_order(rt_camera* c, const TraceParams& p, hipStream_t st) {
     c->order_pending = true;
     c->order_split = k->split;
     c->order_gen = c->layout_gen;
+    c->restores++;
     if ((int64_t)k->mem.size() == n) {
         c->cost_mem = k->mem;
         c->mem_gen = c->layout_gen;
@@ -2153,6 +2173,9 @@ extern "C" int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value) {
         if (value < 0 || value > 4) return fail(RT_ERR_INVALID, "tile order %d (0..4)", value);
         c->tile_order = value;
         return RT_OK;
+    case 10:
+    case 11:
+        return fail(RT_ERR_INVALID, "rt_camera_set_option: key %d is retired (ABI 2)", key);
     default:
         return fail(RT_ERR_INVALID, "rt_camera_set_option: unknown key %d", key);
     }
@@ -2171,7 +2194,10 @@ extern "C" int rt_camera_get_option(const rt_camera* c, int32_t key, int32_t* va
     case kOptDebug: *value = c->debug; return RT_OK;
     case kOptSplitUsed: *value = c->order_split; return RT_OK;
     case kOptFastUsed: *value = c->last_fast; return RT_OK;
+    case kOptOrderRestores: *value = (int32_t)std::min<uint64_t>(c->restores, INT32_MAX); return RT_OK;
     case kOptShadowOrder: *value = c->shadow_order >= 0 ? c->shadow_order : c->any_best; return RT_OK;
+    case 10:
+    case 11: return fail(RT_ERR_INVALID, "rt_camera_get_option: key %d is retired (ABI 2)", key);
     default: return fail(RT_ERR_INVALID, "rt_camera_get_option: unknown key %d", key);
     }
 }
@@ -2293,7 +2319,14 @@ static int run_frames_multiframe(rt_camera* c, const rt_frame_loop* a, int32_t n
         if (split_ok && chunk >= 4 && (rc = ensure_lanes(c, 2, false)) == RT_OK) {
             // two launches of half the frames each, on the render stream and
             // a second lane at the same time (the two-lane loop's overlap of
-            // one grid's tail with another's head, with multi-frame launches)
+            // one grid's tail with another's head, with multi-frame launches).
+            // Both halves write the ring of buffer sets ((seq + f) % nbuf,
+            // nbuf <= RT_LOOP_MAX_BUF, chunks of up to 128 frames), so two
+            // concurrent frames can write the same set: correct only because
+            // every frame of a multi-frame call is the same static frame --
+            // rt_run_frames rejects per-frame transforms (nxforms > 0) and a
+            // gather for RT_LOOP_MULTIFRAME, and this call passes the one
+            // a->xform to both launches.
             const int32_t h1 = chunk / 2;
             hipStream_t s2 = c->lanes[1];
             if ((rc = hip_check(hipEventRecord(c->lane_ev[1], rs), "split fork")) ||

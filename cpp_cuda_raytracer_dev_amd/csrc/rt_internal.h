@@ -55,7 +55,9 @@ enum Option : int32_t {
     kOptFlat = 7,       // flat-list kernel: 9 one pass, 12 the list in 16 chunks (default)
     kOptRaysUsed = 8,   // get only: pixels per wave of the last kernel-3 render
     kOptSplitUsed = 9,  // get only: split tiles at the head of the current cost order (kernel 3)
-    kOptFastUsed = 10,  // get only: whether the last kernel-3 render took the kFast walks
+    // 10, 11: retired (ABI 2; round 4's coop-used and frame-group keys)
+    kOptFastUsed = 12,  // get only: which walks of the last kernel-3 render took the kFast forms (bit mask)
+    kOptOrderRestores = 13,  // get only: kept cost orders restored (restore_order)
     kOptDebug = 100,    // diagnostics: 1 = skip traversal, 2 = per-wave timestamps, 4 = every group
                         // coarse, 8 = coarse kernel on a side stream beside the fine one,
                         // 16 = counted shadow walks stop at occluders (the timed walk's work),

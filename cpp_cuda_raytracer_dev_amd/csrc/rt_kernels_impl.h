@@ -26,6 +26,7 @@
 
 #include "rt_internal.h"
 #include "rt_predicates.h"
+#include "rt_rcp.h"
 
 namespace rt {
 namespace {
@@ -54,18 +55,7 @@ __device__ __forceinline__ float rsqrt21(float x, float y, float z) {
     return r;
 }
 
-// The correctly rounded 1.0f / x (the reference's 1 / r and (float)(1.0 /
-// (double)f)) for |x| in [2^-126, 2^126): the hardware reciprocal and one
-// Newton step with fused multiply-adds.  tools/check_rcp.hip compares it
-// with the division bit for bit over every float of that range (both signs,
-// 4.23e9 values, no difference on the MI355X: profiles/r05/check_rcp.json);
-// callers take it only for waves whose operands all lie in the range.
-__device__ __forceinline__ float rcp_nr(float x) {
-    const float r = __builtin_amdgcn_rcpf(x);
-    const float e = fmaf(-x, r, 1.0f);
-    return fmaf(e, r, r);
-}
-__device__ __forceinline__ bool rcp_nr_ok(float x) { return fabsf(x) >= 0x1p-126f && fabsf(x) < 0x1p126f; }
+// rcp_nr / rcp_nr_ok: rt_rcp.h (shared with tools/check_rcp.hip)
 
 // device_cross / device_dot, TD/vector.cuh:72-77,121-124
 __device__ __forceinline__ void cross3(float& cx, float& cy, float& cz, float ax, float ay,
@@ -1927,12 +1917,14 @@ __device__ __forceinline__ unsigned long long coarse_root(const TraceParams& P, 
 // (2,2,2) to the hit, walked from the light with the reference's rules.
 // One fine tile per block (the tiles covering the root box's screen
 // rectangle, or the whole frame), one unit per wave.
-// Occupancy: a 16-ray block's LDS (26 KB) admits 6 blocks per CU, and 88
-// VGPRs would admit 5 waves per SIMD; asking for 6 makes the compiler fit 80
-// (4 VGPRs spill to scratch in the timed variant).  Measured with two frames
-// in flight: dragon 1080p 13.7k -> 14.7k FPS, the 93 % fill view 940 ->
-// 873 us per frame; one frame at a time unchanged (86.7 -> 88.8 us).  The
-// 8-ray blocks are LDS-bound at 4 and keep their registers.
+// Occupancy: a 16-ray block's LDS (26 KB) admits 6 blocks per CU, and
+// __launch_bounds__ for 6 waves per SIMD caps the registers at 80 (round 2:
+// dragon 1080p 13.7k -> 14.7k FPS with two frames in flight, the 93 % fill
+// view 940 -> 873 us per frame).  On the round-5/6 kernels the timed 16-ray
+// instances fit 80 VGPRs without scratch; only the counting instances (kCount,
+// untimed) spill, and the shadow instances (84 VGPRs) run 5 waves per SIMD.
+// profiles/r06/kernel_resources.txt (tools/kernel_resources.py over the built
+// library) lists every instance's VGPRs, scratch and waves per SIMD.
 #ifndef RT_KD3_OCC
 #define RT_KD3_OCC 6
 #endif

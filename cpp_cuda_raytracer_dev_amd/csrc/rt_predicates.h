@@ -11,10 +11,16 @@
 // one of its edge cases (equality) decided by the double form.  Tiny, NaN and
 // equal operands take the double form itself.  tests/test_predicates.py
 // checks every fast form against its double form on CPU (edge sets plus
-// random sweeps over all binades).  The kernels use the double forms unless
-// built with -DRT_FAST_PREDICATES: on gfx950 the branches of the fast forms
-// cost more than the double arithmetic they skip (0.126 vs 0.118 ms per
-// 1080p dragon frame, tools/ab_session.sh).
+// random sweeps over all binades).  These per-predicate forms (with their
+// equality branches) serve the translated walks only with
+// -DRT_FAST_PREDICATES: on gfx950 their branches cost more than the double
+// arithmetic they skip (0.126 vs 0.118 ms per 1080p dragon frame, round 1).
+// The default kernels instead take branch-free float forms wherever a frame
+// PROVES that no operand is tiny (rt_kernels_impl.h kFast walks, rt_api.cpp
+// fast_proof: every box's maxt0 >= 2^-20, so the entry test is the float
+// mint1 >= maxt0, and the ordering compares use the exact float thresholds
+// k_cam_nodes stores), and the double forms below (the *_ref functions)
+// everywhere else.
 #pragma once
 
 #include <math.h>

@@ -21,7 +21,10 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+/* 2 (round 6): get-only option keys 10 and 11 are retired (rejected; they
+ * were RT_OPT_COOP_USED and RT_OPT_FRAME_GROUP in round 4), RT_OPT_FAST_USED
+ * moved to key 12 and became a bit mask, RT_OPT_ORDER_RESTORES is key 13. */
+#define RT_ABI_VERSION 2
 
 typedef enum rt_status {
     RT_OK = 0,
@@ -418,10 +421,18 @@ int rt_camera_info(const rt_camera* c, int32_t* w, int32_t* h, int32_t* max_dept
  * tile: the 4 units and the second halves).  The frame is the same either
  * way. */
 #define RT_OPT_SPLIT_USED 9
-/* get only: 1 when the last kernel-3 render's frame proved the float entry
- * test (its walks took the single-precision slab and ordering forms; the
- * frame is the same either way), else 0 */
-#define RT_OPT_FAST_USED 10
+/* Keys 10 and 11 are retired (ABI 2): RT_OPT_COOP_USED and
+ * RT_OPT_FRAME_GROUP of round 4; both are rejected. */
+/* get only: which walks of the last kernel-3 render took the exact
+ * single-precision slab and ordering forms (the frame is the same either
+ * way): bit 0 the nearest-hit walk (its frame proved the float entry test),
+ * bit 1 the shadow walk (the light proved it), bit 2 the walk ran under an
+ * object transform; 0 when neither proof held */
+#define RT_OPT_FAST_USED 12
+/* get only: how many times this camera restarted a tiling from the cost
+ * order it last measured there (a camera alternating between two tilings,
+ * e.g. rt_run_frames' multi-frame 32-ray rule and the per-frame 16-ray one) */
+#define RT_OPT_ORDER_RESTORES 13
 int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value);
 int rt_camera_get_option(const rt_camera* c, int32_t key, int32_t* value);
 

@@ -1500,6 +1500,7 @@ def test_multiframe_alternating_loops_kept_order():
                      inflight=_lib.RT_LOOP_MULTIFRAME)
     lanes = R.FrameLoop(s.cam, bufs, mode=0, render_stream=st.cuda_stream, event_every=8, inflight=2)
     used = set()
+    restores = []
     for i in range(6):
         loop = mf if i % 2 == 0 else lanes
         for b in bufs:
@@ -1508,9 +1509,15 @@ def test_multiframe_alternating_loops_kept_order():
         loop.run(60)
         torch.cuda.synchronize()
         used.add(s.cam.get_option(_lib.RT_OPT_RAYS_USED))
+        restores.append(s.cam.get_option(_lib.RT_OPT_ORDER_RESTORES))
         shas = {hashlib.sha256(b.cpu().numpy().view(np.uint32).tobytes()).hexdigest() for b in bufs}
         assert shas == {ent["argb_sha"]}, (i, s.cam.get_option(_lib.RT_OPT_RAYS_USED))
     assert used == {16, 32}
+    # the kept orders are really restored.  The first call of
+    # each tiling measures its order (60 frames hold several cost samples);
+    # from the third call on, every switch restarts from the kept one.
+    assert restores[0] == restores[1] == 0, restores
+    assert all(restores[i] == restores[i - 1] + 1 for i in range(2, 6)), restores
     assert s.cam.device_error(reset=True) == 0
     s.close()
 

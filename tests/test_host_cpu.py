@@ -22,7 +22,7 @@ def test_library_exports_every_declared_symbol():
     missing = [s for s in sorted(decl) if not hasattr(L, s)]
     assert not missing, missing
     assert decl == set(_lib.SIGNATURES), set(_lib.SIGNATURES) ^ decl
-    assert L.rt_abi_version() == 1
+    assert L.rt_abi_version() == 2
 
 
 def test_cpp_facade_and_headless_driver_compile(tmp_path):

@@ -10,11 +10,9 @@
 #include <cstdio>
 #include <cstdint>
 
-__device__ __forceinline__ float rcp_nr(float x) {
-    const float r = __builtin_amdgcn_rcpf(x);
-    const float e = fmaf(-x, r, 1.0f);
-    return fmaf(e, r, r);
-}
+#include "rt_rcp.h"  // the library's rcp_nr itself
+
+using rt::rcp_nr;
 
 __global__ void k_check(uint32_t lo_exp, unsigned long long* bad_per_exp, uint32_t* first_bad) {
     // one thread per (sign, exponent, mantissa): grid-stride over 2 * n_exp * 2^23
