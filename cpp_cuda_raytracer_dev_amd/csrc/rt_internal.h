@@ -63,7 +63,8 @@ enum Option : int32_t {
                         // 16 = counted shadow walks stop at occluders (the timed walk's work),
                         // 32 = counting renders stop after the root test, 64 = order / cost
                         // buffers sized for the current grid only, 256 = no held fine region,
-                        // 512 = no split tiles, 1024 = no two-level iterations, 2048 = no kFast walks
+                        // 512 = no split tiles, 1024 = no two-level iterations, 2048 = no kFast walks,
+                        // 16384 = record-load statistics (diagnostic builds, RT_VMEM_STATS)
     kOptPoolCap = 101,  // tests: shrink kernel 3's item pool (66..kPoolCap) to force its fallback
 };
 constexpr int kPoolCapMax = 640;
@@ -131,10 +132,14 @@ struct TraceParams {
     int32_t fill_blocks;           // blocks after the fine grid filling far groups (fused mode)
     int64_t coarse_groups;         // total coarse groups
     int32_t plain_xf;              // object transform is the identity (rotation 1, offset 0)
-    // kernel 3's kFast walks apply (rt_api.cpp fast_proof): identity
-    // transform, ordered boxes, and every box's entry parameter >= 2^-20
-    // for every ray of the frame
+    // kernel 3's kFast walks apply (rt_api.cpp fast_proof): ordered boxes,
+    // and every box's entry parameter >= 2^-20 for every ray of the frame
+    // (any rotation; with an offset the translated walks take xfast_slot)
     int32_t fast;
+    // shadow walks (round 6): the translated kFast slots apply to a shadow
+    // ray that points to side sh_neg (1: negative) of axis sh_axis with
+    // normal, nonzero components (rt_api.cpp fast_proof_shadow)
+    int32_t fast_sh, sh_axis, sh_neg;
     uint32_t leaf_off;             // byte offset of trec from inode (one allocation; rt_api.cpp prepare_camera_object)
     int32_t tiny_s1;               // some interior record of the camera has the tiny-s1 flag
     int32_t far_rect[4];           // root box's screen rectangle + 2 px (x0, x1, y0, y1; frame pixels)
@@ -152,6 +157,9 @@ struct TraceParams {
     int32_t items;                 // kernel 3 items per lane per iteration (1 or 2)
     int32_t debug;                 // diagnostic builds only: 1 = skip traversal
     unsigned long long* dbg;       // per-wave (t_start, t_end, visits) when non-null
+    // diagnostic builds (-DRT_VMEM_STATS=1) with debug bit 16384: record-load
+    // statistics per walk form (rt_kernels_impl.h vmem_stat), or null
+    unsigned long long* vstat;
     // A multi-frame launch (kernel 3; pf_frames > 0): pf_frames frames of
     // pf_blocks blocks each in one grid, frame-major; frame f writes
     // pf_argb[(pf_seq0 + f) % pf_nbuf].

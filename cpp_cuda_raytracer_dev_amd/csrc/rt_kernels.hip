@@ -77,7 +77,7 @@ int launch_trace(const TraceParams& p, uint32_t mode, uint32_t flags, int kernel
                         : (cnt ? kd_kernel_101(v, r, sh, coarse) : kd_kernel_100(v, r, sh, coarse));
         else fn = wh ? (cnt ? kd_kernel_011(v, r, sh, coarse) : kd_kernel_010(v, r, sh, coarse))
                      : (cnt ? kd_kernel_001(v, r, sh, coarse) : kd_kernel_000(v, r, sh, coarse));
-        if (!coarse && p.pf_frames > 0) grid *= (unsigned)p.pf_frames;  // a multi-frame launch, frame-major
+        if (!coarse && p.pf_frames > 0) grid = (unsigned)p.pf_blocks * (unsigned)p.pf_frames;  // a multi-frame launch, frame-major
         fn<<<grid, coarse ? 128u : threads, 0, s>>>(p);
         int rc = check_launch<void>(coarse ? "k_coarse_kd3" : "k_trace_kd");
         if (rc) return rc;

@@ -125,7 +125,8 @@ __device__ __forceinline__ void put_pixel(const TraceParams& P, int64_t out, uin
 // permutation, so the heavy centre tiles are dispatched first; order 3: the
 // host's permutation by the tiles' measured cost in an earlier frame,
 // heaviest first (centre-out until costs arrive); order 4: the same per XCD
-// over 8 screen regions of equal cost.
+// over 8 screen regions of equal cost; order 5: per XCD over 8 row bands of
+// equal tile count (rt_api.cpp cost_order).
 __device__ __forceinline__ int32_t tile_index(const TraceParams& P, int32_t b) {
     const int32_t nblocks = P.tiles_x * P.block_rows;
     if (P.tile_order == 0) {
@@ -350,6 +351,42 @@ __device__ __forceinline__ void slab_pair_oct(float4 r0, float4 r1, float4 r2, f
     }
 }
 
+// slab_pair_oct for translated walks (round 6): the reference's t = b * (1/r)
+// + od/r per axis (TD/Trixel.cu:76-95), the product of the near bound (lo for
+// r > 0) plus the offset for t0 and of the far bound for t1 -- with the
+// octant known at compile time the selection is fixed; for mixed octants
+// (kOct 8) min / max of the two products select it (lo <= hi, 1/r of the
+// component's sign).  Products as v_pk_mul_f32 pairs, then the offsets.
+template <int kOct>
+__device__ __forceinline__ void slab_pair_xoct(float4 r0, float4 r1, float4 r2, float ix, float iy, float iz, float ox,
+                                               float oy, float oz, float& lt0, float& lt1, float& rt0, float& rt1) {
+    const f2v ax = f2v{r0.x, r0.y} * ix, ay = f2v{r0.z, r0.w} * iy, az = f2v{r1.x, r1.y} * iz;
+    const f2v bx = f2v{r1.z, r1.w} * ix, by = f2v{r2.x, r2.y} * iy, bz = f2v{r2.z, r2.w} * iz;
+    float anx, afx, any, afy, anz, afz, bnx, bfx, bny, bfy, bnz, bfz;
+    if constexpr (kOct >= 8) {
+        anx = fminf(ax.x, ax.y); afx = fmaxf(ax.x, ax.y);
+        any = fminf(ay.x, ay.y); afy = fmaxf(ay.x, ay.y);
+        anz = fminf(az.x, az.y); afz = fmaxf(az.x, az.y);
+        bnx = fminf(bx.x, bx.y); bfx = fmaxf(bx.x, bx.y);
+        bny = fminf(by.x, by.y); bfy = fmaxf(by.x, by.y);
+        bnz = fminf(bz.x, bz.y); bfz = fmaxf(bz.x, bz.y);
+    } else {
+        constexpr bool sx = (kOct & 1) != 0, sy = (kOct & 2) != 0, sz = (kOct & 4) != 0;
+        anx = sx ? ax.x : ax.y; afx = sx ? ax.y : ax.x;
+        any = sy ? ay.x : ay.y; afy = sy ? ay.y : ay.x;
+        anz = sz ? az.x : az.y; afz = sz ? az.y : az.x;
+        bnx = sx ? bx.x : bx.y; bfx = sx ? bx.y : bx.x;
+        bny = sy ? by.x : by.y; bfy = sy ? by.y : by.x;
+        bnz = sz ? bz.x : bz.y; bfz = sz ? bz.y : bz.x;
+    }
+    const f2v o2 = f2v{ox, oy};
+    const f2v la = f2v{anx, any} + o2, lb = f2v{afx, afy} + o2, ra = f2v{bnx, bny} + o2, rb = f2v{bfx, bfy} + o2;
+    lt0 = fmaxf(anz + oz, fmaxf(la.x, la.y));
+    lt1 = fminf(afz + oz, fminf(lb.x, lb.y));
+    rt0 = fmaxf(bnz + oz, fmaxf(ra.x, ra.y));
+    rt1 = fminf(bfz + oz, fminf(rb.x, rb.y));
+}
+
 // Slab test of one node, TD/Trixel.cu:76-95,146: entry/exit parameters and
 // whether the reference descends into the node.
 __device__ __forceinline__ bool slab(const Ray& R, float lx, float hx, float ly, float hy, float lz,
@@ -406,6 +443,32 @@ __device__ __forceinline__ bool leaf_test_cam(const Ray& R, const float4 A, cons
     const float u = pe1 * dot3(qpx, qpy, qpz, tx, ty, tz);
     const float v = pe1 * dot3(R.rx, R.ry, R.rz, Cq.y, Cq.z, Cq.w);
     const float w = pe1 * Dq.x;
+    const bool acc = !(f < kEpsF && f > -kEpsF) & (w < d) &
+                     !((u < kEpsF) | (v < kEpsF) | ((u + v) > 1.0f) | (w < kEpsF));
+    d = acc ? w : d;
+    best = acc ? t : best;
+    return acc;
+}
+
+// leaf_test_rec for the translated kFast walks (round 6: object transforms
+// with an offset, and the shadow rays from the light): the same float
+// expressions, every term computed and selected (no exec-mask branches), and
+// pe1 from rcp_nr as in leaf_test_cam.
+__device__ __forceinline__ bool leaf_test_xf(const Ray& R, const float4 A, const float4 B, const float4 Cq, uint32_t t,
+                                             float& d, uint32_t& best) {
+    const float e1x = A.x, e1y = A.y, e1z = A.z;
+    const float e2x = A.w, e2y = B.x, e2z = B.y;
+    const float dtx = B.z, dty = B.w, dtz = Cq.x;
+    float qpx, qpy, qpz;
+    cross3(qpx, qpy, qpz, R.rx, R.ry, R.rz, e2x, e2y, e2z);
+    const float f = dot3(qpx, qpy, qpz, e1x, e1y, e1z);
+    const float pe1 = __ballot(fabsf(f) >= 0x1p126f) == 0ull ? rcp_nr(f) : 1.0f / f;
+    const float tx = dtx - R.odx, ty = dty - R.ody, tz = dtz - R.odz;
+    const float u = pe1 * dot3(qpx, qpy, qpz, tx, ty, tz);
+    float qx, qy, qz;
+    cross3(qx, qy, qz, tx, ty, tz, e1x, e1y, e1z);
+    const float v = pe1 * dot3(R.rx, R.ry, R.rz, qx, qy, qz);
+    const float w = pe1 * dot3(e2x, e2y, e2z, qx, qy, qz);
     const bool acc = !(f < kEpsF && f > -kEpsF) & (w < d) &
                      !((u < kEpsF) | (v < kEpsF) | ((u + v) > 1.0f) | (w < kEpsF));
     d = acc ? w : d;
@@ -1149,6 +1212,111 @@ __device__ __forceinline__ int fast_slot(const TraceParams& P, uint4* items, int
     return nL + __builtin_popcountll(mR);
 }
 
+// One slot of a translated kFast pool iteration (round 6, verdict r05 items
+// 2-3): the walks of an object moved by an offset (its rays carry the
+// translation od, TD/Trixel.cu:60-66,94-95) and the shadow walks from the
+// light (od = (-2, -2, -2), a12), under a proof that every box's entry
+// parameter is >= 2^-20 for each of their rays (rt_api.cpp fast_proof for the
+// frame; fast_proof_shadow for the light plus trace_unit's per-wave sign
+// check).  The reference's tests, exactly, in single precision:
+//   * entry (TD/Trixel.cu:146): mint1 >= maxt0 (maxt0 >= 2^-20, as kFast);
+//   * the child order against s2 + ds (:155-157): s = s2 + ds is the
+//     reference's float sum, and for |s| >= 2^-20 the double compares are
+//     pred::lt_eps_x / gt_eps_x (the equality case included); a lane whose s
+//     is tiny takes the double form behind a wave-uniform branch;
+//   * s1 + 1e-16 + ds (:150-151): the reference's double expression;
+//   * slabs with the offsets (slab_pair_xoct), the MT test leaf_test_xf.
+// The direction on the cut axis is the component itself and ds the offset's
+// component (r_a * 1 + r_b * 0 + r_c * 0 == r_a for finite nonzero r; a zero
+// offset component's sign does not reach any compare).  kAny: the shadow
+// walk (Lmax and the hit triangle from field 9, no path codes; pushes in
+// the launch's any-hit order kAnyOrd, push_children).  Nearest-hit walks
+// push as fast_slot does.
+template <int kStride, bool kCount, bool kAny, int kAnyOrd, int kOct>
+__device__ __forceinline__ int xfast_slot(const TraceParams& P, uint4* items, int at, const float2* s_ray,
+                                          unsigned long long* s_key, uint32_t* s_tri, uint4 it, bool act, float4 r0,
+                                          float4 r1, float4 r2, float4 r3, uint32_t& n_int, uint32_t& n_leaf,
+                                          uint32_t& n_acc, uint32_t& n_desc) {
+    const float2* rd = s_ray + (size_t)(it.w >> 26);
+    const unsigned long long A = __ballot(act), LEAF = __ballot((it.x & kLeafBit) != 0) & A, INT = A & ~LEAF;
+    const float2 f0 = rd[0], f1 = rd[kStride], f2 = rd[2 * kStride], f6 = rd[6 * kStride], f7 = rd[7 * kStride];
+    const float rx = f0.x, ry = f0.y, rz = f1.x, ix = f1.y, iy = f2.x, iz = f2.y;
+    const float odx = f6.x, ody = f6.y, odz = f7.x;
+    if (LEAF) {
+        Ray Q;
+        Q.rx = rx; Q.ry = ry; Q.rz = rz;
+        Q.odx = odx; Q.ody = ody; Q.odz = odz;
+        const float2 f9 = kAny ? rd[9 * kStride] : make_float2(0.0f, 0.0f);
+        float d = kAny ? f9.x : kDrawDistance;
+        uint32_t best = kMiss;
+        const bool acc = leaf_test_xf(Q, r0, r1, r2, it.x & ~kLeafBit, d, best);
+        const bool mine = __builtin_amdgcn_inverse_ballot_w64(LEAF);
+        Visit v;
+        v.cand = acc && mine && (!kAny || best != __float_as_uint(f9.y));
+        v.ctri = best;
+        v.key = kAny ? 0ull : ((unsigned long long)__float_as_uint(d) << 32) | code_key(it.w & kCodeMarkMask);
+        if (kCount) {
+            n_leaf += mine ? 1u : 0u;
+            n_acc += v.cand ? 1u : 0u;
+        }
+        record_candidate<kAny>(s_key, s_tri, it, v);
+    }
+    if (!INT) return 0;
+    const float2 f3 = rd[3 * kStride], f4 = rd[4 * kStride];
+    float lt0, lt1, rt0, rt1;
+    slab_pair_xoct<kOct>(r0, r1, r2, ix, iy, iz, f3.x, f3.y, f4.x, lt0, lt1, rt0, rt1);
+    const uint32_t lw = __float_as_uint(r3.z), rw = __float_as_uint(r3.w);
+    const uint32_t axis = (lw >> kAxisShift) & 3u;
+    const uint32_t L = lw & ~(3u << kAxisShift), R = rw & ~kTinyS1Bit;
+    const float dir = axis == 2 ? rz : axis == 1 ? ry : rx;
+    const float ds = axis == 2 ? odz : axis == 1 ? ody : odx;
+    const float t0 = __uint_as_float(it.y), t1 = __uint_as_float(it.z);
+    const float mx = t0 * dir, mn = t1 * dir;
+    const float s1 = (float)(((double)rec_s1(r0, r1, axis) + kEps) + (double)ds);
+    const float s2 = rec_s2(r1, r2, axis) + ds;
+    bool lf = pred::lt_eps_x(mx, s2), pa = pred::gt_eps_x(mn, s2);
+    const bool tiny = !(fabsf(s2) >= 0x1p-20f);  // (NaN s2 takes it too: the double form decides)
+    if (__ballot(tiny) & INT) {
+        lf = tiny ? pred::lt_eps_ref(opaque(mx), s2) : lf;
+        pa = tiny ? pred::gt_eps_ref(opaque(mn), s2) : pa;
+    }
+    const unsigned long long LF = __ballot(lf);
+    const unsigned long long PS = (LF & __ballot(pa)) | (~LF & __ballot(fminf(mn, mx) < s1));
+    const unsigned long long mL = INT & (__ballot(lt1 >= lt0) | __ballot((int32_t)L < 0)) & (LF | PS);
+    const unsigned long long mR = INT & (__ballot(rt1 >= rt0) | __ballot((int32_t)R < 0)) & (~LF | PS);
+    if (kCount && __builtin_amdgcn_inverse_ballot_w64(INT)) {  // the reference's counters (count_order)
+        const bool ps = __builtin_amdgcn_inverse_ballot_w64(PS);
+        const bool li = (L & kLeafBit) == 0, ri = (R & kLeafBit) == 0, lp = lt1 >= lt0, rp = rt1 >= rt0;
+        const bool fi = lf ? li : ri, si = lf ? ri : li, fp = lf ? lp : rp, sp = lf ? rp : lp;
+        n_int += (fi ? 1u : 0u) + ((ps && si) ? 1u : 0u);
+        n_desc += ((fi && fp) ? 1u : 0u) + ((ps && si && sp) ? 1u : 0u);
+    }
+    if constexpr (kAny) {
+        // any-hit: no path codes; the launch's push order over (first, second)
+        // (selected field by field: a select of the two uint4 items became a
+        // select of their addresses in scratch)
+        const bool kl = __builtin_amdgcn_inverse_ballot_w64(mL), kr = __builtin_amdgcn_inverse_ballot_w64(mR);
+        const uint32_t l0 = __float_as_uint(lt0), l1 = __float_as_uint(lt1);
+        const uint32_t q0 = __float_as_uint(rt0), q1 = __float_as_uint(rt1);
+        Visit v;
+        v.ca = make_uint4(lf ? L : R, lf ? l0 : q0, lf ? l1 : q1, it.w);
+        v.cb = make_uint4(lf ? R : L, lf ? q0 : l0, lf ? q1 : l1, it.w);
+        v.ka = lf ? kl : kr;
+        v.kb = lf ? kr : kl;
+        return push_children<true, kAnyOrd>(items, at, v);
+    } else {
+        const uint32_t meta = it.w + (it.w & kCodeMarkMask);
+        const int nL = __builtin_popcountll(mL);
+        if (__builtin_amdgcn_inverse_ballot_w64(mL))
+            items[at + (int)lanes_below(mL)] =
+                make_uint4(L, __float_as_uint(lt0), __float_as_uint(lt1), meta | (lf ? 0u : 1u));
+        if (__builtin_amdgcn_inverse_ballot_w64(mR))
+            items[at + nL + (int)lanes_below(mR)] =
+                make_uint4(R, __float_as_uint(rt0), __float_as_uint(rt1), meta | (lf ? 1u : 0u));
+        return nL + __builtin_popcountll(mR);
+    }
+}
+
 // Record loads by the lanes that use them only (kFast walks of 8- and 16-ray
 // units; RT_MASKED_LOADS32 for 32-ray units).  The walk's busiest unit is the
 // vector memory path (r05w: TA busy 0.85, TD busy 0.96 of the knot's cycles),
@@ -1167,6 +1335,60 @@ __device__ __forceinline__ int fast_slot(const TraceParams& P, uint4* items, int
 template <int kStride>
 constexpr bool masked_loads() {
     return kStride == RT_RAY_STRIDE32 ? RT_MASKED_LOADS32 != 0 : RT_MASKED_LOADS != 0;
+}
+
+// Record-load statistics (verdict r05 item 1: "measure live lanes per pop
+// against distinct nodes per pop, and loads per visit by walk form"), in
+// diagnostic builds (-DRT_VMEM_STATS=1, debug bit 16384) only.  Per walk form
+// (0 a single-slot pop, 1 / 2 slot 0 / slot 1 of a two-slot pop, 3 a
+// two-level iteration) and per record group (four dwordx4 wave loads):
+//   [0] groups, [1] live items, [2] loading lanes, [3] the vector memory
+//   path's cycles per wave load by tools/ubench_l1.hip's model (sum over the
+//   16 lane quads of max(1, distinct 128-B lines its loading lanes touch)),
+//   [4] distinct records among the live lanes, [5] distinct 128-B lines.
+#ifndef RT_VMEM_STATS
+#define RT_VMEM_STATS 0
+#endif
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+    for (int off = 32; off >= 1; off >>= 1) v += (uint32_t)__shfl_xor((int)v, off);
+    return v;
+}
+__device__ __forceinline__ void vmem_stat(const TraceParams& P, int form, const float4* addr, bool load, bool live) {
+    if (!RT_VMEM_STATS || !P.vstat) return;
+    const int lane = (int)threadIdx.x & 63;
+    const uint32_t off = (uint32_t)((const char*)addr - (const char*)P.inode);
+    const uint32_t line = off >> 7, rec = off >> 6;
+    const uint32_t v = load ? line : 0xFFFFFFFFu;
+    const uint32_t q0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x00, 0xF, 0xF, true);
+    const uint32_t q1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x55, 0xF, 0xF, true);
+    const uint32_t q2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xAA, 0xF, 0xF, true);
+    const uint32_t q3 = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xFF, 0xF, 0xF, true);
+    const uint32_t d = (q0 != ~0u ? 1u : 0u) + ((q1 != ~0u && q1 != q0) ? 1u : 0u) +
+                       ((q2 != ~0u && q2 != q0 && q2 != q1) ? 1u : 0u) +
+                       ((q3 != ~0u && q3 != q0 && q3 != q1 && q3 != q2) ? 1u : 0u);
+    const uint32_t qcost = wave_sum_u32((lane & 3) == 0 ? (d > 0 ? d : 1u) : 0u);
+    const unsigned long long LIVE = __ballot(live), LOAD = __ballot(load);
+    bool first_rec = live, first_line = live;
+    for (int j = 0; j < 64; j++) {
+        const uint32_t rj = (uint32_t)__builtin_amdgcn_readlane((int)rec, j);
+        const uint32_t lj = (uint32_t)__builtin_amdgcn_readlane((int)line, j);
+        if (((LIVE >> j) & 1ull) && j < lane) {
+            if (rj == rec) first_rec = false;
+            if (lj == line) first_line = false;
+        }
+    }
+    if (lane == 0) {
+        unsigned long long* c = P.vstat + 6 * form;
+        atomicAdd(&c[0], 1ull);
+        atomicAdd(&c[1], (unsigned long long)__builtin_popcountll(LIVE));
+        atomicAdd(&c[2], (unsigned long long)__builtin_popcountll(LOAD));
+        atomicAdd(&c[3], (unsigned long long)qcost);
+    }
+    const unsigned long long FR = __ballot(first_rec), FL = __ballot(first_line);
+    if (lane == 0) {
+        atomicAdd(&P.vstat[6 * form + 4], (unsigned long long)__builtin_popcountll(FR));
+        atomicAdd(&P.vstat[6 * form + 5], (unsigned long long)__builtin_popcountll(FL));
+    }
 }
 
 // Two-level pool iterations (default on; debug bit 1024 or a
@@ -1273,7 +1495,9 @@ __device__ __forceinline__ int two_level_iter(const TraceParams& P, uint4* items
 // value; with masked loads (masked_loads) role 3 loads no record and roles 1
 // and 2 take both boxes' values from role 0, two exchanges per value.  Which
 // nodes are visited and pushed, and every path code, are two_level_iter's.
-template <int kStride, bool kCount, int kOct = 8>
+// kXl (round 6): a translated walk's form (xfast_slot's slabs with the
+// offsets, its ordering against s2 + ds, the translated MT test).
+template <int kStride, bool kCount, int kOct = 8, bool kXl = false>
 __device__ __forceinline__ int two_level_fast(const TraceParams& P, uint4* items, const float2* s_ray,
                                               unsigned long long* s_key, uint32_t* s_tri, int n, int lane,
                                               uint32_t& n_int, uint32_t& n_leaf, uint32_t& n_acc, uint32_t& n_desc) {
@@ -1295,6 +1519,7 @@ __device__ __forceinline__ int two_level_fast(const TraceParams& P, uint4* items
     const float4* pa = child ? (const float4*)((const char*)P.inode + ((2 * it.x + (uint32_t)role) << 6))
                              : record_fast(P, it.x);
     float4 a0, a1, a2, a3;
+    vmem_stat(P, 3, pa, masked_loads<kStride>() ? (role == 0 ? act : child) : true, role == 0 ? act : child);
     if (masked_loads<kStride>()) {
         // only the lanes whose record is used load one: role 0 of a live
         // item, roles 1 and 2 of an expanded one
@@ -1307,9 +1532,15 @@ __device__ __forceinline__ int two_level_fast(const TraceParams& P, uint4* items
     const float2* rd = s_ray + (size_t)(it.w >> 26);
     const float2 f0 = rd[0], f1 = rd[kStride], f2 = rd[2 * kStride];
     const float rx = f0.x, ry = f0.y, rz = f1.x, ix = f1.y, iy = f2.x, iz = f2.y;
+    const float2 z2 = make_float2(0.0f, 0.0f);
+    const float2 f3 = kXl ? rd[3 * kStride] : z2, f4 = kXl ? rd[4 * kStride] : z2;
+    const float2 f6 = kXl ? rd[6 * kStride] : z2, f7 = kXl ? rd[7 * kStride] : z2;
     // the record's child boxes; each lane's own node's (t0, t1)
     float lt0, lt1, rt0, rt1;
-    slab_pair_oct<kOct>(a0, a1, a2, ix, iy, iz, lt0, lt1, rt0, rt1);
+    if constexpr (kXl)
+        slab_pair_xoct<kOct>(a0, a1, a2, ix, iy, iz, f3.x, f3.y, f4.x, lt0, lt1, rt0, rt1);
+    else
+        slab_pair_oct<kOct>(a0, a1, a2, ix, iy, iz, lt0, lt1, rt0, rt1);
     float x0, x1;
     if (masked_loads<kStride>()) {
         // role 0's values of both boxes, to roles 1 (left) and 2 (right)
@@ -1328,14 +1559,32 @@ __device__ __forceinline__ int two_level_fast(const TraceParams& P, uint4* items
     const uint32_t L = lw & ~(3u << kAxisShift), R = rw & ~kTinyS1Bit;
     const float dir = axis == 2 ? rz : axis == 1 ? ry : rx;
     const float mx = t0 * dir, mn = t1 * dir;
-    float s1 = rec_s1(a0, a1, axis);
-    if (P.tiny_s1) {
-        const float s1t = pred::add_eps_ref(opaque(s1));
-        s1 = (rw & kTinyS1Bit) != 0 ? s1t : s1;
+    float s1;
+    bool lf, pgt;
+    if constexpr (kXl) {
+        // xfast_slot's ordering: s2 + ds (the offset's component) through
+        // the exact float compares, s1 + 1e-16 + ds in double
+        const float ds = axis == 2 ? f7.x : axis == 1 ? f6.y : f6.x;
+        s1 = (float)(((double)rec_s1(a0, a1, axis) + kEps) + (double)ds);
+        const float s2 = rec_s2(a1, a2, axis) + ds;
+        lf = pred::lt_eps_x(mx, s2);
+        pgt = pred::gt_eps_x(mn, s2);
+        const bool tiny = !(fabsf(s2) >= 0x1p-20f);
+        if (__ballot(tiny)) {
+            lf = tiny ? pred::lt_eps_ref(opaque(mx), s2) : lf;
+            pgt = tiny ? pred::gt_eps_ref(opaque(mn), s2) : pgt;
+        }
+    } else {
+        s1 = rec_s1(a0, a1, axis);
+        if (P.tiny_s1) {
+            const float s1t = pred::add_eps_ref(opaque(s1));
+            s1 = (rw & kTinyS1Bit) != 0 ? s1t : s1;
+        }
+        lf = mx < a3.y;
+        pgt = mn > a3.x;
     }
-    const bool lf = mx < a3.y;
     const unsigned long long LF = __ballot(lf);
-    const unsigned long long PS = (LF & __ballot(mn > a3.x)) | (~LF & __ballot(fminf(mn, mx) < s1));
+    const unsigned long long PS = (LF & __ballot(pgt)) | (~LF & __ballot(fminf(mn, mx) < s1));
     const unsigned long long KL = (__ballot(lt1 >= lt0) | __ballot((int32_t)L < 0)) & (LF | PS);
     const unsigned long long KR = (__ballot(rt1 >= rt0) | __ballot((int32_t)R < 0)) & (~LF | PS);
     // the children role 0 keeps are visited by roles 1 and 2
@@ -1370,7 +1619,19 @@ __device__ __forceinline__ int two_level_fast(const TraceParams& P, uint4* items
         Ray Q;
         Q.rx = rx; Q.ry = ry; Q.rz = rz;
         uint32_t nlf = 0, na = 0;
-        visit_leaf<false, kCount, false>(Q, make_float4(0.0f, 0.0f, 0.0f, 0.0f), it, a0, a1, a2, a3, v, nlf, na);
+        if constexpr (kXl) {
+            Q.odx = f6.x; Q.ody = f6.y; Q.odz = f7.x;
+            float d = kDrawDistance;
+            uint32_t best = kMiss;
+            const bool acc = leaf_test_xf(Q, a0, a1, a2, it.x & ~kLeafBit, d, best);
+            v.cand = acc;
+            v.ctri = best;
+            v.key = ((unsigned long long)__float_as_uint(d) << 32) | code_key(it.w & kCodeMarkMask);
+            nlf = 1u;
+            na = acc ? 1u : 0u;
+        } else {
+            visit_leaf<false, kCount, false>(Q, make_float4(0.0f, 0.0f, 0.0f, 0.0f), it, a0, a1, a2, a3, v, nlf, na);
+        }
         const bool mine = __builtin_amdgcn_inverse_ballot_w64(LEAF0);
         v.cand = v.cand && mine;
         if (kCount) {
@@ -1388,8 +1649,21 @@ __device__ __forceinline__ int two_level_fast(const TraceParams& P, uint4* items
 // key[ray] = 0; without counters the items of such rays are dropped.
 // Each lane pops up to P.items (1 or 2) items per iteration and fetches their
 // records together, so a lane keeps two memory round trips in flight.
+// kX (round 6): the translated kFast slots (xfast_slot) for a translated
+// nearest-hit walk or a shadow walk whose proof holds; its two-level
+// iterations keep the double forms (two_level_iter).
+#ifndef RT_XMASKED_LOADS
+#define RT_XMASKED_LOADS 1
+#endif
+#ifndef RT_SHMASKED_LOADS
+#define RT_SHMASKED_LOADS 0
+#endif
+// the translated walks' two-level iterations in the xfast forms (two_level_fast<kXl>)
+#ifndef RT_XTWO_LEVEL
+#define RT_XTWO_LEVEL 1
+#endif
 template <int kCap, int kStride, bool kTranslated, bool kCount, bool kAny, int kOrder = 0, bool kFast = false,
-          int kOct = 8>
+          int kOct = 8, bool kX = false>
 __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, const float2* s_ray,
                                           unsigned long long* s_key, uint32_t* s_tri, int n, int lane,
                                           uint32_t& iters, uint32_t& popped, uint32_t& n_int, uint32_t& n_leaf,
@@ -1411,6 +1685,9 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
             popped += (uint32_t)n;
             if (kFast && !kAny)
                 n = two_level_fast<kStride, kCount, kOct>(P, items, s_ray, s_key, s_tri, n, lane, n_int, n_leaf, n_acc, n_desc);
+            else if (kX && !kAny && RT_XTWO_LEVEL)
+                n = two_level_fast<kStride, kCount, kOct, true>(P, items, s_ray, s_key, s_tri, n, lane, n_int, n_leaf,
+                                                               n_acc, n_desc);
             else
                 n = two_level_iter<kStride, kTranslated, kCount, kAny, kOrder, kFast>(P, items, s_ray, s_key, s_tri, n,
                                                                               lane, n_int, n_leaf, n_acc, n_desc);
@@ -1444,10 +1721,19 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
             if (act1 && s_key[it1.w >> 26] == 0ull) act1 = false;
         }
         // both records in flight before either is consumed
-        const float4* p0 = kFast && !kAny ? record_fast(P, it0.x) : record_of(P, it0.x);
-        const float4* p1 = kFast && !kAny ? record_fast(P, it1.x) : record_of(P, it1.x);
+        constexpr bool kFastRec = (kFast && !kAny) || kX;
+        constexpr bool kMasked = (kFast && !kAny && masked_loads<kStride>()) ||
+                                 (kX && (kAny ? RT_SHMASKED_LOADS != 0 : (RT_XMASKED_LOADS != 0 && masked_loads<kStride>())));
+        const float4* p0 = kFastRec ? record_fast(P, it0.x) : record_of(P, it0.x);
+        const float4* p1 = kFastRec ? record_fast(P, it1.x) : record_of(P, it1.x);
         float4 a0, a1, a2, a3, b0, b1, b2, b3;
-        if (kFast && !kAny && masked_loads<kStride>()) {
+        if (take > 64) {
+            vmem_stat(P, 1, p0, true, act0);
+            vmem_stat(P, 2, p1, true, act1);
+        } else {
+            vmem_stat(P, 0, p0, kMasked ? act0 : true, act0);
+        }
+        if (kMasked) {
             // a pop of more than 64 items fills slot 0: both slots load on
             // every lane, issued together; a smaller pop loads slot 0's live
             // lanes only (an exec-masked second group waits for the first
@@ -1472,6 +1758,13 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
             if (take > 64)
                 total += fast_slot<kStride, kCount, kOct>(P, items, base + total, s_ray, s_key, s_tri, it1, act1, b0, b1, b2,
                                                     b3, n_int, n_leaf, n_acc, n_desc);
+        } else if (kX) {
+            total = xfast_slot<kStride, kCount, kAny, (kOrder & 3), kOct>(P, items, base, s_ray, s_key, s_tri, it0, act0, a0,
+                                                                       a1, a2, a3, n_int, n_leaf, n_acc, n_desc);
+            if (take > 64)
+                total += xfast_slot<kStride, kCount, kAny, (kOrder & 3), kOct>(P, items, base + total, s_ray, s_key, s_tri,
+                                                                            it1, act1, b0, b1, b2, b3, n_int, n_leaf,
+                                                                            n_acc, n_desc);
         } else {
         {
             Visit v0;
@@ -1572,10 +1865,11 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
         camera_ray<false, !kTranslated>(P, px, live, cam0, R0, rn0);
         // every live ray's components normal and nonzero (1/r finite), under
         // the frame proof P.fast (rt_api.cpp)
-        fast = !kTranslated && P.fast &&
-               __ballot(live && !(fabsf(R0.rx) >= 0x1p-126f && fabsf(R0.ry) >= 0x1p-126f &&
-                                  fabsf(R0.rz) >= 0x1p-126f)) == 0ull;
-        if (RT_OCT_WALKS && fast) {
+        // (translated walks: the xfast_slot forms under the same proof,
+        // whose margins cover the offsets, rt_api.cpp fast_proof)
+        fast = P.fast && __ballot(live && !(fabsf(R0.rx) >= 0x1p-126f && fabsf(R0.ry) >= 0x1p-126f &&
+                                            fabsf(R0.rz) >= 0x1p-126f)) == 0ull;
+        if (RT_OCT_WALKS && fast) {  // (the octant of the object-space rays)
             const unsigned long long LV = __ballot(live), PX = __ballot(live && R0.rx > 0.0f),
                                      PY = __ballot(live && R0.ry > 0.0f), PZ = __ballot(live && R0.rz > 0.0f);
             if ((PX == 0ull || PX == LV) && (PY == 0ull || PY == LV) && (PZ == 0ull || PZ == LV))
@@ -1593,13 +1887,13 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
         // (bench.py's roofline without the root-miss visits)
         if (kCount && (P.debug & 32)) n = 0;
     }
-    if (!kTranslated && fast) {
+    if (fast) {
         // one instance of the walk per octant (the views' rays look along +z
-        // or -z; x and y change sign across the frame), the mixed one else
-#define RT_OCT_WALK(o)                                                                                          \
-    pool_walk<kCap, RL::kStride, kTranslated, kCount, false, 0, true, o>(P, items, S_.ray, S_.key, S_.tri, n, lane, \
-                                                                          iters, popped, C.n_int, C.n_leaf,         \
-                                                                          C.n_acc, C.n_desc)
+        // or -z; x and y change sign across the frame), the mixed one else;
+        // untranslated walks take the kFast slots, translated ones xfast_slot
+#define RT_OCT_WALK(o)                                                                                               \
+    pool_walk<kCap, RL::kStride, kTranslated, kCount, false, 0, !kTranslated, o, kTranslated>(                         \
+        P, items, S_.ray, S_.key, S_.tri, n, lane, iters, popped, C.n_int, C.n_leaf, C.n_acc, C.n_desc)
         switch (oct) {
         case 0: RT_OCT_WALK(0); break;
         case 1: RT_OCT_WALK(1); break;
@@ -1660,8 +1954,20 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
         }
         __builtin_amdgcn_wave_barrier();
         n = seed_root<kCount>(P, items, Sh, sh_live, lane, C.n_int, C.n_desc);
-        pool_walk<kCap, RL::kStride, true, kCount, true, kShadow - 1>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters,
-                                                                     popped, C.n_int, C.n_leaf, C.n_acc, C.n_desc);
+        // the translated kFast slots when the light's proof holds
+        // (rt_api.cpp fast_proof_shadow: the root box beyond the light's
+        // plane on axis P.sh_axis) and every live shadow ray points into that
+        // side with normal, nonzero components: then every box's entry
+        // parameter is >= 2^-20 for it
+        const float sk = P.sh_axis == 0 ? Sh.rx : P.sh_axis == 1 ? Sh.ry : Sh.rz;
+        const bool sh_ok = fabsf(Sh.rx) >= 0x1p-126f && fabsf(Sh.ry) >= 0x1p-126f && fabsf(Sh.rz) >= 0x1p-126f &&
+                           (P.sh_neg ? sk < 0.0f : sk > 0.0f);
+        if (P.fast_sh && __ballot(sh_live && !sh_ok) == 0ull)
+            pool_walk<kCap, RL::kStride, true, kCount, true, kShadow - 1, false, 8, true>(
+                P, items, S_.ray, S_.key, S_.tri, n, lane, iters, popped, C.n_int, C.n_leaf, C.n_acc, C.n_desc);
+        else
+            pool_walk<kCap, RL::kStride, true, kCount, true, kShadow - 1>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters,
+                                                                         popped, C.n_int, C.n_leaf, C.n_acc, C.n_desc);
         if (lane < kRays) shadowed = S_.key[lane] == 0ull;
     }
     if (P.dbg && lane == 0 && dbg_slot != kNoDbg) {  // diagnostics: the unit's start/end clock (100 MHz) and pool iterations
@@ -1938,6 +2244,8 @@ __device__ __forceinline__ void kd3_block(const TraceParams& P, WaveLds<kRays, k
     Counts C;
     const int32_t ntiles = P.tiles_x * P.block_rows;
     const int32_t bslot = b;  // diagnostics slot of this block
+    // a multi-frame launch's padding blocks (XCD-mapped tile orders)
+    if (b >= ntiles + P.split + P.fill_blocks) return;
     // blocks: 2 per split tile, 1 per other fine tile, then the far fill
     if (b >= ntiles + P.split) {
         // fused far fill: blocks after the fine tiles write the coarse groups,

@@ -102,5 +102,18 @@ RT_HD bool lt_eps_f(float a, float s) { return a < s; }
 RT_HD bool gt_eps_f(float a, float s) { return a > s; }
 RT_HD bool enter_f(float maxt0, float mint1) { return maxt0 > -eps_f() && mint1 >= maxt0; }
 
+// Exact float forms of lt_eps_ref / gt_eps_ref with the equality case
+// decided too (round 6: the translated and shadow kFast walks, whose split
+// values s = s2 + ds are computed per visit, so no threshold can be stored in
+// the record).  For |s| >= 2^-20 no float lies strictly between s and
+// s +/- 1e-16, so for a != s the test is a < s (a > s); at a == s it is
+// whether the double sum s + 1e-16 rounds above s (s - 1e-16 below s): the
+// double spacing beyond s must be below 2e-16, which holds exactly when
+// |s| < 1, or s == -1 (s == +1) whose spacing toward zero is half the
+// spacing of its binade.  Valid for every float a and every s with
+// |s| >= 2^-20, infinities and NaN included (tests/predicates_check.cpp).
+RT_HD bool lt_eps_x(float a, float s) { return a < s || (a == s && (fabsf(s) < 1.0f || s == -1.0f)); }
+RT_HD bool gt_eps_x(float a, float s) { return a > s || (a == s && (fabsf(s) < 1.0f || s == 1.0f)); }
+
 }  // namespace pred
 }  // namespace rt

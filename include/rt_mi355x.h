@@ -390,7 +390,10 @@ int rt_camera_info(const rt_camera* c, int32_t* w, int32_t* h, int32_t* max_dept
  * contiguous, 1: natural, 2: centre-out, 3: heaviest first by the cost an
  * earlier frame measured, default; every 16th frame of kernel 3 writes
  * its units' costs into page-locked host memory, read once that frame's
- * event has completed; no samples while the stream is captured).
+ * event has completed; no samples while the stream is captured; 4: per XCD
+ * (block b on XCD b % 8) over 8 Morton runs of equal cost, heaviest first in
+ * each; 5: per XCD over 8 row bands of equal tile count, heaviest first in
+ * each -- orders 0, 4 and 5 pad multi-frame launches to 8 blocks per frame).
  * Every setting renders the identical frame. */
 #define RT_OPT_KERNEL 1
 #define RT_OPT_TILE_ORDER 2

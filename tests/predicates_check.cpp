@@ -45,6 +45,13 @@ int main(int argc, char** argv) {
             if (bad++ < 10) printf("add_eps_f %a\n", a);
         }
         if (entry_safe(a) && enter_f(a, b) != enter_ref(a, b)) { if (bad++ < 10) printf("enter_f %a %a\n", a, b); }
+        // the per-visit forms of the translated / shadow kFast walks (equal operands included)
+        if (!(fabsf(b) < kSmall)) {
+            if (lt_eps_x(a, b) != lt_eps_ref(a, b)) { if (bad++ < 10) printf("lt_eps_x %a %a\n", a, b); }
+            if (gt_eps_x(a, b) != gt_eps_ref(a, b)) { if (bad++ < 10) printf("gt_eps_x %a %a\n", a, b); }
+            if (lt_eps_x(b, b) != lt_eps_ref(b, b)) { if (bad++ < 10) printf("lt_eps_x= %a\n", b); }
+            if (gt_eps_x(b, b) != gt_eps_ref(b, b)) { if (bad++ < 10) printf("gt_eps_x= %a\n", b); }
+        }
     };
     for (float a : edge)
         for (float b : edge) check(a, b);

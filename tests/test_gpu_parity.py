@@ -46,7 +46,7 @@ def test_small_frames_vs_golden(name, w, h, mode):
 
 
 KERNELS = [(2, 0, 0), (2, 2, 0), (2, 1, 0), (3, 2, 32), (3, 1, 32), (3, 0, 32), (3, 2, 16), (3, 2, 8), (3, 3, 16),
-           (3, 3, 8), (3, 4, 16), (3, 3, 0), (3, 3, 32)]  # (KD kernel, tile order, rays/wave; 0 = automatic)
+           (3, 3, 8), (3, 4, 16), (3, 5, 16), (3, 5, 8), (3, 3, 0), (3, 3, 32)]  # (KD kernel, tile order, rays/wave; 0 = automatic)
 
 
 def _counters_match(cnt, ocnt, kernel):
@@ -1479,6 +1479,39 @@ def test_multiframe_launch_loop(key):
                     xforms=np.stack([np.eye(3, 4, dtype=np.float32).reshape(12)] * 2)).run(4)
 
 
+@pytest.mark.parametrize("order", [0, 4, 5])
+@pytest.mark.parametrize("key", ["dragon_960x540_m0", "knot_1920x1080_m0"])
+def test_multiframe_xcd_orders(key, order):
+    """Round 6 (verdict r05 item 5): the XCD-mapped tile orders pad every
+    frame of a multi-frame launch to a multiple of 8 blocks (the padding
+    blocks exit); every buffer set still holds the oracle's frame, and the
+    cost-ordered ones (4, 5) take their cost samples from single-frame
+    launches first."""
+    import hashlib
+    import torch
+    from cpp_cuda_raytracer_dev_amd import _lib
+    ent = H.frame_hashes()[key]
+    if not H.mesh_matches(ent):
+        pytest.skip("stand-in mesh bits differ on this host")
+    w, h = ent["w"], ent["h"]
+    s = H.GpuScene(ent["scene"], w, h, tile_order=order)
+    dev = torch.device("cuda:0")
+    st = torch.cuda.Stream(device=dev)
+    bufs = [torch.full((w * h,), 0x7BADBEEF, dtype=torch.int32, device=dev) for _ in range(3)]
+    loop = R.FrameLoop(s.cam, bufs, mode=0, render_stream=st.cuda_stream, event_every=1,
+                       inflight=_lib.RT_LOOP_MULTIFRAME)
+    for n in (40, 200):
+        for b in bufs:
+            b.fill_(0x7BADBEEF)
+        torch.cuda.synchronize()
+        loop.run(n)
+        torch.cuda.synchronize()
+        shas = {hashlib.sha256(b.cpu().numpy().view(np.uint32).tobytes()).hexdigest() for b in bufs}
+        assert shas == {ent["argb_sha"]}, (key, order, n)
+    assert s.cam.device_error(reset=True) == 0
+    s.close()
+
+
 def test_multiframe_alternating_loops_kept_order():
     """a small frame whose rays-per-wave rule differs between
     multi-frame launches (32) and the per-frame loop (16) switches tilings on
@@ -1535,31 +1568,81 @@ FAST_POSES = [None,  # the default view (eye at z = -1, looking +z)
               dict(pos=(0.0, 0.1, -0.25), look_at=(0.0, 0.1, 0.0))]    # close in front (large field)
 
 
-@pytest.mark.parametrize("pose", range(len(FAST_POSES)))
-@pytest.mark.parametrize("scene,w,h", [("tester", 320, 180), ("rabbit_70k", 480, 270), ("dragon", 480, 270)])
-def test_fast_walk_same_frame(scene, w, h, pose):
+def _fast_pair(scene, w, h, kw=None, xf=None, shadow=False, rays=None):
+    """Renders a frame with the proof's walks and with debug bit 2048 (the
+    double-promoted forms), counted and timed; returns both (argb, hit,
+    counters, RT_OPT_FAST_USED) after checking counted == timed."""
     from cpp_cuda_raytracer_dev_amd import _lib
-    kw = FAST_POSES[pose]
     outs = []
     for debug in (0, 2048):
-        s = H.GpuScene(scene, w, h, cam_kw=kw, kernel=3, debug=debug)
+        s = H.GpuScene(scene, w, h, cam_kw=kw, kernel=3, debug=debug, rays=rays)
         try:
-            argb, hit, cnt = s.render(0, count=True)
+            argb, hit, cnt = s.render(0, xform=xf, count=True, shadow=shadow)
             used = s.cam.get_option(_lib.RT_OPT_FAST_USED)
-            argb2, hit2, _ = s.render(0)  # the timed (uncounted) instance
+            argb2, hit2, _ = s.render(0, xform=xf, shadow=shadow)  # the timed (uncounted) instance
         finally:
             s.close()
-        _assert_same((argb2, hit2), (argb, hit), f"{scene} pose {pose} debug {debug} counted vs timed")
+        _assert_same((argb2, hit2), (argb, hit), f"{scene} debug {debug} counted vs timed")
         outs.append((argb, hit, [int(x) for x in cnt], used))
     assert outs[1][3] == 0
+    _assert_same(outs[0][:2], outs[1][:2], f"{scene} fast vs double forms")
+    assert outs[0][2] == outs[1][2], (outs[0][2], outs[1][2])
+    return outs
+
+
+@pytest.mark.parametrize("shadow", [False, True])
+@pytest.mark.parametrize("pose", range(len(FAST_POSES)))
+@pytest.mark.parametrize("scene,w,h", [("tester", 320, 180), ("rabbit_70k", 480, 270), ("dragon", 480, 270)])
+def test_fast_walk_same_frame(scene, w, h, pose, shadow):
+    """Round 6: the shadow walks too (xfast_slot under the light's proof,
+    verdict r05 item 2); tester.ply's light lies inside its root box, so its
+    shadow frames keep the double forms (and show no shadows)."""
+    kw = FAST_POSES[pose]
+    outs = _fast_pair(scene, w, h, kw=kw, shadow=shadow)
     if kw is None:
         assert outs[0][3] & 1, "the default view proves the float entry test"
-    _assert_same(outs[0][:2], outs[1][:2], f"{scene} pose {pose} fast vs double forms")
-    assert outs[0][2] == outs[1][2]
-    if kw is None:
-        oargb, ohit, ocnt = H.oracle_render(scene, w, h, 0)
+        if shadow and scene != "tester":
+            assert outs[0][3] & 2, "the light (2, 2, 2) lies beyond the root box: the shadow walks' proof"
+        oargb, ohit, ocnt = H.oracle_render(scene, w, h, 0, shadow=shadow)
         _assert_same(outs[0][:2], (oargb, ohit), f"{scene} fast vs oracle")
-        _counters_match(outs[0][2], ocnt, 3)
+        if not shadow:
+            _counters_match(outs[0][2], ocnt, 3)
+    if shadow and scene == "tester" and kw is None:
+        assert not outs[0][3] & 2  # (the light moves with the camera: other poses may prove it)
+
+
+# Object transforms (verdict r05 item 3: the reference's keyboard path,
+# TD/WinMain.cpp:186-209 -> TD/Camera.cu:254-335): a rotation keeps the
+# untranslated walk (kFast slots under the rotated proof), an offset takes
+# the translated walk's xfast_slot; both must equal the double forms.
+FAST_XFORMS = [_rot_y(17.0), _rot_y(0.0, (0.01, -0.005, 0.02)), _rot_y(-9.0, (0.0, 0.01, 0.0)),
+               _rot_y(31.0, (0.05, 0.02, 0.3)), _rot_y(-52.0, (-0.03, 0.0, -0.2))]
+
+
+@pytest.mark.parametrize("shadow", [False, True])
+@pytest.mark.parametrize("xi", range(len(FAST_XFORMS)))
+@pytest.mark.parametrize("scene", ["rabbit_70k", "dragon"])
+def test_fast_walk_transforms(scene, xi, shadow):
+    xf = FAST_XFORMS[xi]
+    outs = _fast_pair(scene, 480, 270, xf=xf, shadow=shadow)
+    assert outs[0][3] & 5 == 5, f"the transformed frame proves the float entry test ({outs[0][3]})"
+    if shadow:
+        assert outs[0][3] & 2
+    if xi < 2:
+        oargb, ohit, _ = H.oracle_render(scene, 480, 270, 0, xform=xf, shadow=shadow)
+        assert (ohit >= 0).sum() > 100
+        _assert_same(outs[0][:2], (oargb, ohit), f"{scene} xform {xi} fast vs oracle")
+
+
+@pytest.mark.parametrize("rays", [8, 16, 32])
+def test_fast_walk_transform_rays(rays):
+    """Every unit width's translated and shadow fast walks (the 8-, 16- and
+    32-ray instances), against the double forms and the oracle."""
+    xf = FAST_XFORMS[2]
+    outs = _fast_pair("dragon", 480, 270, xf=xf, shadow=True, rays=rays)
+    assert outs[0][3] & 7 == 7
+    oargb, ohit, _ = H.oracle_render("dragon", 480, 270, 0, xform=xf, shadow=True)
+    _assert_same(outs[0][:2], (oargb, ohit), f"dragon rays {rays} fast vs oracle")
 
 
 def test_fast_walk_refused_inside_box():

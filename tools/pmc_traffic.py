@@ -71,9 +71,18 @@ def main():
     counters, n = {}, {}
     valu_util = None
     fpd = 1.0
+    per_cu = {}  # busy / access counters per CU cycle of their own pass
     for d in dirs:
         c, m, f = load(d, kernel_sub, one_frame)
         fpd = max(fpd, f)
+        if c.get("GRBM_GUI_ACTIVE"):
+            # CU cycles of the pass: GRBM_GUI_ACTIVE is summed over the 8
+            # XCDs (GRBM / 8 = the kernel's cycles), times the 256 CUs
+            cu_cycles = c["GRBM_GUI_ACTIVE"] / 8.0 * 256.0
+            for name in ("TA_TA_BUSY_sum", "TD_TD_BUSY_sum", "TD_TC_STALL_sum", "TCP_TOTAL_CACHE_ACCESSES_sum",
+                         "TA_FLAT_READ_WAVEFRONTS_sum"):
+                if name in c:
+                    per_cu[name] = c[name] / cu_cycles
         if "SQ_INSTS_VALU" in c and c.get("GRBM_GUI_ACTIVE"):
             # VALU issue share of the chip's SIMD cycles in this pass: a wave64
             # VALU instruction issues over 2 cycles of a SIMD-32
@@ -92,6 +101,14 @@ def main():
              "frames_per_dispatch": round(fpd, 2), "build_id": build.source_id()}
     if valu_util is not None:
         entry["valu_issue_util"] = round(valu_util, 4)
+    if "TD_TD_BUSY_sum" in per_cu or "TA_TA_BUSY_sum" in per_cu:
+        # the vector memory path per CU cycle (tools/ubench_l1.hip: a wave
+        # load costs sum over its 16 lane quads of max(1, distinct 128-B
+        # lines) TA / TD cycles, 16 at least for 64 lanes x 16 B; the data
+        # unit also stalls on L1 misses): vmem_util is the data unit's busy
+        # share, the busier of the two at every configuration measured
+        entry["vmem"] = {k: round(v, 4) for k, v in per_cu.items()}
+        entry["vmem_util"] = round(max(per_cu.get("TD_TD_BUSY_sum", 0.0), per_cu.get("TA_TA_BUSY_sum", 0.0)), 4)
     if "FETCH_SIZE" in counters and "WRITE_SIZE" in counters:
         fetch, write = counters["FETCH_SIZE"] * 1024.0, counters["WRITE_SIZE"] * 1024.0
         # per frame (one frame per launch unless multi-frame launches)

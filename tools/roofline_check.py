@@ -9,9 +9,11 @@ frac (profiles/<round>/bench/<tag>.json).
 
     python tools/roofline_check.py profiles/r04 [--out profiles/r04/roofline_check.md]
 
-frac = max(HBM bytes / rocprof average / 8 TB/s, VALU issue share): the
-utilisation of the binding resource, as bench.py computes it with its own
-kernel time.  A row agrees when the two are within 5 %.
+frac = max(L2-miss bytes / rocprof average / 8 TB/s, VALU issue share,
+vector-memory (TD busy) share): the utilisation of the binding resource, as
+bench.py computes it with its own kernel time (round 6 adds vmem_util, the
+busy share of the texture data unit, and the traffic over the compulsory
+scene + frame bytes).  A row agrees when the two are within 5 %.
 """
 import argparse
 import csv
@@ -114,19 +116,23 @@ def main():
             rec = rf["flops_per_launch"] / (avg[0] * 1e-6) / 1e12 / rf["peak"]
         elif avg and ent.get("hbm_bytes_per_launch"):
             hbm = ent["hbm_bytes_per_launch"] / (avg[0] * 1e-6) / 1e9 / HBM
-            rec = max(hbm, ent.get("valu_issue_util") or 0.0)
+            rec = max(hbm, ent.get("valu_issue_util") or 0.0, ent.get("vmem_util") or 0.0)
         rows.append({"tag": tag, "workload": b.get("metric_workload") or b["config"].get("workload"),
                      "bench_frac": rf.get("frac"), "bound": rf.get("bound"), "bench_kernel_us": 1e3 * rf["kernel_ms_avg"],
                      "rocprof_avg_us": avg[0] if avg else None, "rocprof_calls": avg[2] if avg else None,
                      "rocprof_source": "per frame of multi-frame launches (kernel trace)" if key and key.endswith("_mf")
                      else "solo frames (--stats average)",
                      "pmc_key": key, "pmc_build": (ent.get("build_id") or "")[:16],
+                     "vmem_util": ent.get("vmem_util"),
+                     "traffic_over_compulsory": (round(ent["hbm_bytes_per_launch"] / rf["compulsory_bytes"], 3)
+                                                 if ent.get("hbm_bytes_per_launch") and rf.get("compulsory_bytes") else None),
                      "bench_build": (b.get("build_id") or "")[:16], "recomputed_frac": rec,
                      "agree_5pct": (abs(rec - rf["frac"]) <= 0.05 * rf["frac"]) if rec and rf.get("frac") else None})
-    out = ["| config | bound | bench frac | bench kernel us | rocprof us (calls or frames) | rocprof source | recomputed frac | within 5 % | PMC build = bench build |",
-           "|---|---|---|---|---|---|---|---|---|"]
+    out = ["| config | bound | bench frac | vmem_util | L2-miss bytes / compulsory | bench kernel us | rocprof us (calls or frames) | rocprof source | recomputed frac | within 5 % | PMC build = bench build |",
+           "|---|---|---|---|---|---|---|---|---|---|---|"]
     for r in rows:
-        out.append(f"| {r['tag']} ({r['workload']}) | {r['bound']} | {r['bench_frac']} | {r['bench_kernel_us']:.2f} | "
+        out.append(f"| {r['tag']} ({r['workload']}) | {r['bound']} | {r['bench_frac']} | {r['vmem_util']} | "
+                   f"{r['traffic_over_compulsory']} | {r['bench_kernel_us']:.2f} | "
                    f"{r['rocprof_avg_us'] and round(r['rocprof_avg_us'], 2)} ({r['rocprof_calls']}) | {r['rocprof_source']} | "
                    f"{r['recomputed_frac'] and round(r['recomputed_frac'], 4)} | {r['agree_5pct']} | "
                    f"{r['pmc_build'] == r['bench_build'] if r['pmc_build'] else 'no PMC entry'} |")
