@@ -1218,6 +1218,7 @@ int fill_params(rt_camera* c, const float* xform, const rt_tile* tile, uint32_t*
     p.inode = c->d_inode;
     p.trec = c->d_trec;
     p.leaf_off = c->leaf_off;
+    p.rec_bytes = c->leaf_off ? (uint32_t)(c->leaf_off + 64 * (uint64_t)c->obj->ntri) : 0u;
     p.tpair = c->d_tpair;
     p.flat_variant = c->flat_variant;
     p.shade = s->d_shade;

@@ -141,6 +141,7 @@ struct TraceParams {
     // normal, nonzero components (rt_api.cpp fast_proof_shadow)
     int32_t fast_sh, sh_axis, sh_neg;
     uint32_t leaf_off;             // byte offset of trec from inode (one allocation; rt_api.cpp prepare_camera_object)
+    uint32_t rec_bytes;            // bytes of that allocation's records (inode + trec; < 4 GiB when leaf_off is set)
     int32_t tiny_s1;               // some interior record of the camera has the tiny-s1 flag
     int32_t far_rect[4];           // root box's screen rectangle + 2 px (x0, x1, y0, y1; frame pixels)
     int32_t far_all;               // every group background: the box lies behind the eye (box_behind)

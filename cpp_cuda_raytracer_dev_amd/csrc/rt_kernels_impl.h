@@ -1649,6 +1649,69 @@ __device__ __forceinline__ int two_level_fast(const TraceParams& P, uint4* items
 // key[ray] = 0; without counters the items of such rays are dropped.
 // Each lane pops up to P.items (1 or 2) items per iteration and fetches their
 // records together, so a lane keeps two memory round trips in flight.
+// Shared record loads (round 6, verdict r05 item 1; RT_SHARED_LOADS).  The
+// vector memory path's cost per wave load is the sum over its 16 lane quads
+// of max(1, distinct 128-B lines its loading lanes touch) cycles
+// (tools/ubench_l1.hip), and a pop's items are runs of the same node for
+// coherent rays: at the knot 1080p a single-slot pop's 42 live lanes touch
+// 8.9 records on average (tools/vmem_stats.py, profiles/r06/vmem/), yet a run
+// that straddles a quad boundary costs that quad a line per run.  So only
+// the first lane of each run (consecutive lanes holding the same ref) loads
+// the record, and the run's other lanes take its 16 dwords from that lane by
+// ds_bpermute (the LDS crossbar, not the vector memory path).  Every lane
+// ends up with the record of its own item, as before.
+// Measured and off (r06e, one box, against RT_SHARED_LOADS 0): the address
+// unit's busy share fell (knot 1080p TA_TA_BUSY 0.77 -> 0.57 per CU cycle)
+// but the data unit stayed busy on 0.92-0.95 of the cycles, stalled on the
+// L1 more (TD_TC_STALL 0.42 -> 0.49), and the 16 ds_bpermute per slot and
+// their waits lengthened every pool iteration: the driver's command 12.44k
+// -> 9.98k FPS (exec-masked run-start loads 10.09k), C4 20.7k -> 17.5k, C3
+// 78.0k -> 66.1k, C5 2,904 -> 2,393.
+#ifndef RT_SHARED_LOADS
+#define RT_SHARED_LOADS 0
+#endif
+// Whether this lane starts a run of equal refs among the active lanes, and
+// the lane of the start of its run (byte address for ds_bpermute).
+__device__ __forceinline__ bool run_start(uint32_t ref, bool act, int lane, int& leader_addr) {
+    const uint32_t key = act ? ref : 0xFFFFFFFFu;  // (no ref is all ones: a leaf's index < 2^31 - 1)
+    // the previous lane's key (DPP wave_shr:1; lane 0 gets the all-ones key)
+    const uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)key, 0x138, 0xF, 0xF, false);
+    const bool start = act && (lane == 0 || prev != key);
+    const unsigned long long S = __ballot(start);
+    const unsigned long long m = S & (~0ull >> (63 - lane));  // starts at or below this lane
+    const int lead = m ? 63 - __builtin_clzll(m) : lane;
+    leader_addr = lead << 2;
+    return start;
+}
+// RT_SHARED_BUF: the run starts' loads as buffer loads whose other lanes
+// read beyond the records (the range check drops them) instead of
+// exec-masked global loads -- no exec-mask branch, so the compiler's wait
+// counts stay exact and slot 1's loads stay in flight while slot 0 is
+// visited (with branches it waits for both groups before slot 0's permutes)
+#ifndef RT_SHARED_BUF
+#define RT_SHARED_BUF 1
+#endif
+typedef unsigned int rt_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 as_f4(rt_u32x4 r) {
+    return make_float4(__uint_as_float(r.x), __uint_as_float(r.y), __uint_as_float(r.z), __uint_as_float(r.w));
+}
+// The record of `ref` (record_fast's offset) through the buffer resource of
+// the camera's records, or zeros without a memory access when !load.
+__device__ __forceinline__ void load_record_buf(__amdgpu_buffer_rsrc_t rsrc, const TraceParams& P, uint32_t ref,
+                                                bool load, float4& r0, float4& r1, float4& r2, float4& r3) {
+    const uint32_t off = load ? (ref << 6) + ((int32_t)ref < 0 ? P.leaf_off : 0u) : 0x80000000u;
+    r0 = as_f4(__builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)off, 0, 0));
+    r1 = as_f4(__builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(off + 16u), 0, 0));
+    r2 = as_f4(__builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(off + 32u), 0, 0));
+    r3 = as_f4(__builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(off + 48u), 0, 0));
+}
+__device__ __forceinline__ float4 share4(float4 v, int addr) {
+    return make_float4(__int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(v.x))),
+                       __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(v.y))),
+                       __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(v.z))),
+                       __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(v.w))));
+}
+
 // kX (round 6): the translated kFast slots (xfast_slot) for a translated
 // nearest-hit walk or a shadow walk whose proof holds; its two-level
 // iterations keep the double forms (two_level_iter).
@@ -1727,13 +1790,35 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
         const float4* p0 = kFastRec ? record_fast(P, it0.x) : record_of(P, it0.x);
         const float4* p1 = kFastRec ? record_fast(P, it1.x) : record_of(P, it1.x);
         float4 a0, a1, a2, a3, b0, b1, b2, b3;
-        if (take > 64) {
-            vmem_stat(P, 1, p0, true, act0);
-            vmem_stat(P, 2, p1, true, act1);
-        } else {
-            vmem_stat(P, 0, p0, kMasked ? act0 : true, act0);
+        constexpr bool kShared = RT_SHARED_LOADS != 0 && kFastRec;
+        int lead0 = 0, lead1 = 0;
+        bool st0 = false, st1 = false;
+        if (kShared) {
+            st0 = run_start(it0.x, act0, lane, lead0);
+            if (take > 64) st1 = run_start(it1.x, act1, lane, lead1);
         }
-        if (kMasked) {
+        if (take > 64) {
+            vmem_stat(P, 1, p0, kShared ? st0 : true, act0);
+            vmem_stat(P, 2, p1, kShared ? st1 : true, act1);
+        } else {
+            vmem_stat(P, 0, p0, kShared ? st0 : kMasked ? act0 : true, act0);
+        }
+        if (kShared && RT_SHARED_BUF) {
+            // the run starts load; the other lanes take their run start's
+            // record (below, by ds_bpermute).  The resource spans the
+            // camera's records (inode, then trec at leaf_off; < 4 GiB)
+            const __amdgpu_buffer_rsrc_t rsrc =
+                __builtin_amdgcn_make_buffer_rsrc((void*)P.inode, (short)0, (int)P.rec_bytes, 0x00020000);
+            load_record_buf(rsrc, P, it0.x, st0, a0, a1, a2, a3);
+            if (take > 64) load_record_buf(rsrc, P, it1.x, st1, b0, b1, b2, b3);
+        } else if (kShared) {
+            if (st0) {
+                a0 = p0[0]; a1 = p0[1]; a2 = p0[2]; a3 = p0[3];
+            }
+            if (take > 64 && st1) {
+                b0 = p1[0]; b1 = p1[1]; b2 = p1[2]; b3 = p1[3];
+            }
+        } else if (kMasked) {
             // a pop of more than 64 items fills slot 0: both slots load on
             // every lane, issued together; a smaller pop loads slot 0's live
             // lanes only (an exec-masked second group waits for the first
@@ -1749,22 +1834,33 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
             b0 = p1[0]; b1 = p1[1]; b2 = p1[2]; b3 = p1[3];
         }
         RT_RECORD_FENCE();
+        if (kShared) {
+            a0 = share4(a0, lead0); a1 = share4(a1, lead0); a2 = share4(a2, lead0); a3 = share4(a3, lead0);
+        }
         // item 0 is visited, recorded and pushed before item 1 is visited, so
         // its results die before item 1's are made (fewer live VGPRs)
         int total = 0;
         if (kFast && !kAny) {
             total = fast_slot<kStride, kCount, kOct>(P, items, base, s_ray, s_key, s_tri, it0, act0, a0, a1, a2, a3, n_int,
                                                n_leaf, n_acc, n_desc);
-            if (take > 64)
+            if (take > 64) {
+                if (kShared) {
+                    b0 = share4(b0, lead1); b1 = share4(b1, lead1); b2 = share4(b2, lead1); b3 = share4(b3, lead1);
+                }
                 total += fast_slot<kStride, kCount, kOct>(P, items, base + total, s_ray, s_key, s_tri, it1, act1, b0, b1, b2,
                                                     b3, n_int, n_leaf, n_acc, n_desc);
+            }
         } else if (kX) {
             total = xfast_slot<kStride, kCount, kAny, (kOrder & 3), kOct>(P, items, base, s_ray, s_key, s_tri, it0, act0, a0,
                                                                        a1, a2, a3, n_int, n_leaf, n_acc, n_desc);
-            if (take > 64)
+            if (take > 64) {
+                if (kShared) {
+                    b0 = share4(b0, lead1); b1 = share4(b1, lead1); b2 = share4(b2, lead1); b3 = share4(b3, lead1);
+                }
                 total += xfast_slot<kStride, kCount, kAny, (kOrder & 3), kOct>(P, items, base + total, s_ray, s_key, s_tri,
                                                                             it1, act1, b0, b1, b2, b3, n_int, n_leaf,
                                                                             n_acc, n_desc);
+            }
         } else {
         {
             Visit v0;

@@ -34,6 +34,22 @@ def code_objects(lib):
                     yield data[base + o:base + o + size]
 
 
+def occupancy(cur):
+    """Waves per SIMD of a k_trace_kd3 instance: by VGPRs (allocation granule
+    8, 512 per SIMD lane, at most 8: MI355X_MICROARCH.md register files) and
+    by LDS (160 KiB per CU, the block's waves spread over 4 SIMDs); the
+    smaller binds.  Other kernels: the VGPR bound only."""
+    alloc = -(-int(cur[".vgpr_count"]) // 8) * 8
+    by_vgpr = min(8, 512 // max(alloc, 8))
+    m = re.search(r"k_trace_kd3ILi(\d+)E", cur[".name"])
+    lds = int(cur[".group_segment_fixed_size"])
+    if not m or lds == 0:
+        return f"waves/SIMD {by_vgpr} (vgpr)"
+    waves_per_block = 4 if int(m.group(1)) <= 16 else 2
+    by_lds = (160 * 1024 // lds) * waves_per_block // 4
+    return f"waves/SIMD {min(by_vgpr, by_lds)} (vgpr {by_vgpr}, lds {by_lds})"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("lib", nargs="?", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
@@ -57,7 +73,7 @@ def main():
                     if a.match in cur[".name"]:
                         print(f"vgpr {cur['.vgpr_count']:>4} sgpr {cur['.sgpr_count']:>4} spill v{cur['.vgpr_spill_count']}"
                               f"/s{cur['.sgpr_spill_count']} lds {cur['.group_segment_fixed_size']:>6} "
-                              f"scratch {cur['.private_segment_fixed_size']:>4}  {cur['.name']}")
+                              f"scratch {cur['.private_segment_fixed_size']:>4}  {occupancy(cur)}  {cur['.name']}")
                     cur = {}
 
 

@@ -18,6 +18,12 @@
 //      (sibling records sharing a line)
 //   7  64 lines, as 0, but only lanes < 16 active (exec-masked loads)
 //   8  16 lines as 5 but the sharers spread (lane l reads line l % 16)
+//   9  buffer loads: lane 4k reads its own line, lanes 4k+1..4k+3 an offset
+//      beyond the buffer's range (the range check drops them)
+//  10  buffer loads, every lane its own line (pattern 0 through a buffer)
+//  11  global loads exec-masked to lane 4k (one lane per quad, own lines)
+//  12  16 lines, lane 4k's line shared by its quad but lanes 4k+1..4k+3 are
+//      exec-masked (the leader-only form of pattern 5)
 // Prints one JSON line per pattern: ns per wave-instruction per CU, and
 // cycles at the measured shader clock (s_memtime against s_memrealtime).
 //
@@ -48,19 +54,30 @@ __device__ __forceinline__ uint32_t offset_of(int lane, int it, int k, int wave)
     return (uint32_t)(((line + rot) & (kLines - 1)) * 128 + byte);
 }
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
 template <int kPat>
 __global__ __launch_bounds__(256) void k_l1(const uint4* __restrict__ table, uint32_t* out, unsigned long long* clk) {
     const int lane = threadIdx.x & 63, wave = (int)(blockIdx.x * 4 + (threadIdx.x >> 6));
     const char* base = (const char*)table;
     uint32_t acc = 0;
     const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)table, (short)0, kLines * 128, 0x00020000);
     for (int it = 0; it < kIters; it++) {
         uint4 v[kLoads];
-        if (kPat == 7 && lane >= 16) {
+        if ((kPat == 7 && lane >= 16) || ((kPat == 11 || kPat == 12) && (lane & 3) != 0)) {
             for (int k = 0; k < kLoads; k++) v[k] = make_uint4(0, 0, 0, 0);
+        } else if (kPat == 9 || kPat == 10) {
+#pragma unroll
+            for (int k = 0; k < kLoads; k++) {
+                const int off = (kPat == 9 && (lane & 3) != 0) ? 0x40000000 : (int)offset_of<0>(lane, it, k, wave);
+                const u32x4 r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
+                v[k] = make_uint4(r.x, r.y, r.z, r.w);
+            }
         } else {
 #pragma unroll
-            for (int k = 0; k < kLoads; k++) v[k] = *(const uint4*)(base + offset_of<kPat>(lane, it, k, wave));
+            for (int k = 0; k < kLoads; k++)
+                v[k] = *(const uint4*)(base + offset_of<kPat == 11 ? 0 : kPat == 12 ? 5 : kPat>(lane, it, k, wave));
         }
 #pragma unroll
         for (int k = 0; k < kLoads; k++) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
@@ -115,6 +132,10 @@ int main(int argc, char** argv) {
     run<6>(table, out, clk, blocks, e0, e1);
     run<7>(table, out, clk, blocks, e0, e1);
     run<8>(table, out, clk, blocks, e0, e1);
+    run<9>(table, out, clk, blocks, e0, e1);
+    run<10>(table, out, clk, blocks, e0, e1);
+    run<11>(table, out, clk, blocks, e0, e1);
+    run<12>(table, out, clk, blocks, e0, e1);
     hipError_t e = hipDeviceSynchronize();
     if (e != hipSuccess) {
         printf("error %s\n", hipGetErrorString(e));
