@@ -863,13 +863,20 @@ __device__ __forceinline__ const float4* record_fast(const TraceParams& P, uint3
 // Lmax, hit triangle)) the visits read.
 // kFast walks read the first three fields only (direction and 1/r: no
 // offsets, and the direction per cut axis is the component itself).
-template <bool kTranslated, int kStride, bool kFast = false>
-__device__ __forceinline__ void ray_of(const float2* rd, Ray& Q, float4& q2, float4& q3, float4& q4) {
+// kOdP (round 6): a translated nearest-hit walk whose LDS holds six fields
+// only -- the offset od and ds per cut axis (r_a * 1 + r_b * 0 + r_c * 0 of
+// od: od's component, up to the sign of a zero, which no compare sees) are
+// the transform's own, uniform over the wave (xf = P.xf).
+template <bool kTranslated, int kStride, bool kFast = false, bool kOdP = false>
+__device__ __forceinline__ void ray_of(const float2* rd, Ray& Q, float4& q2, float4& q3, float4& q4,
+                                       const float* xf = nullptr) {
     const float2 z = make_float2(0.0f, 0.0f);
     const float2 f0 = rd[0], f1 = rd[kStride], f2 = rd[2 * kStride];
     const float2 f3 = kFast ? z : rd[3 * kStride], f4 = kFast ? z : rd[4 * kStride], f5 = kFast ? z : rd[5 * kStride];
-    const float2 f6 = kTranslated ? rd[6 * kStride] : z, f7 = kTranslated ? rd[7 * kStride] : z,
-                 f8 = kTranslated ? rd[8 * kStride] : z, f9 = kTranslated ? rd[9 * kStride] : z;
+    const float2 f6 = kTranslated ? (kOdP ? make_float2(xf[3], xf[7]) : rd[6 * kStride]) : z;
+    const float2 f7 = kTranslated ? (kOdP ? make_float2(xf[11], xf[3]) : rd[7 * kStride]) : z;
+    const float2 f8 = kTranslated ? (kOdP ? make_float2(xf[7], xf[11]) : rd[8 * kStride]) : z;
+    const float2 f9 = kTranslated && !kOdP ? rd[9 * kStride] : z;
     q2 = make_float4(f4.x, f4.y, f5.x, f5.y);
     q3 = make_float4(f6.x, f6.y, f7.x, f7.y);
     q4 = make_float4(f8.x, f8.y, f9.x, f9.y);
@@ -1032,7 +1039,7 @@ __device__ __forceinline__ void visit_interior(const TraceParams& P, const Ray& 
 
 // Visits one item whose record has arrived: a leaf's MT test or an interior
 // node's child ordering and slab tests.
-template <int kStride, bool kTranslated, bool kCount, bool kAny, bool kFast = false>
+template <int kStride, bool kTranslated, bool kCount, bool kAny, bool kFast = false, bool kOdP = false>
 __device__ __forceinline__ void visit_item(const TraceParams& P, const float2* rd, uint4 it, float4 r0, float4 r1,
                                            float4 r2, float4 r3, Visit& o, uint32_t& n_int, uint32_t& n_leaf,
                                            uint32_t& n_acc, uint32_t& n_desc) {
@@ -1041,10 +1048,10 @@ __device__ __forceinline__ void visit_item(const TraceParams& P, const float2* r
     // each path reads its own ray fields (read once before the branch, they
     // spilled 3 VGPRs of the 16-ray instance, no faster)
     if (it.x & kLeafBit) {
-        ray_of<kTranslated, kStride, kFast>(rd, Q, q2, q3, q4);
+        ray_of<kTranslated, kStride, kFast, kOdP>(rd, Q, q2, q3, q4, P.xf);
         visit_leaf<kTranslated, kCount, kAny>(Q, q4, it, r0, r1, r2, r3, o, n_leaf, n_acc);
     } else {
-        ray_of<kTranslated, kStride, kFast>(rd, Q, q2, q3, q4);
+        ray_of<kTranslated, kStride, kFast, kOdP>(rd, Q, q2, q3, q4, P.xf);
         visit_interior<kTranslated, kCount, kFast>(P, Q, q2, q3, q4, it, r0, r1, r2, r3, o, n_int, n_desc);
     }
 }
@@ -1232,14 +1239,16 @@ __device__ __forceinline__ int fast_slot(const TraceParams& P, uint4* items, int
 // walk (Lmax and the hit triangle from field 9, no path codes; pushes in
 // the launch's any-hit order kAnyOrd, push_children).  Nearest-hit walks
 // push as fast_slot does.
-template <int kStride, bool kCount, bool kAny, int kAnyOrd, int kOct>
+template <int kStride, bool kCount, bool kAny, int kAnyOrd, int kOct, bool kOdP = false>
 __device__ __forceinline__ int xfast_slot(const TraceParams& P, uint4* items, int at, const float2* s_ray,
                                           unsigned long long* s_key, uint32_t* s_tri, uint4 it, bool act, float4 r0,
                                           float4 r1, float4 r2, float4 r3, uint32_t& n_int, uint32_t& n_leaf,
                                           uint32_t& n_acc, uint32_t& n_desc) {
     const float2* rd = s_ray + (size_t)(it.w >> 26);
     const unsigned long long A = __ballot(act), LEAF = __ballot((it.x & kLeafBit) != 0) & A, INT = A & ~LEAF;
-    const float2 f0 = rd[0], f1 = rd[kStride], f2 = rd[2 * kStride], f6 = rd[6 * kStride], f7 = rd[7 * kStride];
+    const float2 f0 = rd[0], f1 = rd[kStride], f2 = rd[2 * kStride];
+    const float2 f6 = kOdP ? make_float2(P.xf[3], P.xf[7]) : rd[6 * kStride];
+    const float2 f7 = kOdP ? make_float2(P.xf[11], 0.0f) : rd[7 * kStride];
     const float rx = f0.x, ry = f0.y, rz = f1.x, ix = f1.y, iy = f2.x, iz = f2.y;
     const float odx = f6.x, ody = f6.y, odz = f7.x;
     if (LEAF) {
@@ -1420,7 +1429,7 @@ __device__ __forceinline__ float quad_bcast0(float x) { return __uint_as_float(q
 // One two-level iteration over the whole pool (n <= 16 items); returns the
 // new pool size (<= 4n: an item pushes its two children or its four
 // grandchildren).
-template <int kStride, bool kTranslated, bool kCount, bool kAny, int kOrder, bool kFast>
+template <int kStride, bool kTranslated, bool kCount, bool kAny, int kOrder, bool kFast, bool kOdP = false>
 __device__ __forceinline__ int two_level_iter(const TraceParams& P, uint4* items, const float2* s_ray,
                                               unsigned long long* s_key, uint32_t* s_tri, int n, int lane,
                                               uint32_t& n_int, uint32_t& n_leaf, uint32_t& n_acc, uint32_t& n_desc) {
@@ -1445,7 +1454,7 @@ __device__ __forceinline__ int two_level_iter(const TraceParams& P, uint4* items
     const float4 a0 = pa[0], a1 = pa[1], a2 = pa[2], a3 = pa[3];
     Ray Q;
     float4 q2, q3, q4;
-    ray_of<kTranslated, kStride, kFast>(s_ray + (size_t)(it.w >> 26), Q, q2, q3, q4);
+    ray_of<kTranslated, kStride, kFast, kOdP>(s_ray + (size_t)(it.w >> 26), Q, q2, q3, q4, P.xf);
     // the slab values of the record's two child boxes (role 0: the node's
     // children; roles 1, 2: the child's children), then each lane's node's
     // own values: role 0 the item's, roles 1, 2 what role 0 computed for them
@@ -1497,7 +1506,7 @@ __device__ __forceinline__ int two_level_iter(const TraceParams& P, uint4* items
 // nodes are visited and pushed, and every path code, are two_level_iter's.
 // kXl (round 6): a translated walk's form (xfast_slot's slabs with the
 // offsets, its ordering against s2 + ds, the translated MT test).
-template <int kStride, bool kCount, int kOct = 8, bool kXl = false>
+template <int kStride, bool kCount, int kOct = 8, bool kXl = false, bool kOdP = false>
 __device__ __forceinline__ int two_level_fast(const TraceParams& P, uint4* items, const float2* s_ray,
                                               unsigned long long* s_key, uint32_t* s_tri, int n, int lane,
                                               uint32_t& n_int, uint32_t& n_leaf, uint32_t& n_acc, uint32_t& n_desc) {
@@ -1534,7 +1543,8 @@ __device__ __forceinline__ int two_level_fast(const TraceParams& P, uint4* items
     const float rx = f0.x, ry = f0.y, rz = f1.x, ix = f1.y, iy = f2.x, iz = f2.y;
     const float2 z2 = make_float2(0.0f, 0.0f);
     const float2 f3 = kXl ? rd[3 * kStride] : z2, f4 = kXl ? rd[4 * kStride] : z2;
-    const float2 f6 = kXl ? rd[6 * kStride] : z2, f7 = kXl ? rd[7 * kStride] : z2;
+    const float2 f6 = kXl ? (kOdP ? make_float2(P.xf[3], P.xf[7]) : rd[6 * kStride]) : z2;
+    const float2 f7 = kXl ? (kOdP ? make_float2(P.xf[11], 0.0f) : rd[7 * kStride]) : z2;
     // the record's child boxes; each lane's own node's (t0, t1)
     float lt0, lt1, rt0, rt1;
     if constexpr (kXl)
@@ -1726,7 +1736,7 @@ __device__ __forceinline__ float4 share4(float4 v, int addr) {
 #define RT_XTWO_LEVEL 1
 #endif
 template <int kCap, int kStride, bool kTranslated, bool kCount, bool kAny, int kOrder = 0, bool kFast = false,
-          int kOct = 8, bool kX = false>
+          int kOct = 8, bool kX = false, bool kOdP = false>
 __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, const float2* s_ray,
                                           unsigned long long* s_key, uint32_t* s_tri, int n, int lane,
                                           uint32_t& iters, uint32_t& popped, uint32_t& n_int, uint32_t& n_leaf,
@@ -1749,10 +1759,10 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
             if (kFast && !kAny)
                 n = two_level_fast<kStride, kCount, kOct>(P, items, s_ray, s_key, s_tri, n, lane, n_int, n_leaf, n_acc, n_desc);
             else if (kX && !kAny && RT_XTWO_LEVEL)
-                n = two_level_fast<kStride, kCount, kOct, true>(P, items, s_ray, s_key, s_tri, n, lane, n_int, n_leaf,
-                                                               n_acc, n_desc);
+                n = two_level_fast<kStride, kCount, kOct, true, kOdP>(P, items, s_ray, s_key, s_tri, n, lane, n_int,
+                                                                     n_leaf, n_acc, n_desc);
             else
-                n = two_level_iter<kStride, kTranslated, kCount, kAny, kOrder, kFast>(P, items, s_ray, s_key, s_tri, n,
+                n = two_level_iter<kStride, kTranslated, kCount, kAny, kOrder, kFast, kOdP>(P, items, s_ray, s_key, s_tri, n,
                                                                               lane, n_int, n_leaf, n_acc, n_desc);
             __builtin_amdgcn_wave_barrier();
             continue;
@@ -1851,13 +1861,13 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
                                                     b3, n_int, n_leaf, n_acc, n_desc);
             }
         } else if (kX) {
-            total = xfast_slot<kStride, kCount, kAny, (kOrder & 3), kOct>(P, items, base, s_ray, s_key, s_tri, it0, act0, a0,
+            total = xfast_slot<kStride, kCount, kAny, (kOrder & 3), kOct, kOdP>(P, items, base, s_ray, s_key, s_tri, it0, act0, a0,
                                                                        a1, a2, a3, n_int, n_leaf, n_acc, n_desc);
             if (take > 64) {
                 if (kShared) {
                     b0 = share4(b0, lead1); b1 = share4(b1, lead1); b2 = share4(b2, lead1); b3 = share4(b3, lead1);
                 }
-                total += xfast_slot<kStride, kCount, kAny, (kOrder & 3), kOct>(P, items, base + total, s_ray, s_key, s_tri,
+                total += xfast_slot<kStride, kCount, kAny, (kOrder & 3), kOct, kOdP>(P, items, base + total, s_ray, s_key, s_tri,
                                                                             it1, act1, b0, b1, b2, b3, n_int, n_leaf,
                                                                             n_acc, n_desc);
             }
@@ -1866,7 +1876,7 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
             Visit v0;
             v0.ka = v0.kb = false; v0.cand = false;
             if (act0)
-                visit_item<kStride, kTranslated, kCount, kAny, kFast>(P, s_ray + (size_t)(it0.w >> 26), it0, a0, a1, a2,
+                visit_item<kStride, kTranslated, kCount, kAny, kFast, kOdP>(P, s_ray + (size_t)(it0.w >> 26), it0, a0, a1, a2,
                                                                       a3, v0, n_int, n_leaf, n_acc, n_desc);
             record_candidate<kAny>(s_key, s_tri, it0, v0);
             total += push_children<kAny, (kOrder & 3)>(items, base + total, v0);
@@ -1878,7 +1888,7 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
             Visit v1;
             v1.ka = v1.kb = false; v1.cand = false;
             if (act1)
-                visit_item<kStride, kTranslated, kCount, kAny, kFast>(P, s_ray + (size_t)(it1.w >> 26), it1, b0, b1, b2,
+                visit_item<kStride, kTranslated, kCount, kAny, kFast, kOdP>(P, s_ray + (size_t)(it1.w >> 26), it1, b0, b1, b2,
                                                                       b3, v1, n_int, n_leaf, n_acc, n_desc);
             record_candidate<kAny>(s_key, s_tri, it1, v1);
             total += push_children<kAny, (kOrder & 3)>(items, base + total, v1);
@@ -1943,6 +1953,9 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
                                            int lane, size_t dbg_slot, uint32_t* cost, Counts& C,
                                            int32_t nrows = kRays / 8, int32_t ncols = 8) {
     using RL = RayLayout<kRays>;
+    // a translated instance without shadow rays keeps six ray fields in LDS
+    // and reads the offset from the transform (ray_of kOdP; round 6)
+    constexpr bool kOdP = kTranslated && kRayVec == 3;
     uint4* items = S_.items;
     Pixel px;
     bool live = unit_pixel(P, U, nrows, lane, px, ncols);  // every lane stays for the ballots
@@ -1972,7 +1985,7 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
                 oct = (PX == LV ? 1 : 0) | (PY == LV ? 2 : 0) | (PZ == LV ? 4 : 0);
         }
         if (lane < kRays) {
-            store_ray(&S_.ray[lane], RL::kStride, R0, kTranslated, 0.0f, 0u);
+            store_ray(&S_.ray[lane], RL::kStride, R0, kTranslated && !kOdP, 0.0f, 0u);
             S_.key[lane] = ~0ull;
             S_.tri[lane] = kMiss;
             S_.rn[lane] = rn0;
@@ -1988,7 +2001,7 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
         // or -z; x and y change sign across the frame), the mixed one else;
         // untranslated walks take the kFast slots, translated ones xfast_slot
 #define RT_OCT_WALK(o)                                                                                               \
-    pool_walk<kCap, RL::kStride, kTranslated, kCount, false, 0, !kTranslated, o, kTranslated>(                         \
+    pool_walk<kCap, RL::kStride, kTranslated, kCount, false, 0, !kTranslated, o, kTranslated, kOdP>(                   \
         P, items, S_.ray, S_.key, S_.tri, n, lane, iters, popped, C.n_int, C.n_leaf, C.n_acc, C.n_desc)
         switch (oct) {
         case 0: RT_OCT_WALK(0); break;
@@ -2004,7 +2017,8 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
 #undef RT_OCT_WALK
     }
     else
-        pool_walk<kCap, RL::kStride, kTranslated, kCount, false>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters, popped,
+        pool_walk<kCap, RL::kStride, kTranslated, kCount, false, 0, false, 8, false, kOdP>(P, items, S_.ray, S_.key, S_.tri,
+                                                                                       n, lane, iters, popped,
                                                             C.n_int, C.n_leaf, C.n_acc, C.n_desc);
     float cam[3];
     Ray R;
@@ -2394,7 +2408,9 @@ __device__ __forceinline__ void kd3_block(const TraceParams& P, WaveLds<kRays, k
 template <int kRays, bool kTranslated, bool kWriteHit, bool kCount, int kShadow>
 __global__ RT_KD3_BOUNDS(64 * kd3_waves(kRays)) void k_trace_kd3(TraceParams P) {
     constexpr int kCap = pool_cap_for<kRays>();
-    constexpr int kRayVec = (kTranslated || kShadow) ? 5 : 3;  // float4s of per-ray data in LDS
+    // float4s of per-ray data in LDS: translated primary walks read the
+    // offset from the transform (kOdP), shadow walks keep Lmax and the hit
+    constexpr int kRayVec = kShadow ? 5 : 3;
     __shared__ WaveLds<kRays, kCap, kRayVec> s_lds[kd3_waves(kRays)];
     const int wv = wave_id(), lane = (int)threadIdx.x & 63;
     int32_t b = (int32_t)blockIdx.x;
@@ -2415,7 +2431,7 @@ template <int kRays, bool kTranslated, bool kWriteHit, bool kCount, int kShadow>
 __global__ __launch_bounds__(128) void k_coarse_kd3(TraceParams P) {
     constexpr int kWaves = 2;
     constexpr int kCap = pool_cap_for<kRays>();
-    constexpr int kRayVec = (kTranslated || kShadow) ? 5 : 3;
+    constexpr int kRayVec = kShadow ? 5 : 3;
     constexpr unsigned long long kSub = (1ull << kRays) - 1;
     __shared__ WaveLds<kRays, kCap, kRayVec> s_lds[kWaves];
     const int wv = wave_id(), lane = (int)threadIdx.x & 63;
