@@ -1903,6 +1903,27 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
     }
 }
 
+// The root's visit folded into the seeding of kFast walks (trace_unit).
+#ifndef RT_ROOT_VISIT
+#define RT_ROOT_VISIT 1
+#endif
+// ... and of translated primary walks: off, measured 1.4-1.7 % slower on the
+// moving scenes (r06h; primary +1.5-1.9 %, shadow +0.8-1.0 %), cause not
+// isolated
+#ifndef RT_XROOT_VISIT
+#define RT_XROOT_VISIT 0
+#endif
+// The root record, the same for every lane, through the constant address
+// space (a uniform address there compiles to scalar loads).
+__device__ __forceinline__ void root_record(const TraceParams& P, float4& q0, float4& q1, float4& q2, float4& q3) {
+    typedef const __attribute__((address_space(4))) float cfloat;
+    cfloat* rr = (cfloat*)(P.inode + 4 * (size_t)P.root_ref);
+    q0 = make_float4(rr[0], rr[1], rr[2], rr[3]);
+    q1 = make_float4(rr[4], rr[5], rr[6], rr[7]);
+    q2 = make_float4(rr[8], rr[9], rr[10], rr[11]);
+    q3 = make_float4(rr[12], rr[13], rr[14], rr[15]);
+}
+
 // Per-wave LDS of the wave-cooperative kernel.
 template <int kRays, int kCap, int kRayVec>
 struct WaveLds {
@@ -1990,11 +2011,38 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
             S_.tri[lane] = kMiss;
             S_.rn[lane] = rn0;
         }
-        n = seed_root<kCount>(P, items, R0, live, lane, C.n_int, C.n_desc);
-        // diagnostics (debug bit 32, counting renders): stop after the root
-        // test, so counter [4] is the number of pixels whose root test passes
-        // (bench.py's roofline without the root-miss visits)
-        if (kCount && (P.debug & 32)) n = 0;
+        if (RT_ROOT_VISIT && (!kTranslated || RT_XROOT_VISIT) && fast && !(P.root_ref & kLeafBit) && !(kCount && (P.debug & 32))) {
+            // The root visit in the seed (round 6): every ray that enters the
+            // root box visits the root's record, the same for every lane, so
+            // its 64 B arrive through the scalar cache, and the pool starts
+            // one level down (each ray's kept children, pushed with their
+            // path codes by fast_slot as a popped root item would push them).
+            // A chain-bound unit's pool chain shortens by a level; the visit
+            // set and the counters are the reference's.
+            float t0, t1;
+            const bool has = root_pass<kCount>(P, R0, live, t0, t1, C.n_int, C.n_desc);
+            __builtin_amdgcn_wave_barrier();  // (the rays' LDS fields are written)
+            float4 q0, q1, q2, q3;
+            root_record(P, q0, q1, q2, q3);
+            const uint4 it = make_uint4(P.root_ref, __float_as_uint(t0), __float_as_uint(t1), ((uint32_t)lane << 26) | 1u);
+            if constexpr (kTranslated)
+                n = xfast_slot<RL::kStride, kCount, false, 0, 8, kOdP>(P, items, 0, S_.ray, S_.key, S_.tri, it, has, q0, q1,
+                                                                     q2, q3, C.n_int, C.n_leaf, C.n_acc, C.n_desc);
+            else
+                n = fast_slot<RL::kStride, kCount, 8>(P, items, 0, S_.ray, S_.key, S_.tri, it, has, q0, q1, q2, q3,
+                                                      C.n_int, C.n_leaf, C.n_acc, C.n_desc);
+            __builtin_amdgcn_wave_barrier();
+            // (counted as the pool iteration it replaces: the units' costs,
+            // and so the cost order and its split thresholds, stay as before)
+            iters = 1;
+            popped = (uint32_t)__builtin_popcountll(__ballot(has));
+        } else {
+            n = seed_root<kCount>(P, items, R0, live, lane, C.n_int, C.n_desc);
+            // diagnostics (debug bit 32, counting renders): stop after the root
+            // test, so counter [4] is the number of pixels whose root test passes
+            // (bench.py's roofline without the root-miss visits)
+            if (kCount && (P.debug & 32)) n = 0;
+        }
     }
     if (fast) {
         // one instance of the walk per octant (the views' rays look along +z
@@ -2063,7 +2111,6 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
             S_.key[lane] = ~0ull;
         }
         __builtin_amdgcn_wave_barrier();
-        n = seed_root<kCount>(P, items, Sh, sh_live, lane, C.n_int, C.n_desc);
         // the translated kFast slots when the light's proof holds
         // (rt_api.cpp fast_proof_shadow: the root box beyond the light's
         // plane on axis P.sh_axis) and every live shadow ray points into that
@@ -2072,7 +2119,25 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
         const float sk = P.sh_axis == 0 ? Sh.rx : P.sh_axis == 1 ? Sh.ry : Sh.rz;
         const bool sh_ok = fabsf(Sh.rx) >= 0x1p-126f && fabsf(Sh.ry) >= 0x1p-126f && fabsf(Sh.rz) >= 0x1p-126f &&
                            (P.sh_neg ? sk < 0.0f : sk > 0.0f);
-        if (P.fast_sh && __ballot(sh_live && !sh_ok) == 0ull)
+        const bool sh_fast = P.fast_sh && __ballot(sh_live && !sh_ok) == 0ull;
+        if (RT_ROOT_VISIT && sh_fast && !(P.root_ref & kLeafBit)) {
+            // the root visit in the seed, as for the primary walk (every
+            // shadow ray starts at the light)
+            float t0, t1;
+            const bool has = root_pass<kCount>(P, Sh, sh_live, t0, t1, C.n_int, C.n_desc);
+            float4 q0, q1, q2, q3;
+            root_record(P, q0, q1, q2, q3);
+            const uint4 it = make_uint4(P.root_ref, __float_as_uint(t0), __float_as_uint(t1), ((uint32_t)lane << 26) | 1u);
+            n = xfast_slot<RL::kStride, kCount, true, ((kShadow - 1) & 3), 8>(P, items, 0, S_.ray, S_.key, S_.tri, it, has,
+                                                                             q0, q1, q2, q3, C.n_int, C.n_leaf, C.n_acc,
+                                                                             C.n_desc);
+            __builtin_amdgcn_wave_barrier();
+            iters += 1;
+            popped += (uint32_t)__builtin_popcountll(__ballot(has));
+        } else {
+            n = seed_root<kCount>(P, items, Sh, sh_live, lane, C.n_int, C.n_desc);
+        }
+        if (sh_fast)
             pool_walk<kCap, RL::kStride, true, kCount, true, kShadow - 1, false, 8, true>(
                 P, items, S_.ray, S_.key, S_.tri, n, lane, iters, popped, C.n_int, C.n_leaf, C.n_acc, C.n_desc);
         else
