@@ -800,11 +800,19 @@ __device__ __forceinline__ void camera_ray(const TraceParams& P, const Pixel& px
     camera_ray<false>(P, px, live, cam, R, rn);
 }
 
+// Shadow walks on the segment (round 6): 0 follows the whole ray beyond the
+// hit, as rounds 1-5 did (the same images; A/B builds only -- the oracle's
+// counters are the segment walk's).
+#ifndef RT_SHADOW_SEGMENT
+#define RT_SHADOW_SEGMENT 1
+#endif
 // The reference's root visit (TD/Trixel.cu:53,71-95): a leaf root is always
-// visited, an interior root when its slab test passes.
-template <bool kCount>
+// visited, an interior root when its slab test passes.  kSeg: a shadow
+// segment's walk, which enters a box only where the segment does (its entry
+// parameter below Lmax = lim, round 6; oracle.c trace_shadow).
+template <bool kCount, bool kSeg = false>
 __device__ __forceinline__ bool root_pass(const TraceParams& P, const Ray& R, bool live, float& t0, float& t1,
-                                          uint32_t& n_int, uint32_t& n_desc) {
+                                          uint32_t& n_int, uint32_t& n_desc, float lim = 0.0f) {
     bool has = false;
     t0 = 0.0f; t1 = 0.0f;
     if (live) {
@@ -814,6 +822,7 @@ __device__ __forceinline__ bool root_pass(const TraceParams& P, const Ray& R, bo
             if (kCount) n_int++;
             has = slab(R, P.root_box[0], P.root_box[1], P.root_box[2], P.root_box[3], P.root_box[4],
                        P.root_box[5], t0, t1);
+            if (kSeg && RT_SHADOW_SEGMENT) has = has && t0 < lim;
             if (kCount && has) n_desc++;
         }
     }
@@ -823,11 +832,11 @@ __device__ __forceinline__ bool root_pass(const TraceParams& P, const Ray& R, bo
 
 // Seeds the pool with the root item of every lane whose root test passes (or
 // a leaf root); returns the item count.
-template <bool kCount>
+template <bool kCount, bool kSeg = false>
 __device__ __forceinline__ int seed_root(const TraceParams& P, uint4* items, const Ray& R, bool live, int lane,
-                                         uint32_t& n_int, uint32_t& n_desc) {
+                                         uint32_t& n_int, uint32_t& n_desc, float lim = 0.0f) {
     float r0t0, r0t1;
-    const bool has = root_pass<kCount>(P, R, live, r0t0, r0t1, n_int, n_desc);
+    const bool has = root_pass<kCount, kSeg>(P, R, live, r0t0, r0t1, n_int, n_desc, lim);
     const unsigned long long b = __ballot(has);
     const uint32_t off = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
     if (has) items[off] = make_uint4(P.root_ref, __float_as_uint(r0t0), __float_as_uint(r0t1), ((uint32_t)lane << 26) | 1u);
@@ -943,7 +952,9 @@ __device__ __forceinline__ float opaque(float x) {
 // mint1 >= maxt0: P.fast holds only when every box's maxt0 is >= 2^-20 for
 // every ray of the frame (rt_api.cpp fast_proof), where maxt0 - 1e-16 rounds
 // to a double above the float below maxt0.
-template <bool kTranslated, bool kCount, bool kFast = false>
+// kAny: a shadow segment's walk, which enters a child box only where the
+// segment does: its entry parameter below Lmax (q4.z; root_pass).
+template <bool kTranslated, bool kCount, bool kFast = false, bool kAny = false>
 __device__ __forceinline__ void order_node(const TraceParams& P, const Ray& Q, float4 q2, float4 q3, float4 q4,
                                            float t0, float t1, float4 r0, float4 r1, float4 r2, float4 r3, float lt0,
                                            float lt1, float rt0, float rt1, bool real, Order& o, uint32_t& n_int,
@@ -984,8 +995,8 @@ __device__ __forceinline__ void order_node(const TraceParams& P, const Ray& Q, f
     // every term computed, then selected (no exec-mask branches)
     const bool pb = (mn < s1) | (mx < s1);
     const bool push_second = (left_first & pa) | (!left_first & pb);
-    const bool lpass = kFast ? lt1 >= lt0 : pred::enter_ref(lt0, lt1);
-    const bool rpass = kFast ? rt1 >= rt0 : pred::enter_ref(rt0, rt1);
+    const bool lpass = (kFast ? lt1 >= lt0 : pred::enter_ref(lt0, lt1)) && (!kAny || !RT_SHADOW_SEGMENT || lt0 < q4.z);
+    const bool rpass = (kFast ? rt1 >= rt0 : pred::enter_ref(rt0, rt1)) && (!kAny || !RT_SHADOW_SEGMENT || rt0 < q4.z);
     const uint32_t first = left_first ? L : Rr;
     const uint32_t second = left_first ? Rr : L;
     const bool first_leaf = (first & kLeafBit) != 0, second_leaf = (second & kLeafBit) != 0;
@@ -1017,7 +1028,7 @@ __device__ __forceinline__ void child_slabs(const Ray& Q, float4 r0, float4 r1, 
 
 // An interior item whose child-box record (r0..r3) has arrived: the node's
 // child ordering (TD/Trixel.cu:146-170) and the children's slab tests.
-template <bool kTranslated, bool kCount, bool kFast = false>
+template <bool kTranslated, bool kCount, bool kFast = false, bool kAny = false>
 __device__ __forceinline__ void visit_interior(const TraceParams& P, const Ray& Q, float4 q2, float4 q3, float4 q4,
                                                uint4 it, float4 r0, float4 r1, float4 r2, float4 r3, Visit& o,
                                                uint32_t& n_int, uint32_t& n_desc) {
@@ -1027,7 +1038,7 @@ __device__ __forceinline__ void visit_interior(const TraceParams& P, const Ray& 
     float lt0, lt1, rt0, rt1;
     child_slabs<kFast>(Q, r0, r1, r2, lt0, lt1, rt0, rt1);
     Order od;
-    order_node<kTranslated, kCount, kFast>(P, Q, q2, q3, q4, __uint_as_float(it.y), __uint_as_float(it.z), r0, r1, r2,
+    order_node<kTranslated, kCount, kFast, kAny>(P, Q, q2, q3, q4, __uint_as_float(it.y), __uint_as_float(it.z), r0, r1, r2,
                                            r3, lt0, lt1, rt0, rt1, true, od, n_int, n_desc);
     const uint32_t meta_first = (ray << 26) | (marked << 1);
     const uint32_t meta_second = meta_first | 1u;
@@ -1052,7 +1063,7 @@ __device__ __forceinline__ void visit_item(const TraceParams& P, const float2* r
         visit_leaf<kTranslated, kCount, kAny>(Q, q4, it, r0, r1, r2, r3, o, n_leaf, n_acc);
     } else {
         ray_of<kTranslated, kStride, kFast, kOdP>(rd, Q, q2, q3, q4, P.xf);
-        visit_interior<kTranslated, kCount, kFast>(P, Q, q2, q3, q4, it, r0, r1, r2, r3, o, n_int, n_desc);
+        visit_interior<kTranslated, kCount, kFast, kAny>(P, Q, q2, q3, q4, it, r0, r1, r2, r3, o, n_int, n_desc);
     }
 }
 
@@ -1274,6 +1285,13 @@ __device__ __forceinline__ int xfast_slot(const TraceParams& P, uint4* items, in
     const float2 f3 = rd[3 * kStride], f4 = rd[4 * kStride];
     float lt0, lt1, rt0, rt1;
     slab_pair_xoct<kOct>(r0, r1, r2, ix, iy, iz, f3.x, f3.y, f4.x, lt0, lt1, rt0, rt1);
+    // a shadow segment enters a box only below Lmax (root_pass): the exit
+    // parameter of a box it does not enter is set below its entry
+    if constexpr (kAny && RT_SHADOW_SEGMENT) {
+        const float lim = rd[9 * kStride].x;
+        lt1 = lt0 < lim ? lt1 : -INFINITY;
+        rt1 = rt0 < lim ? rt1 : -INFINITY;
+    }
     const uint32_t lw = __float_as_uint(r3.z), rw = __float_as_uint(r3.w);
     const uint32_t axis = (lw >> kAxisShift) & 3u;
     const uint32_t L = lw & ~(3u << kAxisShift), R = rw & ~kTinyS1Bit;
@@ -1464,7 +1482,7 @@ __device__ __forceinline__ int two_level_iter(const TraceParams& P, uint4* items
     const float t0 = role == 0 ? __uint_as_float(it.y) : role == 1 ? xl0 : xr0;
     const float t1 = role == 0 ? __uint_as_float(it.z) : role == 1 ? xl1 : xr1;
     Order o;
-    order_node<kTranslated, kCount, kFast>(P, Q, q2, q3, q4, t0, t1, a0, a1, a2, a3, at0, at1, bt0, bt1, false, o, n_int,
+    order_node<kTranslated, kCount, kFast, kAny>(P, Q, q2, q3, q4, t0, t1, a0, a1, a2, a3, at0, at1, bt0, bt1, false, o, n_int,
                                            n_desc);
     // role 0's verdict on its node's children, to roles 1 and 2
     const uint32_t fl = quad_bcast0((o.left_first ? 1u : 0u) | (o.ka ? 2u : 0u) | (o.kb ? 4u : 0u));
@@ -2124,7 +2142,7 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
             // the root visit in the seed, as for the primary walk (every
             // shadow ray starts at the light)
             float t0, t1;
-            const bool has = root_pass<kCount>(P, Sh, sh_live, t0, t1, C.n_int, C.n_desc);
+            const bool has = root_pass<kCount, true>(P, Sh, sh_live, t0, t1, C.n_int, C.n_desc, lmax);
             float4 q0, q1, q2, q3;
             root_record(P, q0, q1, q2, q3);
             const uint4 it = make_uint4(P.root_ref, __float_as_uint(t0), __float_as_uint(t1), ((uint32_t)lane << 26) | 1u);
@@ -2135,7 +2153,7 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
             iters += 1;
             popped += (uint32_t)__builtin_popcountll(__ballot(has));
         } else {
-            n = seed_root<kCount>(P, items, Sh, sh_live, lane, C.n_int, C.n_desc);
+            n = seed_root<kCount, true>(P, items, Sh, sh_live, lane, C.n_int, C.n_desc, lmax);
         }
         if (sh_fast)
             pool_walk<kCap, RL::kStride, true, kCount, true, kShadow - 1, false, 8, true>(
@@ -2266,14 +2284,16 @@ __device__ __forceinline__ bool root_certain_miss_xf(const TraceParams& P, int32
 // at most a few ulps of M = (|near| + |far| + |od|) / |D|).  A margin of
 // 1e-4 M_max + 1e-3 (|L0| + |U1|) + 1e-12 above that rounding makes
 // L0 > U1 + margin a miss of every pixel's exact test (mint1 < maxt0 -
-// 1e-16), and U1 < -margin one too (maxt0 <= mint1 + 1e-16 < 0).
+// 1e-16), and U1 < -margin one too (maxt0 <= mint1 + 1e-16 < 0); so is
+// U0 < -margin with U0 = max_i max t0_i >= every pixel's maxt0 (an eye
+// inside the root box, round 6: every entry lies behind it).
 __device__ __forceinline__ bool group_certain_miss(const TraceParams& P, const Unit& G) {
     const int32_t y0 = (P.rank + G.slot * P.nranks) * kTileH + G.yin;
     const float fx0 = (float)(uint32_t)G.x0, fx1 = (float)(uint32_t)(G.x0 + 7);
     const float fy0 = (float)(uint32_t)y0, fy1 = (float)(uint32_t)(y0 + 7);
     const float* X = P.xf;
     const float* b = P.root_box;
-    float L0 = -INFINITY, U1 = INFINITY, mmax = 0.0f;
+    float L0 = -INFINITY, U1 = INFINITY, U0 = -INFINITY, mmax = 0.0f;
 #pragma unroll
     for (int i = 0; i < 3; i++) {
         const float x0 = X[4 * i], x1 = X[4 * i + 1], x2 = X[4 * i + 2], od = X[4 * i + 3];
@@ -2294,12 +2314,13 @@ __device__ __forceinline__ bool group_certain_miss(const TraceParams& P, const U
         // t = n / D over D in [dlo, dhi] (one sign): extremes at the ends
         const float a0 = n0 / dlo, a1 = n0 / dhi, c0 = n1 / dlo, c1 = n1 / dhi;
         L0 = fmaxf(L0, fminf(a0, a1));
+        U0 = fmaxf(U0, fmaxf(a0, a1));
         U1 = fminf(U1, fmaxf(c0, c1));
         mmax = fmaxf(mmax, (fabsf(lo) + fabsf(hi) + fabsf(od)) / fminf(fabsf(dlo), fabsf(dhi)));
     }
-    if (!(fabsf(L0) < 1e30f && fabsf(U1) < 1e30f && mmax < 1e30f)) return false;
-    const float margin = 1e-4f * mmax + 1e-3f * (fabsf(L0) + fabsf(U1)) + 1e-12f;
-    return L0 > U1 + margin || U1 < -margin;
+    if (!(fabsf(L0) < 1e30f && fabsf(U1) < 1e30f && fabsf(U0) < 1e30f && mmax < 1e30f)) return false;
+    const float margin = 1e-4f * mmax + 1e-3f * (fabsf(L0) + fabsf(U1) + fabsf(U0)) + 1e-12f;
+    return L0 > U1 + margin || U1 < -margin || U0 < -margin;
 }
 
 //

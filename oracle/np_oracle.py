@@ -193,9 +193,11 @@ def _mt_accept(u, v, w, d):
     return (w < d) and not ((D(u) < EPS) or (D(v) < EPS) or (D(F(u + v)) > D(1) + EPS) or (D(w) < EPS))
 
 
-def _walk(S, r, od, on_leaf):
+def _walk(S, r, od, on_leaf, lim=None):
     """The DFS of intersect_voxel_cuda (TD/Trixel.cu:70-170) for direction r and
-    translation od; on_leaf(t, u, v, w) sees every non-degenerate MT test."""
+    translation od; on_leaf(t, u, v, w) sees every non-degenerate MT test.
+    lim: a shadow segment's walk enters a box only below lim (oracle.c
+    trace_shadow)."""
     inv = [F(F(1) / r[k]) for k in range(3)]
     o = [F(od[k] / r[k]) for k in range(3)]
     stack = [0]
@@ -224,7 +226,7 @@ def _walk(S, r, od, on_leaf):
         ds = F(F(F(od[0] * cf[0]) + F(od[1] * cf[1])) + F(od[2] * cf[2]))
         maxt0 = np.fmax(F(t0[2] + o[2]), np.fmax(F(t0[0] + o[0]), F(t0[1] + o[1])))
         mint1 = np.fmin(F(t1[2] + o[2]), np.fmin(F(t1[0] + o[0]), F(t1[1] + o[1])))
-        if D(mint1) >= D(maxt0) - EPS and D(maxt0) > -EPS:
+        if D(mint1) >= D(maxt0) - EPS and D(maxt0) > -EPS and (lim is None or maxt0 < lim):
             maxt0, mint1 = F(maxt0 * dr), F(mint1 * dr)
             s1 = F(D(vx["s1"]) + EPS + D(ds))
             s2 = F(vx["s2"] + ds)
@@ -278,7 +280,7 @@ def trace_shadow(S, rmi, d, ray):
         if t != rmi and _mt_accept(u, v, w, lmax):
             hit[0] = True
 
-    _walk(S, list(s), (F(-2), F(-2), F(-2)), leaf)
+    _walk(S, list(s), (F(-2), F(-2), F(-2)), leaf, lim=lmax)
     return hit[0]
 
 

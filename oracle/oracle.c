@@ -717,6 +717,13 @@ static int trace_kd(const orc_scene* s, const float* X, const float cam_rmd[3],
  *   - it is shadowed iff some visited leaf other than the hit triangle passes
  *     the MT tests (TD/Trixel.cu:104-120) with w < Lmax,
  *     Lmax = |H - (2,2,2)| * (1 - 2^-10) (a relative bias, exact in f32);
+ *   - the walk is the segment's: a box is entered only where the segment
+ *     enters it, i.e. the reference's entry test (TD/Trixel.cu:95) with its
+ *     entry parameter also below Lmax (maxt0 < Lmax, the float maxt0 of the
+ *     test).  Round 6: before it the walk followed the whole ray beyond H;
+ *     every committed shadow frame is the same image with either walk
+ *     (tests/golden/frame_hashes.json), and the segment's walk visits
+ *     24-45 % fewer nodes;
  *   - a shadowed pixel keeps point_rad = 0, so the reference's formula gives
  *     0/0 -> (u8)NaN = 0 in every channel: 0x00000000 (H14).
  * Any-hit is an OR over the visited leaves, so the result does not depend on
@@ -770,7 +777,7 @@ static int trace_shadow(const orc_scene* s, const float r[3], const float od[3],
         float ds = ((odx * cf[0]) + (ody * cf[1]) + (odz * cf[2]));
         float maxt0 = fmaxf(t0z + odz / rz, fmaxf(t0x + odx / rx, t0y + ody / ry));
         float mint1 = fminf(t1z + odz / rz, fminf(t1x + odx / rx, t1y + ody / ry));
-        if ((double)mint1 >= (double)maxt0 - ORC_EPS && (double)maxt0 > -ORC_EPS) {
+        if ((double)mint1 >= (double)maxt0 - ORC_EPS && (double)maxt0 > -ORC_EPS && maxt0 < L) {
             cnt[ORC_CNT_DESCEND]++;
             maxt0 *= dir; mint1 *= dir;
             float s1 = (float)((double)s->s1[cni] + ORC_EPS + (double)ds);
