@@ -34,6 +34,7 @@ RT_OPT_RAYS_USED = 8
 RT_OPT_SPLIT_USED = 9
 RT_OPT_FAST_USED = 12
 RT_OPT_ORDER_RESTORES = 13
+RT_OPT_FINE_TILES = 14
 RT_SCENE_ORDER = 1
 RT_SCENE_TREELET_HEIGHT = 2
 RT_SCENE_TWO_LEVEL_DEPTH = 3

@@ -176,6 +176,7 @@ struct rt_camera {
     int rays = 0;                    // kOptRays: pixels per wave of kernel 3 (0: auto_rays)
     int last_rays = 0;               // the pixels per wave the last kernel-3 render used
     int last_fast = 0;               // whether it took the kFast walks (fast_proof)
+    int64_t last_fine = 0;           // kOptFineTiles: fine tiles of the last kernel-3 render
     int items = 2;                   // kOptItems: items per lane per pool iteration
     int flat_variant = 12;           // kOptFlat: flat-list kernel form
     // chunked flat forms: one per-pixel key buffer per stream that renders
@@ -881,7 +882,11 @@ bool fast_proof_shadow(const FrameGeom& g, TraceParams& p) {
     return false;
 }
 
-bool root_rect(const FrameGeom& g, const TraceParams& p, double r[4]) {
+// The root box's corners shifted by the object offset, in the pixel frame:
+// q = A^-1 (c + od) = (a, b, s), the pixel of a point being (a / s, b / s)
+// and s its depth along the rays (s > 0 in front of the eye).  False when A
+// is singular.
+bool root_corners(const FrameGeom& g, const TraceParams& p, double q[8][3]) {
     const float* X = p.xf;
     const float* cols[3] = {g.u_mod, g.v_mod, g.n_mod};
     double A[3][3];
@@ -905,15 +910,22 @@ bool root_rect(const FrameGeom& g, const TraceParams& p, double r[4]) {
     inv[2][1] = (A[0][1] * A[2][0] - A[0][0] * A[2][1]) / det;
     inv[2][2] = (A[0][0] * A[1][1] - A[0][1] * A[1][0]) / det;
     const double od[3] = {X[3], X[7], X[11]};
-    r[0] = r[2] = INFINITY;
-    r[1] = r[3] = -INFINITY;
     for (int k = 0; k < 8; k++) {
         const double cc[3] = {p.root_box[(k & 1) ? 1 : 0] + od[0], p.root_box[(k & 2) ? 3 : 2] + od[1],
                               p.root_box[(k & 4) ? 5 : 4] + od[2]};
-        double q[3];
-        for (int i = 0; i < 3; i++) q[i] = inv[i][0] * cc[0] + inv[i][1] * cc[1] + inv[i][2] * cc[2];
-        if (!(q[2] > 1e-9 * (fabs(q[0]) + fabs(q[1]) + fabs(q[2])))) return false;
-        const double x = q[0] / q[2], y = q[1] / q[2];
+        for (int i = 0; i < 3; i++) q[k][i] = inv[i][0] * cc[0] + inv[i][1] * cc[1] + inv[i][2] * cc[2];
+    }
+    return true;
+}
+
+bool root_rect(const FrameGeom& g, const TraceParams& p, double r[4]) {
+    double q[8][3];
+    if (!root_corners(g, p, q)) return false;
+    r[0] = r[2] = INFINITY;
+    r[1] = r[3] = -INFINITY;
+    for (int k = 0; k < 8; k++) {
+        if (!(q[k][2] > 1e-9 * (fabs(q[k][0]) + fabs(q[k][1]) + fabs(q[k][2])))) return false;
+        const double x = q[k][0] / q[k][2], y = q[k][1] / q[k][2];
         if (!std::isfinite(x) || !std::isfinite(y)) return false;
         r[0] = std::min(r[0], x); r[1] = std::max(r[1], x);
         r[2] = std::min(r[2], y); r[3] = std::max(r[3], y);
@@ -921,6 +933,68 @@ bool root_rect(const FrameGeom& g, const TraceParams& p, double r[4]) {
     r[0] = floor(r[0]) - 1; r[1] = ceil(r[1]) + 1;
     r[2] = floor(r[2]) - 1; r[3] = ceil(r[3]) + 1;
     return true;
+}
+
+// The screen rectangle of a root box that straddles the eye plane (round 6:
+// an object moved to the camera's depth, `--animate`), a work-packing hint
+// for the unfused (coarse-group) path only.  The pixels whose rays meet the
+// box in front of the eye are the images (a/s, b/s) of the box's part with
+// s > 0, a polytope whose vertices are the corners with s > 0 and the edges'
+// crossings of s = 0; a/s and b/s are linear-fractional, so their extremes
+// over it lie at the corners with s > 0, or are unbounded towards the sign of
+// a (b) at a crossing.  Returns 0 when no rectangle helps (singular A, a
+// crossing at a = 0 or b = 0); 1 with the (possibly half-unbounded)
+// rectangle; 2 when the eye lies inside the box, where every ray's entry
+// parameter maxt0 is negative (TD/Trixel.cu:95 fails), or no corner lies in
+// front of the eye (a box behind the eye plane that box_behind's margins do
+// not cover): the whole frame goes to coarse groups, whose certain-miss and
+// root tests are exact.
+int root_rect_clipped(const FrameGeom& g, const TraceParams& p, double r[4]) {
+    const double od[3] = {p.xf[3], p.xf[7], p.xf[11]};
+    bool inside = true;
+    for (int k = 0; k < 3; k++) {
+        const double lo = (double)p.root_box[2 * k] + od[k], hi = (double)p.root_box[2 * k + 1] + od[k];
+        const double m = 1e-6 * std::max(1.0, std::max(fabs(lo), fabs(hi)));
+        inside = inside && lo < -m && hi > m;
+    }
+    if (inside) {
+        r[0] = r[2] = 1.0;
+        r[1] = r[3] = -1.0;  // empty
+        return 2;
+    }
+    double q[8][3];
+    if (!root_corners(g, p, q)) return 0;
+    r[0] = r[2] = INFINITY;
+    r[1] = r[3] = -INFINITY;
+    bool front = false;
+    for (int k = 0; k < 8; k++) {
+        if (q[k][2] > 0.0) {
+            front = true;
+            const double x = q[k][0] / q[k][2], y = q[k][1] / q[k][2];
+            if (!std::isfinite(x) || !std::isfinite(y)) return 0;
+            r[0] = std::min(r[0], x); r[1] = std::max(r[1], x);
+            r[2] = std::min(r[2], y); r[3] = std::max(r[3], y);
+        }
+        for (int bit = 1; bit < 8; bit <<= 1) {  // each edge once, from its corner with the bit clear
+            const int n = k | bit;
+            if (n == k) continue;
+            const double s0 = q[k][2], s1 = q[n][2];
+            if (!((s0 > 0.0) != (s1 > 0.0))) continue;
+            const double f = s0 / (s0 - s1);
+            const double a = q[k][0] + (q[n][0] - q[k][0]) * f, b = q[k][1] + (q[n][1] - q[k][1]) * f;
+            if (!(a != 0.0 && b != 0.0) || !std::isfinite(a) || !std::isfinite(b)) return 0;
+            if (a > 0.0) r[1] = INFINITY; else r[0] = -INFINITY;
+            if (b > 0.0) r[3] = INFINITY; else r[2] = -INFINITY;
+        }
+    }
+    if (!front) {
+        r[0] = r[2] = 1.0;
+        r[1] = r[3] = -1.0;  // empty
+        return 2;
+    }
+    r[0] = floor(r[0]) - 1; r[1] = ceil(r[1]) + 1;
+    r[2] = floor(r[2]) - 1; r[3] = ceil(r[3]) + 1;
+    return 1;
 }
 
 // Whether the (translated) root box lies behind the eye for every pixel's ray
@@ -1014,10 +1088,25 @@ bool set_fine_region(const FrameGeom& c, TraceParams& p, int per_wave, bool fuse
     p.fill_blocks = 0;
     p.far_all = 0;
     double r[4];
+    bool clipped = false;
     // coarse groups are indexed in 32 bits (k_coarse_kd3)
     if (per_wave <= 0 || (int64_t)p.nslots * p.groups_x >= ((int64_t)1 << 31)) return false;
     if (!root_rect(c, p, r)) {
-        if (!behind_ok || !box_behind(c, p)) return false;
+        // a box at the eye's depth (not wholly behind it): the clipped
+        // rectangle on the unfused path, or every group coarse when the eye
+        // is inside the box (round 6: such poses of a moving object ran the
+        // whole frame as fine units, 73-87 us for an empty frame)
+        const bool behind = behind_ok && box_behind(c, p);
+        if (!behind && behind_ok && !(c.debug & 8192)) {  // (debug bit 8192: off)
+            double rc[4];
+            if (root_rect_clipped(c, p, rc) > 0) {
+                if (fused) return set_fine_region(c, p, per_wave, false, behind_ok);
+                for (int k = 0; k < 4; k++) r[k] = rc[k];
+                clipped = true;
+                goto have_rect;
+            }
+        }
+        if (!behind) return false;
         // the box behind the eye for every pixel: no fine tiles, every group
         // background (far_all), filled by the fine kernel's blocks under any
         // transform
@@ -1031,10 +1120,15 @@ bool set_fine_region(const FrameGeom& c, TraceParams& p, int per_wave, bool fuse
         p.far_all = 1;
         return true;
     }
+have_rect:
     // r is the projection widened by a pixel; far groups lie 2 more outside
+    // (not for a clipped rectangle: its groups outside keep the coarse
+    // kernel's certain-miss and exact tests)
     auto clampi = [](double v) { return (int32_t)std::max(-1e9, std::min(1e9, v)); };
-    p.far_rect[0] = clampi(r[0] - 2); p.far_rect[1] = clampi(r[1] + 2);
-    p.far_rect[2] = clampi(r[2] - 2); p.far_rect[3] = clampi(r[3] + 2);
+    if (!clipped) {
+        p.far_rect[0] = clampi(r[0] - 2); p.far_rect[1] = clampi(r[1] + 2);
+        p.far_rect[2] = clampi(r[2] - 2); p.far_rect[3] = clampi(r[3] + 2);
+    }
     if (fused) {  // fine tiles over everything within the far rectangle
         r[0] -= 2; r[1] += 2; r[2] -= 2; r[3] += 2;
     }
@@ -1792,6 +1886,7 @@ static int render_common(rt_camera* c, const float* xform, uint32_t mode, uint32
         // shadow render), bit 2: under an object transform
         c->last_fast = (p.fast ? 1 : 0) | ((p.fast_sh && (flags & RT_FLAG_SHADOW)) ? 2 : 0) |
                        ((p.fast && !p.plain_xf) ? 4 : 0);
+        c->last_fine = (int64_t)p.tiles_x * p.block_rows;
     }
     int trial;
     p.any_order = any_order_for(c, flags, stream, trial) | ((c->debug & 16) ? 4 : 0);
@@ -2288,6 +2383,7 @@ extern "C" int rt_camera_get_option(const rt_camera* c, int32_t key, int32_t* va
     case kOptSplitUsed: *value = c->order_split; return RT_OK;
     case kOptFastUsed: *value = c->last_fast; return RT_OK;
     case kOptOrderRestores: *value = (int32_t)std::min<uint64_t>(c->restores, INT32_MAX); return RT_OK;
+    case kOptFineTiles: *value = (int32_t)std::min<int64_t>(c->last_fine, INT32_MAX); return RT_OK;
     case kOptShadowOrder: *value = c->shadow_order >= 0 ? c->shadow_order : c->any_best; return RT_OK;
     case 10:
     case 11: return fail(RT_ERR_INVALID, "rt_camera_get_option: key %d is retired (ABI 2)", key);

@@ -58,12 +58,14 @@ enum Option : int32_t {
     // 10, 11: retired (ABI 2; round 4's coop-used and frame-group keys)
     kOptFastUsed = 12,  // get only: which walks of the last kernel-3 render took the kFast forms (bit mask)
     kOptOrderRestores = 13,  // get only: kept cost orders restored (restore_order)
+    kOptFineTiles = 14,  // get only: fine tiles (one kRays unit per wave) of the last kernel-3 render
     kOptDebug = 100,    // diagnostics: 1 = skip traversal, 2 = per-wave timestamps, 4 = every group
                         // coarse, 8 = coarse kernel on a side stream beside the fine one,
                         // 16 = counted shadow walks stop at occluders (the timed walk's work),
                         // 32 = counting renders stop after the root test, 64 = order / cost
                         // buffers sized for the current grid only, 256 = no held fine region,
                         // 512 = no split tiles, 1024 = no two-level iterations, 2048 = no kFast walks,
+                        // 8192 = no clipped rectangle for a root box at the eye's depth,
                         // 16384 = record-load statistics (diagnostic builds, RT_VMEM_STATS)
     kOptPoolCap = 101,  // tests: shrink kernel 3's item pool (66..kPoolCap) to force its fallback
 };

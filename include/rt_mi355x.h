@@ -47,7 +47,8 @@ typedef enum rt_status {
 #define RT_FLAG_COUNT 2u       /* accumulate traversal counters (rt_camera_counters)  */
 /* One shadow ray per hit pixel (config C5; the reference's commented-out hook
  * at TD/Camera.cu:28-34).  The segment from the light (2,2,2) to the hit is
- * walked with the reference's traversal rules; a pixel with an occluder
+ * walked with the reference's traversal rules, entering a box only where the
+ * segment enters it (entry parameter below Lmax, round 6); a pixel with an occluder
  * (any triangle but its own, w < 0.999*|segment|) is 0x00000000.  KD mode and
  * the wave-cooperative kernel only; the shadow rays'
  * visits are added to the same counters. */
@@ -436,6 +437,9 @@ int rt_camera_info(const rt_camera* c, int32_t* w, int32_t* h, int32_t* max_dept
  * order it last measured there (a camera alternating between two tilings,
  * e.g. rt_run_frames' multi-frame 32-ray rule and the per-frame 16-ray one) */
 #define RT_OPT_ORDER_RESTORES 13
+/* get only: the fine tiles (one kRays-pixel unit per wave) of the last
+ * kernel-3 render; every other 8x8 group was a coarse or far group */
+#define RT_OPT_FINE_TILES 14
 int rt_camera_set_option(rt_camera* c, int32_t key, int32_t value);
 int rt_camera_get_option(const rt_camera* c, int32_t key, int32_t* value);
 

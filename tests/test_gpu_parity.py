@@ -749,6 +749,63 @@ def test_coarse_general_transforms(k, debug):
     _assert_same((argb2, hit2), (oargb, ohit), f"xf {k} debug {debug} (no counters)")
 
 
+# A root box at the eye's depth (round 6): an object moved beside or around
+# the camera (the keyboard path's `--animate` poses reach it).  Its rectangle
+# comes from the box's part in front of the eye (root_rect_clipped), and an
+# eye inside the box sends every group to the coarse kernel's exact root test
+# (no ray enters such a box, TD/Trixel.cu:95).  Debug bit 8192: the previous
+# whole-frame fine grid.  The frames are the oracle's either way.
+def _xlate(t, deg=0.0):
+    x = _rot_y(deg)
+    x[3], x[7], x[11] = t
+    return x
+
+
+_STRADDLE = [((0.10, 0.0, -0.958463), 0.0), ((-0.067, 0.0, -0.953463), 0.0), ((0.0, 0.075, -0.958463), 0.0),
+             ((0.0, -0.095, -0.948463), 0.0), ((0.10, 0.0, -0.958463), 12.0), ((0.03, 0.0, -0.998463), 0.0),
+             ((0.0, -0.0101542, -0.998463), 30.0), ((-0.5, 0.0, -1.1), 0.0), ((-0.5, 0.0, -1.1), -20.0)]
+
+
+@pytest.mark.parametrize("k", range(len(_STRADDLE)))
+def test_root_box_at_eye_depth(k):
+    t, deg = _STRADDLE[k]
+    xf = _xlate(t, deg)
+    from cpp_cuda_raytracer_dev_amd import _lib
+    oargb, ohit, ocnt = H.oracle_render("rabbit_70k", 240, 136, 0, xform=xf)
+    fine = {}
+    for debug in (None, 8192):
+        s = H.GpuScene("rabbit_70k", 240, 136, kernel=3, debug=debug)
+        argb, hit, cnt = s.render(0, xform=xf, count=True)
+        _assert_same((argb, hit), (oargb, ohit), f"straddle {k} debug {debug}")
+        _counters_match(cnt, ocnt, 3)
+        argb2, hit2, _ = s.render(0, xform=xf, shadow=True)
+        sargb, shit, _ = H.oracle_render("rabbit_70k", 240, 136, 0, xform=xf, shadow=True)
+        _assert_same((argb2, hit2), (sargb, shit), f"straddle {k} debug {debug} shadow")
+        fine[debug] = s.cam.get_option(_lib.RT_OPT_FINE_TILES)
+        s.close()
+    # the whole frame was fine before; the clipped rectangle (or none, for an
+    # eye inside the box) leaves fewer fine tiles
+    assert fine[8192] == (240 // 8) * (136 // 8), fine
+    assert fine[None] < fine[8192], fine
+
+
+def test_camera_inside_root_box():
+    """An untransformed object with the eye inside its root box: no ray enters
+    the box, the groups run the coarse kernel's exact test, not fine units."""
+    from cpp_cuda_raytracer_dev_amd import _lib
+    pose = dict(pos=(-0.01, 0.11, -0.02), look_at=(-0.01, 0.11, 1.0))
+    for debug in (None, 8192):
+        s = H.GpuScene("rabbit_70k", 240, 136, cam_kw=pose, kernel=3, debug=debug)
+        argb, hit, cnt = s.render(0, count=True)
+        oargb, ohit, ocnt = H.oracle_render("rabbit_70k", 240, 136, 0, cam_kw=pose)
+        _assert_same((argb, hit), (oargb, ohit), f"inside debug {debug}")
+        _counters_match(cnt, ocnt, 3)
+        assert (ohit < 0).all()
+        tiles = s.cam.get_option(_lib.RT_OPT_FINE_TILES)
+        assert tiles == (0 if debug is None else (240 // 8) * (136 // 8)), (debug, tiles)
+        s.close()
+
+
 @pytest.mark.parametrize("debug", [None, 4])
 def test_coarse_shadow(debug):
     s = H.GpuScene("dragon", 960, 540, kernel=3, debug=debug)
