@@ -1746,6 +1746,61 @@ __device__ __forceinline__ float4 share4(float4 v, int addr) {
 #ifndef RT_XMASKED_LOADS
 #define RT_XMASKED_LOADS 1
 #endif
+// Quad-transposed record loads (round 6, kFast one-level pops): in load j
+// the four lanes of a quad fetch the four 16-B quarters of quad lane j's
+// 64-B record (lane r the quarter r ^ j), so every quad touches one line per
+// load -- the L1 / texture units' floor of 16 quad-cycles per wave load
+// (profiles/r06/ubench: a load costs the sum over its quads of the distinct
+// lines each touches) -- and a 4 x 4 exchange inside the quad (lane-bit
+// selects and DPP xor reads) returns each lane its own record.
+#ifndef RT_QUAD_LOADS
+#define RT_QUAD_LOADS 0
+#endif
+template <int kCtrl>
+__device__ __forceinline__ float dpp_f(float x) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), kCtrl, 0xF, 0xF, true));
+}
+template <int kCtrl>
+__device__ __forceinline__ uint32_t dpp_u(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, kCtrl, 0xF, 0xF, true);
+}
+// The byte offset of an item's record from P.inode (record_fast).
+__device__ __forceinline__ uint32_t rec_off(const TraceParams& P, uint32_t ref) {
+    return (ref << 6) + ((int32_t)ref < 0 ? P.leaf_off : 0u);
+}
+// Load j: quad lane r fetches quarter r ^ j of quad lane j's record (every
+// lane of the wave active).
+__device__ __forceinline__ void quad_load(const TraceParams& P, uint32_t off, int lane, float4& x0, float4& x1,
+                                          float4& x2, float4& x3) {
+    const char* base = (const char*)P.inode;
+    const uint32_t q = ((uint32_t)lane & 3u) << 4;
+    const uint32_t o0 = dpp_u<0x00>(off), o1 = dpp_u<0x55>(off), o2 = dpp_u<0xAA>(off), o3 = dpp_u<0xFF>(off);
+    x0 = *(const float4*)(base + o0 + q);
+    x1 = *(const float4*)(base + o1 + (q ^ 0x10u));
+    x2 = *(const float4*)(base + o2 + (q ^ 0x20u));
+    x3 = *(const float4*)(base + o3 + (q ^ 0x30u));
+}
+// One component of the exchange: lane r holds x_j = (quarter r ^ j of lane
+// j's record); y_m = quarter m of lane r's own record = lane (r ^ m)'s
+// x_r, read by a DPP xor-m of t_m, where t_m(s) = x_(s ^ m) (selects by the
+// lane's bits).
+__device__ __forceinline__ void quad_xpose1(float x0, float x1, float x2, float x3, bool b0, bool b1, float& y0,
+                                            float& y1, float& y2, float& y3) {
+    const float p0 = b0 ? x1 : x0, p1 = b0 ? x0 : x1, p2 = b0 ? x3 : x2, p3 = b0 ? x2 : x3;
+    y0 = b1 ? p2 : p0;
+    y1 = dpp_f<0xB1>(b1 ? p3 : p1);  // quad_perm [1,0,3,2]
+    y2 = dpp_f<0x4E>(b1 ? p0 : p2);  // [2,3,0,1]
+    y3 = dpp_f<0x1B>(b1 ? p1 : p3);  // [3,2,1,0]
+}
+__device__ __forceinline__ void quad_xpose(float4& a0, float4& a1, float4& a2, float4& a3, int lane) {
+    const bool b0 = (lane & 1) != 0, b1 = (lane & 2) != 0;
+    float4 y0, y1, y2, y3;
+    quad_xpose1(a0.x, a1.x, a2.x, a3.x, b0, b1, y0.x, y1.x, y2.x, y3.x);
+    quad_xpose1(a0.y, a1.y, a2.y, a3.y, b0, b1, y0.y, y1.y, y2.y, y3.y);
+    quad_xpose1(a0.z, a1.z, a2.z, a3.z, b0, b1, y0.z, y1.z, y2.z, y3.z);
+    quad_xpose1(a0.w, a1.w, a2.w, a3.w, b0, b1, y0.w, y1.w, y2.w, y3.w);
+    a0 = y0; a1 = y1; a2 = y2; a3 = y3;
+}
 #ifndef RT_SHMASKED_LOADS
 #define RT_SHMASKED_LOADS 0
 #endif
@@ -1819,6 +1874,7 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
         const float4* p1 = kFastRec ? record_fast(P, it1.x) : record_of(P, it1.x);
         float4 a0, a1, a2, a3, b0, b1, b2, b3;
         constexpr bool kShared = RT_SHARED_LOADS != 0 && kFastRec;
+        constexpr bool kQuad = RT_QUAD_LOADS != 0 && kFast && !kAny && !kX && !kShared;
         int lead0 = 0, lead1 = 0;
         bool st0 = false, st1 = false;
         if (kShared) {
@@ -1831,7 +1887,11 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
         } else {
             vmem_stat(P, 0, p0, kShared ? st0 : kMasked ? act0 : true, act0);
         }
-        if (kShared && RT_SHARED_BUF) {
+        if (kQuad) {
+            // every lane (idle ones re-read item base's record, a valid one)
+            quad_load(P, rec_off(P, it0.x), lane, a0, a1, a2, a3);
+            if (take > 64) quad_load(P, rec_off(P, it1.x), lane, b0, b1, b2, b3);
+        } else if (kShared && RT_SHARED_BUF) {
             // the run starts load; the other lanes take their run start's
             // record (below, by ds_bpermute).  The resource spans the
             // camera's records (inode, then trec at leaf_off; < 4 GiB)
@@ -1862,6 +1922,7 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
             b0 = p1[0]; b1 = p1[1]; b2 = p1[2]; b3 = p1[3];
         }
         RT_RECORD_FENCE();
+        if (kQuad) quad_xpose(a0, a1, a2, a3, lane);
         if (kShared) {
             a0 = share4(a0, lead0); a1 = share4(a1, lead0); a2 = share4(a2, lead0); a3 = share4(a3, lead0);
         }
@@ -1872,6 +1933,7 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
             total = fast_slot<kStride, kCount, kOct>(P, items, base, s_ray, s_key, s_tri, it0, act0, a0, a1, a2, a3, n_int,
                                                n_leaf, n_acc, n_desc);
             if (take > 64) {
+                if (kQuad) quad_xpose(b0, b1, b2, b3, lane);
                 if (kShared) {
                     b0 = share4(b0, lead1); b1 = share4(b1, lead1); b2 = share4(b2, lead1); b3 = share4(b3, lead1);
                 }
