@@ -1983,6 +1983,13 @@ __device__ __forceinline__ void pool_walk(const TraceParams& P, uint4* items, co
     }
 }
 
+// One instance of the shadow walk per octant of its rays (round 6; the
+// primary walk's RT_OCT_WALKS): the slab_pair_xoct near / far selects are
+// compile-time.  C5 3,783 -> 3,838 FPS, knot + shadows 6,276 -> 6,369,
+// dragon + shadows 9,092 -> 9,203 (r06r, interleaved).
+#ifndef RT_SH_OCT
+#define RT_SH_OCT 1
+#endif
 // The root's visit folded into the seeding of kFast walks (trace_unit).
 #ifndef RT_ROOT_VISIT
 #define RT_ROOT_VISIT 1
@@ -2217,10 +2224,34 @@ __device__ __forceinline__ void trace_unit(const TraceParams& P, WaveLds<kRays, 
         } else {
             n = seed_root<kCount, true>(P, items, Sh, sh_live, lane, C.n_int, C.n_desc, lmax);
         }
-        if (sh_fast)
-            pool_walk<kCap, RL::kStride, true, kCount, true, kShadow - 1, false, 8, true>(
-                P, items, S_.ray, S_.key, S_.tri, n, lane, iters, popped, C.n_int, C.n_leaf, C.n_acc, C.n_desc);
-        else
+        int sh_oct = 8;  // the octant every live shadow ray lies in (slab_pair_xoct), 8 = mixed
+        if (RT_SH_OCT && sh_fast) {
+            const unsigned long long LV = __ballot(sh_live), PX = __ballot(sh_live && Sh.rx > 0.0f),
+                                     PY = __ballot(sh_live && Sh.ry > 0.0f), PZ = __ballot(sh_live && Sh.rz > 0.0f);
+            if ((PX == 0ull || PX == LV) && (PY == 0ull || PY == LV) && (PZ == 0ull || PZ == LV))
+                sh_oct = (PX == LV ? 1 : 0) | (PY == LV ? 2 : 0) | (PZ == LV ? 4 : 0);
+        }
+        if (sh_fast) {
+#define RT_SH_WALK(o)                                                                                                \
+    pool_walk<kCap, RL::kStride, true, kCount, true, kShadow - 1, false, o, true>(                                     \
+        P, items, S_.ray, S_.key, S_.tri, n, lane, iters, popped, C.n_int, C.n_leaf, C.n_acc, C.n_desc)
+            if (RT_SH_OCT) {
+                switch (sh_oct) {
+                case 0: RT_SH_WALK(0); break;
+                case 1: RT_SH_WALK(1); break;
+                case 2: RT_SH_WALK(2); break;
+                case 3: RT_SH_WALK(3); break;
+                case 4: RT_SH_WALK(4); break;
+                case 5: RT_SH_WALK(5); break;
+                case 6: RT_SH_WALK(6); break;
+                case 7: RT_SH_WALK(7); break;
+                default: RT_SH_WALK(8); break;
+                }
+            } else {
+                RT_SH_WALK(8);
+            }
+#undef RT_SH_WALK
+        } else
             pool_walk<kCap, RL::kStride, true, kCount, true, kShadow - 1>(P, items, S_.ray, S_.key, S_.tri, n, lane, iters,
                                                                          popped, C.n_int, C.n_leaf, C.n_acc, C.n_desc);
         if (lane < kRays) shadowed = S_.key[lane] == 0ull;
@@ -2478,7 +2509,8 @@ __device__ __forceinline__ unsigned long long coarse_root(const TraceParams& P, 
 
 // kShadow: a second pool walk traces one shadow ray per hit (SURVEY.md §8a
 // a12; definition in oracle/oracle.c trace_shadow): the segment from the light
-// (2,2,2) to the hit, walked from the light with the reference's rules.
+// (2,2,2) to the hit, walked from the light with the reference's rules and
+// entering only the boxes the segment enters (entry parameter below Lmax).
 // One fine tile per block (the tiles covering the root box's screen
 // rectangle, or the whole frame), one unit per wave.
 // Occupancy: a 16-ray block's LDS (26 KB) admits 6 blocks per CU, and
