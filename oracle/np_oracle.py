@@ -266,9 +266,11 @@ def trace_kd(S, X, cam_rmd):
 SHADOW_SCALE = F(0.9990234375)  # 1 - 2^-10
 
 
-def trace_shadow(S, rmi, d, ray):
+def trace_shadow(S, rmi, d, ray, segment=True):
     """The shadow segment of a hit (oracle.c trace_shadow): from the light
-    (2,2,2) to H = d*r - od, walked from the light; True if occluded."""
+    (2,2,2) to H = d*r - od, walked from the light; True if occluded.
+    segment=False: rounds 1-5's walk of the whole ray beyond H (tests only:
+    the round-6 segment walk gives the same images)."""
     r, od = ray
     sv = [F(F(F(d * r[k]) - od[k]) - F(2)) for k in range(3)]
     L2 = F(F(F(sv[0] * sv[0]) + F(sv[1] * sv[1])) + F(sv[2] * sv[2]))
@@ -280,7 +282,7 @@ def trace_shadow(S, rmi, d, ray):
         if t != rmi and _mt_accept(u, v, w, lmax):
             hit[0] = True
 
-    _walk(S, list(s), (F(-2), F(-2), F(-2)), leaf, lim=lmax)
+    _walk(S, list(s), (F(-2), F(-2), F(-2)), leaf, lim=lmax if segment else None)
     return hit[0]
 
 
@@ -330,7 +332,7 @@ def phong(pnt, nrm, rmd, rad):
 RAD = (F(0.1), F(0.55), F(0.2))
 
 
-def render(points9, nodes, cam, mode=0, xform=None, shadow=False):
+def render(points9, nodes, cam, mode=0, xform=None, shadow=False, segment=True):
     S = prepare(points9, nodes if mode == 0 else None, cam)
     X = IDENT if xform is None else np.asarray(xform, F)
     w, h = cam["w"], cam["h"]
@@ -348,7 +350,7 @@ def render(points9, nodes, cam, mode=0, xform=None, shadow=False):
                 hit[i] = rmi
                 if rmi >= 0:
                     argb[i] = phong(out[0], out[1], rmd, RAD)
-                    if shadow and trace_shadow(S, rmi, d, ray):
+                    if shadow and trace_shadow(S, rmi, d, ray, segment):
                         argb[i] = 0
     return argb, hit
 

@@ -328,6 +328,26 @@ def test_shadow_oracle_matches_recorded_hashes(name, w, h):
     assert (cnt == g[key + "_counters"]).all()
 
 
+@pytest.mark.parametrize("name,w,h", [("dump", 40, 24), ("rabbit_70k", 64, 36), ("tester", 48, 27)])
+def test_shadow_segment_walk_same_images(name, w, h):
+    """Round 6: the shadow walk enters a box only below Lmax (oracle.c
+    trace_shadow).  The numpy restatement walking the whole ray beyond the
+    hit, as rounds 1-5 defined it, gives the same images, and the segment walk
+    the committed golden ones."""
+    from cpp_cuda_raytracer_dev_amd import scenes
+    from oracle import np_oracle as N
+    v, a, ix = scenes.fixture_mesh(name)
+    pts, boxes = N.assemble(v, a, ix)
+    nodes, cam = N.build_kd(boxes), N.camera(w, h)
+    seg, seg_hit = N.render(pts, nodes, cam, 0, shadow=True)
+    ray, ray_hit = N.render(pts, nodes, cam, 0, shadow=True, segment=False)
+    assert (seg_hit == ray_hit).all() and (seg == ray).all()
+    g = H.golden()
+    key = f"{name}_{w}x{h}_shadow"
+    if key + "_argb" in g.files:
+        assert (seg == g[key + "_argb"]).all()
+
+
 def test_shadow_only_darkens_hit_pixels():
     """Shadows change nothing but the colour of some hit pixels (to 0), and
     add the shadow walks' visits to the counters."""
